@@ -1,0 +1,256 @@
+#!/usr/bin/env python3
+"""bench.py — MCMC steps×chains/sec on the D=32 Gaussian target (BASELINE cfg 2).
+
+One "step" = one MCMC iteration of every chain on every GPU: proposal,
+log-prior, log-likelihood, MH accept/reject, rolling acceptance and the full
+per-step histories (θ, θ°, ll, accept bit) written to HBM — the reference's
+run! outputs (src/run.jl:237-239, 319, 333-334).  Chains are sharded
+embarrassingly: rank r owns global chain ids [r·C, (r+1)·C) (weak scaling,
+no data-path collective).  Diagnostics (split-R̂, acceptance) are reduced once
+after the timed region with one all-reduce.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "extensiblemcmc.jl_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000)
+    ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--chains-per-gpu", type=int, default=65536)
+    ap.add_argument("--history", choices=["full", "accept_only"], default="full")
+    ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
+    ap.add_argument("--lpc", type=int, default=0)
+    ap.add_argument("--steps-per-launch", type=int, default=100)
+    ap.add_argument("--reps", type=int, default=1, help="repeat the timed region; report the median")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(w, seconds, ll_mode):
+    """The oracle (C restatement, OpenMP over chains) on a bounded sample of the
+    same workload, histories included, on this host's cores."""
+    from oracle import oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = max(1, min(threads, 16))
+    C = 256 * threads
+    chunk = 50
+    st = O.OracleState(np.zeros((C, w.D)))
+    hist = O.alloc_history(C, w.D, chunk)
+    it = 1
+    O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
+              ll_mode=ll_mode, nthreads=threads, hist=hist)  # warm (page faults, caches)
+    it += chunk
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
+                  ll_mode=ll_mode, nthreads=threads, hist=hist)
+        it += chunk
+        steps += chunk
+    dt = time.perf_counter() - t0
+    return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{C} chains x {steps} iterations of the same D=32 workload ({w.nobs} obs, "
+                      f"{'per-observation' if ll_mode == 0 else 'sufficient-statistic'} log-likelihood, "
+                      f"full histories), oracle/liboracle.so, {dt:.1f} s"}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from extensible_mcmc import _lib as L
+    from extensible_mcmc import diagnostics as DG
+    from extensible_mcmc import workloads as W
+    from extensible_mcmc.engine import Engine, EngineConfig
+
+    Cg = a.chains_per_gpu
+    w = W.cfg2(Cg)
+    ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
+    hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
+    M = a.warmup + a.steps * a.reps
+    eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=rank * Cg,
+                              device=local, history_mode=hist, lanes_per_chain=a.lpc,
+                              steps_per_launch=a.steps_per_launch))
+    eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
+    eng.set_state(np.zeros((Cg, w.D)))
+    if a.warmup:
+        eng.run_iters(1, a.warmup)
+    eng.synchronize()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier(device_ids=[local])
+
+    times, kern = [], []
+    it = a.warmup + 1
+    for _ in range(a.reps):
+        eng.set_timing(True)
+        barrier()
+        eng.synchronize()
+        if dist is not None:
+            import torch
+
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.run_iters(it, a.steps)
+        eng.synchronize()
+        if dist is not None:
+            torch.cuda.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        ms, launches, nbytes = eng.get_timing(reset=True)
+        eng.set_timing(False)
+        kern.append((ms, launches, nbytes))
+        if dist is not None:
+            t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        times.append(dt)
+        it += a.steps
+    order = np.argsort(times)
+    mid = int(order[len(order) // 2])
+    dt = times[mid]
+    ms, launches, nbytes = kern[mid]
+
+    # diagnostics over the timed window: one all-reduce of 3·D+3 doubles
+    mom = eng.moments_window(a.warmup + 1, a.steps, split=True) if hist == L.HIST_FULL else None
+    if mom is not None and dist is not None:
+        mom = DG.allreduce_sums(mom, w.D, device=f"cuda:{local}")
+    diag = DG.rhat_from_sums(mom) if mom is not None else None
+
+    if rank != 0:
+        dist.destroy_process_group()
+        return
+
+    total_chains = Cg * world
+    value = total_chains * a.steps / dt
+    avg_launch_s = ms / 1e3 / launches
+    bytes_per_launch = nbytes / launches
+    achieved = bytes_per_launch / avg_launch_s / 1e9
+    traffic = None
+    pmc = ROOT / "profiles" / "pmc_traffic.json"
+    kname = eng.kernel_name()
+    if pmc.exists():
+        try:
+            tb = json.loads(pmc.read_text()).get(kname)
+            if tb:
+                traffic = tb["bytes_per_chain_step"] * Cg * (a.steps / launches)
+        except Exception:
+            traffic = None
+
+    out = {
+        "metric": "MCMC steps×chains/sec on D=32 Gaussian, 1/2/4/8 MI355X; accept-rate parity",
+        "value": value,
+        "unit": "chain-steps/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": dt / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (GsnTargetLaw(μ*, I32), 10 obs from numpy default_rng(20261015)), θinit = 0",
+        "config": {
+            "workload": f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64",
+            "chains_per_gpu": Cg,
+            "total_chains": total_chains,
+            "dim": w.D,
+            "num_obs": w.nobs,
+            "proposal": "GaussianRandomWalk(σ²I32), σ=2.38/√(D·n)",
+            "prior": "ImproperPrior",
+            "history": a.history,
+            "ll_mode": a.ll_mode,
+            "chain_stats": "rolling acceptance (chain_statistics.jl:51-65)",
+            "steps_per_launch": a.steps_per_launch,
+            "kernel": kname,
+            "parallelism": f"chain-sharded x{world}",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": kname,
+            "algorithmic_bytes_per_launch": bytes_per_launch,
+            "avg_launch_ms": avg_launch_s * 1e3,
+            "launches": launches,
+            "bytes_per_chain_step": (16 * w.D + 8 + 0.125) if hist == L.HIST_FULL else 0.125,
+        },
+        "kernel_chain_steps_per_s": Cg * a.steps / (ms / 1e3),
+    }
+    if diag is not None:
+        out["diagnostics"] = {"accept_rate": diag["accept_rate"], "max_split_rhat": float(np.max(diag["rhat"])),
+                              "max_abs_mean_minus_xbar": float(np.max(np.abs(diag["mean"] - w.obs.mean(0))))}
+    if world == 1 and not a.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds, ll_mode)
+            out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
+        except Exception as e:  # the oracle is a reported baseline, never the measured path
+            out["cpu_baseline"] = {"error": repr(e)}
+        try:
+            out["parity"] = parity_sample(eng, w, a, ll_mode)
+        except Exception as e:
+            out["parity"] = {"error": repr(e)}
+    print(json.dumps(out))
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def parity_sample(eng, w, a, ll_mode, n=8):
+    """Replay n random chains of the measured run on the oracle (bitwise)."""
+    from extensible_mcmc import _lib as L
+    from oracle import oracle as O
+
+    rng = np.random.default_rng(123)
+    picks = np.sort(rng.choice(w.num_chains, n, replace=False))
+    S = a.warmup + a.steps * a.reps
+    acc = eng.get_history(L.H_ACCEPT, 1, S)[:, 0]
+    theta, ll = eng.get_state()
+    ok_acc = ok_th = True
+    for c in picks:
+        st = O.OracleState(np.zeros((1, w.D)))
+        h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
+                      chain0=int(c), ll_mode=ll_mode, history=True)
+        ok_acc &= bool(np.array_equal(acc[:, c], h["acc"][:, 0]))
+        ok_th &= bool(np.array_equal(theta[c], st.theta[0]) and ll[c] == st.ll[0])
+    return {"chains_replayed": int(n), "iterations": int(S), "accept_stream_bitwise": ok_acc,
+            "final_theta_ll_bitwise": ok_th}
+
+
+if __name__ == "__main__":
+    main()

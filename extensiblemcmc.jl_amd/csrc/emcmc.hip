@@ -1,0 +1,835 @@
+// emcmc.hip — libemcmc.so: C ABI (include/emcmc.h) over the gfx950 MCMC step
+// kernels in emcmc_kernels.h.  Build: see extensiblemcmc.jl_amd/Makefile
+// (hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared).
+//
+// The host side here plays the role of the reference's workspace/backend
+// layer (src/workspaces.jl, src/mcmc.jl): it owns the chain state (SoA in
+// HBM), factorises the Gaussian covariances once (the reference re-factorises
+// at every MvNormal construction, random_walk.jl:147,167 and
+// gsn_target.jl:20 — same matrices, so the same factor), and turns a schedule
+// of (mcmciter, pidx) steps into fused multi-step launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/emcmc.h"
+#include "emcmc_kernels.h"
+
+using namespace emcmc;
+
+namespace {
+
+constexpr uint32_t kDefaultRollWindow = 100;  // chain_statistics.jl:27
+constexpr uint32_t kDefaultStepsPerLaunch = 64;
+constexpr size_t kMaxLds = 64 * 1024;
+
+// ----------------------------------------------------------------------------
+// Canonical Cholesky (lower factor L of the upper-stored symmetric Σ), the
+// order oracle/emcmc_oracle.c restates.  Returns false if Σ is not positive
+// definite (the reference throws PosDefException from cholesky()).
+bool cholesky_upper_colmajor(const double *S, int D, std::vector<double> &L) {
+    L.assign((size_t)D * D, 0.0);
+    for (int j = 0; j < D; ++j) {
+        double s = S[j + (size_t)j * D];
+        for (int k = 0; k < j; ++k) s = s - L[(size_t)j * D + k] * L[(size_t)j * D + k];
+        if (!(s > 0.0)) return false;
+        const double ljj = std::sqrt(s);
+        L[(size_t)j * D + j] = ljj;
+        for (int i = j + 1; i < D; ++i) {
+            double t = S[j + (size_t)i * D];  // Σ(j,i), upper triangle
+            for (int k = 0; k < j; ++k) t = t - L[(size_t)i * D + k] * L[(size_t)j * D + k];
+            L[(size_t)i * D + j] = t / ljj;
+        }
+    }
+    return true;
+}
+
+bool is_diag_upper(const double *S, int D) {
+    for (int i = 0; i < D; ++i)
+        for (int j = i + 1; j < D; ++j)
+            if (S[i + (size_t)j * D] != 0.0) return false;
+    return true;
+}
+
+// logdet of a Cholesky factor as LinearAlgebra.logdet(::Cholesky): dd + dd
+double logdet_chol(const std::vector<double> &L, int D) {
+    double dd = 0.0;
+    for (int i = 0; i < D; ++i) dd = dd + log_pos(L[(size_t)i * D + i]);
+    return dd + dd;
+}
+
+// Distributions.mvnormal_c0: −(D·log2π + logdet)/2
+double mvnormal_c0(int D, double logdet) { return -((double)D * kLog2Pi + logdet) / 2.0; }
+
+// host restatement of the canonical blocked sum (used for S_c)
+double canon_sum_host(const double *v, int D) {
+    const int BLK = (D % 8 == 0 && D >= 16) ? 8 : D;
+    const int NB = D / BLK;
+    std::vector<double> b(NB);
+    for (int k = 0; k < NB; ++k) {
+        double s = v[k * BLK];
+        for (int i = 1; i < BLK; ++i) s = s + v[k * BLK + i];
+        b[k] = s;
+    }
+    int n = NB;
+    while (n > 1) {
+        for (int i = 0; i < n / 2; ++i) b[i] = b[2 * i] + b[2 * i + 1];
+        if (n & 1) b[n / 2] = b[n - 1];
+        n = (n + 1) / 2;
+    }
+    return b[0];
+}
+
+struct UpdateHost {
+    uint32_t kernel = 0, prior = 0, adaptation = 0;
+    std::vector<uint32_t> coords;
+    std::vector<double> sigma, L, invdiag;
+    bool diag = false;
+    double c0 = 0.0;
+};
+
+struct TargetHost {
+    uint32_t dim = 0, ll_mode = 0;
+    uint64_t nobs = 0;
+    std::vector<double> mu, sigma, L, invdiag, obs, xbar;
+    bool diag = false;
+    double c0 = 0.0, S_c = 0.0;
+};
+
+using KernelFn = void (*)(StepParams);
+
+struct Variant {
+    KernelFn fn = nullptr;
+    int lpc = 1;
+    bool dense = false;
+    std::string name;
+};
+
+}  // namespace
+
+struct emcmc_handle {
+    emcmc_config cfg{};
+    hipStream_t stream = nullptr;
+    std::string err;
+    std::vector<UpdateHost> updates;
+    TargetHost target;
+    bool target_set = false, allocated = false;
+    uint64_t stats_N = 1;  // GenericChainStats.N (chain_statistics.jl:34)
+    // device buffers
+    double *d_theta = nullptr, *d_ll = nullptr, *d_ra = nullptr;
+    uint64_t *d_ring = nullptr;
+    uint32_t *d_nacc = nullptr, *d_faults = nullptr;
+    double *d_hist_theta = nullptr, *d_hist_prop = nullptr, *d_hist_ll = nullptr;
+    uint8_t *d_hist_acc = nullptr;
+    double *d_consts = nullptr, *d_obs = nullptr;
+    uint32_t *d_iters = nullptr;
+    size_t iters_cap = 0;
+    double *d_scratch = nullptr;  // diagnostics
+    size_t scratch_bytes = 0;
+    uint64_t row_bytes = 0;
+    // dispatch
+    Variant var;
+    size_t lds_bytes = 0;
+    // timing
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    std::vector<hipEvent_t> ev_pool;
+    double timed_ms = 0.0;
+    uint64_t timed_launches = 0;
+    double timed_bytes = 0.0;
+    double pending_bytes = 0.0;
+};
+
+namespace {
+
+emcmc_status fail(emcmc_handle *h, emcmc_status st, const char *fmt, ...) {
+    if (h) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof buf, fmt, ap);
+        va_end(ap);
+        h->err = buf;
+    }
+    return st;
+}
+
+#define HIPCHK(h, expr)                                                                       \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail((h), e_ == hipErrorOutOfMemory ? EMCMC_OUT_OF_MEMORY : EMCMC_HIP_ERROR, \
+                        "%s failed: %s", #expr, hipGetErrorString(e_));                       \
+    } while (0)
+
+// ---- kernel table -----------------------------------------------------------
+struct Key {
+    int D, lpc, full, ll, dense;
+};
+
+template <int D, int LPC, bool FULL, int LL>
+KernelFn diag_fn() {
+    return &rwm_gsn_diag_kernel<D, LPC, FULL, LL>;
+}
+template <int D, bool FULL, int LL>
+KernelFn dense_fn() {
+    return &rwm_gsn_dense_kernel<D, FULL, LL>;
+}
+
+#define DIAG4(D, LPC)                                                                  \
+    {{D, LPC, 1, 0, 0}, diag_fn<D, LPC, true, 0>()}, {{D, LPC, 1, 1, 0}, diag_fn<D, LPC, true, 1>()}, \
+        {{D, LPC, 0, 0, 0}, diag_fn<D, LPC, false, 0>()}, {{D, LPC, 0, 1, 0}, diag_fn<D, LPC, false, 1>()}
+#define DENSE4(D)                                                                        \
+    {{D, 1, 1, 0, 1}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1}, dense_fn<D, true, 1>()},   \
+        {{D, 1, 0, 0, 1}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1}, dense_fn<D, false, 1>()}
+
+struct Entry {
+    Key k;
+    KernelFn fn;
+};
+
+const std::vector<Entry> &kernel_table() {
+    static const std::vector<Entry> t = {
+        DIAG4(1, 1),  DIAG4(2, 1),  DIAG4(3, 1),  DIAG4(4, 1),  DIAG4(8, 1),
+        DIAG4(16, 1), DIAG4(16, 2), DIAG4(32, 1), DIAG4(32, 2), DIAG4(32, 4),
+        DIAG4(64, 2), DIAG4(64, 4), DENSE4(1),    DENSE4(2),    DENSE4(3),
+        DENSE4(4),    DENSE4(8),
+    };
+    return t;
+}
+
+KernelFn lookup(int D, int lpc, bool full, int ll, bool dense) {
+    for (const auto &e : kernel_table())
+        if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == (int)dense)
+            return e.fn;
+    return nullptr;
+}
+
+int auto_lpc(int D) {
+    if (D % 32 == 0) return 4;
+    if (D % 16 == 0) return 2;
+    return 1;
+}
+
+emcmc_status ensure_alloc(emcmc_handle *h) {
+    if (h->allocated) return EMCMC_OK;
+    if (h->updates.empty()) return fail(h, EMCMC_STATE_ERROR, "no update added (emcmc_add_update)");
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, M = h->cfg.num_mcmc_steps;
+    const uint64_t P = h->updates.size();
+    HIPCHK(h, hipMalloc(&h->d_theta, C * D * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_ll, C * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_ra, C * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_ring, 2 * C * sizeof(uint64_t)));
+    HIPCHK(h, hipMalloc(&h->d_nacc, C * sizeof(uint32_t)));
+    HIPCHK(h, hipMalloc(&h->d_faults, C * sizeof(uint32_t)));
+    h->row_bytes = ((C + 63) / 64) * 8;
+    HIPCHK(h, hipMalloc(&h->d_hist_acc, M * P * h->row_bytes));
+    HIPCHK(h, hipMemsetAsync(h->d_hist_acc, 0, M * P * h->row_bytes, h->stream));
+    if (h->cfg.history_mode == EMCMC_HIST_FULL) {
+        HIPCHK(h, hipMalloc(&h->d_hist_theta, M * P * C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_hist_prop, M * P * C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_hist_ll, M * P * C * sizeof(double)));
+    }
+    h->allocated = true;
+    return EMCMC_OK;
+}
+
+emcmc_status select_variant(emcmc_handle *h) {
+    if (!h->target_set || h->updates.empty()) return EMCMC_OK;
+    const UpdateHost &u = h->updates[0];
+    const int D = (int)h->cfg.dim;
+    const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
+    const int ll = (int)h->target.ll_mode;
+    const bool diag = u.diag && h->target.diag;
+    Variant v;
+    if (diag) {
+        int lpc = h->cfg.lanes_per_chain ? (int)h->cfg.lanes_per_chain : auto_lpc(D);
+        v.fn = lookup(D, lpc, full, ll, false);
+        if (!v.fn && !h->cfg.lanes_per_chain) {
+            lpc = 1;
+            v.fn = lookup(D, 1, full, ll, false);
+        }
+        v.lpc = lpc;
+        v.dense = false;
+    } else {
+        v.fn = lookup(D, 1, full, ll, true);
+        v.lpc = 1;
+        v.dense = true;
+    }
+    if (!v.fn)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "no device kernel for D=%d (%s, lanes_per_chain=%u); instantiated: diag D∈{1,2,3,4,8,16,32,64}, "
+                    "dense D∈{1,2,3,4,8}",
+                    D, diag ? "diagonal" : "dense", h->cfg.lanes_per_chain);
+    char nm[160];
+    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s>", v.dense ? "dense" : "diag", D, v.lpc,
+             full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
+    v.name = nm;
+    // constants for this variant
+    std::vector<double> c;
+    const TargetHost &t = h->target;
+    if (!v.dense) {
+        c.resize(4 * (size_t)D);
+        for (int i = 0; i < D; ++i) {
+            c[i] = u.L[(size_t)i * D + i];
+            c[D + i] = u.invdiag[i];
+            c[2 * D + i] = t.invdiag[i];
+            c[3 * D + i] = t.xbar[i];
+        }
+    } else {
+        const size_t DD = (size_t)D * D;
+        c.resize(2 * DD + 3 * (size_t)D);
+        std::copy(u.L.begin(), u.L.end(), c.begin());
+        std::copy(u.invdiag.begin(), u.invdiag.end(), c.begin() + DD);
+        std::copy(t.L.begin(), t.L.end(), c.begin() + DD + D);
+        std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
+        std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
+    }
+    const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
+    const size_t lds = (c.size() + obs_doubles) * sizeof(double);
+    if (lds > kMaxLds)
+        return fail(h, EMCMC_INVALID_ARG,
+                    "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu",
+                    lds, kMaxLds, (unsigned long long)t.nobs);
+    if (h->d_consts) (void)hipFree(h->d_consts);
+    HIPCHK(h, hipMalloc(&h->d_consts, c.size() * sizeof(double)));
+    HIPCHK(h, hipMemcpy(h->d_consts, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (h->d_obs) (void)hipFree(h->d_obs);
+    h->d_obs = nullptr;
+    if (t.nobs) {
+        HIPCHK(h, hipMalloc(&h->d_obs, t.obs.size() * sizeof(double)));
+        HIPCHK(h, hipMemcpy(h->d_obs, t.obs.data(), t.obs.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    h->lds_bytes = lds;
+    h->var = v;
+    return EMCMC_OK;
+}
+
+double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps) {
+    const double C = (double)h->cfg.num_chains, D = (double)h->cfg.dim;
+    const double per_step = (h->cfg.history_mode == EMCMC_HIST_FULL) ? (16.0 * D + 8.0 + 0.125) : 0.125;
+    const double state = 16.0 * D + 2 * 8 + 2 * 8 + 2 * 16 + 2 * 4 + 2 * 4;  // θ, ll, ra, ring, nacc, faults (R+W)
+    return C * ((double)nsteps * per_step + state);
+}
+
+hipEvent_t get_event(emcmc_handle *h) {
+    if (!h->ev_pool.empty()) {
+        hipEvent_t e = h->ev_pool.back();
+        h->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+emcmc_status drain_timing(emcmc_handle *h) {
+    for (auto &p : h->ev) {
+        float ms = 0.f;
+        HIPCHK(h, hipEventSynchronize(p.second));
+        HIPCHK(h, hipEventElapsedTime(&ms, p.first, p.second));
+        h->timed_ms += ms;
+        h->timed_launches += 1;
+        h->ev_pool.push_back(p.first);
+        h->ev_pool.push_back(p.second);
+    }
+    h->ev.clear();
+    h->timed_bytes += h->pending_bytes;
+    h->pending_bytes = 0.0;
+    return EMCMC_OK;
+}
+
+}  // namespace
+
+// ============================================================================
+extern "C" {
+
+emcmc_status emcmc_device_count(int *count) {
+    if (!count) return EMCMC_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    *count = n;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
+    if (!out || !cfg) return EMCMC_INVALID_ARG;
+    *out = nullptr;
+    if (cfg->abi_version != EMCMC_ABI_VERSION) return EMCMC_INVALID_ARG;
+    if (cfg->dim == 0 || cfg->num_chains == 0 || cfg->num_mcmc_steps == 0) return EMCMC_INVALID_ARG;
+    if (cfg->first_chain_id + cfg->num_chains > (1ull << 32)) return EMCMC_INVALID_ARG;  // 32-bit chain ids
+    if (cfg->num_mcmc_steps >= (1ull << 32)) return EMCMC_INVALID_ARG;
+    if (cfg->history_mode > EMCMC_HIST_ACCEPT_ONLY) return EMCMC_INVALID_ARG;
+    if (cfg->roll_window > 128) return EMCMC_INVALID_ARG;
+    if (cfg->lanes_per_chain != 0 && cfg->lanes_per_chain != 1 && cfg->lanes_per_chain != 2 &&
+        cfg->lanes_per_chain != 4)
+        return EMCMC_INVALID_ARG;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return EMCMC_NO_DEVICE;
+    if (cfg->device < 0 || cfg->device >= n) return EMCMC_INVALID_ARG;
+    if (hipSetDevice(cfg->device) != hipSuccess) return EMCMC_HIP_ERROR;
+    auto *h = new emcmc_handle();
+    h->cfg = *cfg;
+    if (h->cfg.roll_window == 0) h->cfg.roll_window = kDefaultRollWindow;
+    if (h->cfg.steps_per_launch == 0) h->cfg.steps_per_launch = kDefaultStepsPerLaunch;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return EMCMC_HIP_ERROR;
+    }
+    *out = h;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
+    if (!h || !u) return EMCMC_INVALID_ARG;
+    if (h->allocated) return fail(h, EMCMC_STATE_ERROR, "updates must be added before set_state/run");
+    const uint32_t D = h->cfg.dim;
+    if (u->num_coords == 0 || !u->coords) return fail(h, EMCMC_INVALID_ARG, "update needs coords");
+    for (uint32_t i = 0; i < u->num_coords; ++i)
+        if (u->coords[i] >= D) return fail(h, EMCMC_INVALID_ARG, "coord %u out of range (D=%u)", u->coords[i], D);
+    if (u->kernel != EMCMC_RW_GAUSSIAN)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "transition kernel %u has no device plugin yet", u->kernel);
+    if (u->prior != EMCMC_PRIOR_IMPROPER)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin yet", u->prior);
+    if (u->adaptation != EMCMC_ADPT_NONE)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "adaptation %u has no device plugin yet", u->adaptation);
+    if (u->pos)
+        for (uint32_t i = 0; i < u->num_coords; ++i)
+            if (u->pos[i]) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "positivity-restricted coordinates not on device yet");
+    if (!h->updates.empty())
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "multi-update (Metropolis-within-Gibbs) schedules not on device yet");
+    if (u->num_coords != D) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device path updates all coordinates jointly");
+    for (uint32_t i = 0; i < D; ++i)
+        if (u->coords[i] != i) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device path needs coords = 1:D in order");
+    if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");
+    UpdateHost uh;
+    uh.kernel = u->kernel;
+    uh.prior = u->prior;
+    uh.adaptation = u->adaptation;
+    uh.coords.assign(u->coords, u->coords + u->num_coords);
+    const int n = (int)u->num_coords;
+    uh.sigma.assign(u->sigma, u->sigma + (size_t)n * n);
+    if (!cholesky_upper_colmajor(uh.sigma.data(), n, uh.L))
+        return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk Σ is not positive definite");
+    uh.invdiag.resize(n);
+    for (int i = 0; i < n; ++i) uh.invdiag[i] = 1.0 / uh.L[(size_t)i * n + i];
+    uh.diag = is_diag_upper(uh.sigma.data(), n);
+    uh.c0 = mvnormal_c0(n, logdet_chol(uh.L, n));
+    h->updates.push_back(std::move(uh));
+    return select_variant(h);
+}
+
+emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t) {
+    if (!h || !t) return EMCMC_INVALID_ARG;
+    if (t->kind != EMCMC_TARGET_GSN) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "target kind %u", t->kind);
+    const uint32_t d = t->dim;
+    if (d != h->cfg.dim)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device GsnTargetLaw needs state = μ (d=%u, D=%u)", d, h->cfg.dim);
+    if (!t->mu || !t->sigma || (t->num_obs && !t->obs)) return fail(h, EMCMC_INVALID_ARG, "null target arrays");
+    if (t->num_obs == 0) return fail(h, EMCMC_INVALID_ARG, "GsnTargetLaw needs observations");
+    if (t->ll_mode > EMCMC_LL_SUFFSTAT) return fail(h, EMCMC_INVALID_ARG, "ll_mode");
+    TargetHost th;
+    th.dim = d;
+    th.ll_mode = t->ll_mode;
+    th.nobs = t->num_obs;
+    th.mu.assign(t->mu, t->mu + d);
+    th.sigma.assign(t->sigma, t->sigma + (size_t)d * d);
+    th.obs.assign(t->obs, t->obs + t->num_obs * d);
+    if (!cholesky_upper_colmajor(th.sigma.data(), (int)d, th.L))
+        return fail(h, EMCMC_INVALID_ARG, "GsnTargetLaw Σ is not positive definite");
+    th.invdiag.resize(d);
+    for (uint32_t i = 0; i < d; ++i) th.invdiag[i] = 1.0 / th.L[(size_t)i * d + i];
+    th.diag = is_diag_upper(th.sigma.data(), (int)d);
+    th.c0 = mvnormal_c0((int)d, logdet_chol(th.L, (int)d));
+    // x̄ = (Σ_k x_k)/n and S_c = Σ_k ‖L⁻¹(x_k − x̄)‖² (canonical order, as oracle/)
+    th.xbar.assign(d, 0.0);
+    for (uint32_t i = 0; i < d; ++i) {
+        double s = 0.0;
+        for (uint64_t k = 0; k < th.nobs; ++k) s = s + th.obs[k * d + i];
+        th.xbar[i] = s / (double)th.nobs;
+    }
+    double Sc = 0.0;
+    std::vector<double> y(d), v(d);
+    for (uint64_t k = 0; k < th.nobs; ++k) {
+        for (uint32_t i = 0; i < d; ++i) {
+            double acc = th.obs[k * d + i] - th.xbar[i];
+            for (uint32_t j = 0; j < i; ++j) acc = std::fma(-th.L[(size_t)i * d + j], y[j], acc);
+            y[i] = acc * th.invdiag[i];
+            v[i] = y[i] * y[i];
+        }
+        Sc = Sc + canon_sum_host(v.data(), (int)d);
+    }
+    th.S_c = Sc;
+    h->target = std::move(th);
+    h->target_set = true;
+    return select_variant(h);
+}
+
+emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {
+    if (!h || !theta) return EMCMC_INVALID_ARG;
+    emcmc_status st = ensure_alloc(h);
+    if (st) return st;
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    HIPCHK(h, hipMemcpyAsync(h->d_theta, theta, C * D * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    std::vector<double> l(C, -INFINITY);
+    if (ll) std::copy(ll, ll + C, l.begin());
+    HIPCHK(h, hipMemcpyAsync(h->d_ll, l.data(), C * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_ring, 0, 2 * C * sizeof(uint64_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_nacc, 0, C * sizeof(uint32_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_faults, 0, C * sizeof(uint32_t), h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));  // host vector l goes out of scope
+    h->stats_N = 1;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps) {
+    if (!h || (!steps && num_steps)) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
+    if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
+    if (!h->var.fn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
+    const uint32_t P = (uint32_t)h->updates.size();
+    for (uint64_t i = 0; i < num_steps; ++i) {
+        if (steps[i].pidx < 1 || steps[i].pidx > P) return fail(h, EMCMC_INVALID_ARG, "step %llu: pidx", (unsigned long long)i);
+        if (steps[i].mcmciter < 1 || steps[i].mcmciter > h->cfg.num_mcmc_steps)
+            return fail(h, EMCMC_INVALID_ARG, "step %llu: mcmciter %u outside 1..M", (unsigned long long)i,
+                        steps[i].mcmciter);
+    }
+    const uint64_t C = h->cfg.num_chains;
+    const int lpc = h->var.lpc;
+    const uint64_t threads = C * (uint64_t)lpc;
+    const dim3 block(256), grid((unsigned)((threads + 255) / 256));
+    const TargetHost &t = h->target;
+    StepParams p{};
+    p.theta = h->d_theta;
+    p.ll = h->d_ll;
+    p.ra = h->d_ra;
+    p.ring = h->d_ring;
+    p.nacc = h->d_nacc;
+    p.faults = h->d_faults;
+    p.hist_theta = h->d_hist_theta;
+    p.hist_prop = h->d_hist_prop;
+    p.hist_ll = h->d_hist_ll;
+    p.hist_acc = h->d_hist_acc;
+    p.consts = h->d_consts;
+    p.obs = h->d_obs;
+    p.C = C;
+    p.row_bytes = h->row_bytes;
+    p.chain0 = (uint32_t)h->cfg.first_chain_id;
+    p.key0 = (uint32_t)h->cfg.seed;
+    p.key1 = (uint32_t)(h->cfg.seed >> 32);
+    p.P = P;
+    p.W = h->cfg.roll_window;
+    p.nobs = (uint32_t)t.nobs;
+    p.rw_c0 = h->updates[0].c0;
+    p.t_c0 = t.c0;
+    p.n_tc0 = (double)t.nobs * t.c0;
+    p.S_c = t.S_c;
+    p.nobs_d = (double)t.nobs;
+    const uint64_t K = h->cfg.steps_per_launch;
+    uint64_t i = 0;
+    while (i < num_steps) {
+        // maximal run of ≤ K steps of the same update
+        uint64_t j = i + 1;
+        bool consecutive = true;
+        while (j < num_steps && j - i < K && steps[j].pidx == steps[i].pidx) {
+            if (steps[j].mcmciter != steps[j - 1].mcmciter + 1) consecutive = false;
+            ++j;
+        }
+        const uint64_t n = j - i;
+        p.pidx0 = steps[i].pidx - 1;
+        p.iter0 = steps[i].mcmciter;
+        p.nsteps = (uint32_t)n;
+        p.N0 = h->stats_N;
+        p.iters = nullptr;
+        if (!consecutive) {
+            if (h->iters_cap < n) {
+                HIPCHK(h, hipStreamSynchronize(h->stream));
+                if (h->d_iters) (void)hipFree(h->d_iters);
+                HIPCHK(h, hipMalloc(&h->d_iters, n * sizeof(uint32_t)));
+                h->iters_cap = n;
+            }
+            std::vector<uint32_t> its(n);
+            for (uint64_t q = 0; q < n; ++q) its[q] = steps[i + q].mcmciter;
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            HIPCHK(h, hipMemcpy(h->d_iters, its.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+            p.iters = h->d_iters;
+        }
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->timing) {
+            e0 = get_event(h);
+            e1 = get_event(h);
+            HIPCHK(h, hipEventRecord(e0, h->stream));
+        }
+        void *args[] = {&p};
+        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.fn), grid, block, args, h->lds_bytes,
+                                  h->stream));
+        if (h->timing) {
+            HIPCHK(h, hipEventRecord(e1, h->stream));
+            h->ev.emplace_back(e0, e1);
+            h->pending_bytes += bytes_per_launch(h, n);
+        }
+        h->stats_N += n;
+        i = j;
+    }
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_synchronize(emcmc_handle *h) {
+    if (!h) return EMCMC_INVALID_ARG;
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (!h->allocated) return EMCMC_OK;
+    std::vector<uint32_t> f(h->cfg.num_chains);
+    HIPCHK(h, hipMemcpy(f.data(), h->d_faults, f.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (uint32_t x : f)
+        if (x) return fail(h, EMCMC_CHAIN_FAULT, "at least one chain raised a fault (emcmc_get_faults)");
+    return EMCMC_OK;
+}
+
+void emcmc_destroy(emcmc_handle *h) {
+    if (!h) return;
+    (void)hipSetDevice(h->cfg.device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    for (auto &p : h->ev) {
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+    void *bufs[] = {h->d_theta,     h->d_ll,        h->d_ra,      h->d_ring,     h->d_nacc,  h->d_faults,
+                    h->d_hist_theta, h->d_hist_prop, h->d_hist_ll, h->d_hist_acc, h->d_consts, h->d_obs,
+                    h->d_iters,     h->d_scratch};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    if (h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+}
+
+const char *emcmc_last_error(const emcmc_handle *h) { return h ? h->err.c_str() : "null handle"; }
+
+emcmc_status emcmc_get_state(emcmc_handle *h, double *theta, double *ll) {
+    if (!h) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    if (theta) HIPCHK(h, hipMemcpy(theta, h->d_theta, C * D * sizeof(double), hipMemcpyDeviceToHost));
+    if (ll) HIPCHK(h, hipMemcpy(ll, h->d_ll, C * sizeof(double), hipMemcpyDeviceToHost));
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_chain_stats(emcmc_handle *h, double *rolling_ar, uint64_t *accepted) {
+    if (!h) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t C = h->cfg.num_chains;
+    if (rolling_ar) HIPCHK(h, hipMemcpy(rolling_ar, h->d_ra, C * sizeof(double), hipMemcpyDeviceToHost));
+    if (accepted) {
+        std::vector<uint32_t> a(C);
+        HIPCHK(h, hipMemcpy(a.data(), h->d_nacc, C * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c) accepted[c] = a[c];
+    }
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults) {
+    if (!h || !faults) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(faults, h->d_faults, h->cfg.num_chains * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return EMCMC_OK;
+}
+
+static emcmc_status hist_geometry(emcmc_handle *h, uint32_t which, void **base, size_t *row) {
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, P = h->updates.size();
+    switch (which) {
+    case EMCMC_H_STATE: *base = h->d_hist_theta; *row = P * C * D * sizeof(double); break;
+    case EMCMC_H_PROPOSAL: *base = h->d_hist_prop; *row = P * C * D * sizeof(double); break;
+    case EMCMC_H_LL: *base = h->d_hist_ll; *row = P * C * sizeof(double); break;
+    case EMCMC_H_ACCEPT: *base = h->d_hist_acc; *row = P * h->row_bytes; break;
+    default: return fail(h, EMCMC_INVALID_ARG, "unknown history %u", which);
+    }
+    if (!*base) return fail(h, EMCMC_STATE_ERROR, "history %u not retained in this history_mode", which);
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_history(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
+                               void *host_out, size_t host_bytes) {
+    if (!h || !host_out) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (iter_first < 1 || iter_first + num_iters - 1 > h->cfg.num_mcmc_steps)
+        return fail(h, EMCMC_INVALID_ARG, "iteration window outside 1..M");
+    void *base = nullptr;
+    size_t row = 0;
+    emcmc_status st = hist_geometry(h, which, &base, &row);
+    if (st) return st;
+    if (host_bytes < row * num_iters) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(host_out, (const uint8_t *)base + (iter_first - 1) * row, row * num_iters,
+                        hipMemcpyDeviceToHost));
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_history_chains(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
+                                      uint64_t chain_first, uint64_t num_chains, void *host_out, size_t host_bytes) {
+    if (!h || !host_out) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (which == EMCMC_H_ACCEPT) return fail(h, EMCMC_INVALID_ARG, "accept bits: use emcmc_get_history");
+    if (iter_first < 1 || num_iters == 0 || iter_first + num_iters - 1 > h->cfg.num_mcmc_steps)
+        return fail(h, EMCMC_INVALID_ARG, "iteration window outside 1..M");
+    const uint64_t C = h->cfg.num_chains, P = h->updates.size();
+    if (num_chains == 0 || chain_first + num_chains > C) return fail(h, EMCMC_INVALID_ARG, "chain window");
+    void *base = nullptr;
+    size_t row = 0;
+    emcmc_status st = hist_geometry(h, which, &base, &row);
+    if (st) return st;
+    const size_t per_chain = (which == EMCMC_H_LL) ? sizeof(double) : h->cfg.dim * sizeof(double);
+    const size_t width = num_chains * per_chain, spitch = C * per_chain;
+    const size_t height = num_iters * P;
+    if (host_bytes < width * height) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint8_t *src = (const uint8_t *)base + (iter_first - 1) * row + chain_first * per_chain;
+    HIPCHK(h, hipMemcpy2D(host_out, width, src, spitch, width, height, hipMemcpyDeviceToHost));
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dptr, size_t *bytes) {
+    if (!h || !dptr || !bytes) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    size_t row = 0;
+    emcmc_status st = hist_geometry(h, which, dptr, &row);
+    if (st) return st;
+    *bytes = row * h->cfg.num_mcmc_steps;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t num_iters, int split,
+                                  double *out3d, emcmc_moments *info) {
+    if (!h || !out3d) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (!h->d_hist_theta) return fail(h, EMCMC_STATE_ERROR, "moments need EMCMC_HIST_FULL");
+    if (iter_first < 1 || num_iters < 2 || iter_first + num_iters - 1 > h->cfg.num_mcmc_steps)
+        return fail(h, EMCMC_INVALID_ARG, "iteration window");
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, P = h->updates.size();
+    const uint32_t halves = split ? 2u : 1u;
+    const size_t need = 2 * C * D * halves * sizeof(double) + 3 * D * sizeof(double) + 64;
+    if (h->scratch_bytes < need) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (h->d_scratch) (void)hipFree(h->d_scratch);
+        HIPCHK(h, hipMalloc(&h->d_scratch, need));
+        h->scratch_bytes = need;
+    }
+    double *mean = h->d_scratch, *var = mean + C * D * halves, *o = var + C * D * halves;
+    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(o + 3 * D);
+    const uint64_t total = C * D * halves;
+    const uint64_t slot0 = (iter_first - 1) * P + (P - 1);  // state after the last update of the iteration
+    hipLaunchKernelGGL(chain_moments_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, h->stream,
+                       h->d_hist_theta, C, (uint32_t)D, slot0, (uint32_t)P, (uint32_t)num_iters, halves, mean, var);
+    HIPCHK(h, hipGetLastError());
+    hipLaunchKernelGGL(moments_reduce_kernel, dim3((unsigned)D), dim3(256), 0, h->stream, mean, var, C,
+                       (uint32_t)D, halves, o);
+    HIPCHK(h, hipGetLastError());
+    HIPCHK(h, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), h->stream));
+    const uint64_t words = num_iters * P * h->row_bytes / 8;
+    hipLaunchKernelGGL(popcount_kernel, dim3(1024), dim3(256), 0, h->stream,
+                       reinterpret_cast<const uint64_t *>(h->d_hist_acc + (iter_first - 1) * P * h->row_bytes),
+                       words, cnt);
+    HIPCHK(h, hipGetLastError());
+    unsigned long long acc = 0;
+    HIPCHK(h, hipMemcpyAsync(out3d, o, 3 * D * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipMemcpyAsync(&acc, cnt, sizeof acc, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (info) {
+        info->num_chains = C * halves;
+        info->num_draws = num_iters / halves;
+        info->accepted = acc;
+        info->proposed = C * num_iters * P;
+    }
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_set_timing(emcmc_handle *h, int enable) {
+    if (!h) return EMCMC_INVALID_ARG;
+    h->timing = enable != 0;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_timing(emcmc_handle *h, double *total_ms, uint64_t *launches, double *algorithmic_bytes,
+                              int reset) {
+    if (!h) return EMCMC_INVALID_ARG;
+    emcmc_status st = drain_timing(h);
+    if (st) return st;
+    if (total_ms) *total_ms = h->timed_ms;
+    if (launches) *launches = h->timed_launches;
+    if (algorithmic_bytes) *algorithmic_bytes = h->timed_bytes;
+    if (reset) {
+        h->timed_ms = 0.0;
+        h->timed_launches = 0;
+        h->timed_bytes = 0.0;
+    }
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_kernel_name(emcmc_handle *h, char *buf, size_t buflen) {
+    if (!h || !buf || buflen == 0) return EMCMC_INVALID_ARG;
+    snprintf(buf, buflen, "%s", h->var.name.empty() ? "(none)" : h->var.name.c_str());
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_probe_variates(int device, uint64_t seed, uint32_t pidx0, uint32_t dim, uint64_t n,
+                                  const uint32_t *chains, const uint32_t *iters, double *z, double *E) {
+    if (!chains || !iters || !z || !E || dim == 0) return EMCMC_INVALID_ARG;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMCMC_NO_DEVICE;
+    if (device < 0 || device >= nd || hipSetDevice(device) != hipSuccess) return EMCMC_INVALID_ARG;
+    if (n == 0) return EMCMC_OK;
+    uint32_t *dc = nullptr, *di = nullptr;
+    double *dz = nullptr, *dE = nullptr;
+    emcmc_status st = EMCMC_OK;
+    if (hipMalloc(&dc, n * 4) || hipMalloc(&di, n * 4) || hipMalloc(&dz, n * dim * 8) || hipMalloc(&dE, n * 8)) {
+        st = EMCMC_OUT_OF_MEMORY;
+    } else if (hipMemcpy(dc, chains, n * 4, hipMemcpyHostToDevice) ||
+               hipMemcpy(di, iters, n * 4, hipMemcpyHostToDevice)) {
+        st = EMCMC_HIP_ERROR;
+    } else {
+        hipLaunchKernelGGL(probe_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+                           (uint32_t)seed, (uint32_t)(seed >> 32), pidx0, dim, n, dc, di, dz, dE);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(z, dz, n * dim * 8, hipMemcpyDeviceToHost) || hipMemcpy(E, dE, n * 8, hipMemcpyDeviceToHost))
+            st = EMCMC_HIP_ERROR;
+    }
+    (void)hipFree(dc);
+    (void)hipFree(di);
+    (void)hipFree(dz);
+    (void)hipFree(dE);
+    return st;
+}
+
+emcmc_status emcmc_probe_log(int device, const double *x, double *y, uint64_t n) {
+    if (!x || !y) return EMCMC_INVALID_ARG;
+    int nd = 0;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMCMC_NO_DEVICE;
+    if (device < 0 || device >= nd || hipSetDevice(device) != hipSuccess) return EMCMC_INVALID_ARG;
+    if (n == 0) return EMCMC_OK;
+    double *dx = nullptr, *dy = nullptr;
+    emcmc_status st = EMCMC_OK;
+    if (hipMalloc(&dx, n * 8) || hipMalloc(&dy, n * 8)) {
+        st = EMCMC_OUT_OF_MEMORY;
+    } else if (hipMemcpy(dx, x, n * 8, hipMemcpyHostToDevice)) {
+        st = EMCMC_HIP_ERROR;
+    } else {
+        hipLaunchKernelGGL(probe_log_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dx, dy, n);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
+            hipMemcpy(y, dy, n * 8, hipMemcpyDeviceToHost))
+            st = EMCMC_HIP_ERROR;
+    }
+    (void)hipFree(dx);
+    (void)hipFree(dy);
+    return st;
+}
+
+}  // extern "C"

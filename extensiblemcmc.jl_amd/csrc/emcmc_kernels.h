@@ -1,0 +1,544 @@
+// emcmc_kernels.h — fused many-chain Metropolis–Hastings step kernels (gfx950).
+//
+// One launch runs `nsteps` consecutive schedule steps of ONE update for all
+// chains; θ, ll and the rolling-acceptance state stay in VGPRs across those
+// steps and only the per-step history streams leave the CU.  Each chain is
+// owned by LPC ∈ {1,2,4} adjacent lanes of a wave (a "quad" for LPC=4), each
+// lane holding D/LPC coordinates; per-chain sums combine across those lanes
+// with DPP quad permutes.
+//
+// Per step and chain this fuses (reference src/ paths):
+//   update_workspaces!        run.jl:101-112    (register carry of θ and ll)
+//   proposal!/rand!           updates.jl:191-196, random_walk.jl:145-159
+//   set_proposal!             run.jl:221-240    (state_proposal_history write)
+//   compute_ll!/loglikelihood run.jl:251-260, gsn_target.jl:23-29
+//   accept_reject!            run.jl:268-281    (llr order, Exponential draw)
+//   log_transition_density    run.jl:344-367, random_walk.jl:161-171
+//   log_prior                 run.jl:374-385, priors.jl:18-19
+//   register_accept_reject_results!/set_chain_param!  run.jl:299-335
+//   update_stats! rolling acceptance  chain_statistics.jl:51-65
+//
+// Summation order (defines the bits, shared with oracle/): a length-D sum is
+// split into blocks of 8 consecutive coordinates when D % 8 == 0 and D ≥ 16
+// (else one block); each block sums left to right; blocks combine by a
+// pairwise tree over adjacent blocks (odd tail carried up).  See DESIGN.md.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "emcmc_math.h"
+
+namespace emcmc {
+
+struct StepParams {
+    // carried chain state (SoA over chains, row-major [C][D] for θ)
+    double *theta;     // [C][D]
+    double *ll;        // [C]
+    double *ra;        // [C] rolling acceptance (current value)
+    uint64_t *ring;    // [C][2] acceptance bits of the last 128 iterations
+    uint32_t *nacc;    // [C] accepted proposals
+    uint32_t *faults;  // [C]
+    // history streams (FULL mode), slot = (mcmciter-1)*P + pidx0
+    double *hist_theta;  // [M*P][C][D]
+    double *hist_prop;   // [M*P][C][D]
+    double *hist_ll;     // [M*P][C]
+    uint8_t *hist_acc;   // [M*P][Cw*8] bytes, bit c of row = chain c
+    // device constants (see DeviceConsts layout in emcmc.hip)
+    const double *consts;
+    const double *obs;    // [nobs][D]
+    const uint32_t *iters;  // [nsteps] mcmciter per step, or nullptr → iter0 + s
+    uint64_t C;
+    uint64_t row_bytes;   // bytes per accept-bit row (= Cw*8)
+    uint32_t chain0;      // global id of local chain 0
+    uint32_t key0, key1;  // seed
+    uint32_t iter0;
+    uint32_t nsteps;
+    uint32_t pidx0;       // 0-based update index
+    uint32_t P;           // number of updates
+    uint32_t W;           // roll window (≤ 128)
+    uint32_t nobs;
+    uint32_t _pad;
+    uint64_t N0;          // GenericChainStats.N before the first step of this launch
+    double rw_c0;         // −(D·log2π + logdet Σ_rw)/2
+    double t_c0;          // −(D·log2π + logdet Σ_t)/2
+    double n_tc0;         // nobs · t_c0     (SUFFSTAT)
+    double S_c;           // Σ_k ‖L_t⁻¹(x_k − x̄)‖²  (SUFFSTAT)
+    double nobs_d;        // (double) nobs
+};
+
+// constants layout (offsets in doubles), D = dimension
+//   diag kernels : [0,D) L_rw diag | [D,2D) 1/L_rw | [2D,3D) 1/L_t | [3D,4D) x̄
+//   dense kernels: [0,D²) L_rw (row-major lower) | [D²,D²+D) 1/diag(L_rw)
+//                  | [D²+D, 2D²+D) L_t | [2D²+D, 2D²+2D) 1/diag(L_t) | [2D²+2D, 2D²+3D) x̄
+constexpr int LL_PER_OBS = 0;
+constexpr int LL_SUFFSTAT = 1;
+
+// ---------------------------------------------------------------------------
+// cross-lane helpers (DPP quad permutes; 64-bit values move as two dwords)
+template <int CTRL>
+__device__ __forceinline__ double dpp_perm(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+// quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2)
+template <int LPC>
+__device__ __forceinline__ double lane_tree(double s) {
+    if constexpr (LPC >= 2) s = s + dpp_perm<0xB1>(s);
+    if constexpr (LPC >= 4) s = s + dpp_perm<0x4E>(s);
+    return s;
+}
+
+// canonical blocked-8 pairwise sum of the lane's NV values, then across lanes
+template <int D>
+struct SumShape {
+    static constexpr int BLK = (D % 8 == 0 && D >= 16) ? 8 : D;
+    static constexpr int NB = D / BLK;
+};
+
+template <int N>
+__device__ __forceinline__ double tree_inplace(double (&b)[N]) {
+    int n = N;
+#pragma unroll
+    for (int lvl = 0; lvl < 8; ++lvl) {
+        if (n <= 1) break;
+#pragma unroll
+        for (int i = 0; i < N / 2; ++i)
+            if (i < n / 2) b[i] = b[2 * i] + b[2 * i + 1];
+        if (n & 1) b[n / 2] = b[n - 1];
+        n = (n + 1) / 2;
+    }
+    return b[0];
+}
+
+template <int D, int LPC, int NV>
+__device__ __forceinline__ double canon_sum(const double (&v)[NV]) {
+    constexpr int BLK = SumShape<D>::BLK;
+    constexpr int BPL = NV / BLK;
+    double b[BPL];
+#pragma unroll
+    for (int k = 0; k < BPL; ++k) {
+        double s = v[k * BLK];
+#pragma unroll
+        for (int i = 1; i < BLK; ++i) s = s + v[k * BLK + i];
+        b[k] = s;
+    }
+    double s = tree_inplace<BPL>(b);
+    return lane_tree<LPC>(s);
+}
+
+// compact one accept bit per chain out of a 64-lane ballot (LPC lanes/chain)
+template <int LPC>
+__device__ __forceinline__ uint64_t compact_ballot(uint64_t m) {
+    if constexpr (LPC == 1) {
+        return m;
+    } else if constexpr (LPC == 2) {
+        m &= 0x5555555555555555ull;
+        m = (m | (m >> 1)) & 0x3333333333333333ull;
+        m = (m | (m >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+        m = (m | (m >> 4)) & 0x00FF00FF00FF00FFull;
+        m = (m | (m >> 8)) & 0x0000FFFF0000FFFFull;
+        m = (m | (m >> 16)) & 0x00000000FFFFFFFFull;
+        return m;
+    } else {
+        m &= 0x1111111111111111ull;
+        m = (m | (m >> 3)) & 0x0303030303030303ull;
+        m = (m | (m >> 6)) & 0x000F000F000F000Full;
+        m = (m | (m >> 12)) & 0x000000FF000000FFull;
+        m = (m | (m >> 24)) & 0x000000000000FFFFull;
+        return m;
+    }
+}
+
+template <int LPC>
+__device__ __forceinline__ void store_acc_bits(uint8_t *row, uint64_t chain_first, uint64_t bits) {
+    // chain_first is a multiple of 64/LPC: the wave's bits are one aligned word
+    uint8_t *p = row + (chain_first >> 3);
+    if constexpr (LPC == 1) *reinterpret_cast<uint64_t *>(p) = bits;
+    else if constexpr (LPC == 2) *reinterpret_cast<uint32_t *>(p) = (uint32_t)bits;
+    else *reinterpret_cast<uint16_t *>(p) = (uint16_t)bits;
+}
+
+// rolling acceptance, chain_statistics.jl:53-65 (N = cs.N before increment)
+__device__ __forceinline__ double rolling_update(double ra, uint64_t &r0, uint64_t &r1, uint32_t iter,
+                                                 uint32_t W, uint64_t N, bool acc) {
+    int out = 0;
+    if (iter > W) {
+        const uint32_t j = (iter - W) & 127u;
+        const uint64_t w = (j & 64u) ? r1 : r0;
+        out = (int)((w >> (j & 63u)) & 1ull);
+    }
+    const uint64_t mn = (N < (uint64_t)W) ? N : (uint64_t)W;
+    const double nra = (ra * (double)W + (double)((int)acc - out)) / (double)mn;
+    const uint32_t jw = iter & 127u;
+    const uint64_t bit = 1ull << (jw & 63u);
+    if (jw & 64u) r1 = acc ? (r1 | bit) : (r1 & ~bit);
+    else r0 = acc ? (r0 | bit) : (r0 & ~bit);
+    return nra;
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal Gaussian RW proposal + diagonal Gaussian target (cfg 2 fast path).
+// GaussianRandomWalk(Σ_rw) with Σ_rw diagonal, GsnTargetLaw(μ, Σ_t) with Σ_t
+// diagonal, coords = 1:D, ImproperPrior, P = 1 schedule slot per step.
+template <int D, int LPC, bool FULL, int LLMODE>
+__global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
+    static_assert(D % LPC == 0, "D must split evenly over the chain's lanes");
+    constexpr int DPL = D / LPC;  // coordinates per lane
+    static_assert(LPC == 1 || DPL % 8 == 0, "multi-lane chains need whole 8-blocks");
+    static_assert(LPC == 1 || DPL % 2 == 0, "normal pairs must not straddle lanes");
+    constexpr int PPL = (DPL + 1) / 2;
+
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const uint32_t nobs = a.nobs;
+    const int nconst = 4 * D;
+    const int nload = (LLMODE == LL_PER_OBS) ? nconst + (int)nobs * D : nconst;
+    for (int i = threadIdx.x; i < nload; i += blockDim.x)
+        lds[i] = (i < nconst) ? a.consts[i] : a.obs[i - nconst];
+    __syncthreads();
+    const double *Lrw = lds;
+    const double *iLrw = lds + D;
+    const double *iLt = lds + 2 * D;
+    const double *xbar = lds + 3 * D;
+    const double *X = lds + 4 * D;
+
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t chain = tid / LPC;
+    const int sub = (int)(tid % LPC);
+    if (chain >= a.C) return;
+    const int d0 = sub * DPL;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+
+    double th[DPL];
+    {
+        const double *src = a.theta + chain * D + d0;
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) th[i] = src[i];
+    }
+    double ll = a.ll[chain];
+    double ra = a.ra[chain];
+    uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
+    uint32_t nacc = a.nacc[chain];
+    uint32_t faults = a.faults[chain];
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iters ? a.iters[s] : a.iter0 + s;
+        const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
+        // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151)
+        double thp[DPL];
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+            const u32x4 r = draw(a.key0, a.key1, gid, iter, (uint32_t)(d0 / 2 + j), a.pidx0, 0);
+            double z0, z1;
+            box_muller(r, z0, z1);
+            thp[2 * j] = th[2 * j] + Lrw[d0 + 2 * j] * z0;
+            if (2 * j + 1 < DPL) thp[2 * j + 1] = th[2 * j + 1] + Lrw[d0 + 2 * j + 1] * z1;
+        }
+        // ---- log_transition_density both ways (random_walk.jl:161-171):
+        // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
+        double ltd;
+        {
+            double v[DPL];
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) {
+                const double y = (thp[i] - th[i]) * iLrw[d0 + i];
+                v[i] = y * y;
+            }
+            ltd = a.rw_c0 - canon_sum<D, LPC>(v) / 2.0;
+        }
+        // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            llp = 0.0;
+            for (uint32_t k = 0; k < nobs; ++k) {
+                const double *xk = X + (size_t)k * D + d0;
+                double v[DPL];
+#pragma unroll
+                for (int i = 0; i < DPL; ++i) {
+                    const double y = (xk[i] - thp[i]) * iLt[d0 + i];
+                    v[i] = y * y;
+                }
+                llp = llp + (a.t_c0 - canon_sum<D, LPC>(v) / 2.0);
+            }
+        } else {
+            double v[DPL];
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) {
+                const double y = (xbar[d0 + i] - thp[i]) * iLt[d0 + i];
+                v[i] = y * y;
+            }
+            const double qv = canon_sum<D, LPC>(v);
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
+        // ---- accept_reject! (run.jl:271-278), left-associative as written
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double E = exp1(draw(a.key0, a.key1, gid, iter, kBlockAccept, a.pidx0, 0));
+        const bool acc = E > -llr;
+        // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
+        if constexpr (FULL) {
+            double *dst = a.hist_prop + (slot * a.C + chain) * D + d0;
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) __builtin_nontemporal_store(thp[i], dst + i);
+        }
+        // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            double *dst = a.hist_theta + (slot * a.C + chain) * D + d0;
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) __builtin_nontemporal_store(th[i], dst + i);
+            if (sub == 0) __builtin_nontemporal_store(ll, a.hist_ll + slot * a.C + chain);
+        }
+        {
+            const uint64_t m = compact_ballot<LPC>(__ballot(acc));
+            if ((threadIdx.x & 63) == 0)
+                store_acc_bits<LPC>(a.hist_acc + slot * a.row_bytes, chain, m);
+        }
+        // ---- update_stats! rolling acceptance (chain_statistics.jl:53-65)
+        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, acc);
+    }
+
+    if (sub == 0) {
+        a.ll[chain] = ll;
+        a.ra[chain] = ra;
+        a.ring[2 * chain] = r0;
+        a.ring[2 * chain + 1] = r1;
+        a.nacc[chain] = nacc;
+        a.faults[chain] = faults;
+    }
+    {
+        double *dst = a.theta + chain * D + d0;
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) dst[i] = th[i];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Dense Gaussian RW proposal (lower Cholesky factor of Σ_rw) + dense Gaussian
+// target (lower Cholesky factor of Σ_t): the general GsnTargetLaw case
+// (cfg 1: GsnTargetLaw([1,2], [1 .5; .5 1])).  One lane per chain.
+template <int D, bool FULL, int LLMODE>
+__global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) {
+    constexpr int PP = (D + 1) / 2;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const uint32_t nobs = a.nobs;
+    const int nconst = 2 * D * D + 3 * D;
+    const int nload = (LLMODE == LL_PER_OBS) ? nconst + (int)nobs * D : nconst;
+    for (int i = threadIdx.x; i < nload; i += blockDim.x)
+        lds[i] = (i < nconst) ? a.consts[i] : a.obs[i - nconst];
+    __syncthreads();
+    const double *Lrw = lds;
+    const double *iLrw = lds + D * D;
+    const double *Lt = lds + D * D + D;
+    const double *iLt = lds + 2 * D * D + D;
+    const double *xbar = lds + 2 * D * D + 2 * D;
+    const double *X = lds + 2 * D * D + 3 * D;
+
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+
+    double th[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) th[i] = a.theta[chain * D + i];
+    double ll = a.ll[chain];
+    double ra = a.ra[chain];
+    uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
+    uint32_t nacc = a.nacc[chain];
+    uint32_t faults = a.faults[chain];
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iters ? a.iters[s] : a.iter0 + s;
+        const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
+        double z[2 * PP];
+#pragma unroll
+        for (int j = 0; j < PP; ++j) {
+            const u32x4 r = draw(a.key0, a.key1, gid, iter, (uint32_t)j, a.pidx0, 0);
+            box_muller(r, z[2 * j], z[2 * j + 1]);
+        }
+        double thp[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            double acc = Lrw[i * D] * z[0];
+#pragma unroll
+            for (int j = 1; j <= i; ++j) acc = fma(Lrw[i * D + j], z[j], acc);
+            thp[i] = th[i] + acc;
+        }
+        double ltd;
+        {
+            double y[D], v[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                double acc = thp[i] - th[i];
+#pragma unroll
+                for (int j = 0; j < i; ++j) acc = fma(-Lrw[i * D + j], y[j], acc);
+                y[i] = acc * iLrw[i];
+                v[i] = y[i] * y[i];
+            }
+            ltd = a.rw_c0 - canon_sum<D, 1>(v) / 2.0;
+        }
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            llp = 0.0;
+            for (uint32_t k = 0; k < nobs; ++k) {
+                const double *xk = X + (size_t)k * D;
+                double y[D], v[D];
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    double acc = xk[i] - thp[i];
+#pragma unroll
+                    for (int j = 0; j < i; ++j) acc = fma(-Lt[i * D + j], y[j], acc);
+                    y[i] = acc * iLt[i];
+                    v[i] = y[i] * y[i];
+                }
+                llp = llp + (a.t_c0 - canon_sum<D, 1>(v) / 2.0);
+            }
+        } else {
+            double y[D], v[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                double acc = xbar[i] - thp[i];
+#pragma unroll
+                for (int j = 0; j < i; ++j) acc = fma(-Lt[i * D + j], y[j], acc);
+                y[i] = acc * iLt[i];
+                v[i] = y[i] * y[i];
+            }
+            const double qv = canon_sum<D, 1>(v);
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double E = exp1(draw(a.key0, a.key1, gid, iter, kBlockAccept, a.pidx0, 0));
+        const bool acc = E > -llr;
+        if constexpr (FULL) {
+            double *dst = a.hist_prop + (slot * a.C + chain) * D;
+#pragma unroll
+            for (int i = 0; i < D; ++i) __builtin_nontemporal_store(thp[i], dst + i);
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            double *dst = a.hist_theta + (slot * a.C + chain) * D;
+#pragma unroll
+            for (int i = 0; i < D; ++i) __builtin_nontemporal_store(th[i], dst + i);
+            __builtin_nontemporal_store(ll, a.hist_ll + slot * a.C + chain);
+        }
+        {
+            const uint64_t m = __ballot(acc);
+            if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
+        }
+        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, acc);
+    }
+    a.ll[chain] = ll;
+    a.ra[chain] = ra;
+    a.ring[2 * chain] = r0;
+    a.ring[2 * chain + 1] = r1;
+    a.nacc[chain] = nacc;
+    a.faults[chain] = faults;
+#pragma unroll
+    for (int i = 0; i < D; ++i) a.theta[chain * D + i] = th[i];
+}
+
+// ---------------------------------------------------------------------------
+// Diagnostics: per-(half-)chain mean and unbiased variance of θ over a window
+// of history slots, then a deterministic tree reduction over chains.
+__global__ void __launch_bounds__(256)
+chain_moments_kernel(const double *__restrict__ hist, uint64_t C, uint32_t D, uint64_t slot0,
+                     uint32_t slot_stride, uint32_t n, uint32_t halves, double *__restrict__ mean_out,
+                     double *__restrict__ var_out) {
+    // one thread per (chain, dim, half)
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t total = C * D * halves;
+    if (t >= total) return;
+    const uint32_t h = (uint32_t)(t / (C * D));
+    const uint64_t cd = t % (C * D);
+    const uint32_t len = n / halves;
+    const uint64_t first = slot0 + (uint64_t)h * len * slot_stride;
+    double s = 0.0;
+    for (uint32_t i = 0; i < len; ++i) s = s + hist[(first + (uint64_t)i * slot_stride) * C * D + cd];
+    const double m = s / (double)len;
+    double q = 0.0;
+    for (uint32_t i = 0; i < len; ++i) {
+        const double e = hist[(first + (uint64_t)i * slot_stride) * C * D + cd] - m;
+        q = q + e * e;
+    }
+    mean_out[t] = m;
+    var_out[t] = (len > 1) ? q / (double)(len - 1) : 0.0;
+}
+
+// out[d] = Σ over (half-)chains of f(x), f ∈ {x, x², y}: one block per d,
+// fixed chunking → deterministic for a given (C, halves).
+__global__ void __launch_bounds__(256)
+moments_reduce_kernel(const double *__restrict__ mean_in, const double *__restrict__ var_in, uint64_t C,
+                      uint32_t D, uint32_t halves, double *__restrict__ out3d) {
+    const uint32_t d = blockIdx.x;
+    __shared__ double sm[3][256];
+    double a = 0.0, b = 0.0, c = 0.0;
+    const uint64_t rows = C * halves;
+    for (uint64_t r = threadIdx.x; r < rows; r += blockDim.x) {
+        const uint64_t h = r / C, ch = r % C;
+        const uint64_t idx = h * C * D + ch * D + d;
+        const double m = mean_in[idx];
+        a = a + m;
+        b = b + m * m;
+        c = c + var_in[idx];
+    }
+    sm[0][threadIdx.x] = a;
+    sm[1][threadIdx.x] = b;
+    sm[2][threadIdx.x] = c;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+            sm[0][threadIdx.x] = sm[0][threadIdx.x] + sm[0][threadIdx.x + w];
+            sm[1][threadIdx.x] = sm[1][threadIdx.x] + sm[1][threadIdx.x + w];
+            sm[2][threadIdx.x] = sm[2][threadIdx.x] + sm[2][threadIdx.x + w];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        out3d[d] = sm[0][0];
+        out3d[D + d] = sm[1][0];
+        out3d[2 * D + d] = sm[2][0];
+    }
+}
+
+// accepted proposals in a window of accept-bit rows (integer → deterministic)
+__global__ void __launch_bounds__(256)
+popcount_kernel(const uint64_t *__restrict__ bits, uint64_t words, unsigned long long *__restrict__ out) {
+    uint64_t acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        acc += (uint64_t)__popcll(bits[i]);
+    if (acc) atomicAdd(out, (unsigned long long)acc);
+}
+
+// self-test probes
+__global__ void __launch_bounds__(256)
+probe_variates_kernel(uint32_t key0, uint32_t key1, uint32_t pidx0, uint32_t D, uint64_t n,
+                      const uint32_t *__restrict__ chains, const uint32_t *__restrict__ iters, double *__restrict__ z,
+                      double *__restrict__ E) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    for (uint32_t j = 0; j < (D + 1) / 2; ++j) {
+        double a, b;
+        box_muller(draw(key0, key1, chains[t], iters[t], j, pidx0, 0), a, b);
+        z[t * D + 2 * j] = a;
+        if (2 * j + 1 < D) z[t * D + 2 * j + 1] = b;
+    }
+    E[t] = exp1(draw(key0, key1, chains[t], iters[t], kBlockAccept, pidx0, 0));
+}
+
+__global__ void __launch_bounds__(256) probe_log_kernel(const double *__restrict__ x, double *__restrict__ y,
+                                                        uint64_t n) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) y[t] = log_pos(x[t]);
+}
+
+}  // namespace emcmc

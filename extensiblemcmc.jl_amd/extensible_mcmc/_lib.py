@@ -1,0 +1,215 @@
+"""ctypes binding of the C ABI in include/emcmc.h (libemcmc.so).
+
+This is the Python-side twin of the Julia ``ccall`` shim in
+``extensiblemcmc.jl_amd/julia/ExtensibleMCMCHip.jl``.  The library is built
+in-tree by ``make -C extensiblemcmc.jl_amd`` (``__graft_entry__.build()``).
+There is no fallback: if the shared object is missing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+ABI_VERSION = 1
+
+OK = 0
+INVALID_ARG = 1
+HIP_ERROR = 2
+RCCL_ERROR = 3
+UNSUPPORTED_PLUGIN = 4
+CHAIN_FAULT = 5
+OUT_OF_MEMORY = 6
+NO_DEVICE = 7
+STATE_ERROR = 8
+
+STATUS_NAMES = {
+    0: "EMCMC_OK",
+    1: "EMCMC_INVALID_ARG",
+    2: "EMCMC_HIP_ERROR",
+    3: "EMCMC_RCCL_ERROR",
+    4: "EMCMC_UNSUPPORTED_PLUGIN",
+    5: "EMCMC_CHAIN_FAULT",
+    6: "EMCMC_OUT_OF_MEMORY",
+    7: "EMCMC_NO_DEVICE",
+    8: "EMCMC_STATE_ERROR",
+}
+
+RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX = 1, 2, 3
+PRIOR_IMPROPER, PRIOR_IMPROPER_POS = 0, 1
+ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO = 0, 1, 2
+TARGET_GSN = 1
+LL_PER_OBS, LL_SUFFSTAT = 0, 1
+HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
+H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
+FAULT_NONFINITE_LL = 1
+
+
+class EmcmcConfig(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_uint32),
+        ("dim", C.c_uint32),
+        ("num_chains", C.c_uint64),
+        ("first_chain_id", C.c_uint64),
+        ("num_mcmc_steps", C.c_uint64),
+        ("seed", C.c_uint64),
+        ("device", C.c_int32),
+        ("history_mode", C.c_uint32),
+        ("roll_window", C.c_uint32),
+        ("lanes_per_chain", C.c_uint32),
+        ("steps_per_launch", C.c_uint32),
+        ("reserved", C.c_uint32 * 7),
+    ]
+
+
+class EmcmcUpdateDesc(C.Structure):
+    _fields_ = [
+        ("kernel", C.c_uint32),
+        ("prior", C.c_uint32),
+        ("adaptation", C.c_uint32),
+        ("num_coords", C.c_uint32),
+        ("coords", C.POINTER(C.c_uint32)),
+        ("sigma", C.POINTER(C.c_double)),
+        ("epsilon", C.POINTER(C.c_double)),
+        ("pos", C.POINTER(C.c_uint8)),
+        ("reserved_ptr", C.c_void_p * 4),
+        ("reserved_f64", C.c_double * 4),
+    ]
+
+
+class EmcmcTargetDesc(C.Structure):
+    _fields_ = [
+        ("kind", C.c_uint32),
+        ("dim", C.c_uint32),
+        ("mu", C.POINTER(C.c_double)),
+        ("sigma", C.POINTER(C.c_double)),
+        ("num_obs", C.c_uint64),
+        ("obs", C.POINTER(C.c_double)),
+        ("ll_mode", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class EmcmcStep(C.Structure):
+    _fields_ = [("mcmciter", C.c_uint32), ("pidx", C.c_uint32)]
+
+
+class EmcmcMoments(C.Structure):
+    _fields_ = [
+        ("num_chains", C.c_uint64),
+        ("num_draws", C.c_uint64),
+        ("accepted", C.c_uint64),
+        ("proposed", C.c_uint64),
+    ]
+
+
+# every symbol declared in include/emcmc.h, with its ctypes signature
+_H = C.c_void_p
+_ST = C.c_int
+SIGNATURES = {
+    "emcmc_device_count": (_ST, [C.POINTER(C.c_int)]),
+    "emcmc_create": (_ST, [C.POINTER(_H), C.POINTER(EmcmcConfig)]),
+    "emcmc_add_update": (_ST, [_H, C.POINTER(EmcmcUpdateDesc)]),
+    "emcmc_set_target": (_ST, [_H, C.POINTER(EmcmcTargetDesc)]),
+    "emcmc_set_state": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "emcmc_run": (_ST, [_H, C.POINTER(EmcmcStep), C.c_uint64]),
+    "emcmc_synchronize": (_ST, [_H]),
+    "emcmc_destroy": (None, [_H]),
+    "emcmc_last_error": (C.c_char_p, [_H]),
+    "emcmc_get_state": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "emcmc_get_chain_stats": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "emcmc_get_faults": (_ST, [_H, C.POINTER(C.c_uint32)]),
+    "emcmc_get_history": (_ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]),
+    "emcmc_get_history_chains": (
+        _ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
+    ),
+    "emcmc_history_device_ptr": (_ST, [_H, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "emcmc_moments_window": (
+        _ST,
+        [_H, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double), C.POINTER(EmcmcMoments)],
+    ),
+    "emcmc_set_timing": (_ST, [_H, C.c_int]),
+    "emcmc_get_timing": (
+        _ST,
+        [_H, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.c_int],
+    ),
+    "emcmc_kernel_name": (_ST, [_H, C.c_char_p, C.c_size_t]),
+    "emcmc_probe_variates": (
+        _ST,
+        [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+         C.POINTER(C.c_double), C.POINTER(C.c_double)],
+    ),
+    "emcmc_probe_log": (_ST, [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64]),
+}
+
+PKG_ROOT = Path(__file__).resolve().parent.parent  # extensiblemcmc.jl_amd/
+LIB_PATH = Path(os.environ.get("EMCMC_LIB", PKG_ROOT / "lib" / "libemcmc.so"))
+
+
+class EMCMCError(RuntimeError):
+    """A non-OK emcmc_status, with the library's last error message."""
+
+    def __init__(self, status: int, where: str, message: str = ""):
+        self.status = status
+        super().__init__(f"{where}: {STATUS_NAMES.get(status, status)}" + (f" — {message}" if message else ""))
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libemcmc.so (raises if it was not built: there is no CPU fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise ImportError(
+                f"libemcmc.so not found at {LIB_PATH}; build it with `make -C {PKG_ROOT}` "
+                "or `python -c 'import __graft_entry__ as g; g.build()'`"
+            )
+        L = C.CDLL(str(LIB_PATH))
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def dptr(a: np.ndarray):
+    assert a.dtype == np.float64 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def u32ptr(a: np.ndarray):
+    assert a.dtype == np.uint32 and a.flags.c_contiguous
+    return a.ctypes.data_as(C.POINTER(C.c_uint32))
+
+
+def probe_variates(seed: int, chains, iters, dim: int, pidx0: int = 0, device: int = 0):
+    ch = np.ascontiguousarray(chains, dtype=np.uint32)
+    it = np.ascontiguousarray(iters, dtype=np.uint32)
+    n = ch.size
+    z = np.empty((n, dim))
+    E = np.empty(n)
+    st = lib().emcmc_probe_variates(device, seed & 0xFFFFFFFFFFFFFFFF, pidx0, dim, n, u32ptr(ch), u32ptr(it),
+                                    dptr(z), dptr(E))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_probe_variates")
+    return z, E
+
+
+def probe_log(x, device: int = 0):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    st = lib().emcmc_probe_log(device, dptr(x), dptr(y), x.size)
+    if st != OK:
+        raise EMCMCError(st, "emcmc_probe_log")
+    return y
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    lib().emcmc_device_count(C.byref(n))
+    return int(n.value)

@@ -1,0 +1,231 @@
+"""Thin object wrapper over one ``emcmc_handle`` (one shard of chains on one GPU).
+
+Every method is a direct call through the C ABI (include/emcmc.h); nothing here
+computes on the host beyond packing arguments.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+@dataclass
+class EngineConfig:
+    dim: int
+    num_chains: int
+    num_mcmc_steps: int
+    seed: int = 0
+    first_chain_id: int = 0
+    device: int = 0
+    history_mode: int = L.HIST_FULL
+    roll_window: int = 100
+    lanes_per_chain: int = 0
+    steps_per_launch: int = 0
+
+
+class Engine:
+    def __init__(self, cfg: EngineConfig):
+        self.cfg = cfg
+        self._lib = L.lib()
+        c = L.EmcmcConfig()
+        c.abi_version = L.ABI_VERSION
+        c.dim = cfg.dim
+        c.num_chains = cfg.num_chains
+        c.first_chain_id = cfg.first_chain_id
+        c.num_mcmc_steps = cfg.num_mcmc_steps
+        c.seed = cfg.seed & 0xFFFFFFFFFFFFFFFF
+        c.device = cfg.device
+        c.history_mode = cfg.history_mode
+        c.roll_window = cfg.roll_window
+        c.lanes_per_chain = cfg.lanes_per_chain
+        c.steps_per_launch = cfg.steps_per_launch
+        h = C.c_void_p()
+        st = self._lib.emcmc_create(C.byref(h), C.byref(c))
+        if st != L.OK:
+            raise L.EMCMCError(st, "emcmc_create", "" if st != L.NO_DEVICE else "no HIP device visible")
+        self._h = h
+        self.num_updates = 0
+
+    # -- plumbing -------------------------------------------------------------
+    def _check(self, st: int, where: str):
+        if st != L.OK:
+            msg = self._lib.emcmc_last_error(self._h)
+            raise L.EMCMCError(st, where, msg.decode() if msg else "")
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.emcmc_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- setup ------------------------------------------------------------------
+    def add_gaussian_rw_update(self, coords0, sigma, prior=L.PRIOR_IMPROPER, adaptation=L.ADPT_NONE, pos=None):
+        coords = np.ascontiguousarray(coords0, dtype=np.uint32)
+        S = np.asfortranarray(np.asarray(sigma, dtype=np.float64).reshape(len(coords), len(coords)))
+        Sf = np.ascontiguousarray(S.ravel(order="F"))
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.RW_GAUSSIAN
+        u.prior = prior
+        u.adaptation = adaptation
+        u.num_coords = len(coords)
+        u.coords = L.u32ptr(coords)
+        u.sigma = L.dptr(Sf)
+        if pos is not None:
+            p = np.ascontiguousarray(pos, dtype=np.uint8)
+            u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
+        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
+        self.num_updates += 1
+
+    def add_update_desc(self, u: L.EmcmcUpdateDesc, keepalive=()):
+        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
+        self.num_updates += 1
+
+    def set_gsn_target(self, mu, sigma, obs, ll_mode=L.LL_PER_OBS):
+        mu = np.ascontiguousarray(mu, dtype=np.float64)
+        d = mu.shape[0]
+        Sf = np.ascontiguousarray(np.asarray(sigma, dtype=np.float64).reshape(d, d).ravel(order="F"))
+        X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, d))
+        t = L.EmcmcTargetDesc()
+        t.kind = L.TARGET_GSN
+        t.dim = d
+        t.mu = L.dptr(mu)
+        t.sigma = L.dptr(Sf)
+        t.num_obs = X.shape[0]
+        t.obs = L.dptr(X)
+        t.ll_mode = ll_mode
+        self._check(self._lib.emcmc_set_target(self._h, C.byref(t)), "emcmc_set_target")
+
+    def set_state(self, theta, ll=None):
+        th = np.ascontiguousarray(theta, dtype=np.float64).reshape(self.cfg.num_chains, self.cfg.dim)
+        llp = None
+        if ll is not None:
+            la = np.ascontiguousarray(ll, dtype=np.float64).reshape(self.cfg.num_chains)
+            llp = L.dptr(la)
+        self._check(self._lib.emcmc_set_state(self._h, L.dptr(th), llp), "emcmc_set_state")
+
+    # -- run ----------------------------------------------------------------------
+    def run(self, steps):
+        """steps: iterable of (mcmciter, pidx) pairs, 1-based (schedule.jl order)."""
+        arr = np.ascontiguousarray(np.asarray(steps, dtype=np.uint32).reshape(-1, 2))
+        n = arr.shape[0]
+        if n == 0:
+            return
+        ptr = arr.ctypes.data_as(C.POINTER(L.EmcmcStep))
+        self._check(self._lib.emcmc_run(self._h, ptr, n), "emcmc_run")
+
+    def run_iters(self, iter_first: int, n: int, pidx: int = 1):
+        it = np.arange(iter_first, iter_first + n, dtype=np.uint32)
+        steps = np.stack([it, np.full(n, pidx, dtype=np.uint32)], axis=1)
+        self.run(steps)
+
+    def synchronize(self, allow_faults=False):
+        st = self._lib.emcmc_synchronize(self._h)
+        if st == L.CHAIN_FAULT and allow_faults:
+            return False
+        self._check(st, "emcmc_synchronize")
+        return True
+
+    # -- read back ------------------------------------------------------------------
+    def get_state(self):
+        th = np.empty((self.cfg.num_chains, self.cfg.dim), dtype=np.float64)
+        ll = np.empty(self.cfg.num_chains, dtype=np.float64)
+        self._check(self._lib.emcmc_get_state(self._h, L.dptr(th), L.dptr(ll)), "emcmc_get_state")
+        return th, ll
+
+    def get_chain_stats(self):
+        ra = np.empty(self.cfg.num_chains, dtype=np.float64)
+        acc = np.empty(self.cfg.num_chains, dtype=np.uint64)
+        self._check(
+            self._lib.emcmc_get_chain_stats(self._h, L.dptr(ra), acc.ctypes.data_as(C.POINTER(C.c_uint64))),
+            "emcmc_get_chain_stats",
+        )
+        return ra, acc
+
+    def get_faults(self):
+        f = np.empty(self.cfg.num_chains, dtype=np.uint32)
+        self._check(self._lib.emcmc_get_faults(self._h, L.u32ptr(f)), "emcmc_get_faults")
+        return f
+
+    def get_history(self, which: int, iter_first: int, num_iters: int):
+        """Returns the raw window; shapes: STATE/PROPOSAL [n][P][C][D], LL [n][P][C],
+        ACCEPT [n][P][C] bool (unpacked from the bit rows)."""
+        P, Cn, D = self.num_updates, self.cfg.num_chains, self.cfg.dim
+        if which in (L.H_STATE, L.H_PROPOSAL):
+            out = np.empty((num_iters, P, Cn, D), dtype=np.float64)
+        elif which == L.H_LL:
+            out = np.empty((num_iters, P, Cn), dtype=np.float64)
+        elif which == L.H_ACCEPT:
+            words = (Cn + 63) // 64
+            out = np.empty((num_iters, P, words), dtype=np.uint64)
+        else:
+            raise ValueError(which)
+        self._check(
+            self._lib.emcmc_get_history(self._h, which, iter_first, num_iters, out.ctypes.data, out.nbytes),
+            "emcmc_get_history",
+        )
+        if which == L.H_ACCEPT:
+            bits = np.unpackbits(out.view(np.uint8), axis=-1, bitorder="little")
+            return bits[..., :Cn].astype(bool)
+        return out
+
+    def get_history_chains(self, which: int, iter_first: int, num_iters: int, chain_first: int, num_chains: int):
+        """History window for a chain range: STATE/PROPOSAL [n][P][c][D], LL [n][P][c]."""
+        P, D = self.num_updates, self.cfg.dim
+        if which in (L.H_STATE, L.H_PROPOSAL):
+            out = np.empty((num_iters, P, num_chains, D), dtype=np.float64)
+        elif which == L.H_LL:
+            out = np.empty((num_iters, P, num_chains), dtype=np.float64)
+        else:
+            raise ValueError("accept bits: use get_history")
+        self._check(
+            self._lib.emcmc_get_history_chains(self._h, which, iter_first, num_iters, chain_first, num_chains,
+                                               out.ctypes.data, out.nbytes),
+            "emcmc_get_history_chains",
+        )
+        return out
+
+    def moments_window(self, iter_first: int, num_iters: int, split: bool = True):
+        out = np.empty(3 * self.cfg.dim, dtype=np.float64)
+        info = L.EmcmcMoments()
+        self._check(
+            self._lib.emcmc_moments_window(self._h, iter_first, num_iters, int(split), L.dptr(out), C.byref(info)),
+            "emcmc_moments_window",
+        )
+        D = self.cfg.dim
+        return {
+            "sum_mean": out[:D].copy(),
+            "sum_mean_sq": out[D : 2 * D].copy(),
+            "sum_var": out[2 * D :].copy(),
+            "num_chains": int(info.num_chains),
+            "num_draws": int(info.num_draws),
+            "accepted": int(info.accepted),
+            "proposed": int(info.proposed),
+        }
+
+    # -- timing ------------------------------------------------------------------------
+    def set_timing(self, enable: bool):
+        self._check(self._lib.emcmc_set_timing(self._h, int(enable)), "emcmc_set_timing")
+
+    def get_timing(self, reset: bool = False):
+        ms = C.c_double()
+        n = C.c_uint64()
+        b = C.c_double()
+        self._check(
+            self._lib.emcmc_get_timing(self._h, C.byref(ms), C.byref(n), C.byref(b), int(reset)),
+            "emcmc_get_timing",
+        )
+        return float(ms.value), int(n.value), float(b.value)
+
+    def kernel_name(self) -> str:
+        buf = C.create_string_buffer(256)
+        self._check(self._lib.emcmc_kernel_name(self._h, buf, 256), "emcmc_kernel_name")
+        return buf.value.decode()

@@ -1,0 +1,350 @@
+"""Transition kernels, priors, adaptation schemes and updates — the reference's
+plugin surface (src/transition_kernels/*.jl, src/priors.jl, src/updates.jl),
+as host-side descriptors.
+
+These classes carry the constructor semantics of the reference (argument
+defaults, assertions, scalar/vector promotion).  The per-step arithmetic
+(``rand!``, ``logpdf``, ``log_prior``, ``register!``/``readjust!``) runs on the
+device; ``to_device`` packs a descriptor for ``emcmc_add_update`` and raises
+``UnsupportedPlugin`` for combinations without a device kernel yet.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Callable, Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+class UnsupportedPlugin(NotImplementedError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# abstract hierarchy (src/types.jl:8-125)
+class MCMCUpdate:
+    pass
+
+
+class MCMCParamUpdate(MCMCUpdate):
+    pass
+
+
+class MCMCGradientBasedUpdate(MCMCParamUpdate):
+    pass
+
+
+class MCMCConjugateUpdate(MCMCUpdate):
+    pass
+
+
+class MCMCConjugateParamUpdate(MCMCParamUpdate):
+    pass
+
+
+class MCMCImputation(MCMCUpdate):
+    pass
+
+
+class MCMCUpdateDecorator:
+    pass
+
+
+def isdecorator(u) -> bool:
+    """types.jl:65"""
+    return isinstance(u, MCMCUpdateDecorator)
+
+
+class TransitionKernel:
+    pass
+
+
+class RandomWalk(TransitionKernel):
+    pass
+
+
+class Adaptation:
+    pass
+
+
+class MCMCBackend:
+    pass
+
+
+class Prior:
+    def logpdf(self, theta):
+        raise NotImplementedError(f"logpdf not implemented for prior {type(self).__name__}.")
+
+
+# flags (types.jl:122-125)
+class Previous:
+    pass
+
+
+class Proposal:
+    pass
+
+
+class PreMCMCStep:
+    pass
+
+
+class PostMCMCStep:
+    pass
+
+
+# ---------------------------------------------------------------------------
+# priors (src/priors.jl)
+class ImproperPrior(Prior):
+    """Flat prior, logpdf = 0.0 (priors.jl:18-19)."""
+
+    def logpdf(self, theta):
+        return 0.0
+
+
+class ImproperPosPrior(Prior):
+    """Flat prior on positive coordinates, logpdf = −Σ log θ (priors.jl:25-26)."""
+
+    def logpdf(self, theta):
+        theta = np.asarray(theta, dtype=float)
+        if np.any(theta < 0):
+            raise ValueError("DomainError: log of a negative number (priors.jl:26)")
+        return -float(np.sum(np.log(theta)))
+
+
+class StandardPrior(Prior):
+    """StandardPrior(dist) with a scipy-like ``logpdf`` (priors.jl:35-39)."""
+
+    def __init__(self, dist):
+        self.dist = dist
+
+    def logpdf(self, theta):
+        return float(np.sum(self.dist.logpdf(theta)))
+
+
+class ProductPrior(Prior):
+    """ProductPrior(dists, dims) (priors.jl:60-88)."""
+
+    def __init__(self, dists, dims):
+        idx, last = [], 0
+        for d in dims:
+            idx.append(slice(last, last + d))
+            last += d
+        self.dists, self.idx = tuple(dists), tuple(idx)
+
+    def logpdf(self, theta):
+        theta = np.asarray(theta, dtype=float)
+        lp = 0.0
+        for dist, ix in zip(self.dists, self.idx):
+            lp += float(np.sum(dist.logpdf(theta[ix])))
+        return lp
+
+
+# ---------------------------------------------------------------------------
+# random walkers (src/transition_kernels/random_walk.jl)
+def _pos_default(n, pos):
+    return np.zeros(n, dtype=bool) if pos is None else np.asarray(pos, dtype=bool).reshape(n)
+
+
+class UniformRandomWalk(RandomWalk):
+    """``UniformRandomWalk(ϵ, pos=false)`` (random_walk.jl:45-56)."""
+
+    def __init__(self, eps, pos=None):
+        eps_a = np.atleast_1d(np.asarray(eps, dtype=float))
+        assert np.all(eps_a > 0.0), "@assert all(ϵ .> 0.0)"
+        self.eps = eps_a
+        self.pos = _pos_default(eps_a.size, pos)
+
+    def __len__(self):
+        return self.eps.size
+
+
+class GaussianRandomWalk(RandomWalk):
+    """``GaussianRandomWalk(Σ, pos=nothing)`` (random_walk.jl:123-136)."""
+
+    def __init__(self, Sigma, pos=None):
+        S = np.asarray(Sigma, dtype=float)
+        if S.ndim == 0:
+            S = S.reshape(1, 1)
+        if S.ndim == 1:  # a length-1 vector, as in GaussianRandomWalk([1.0])
+            S = np.diag(S) if S.size > 1 else S.reshape(1, 1)
+        assert S.shape[0] == S.shape[1], "@assert size(Σ, 1) == size(Σ, 2)"
+        self.Sigma = S
+        self.pos = _pos_default(S.shape[0], pos)
+
+    def __len__(self):
+        return self.Sigma.shape[0]
+
+
+class GaussianRandomWalkMix(RandomWalk):
+    """``GaussianRandomWalkMix(Σ_A, Σ_B, λ=0.5, pos=nothing)`` (random_walk.jl:193-210)."""
+
+    def __init__(self, Sigma_A, Sigma_B, lam=0.5, pos=None):
+        assert 0.0 <= lam <= 1.0, "@assert 0.0 <= λ <= 1.0"
+        A, B = np.asarray(Sigma_A, dtype=float), np.asarray(Sigma_B, dtype=float)
+        assert A.shape == B.shape, "@assert size(Σ_A) == size(Σ_B)"
+        self.gsn_A = GaussianRandomWalk(A, pos)
+        self.gsn_B = GaussianRandomWalk(B, pos)
+        self.lam = float(lam)
+
+    def __len__(self):
+        return len(self.gsn_A)
+
+
+# ---------------------------------------------------------------------------
+# adaptation (src/transition_kernels/adaptation.jl)
+class NoAdaptation(Adaptation):
+    """adaptation.jl:26"""
+
+    def __eq__(self, o):
+        return isinstance(o, NoAdaptation)
+
+
+_UNIF_DEFAULTS = (("scale", 1.0), ("min", 1e-12), ("max", 1e7), ("offset", 1e2))
+
+
+def _assure_scalar(v):
+    """utility_functions.jl:16-21"""
+    if np.isscalar(v):
+        return v
+    v = list(np.atleast_1d(v))
+    assert len(v) == 1
+    return v[0]
+
+
+class AdaptationUnifRW(Adaptation):
+    """``AdaptationUnifRW(θ; adapt_every_k_steps=100, target_accpt_rate=0.234,
+    scale=1.0, min=1e-12, max=1e7, offset=1e2)`` (adaptation.jl:51-105).
+
+    Field semantics match the reference: scalar fields when every vector-like
+    kwarg has length 1 (``T = Float64``), per-coordinate vectors otherwise; ``N``
+    = length(θ).  ``kind`` records the reference's element type T
+    ("scalar" | "vector" | "svector") so that ``==`` follows adaptation.jl:206-213.
+    """
+
+    FIELDS = ("proposed", "accepted", "target_accpt_rate", "adapt_every_k_steps", "scale", "min", "max",
+              "offset", "N")
+
+    def __init__(self, theta=None, *, _raw=None, static=False, **kwargs):
+        if _raw is not None:  # AdaptationUnifRW{T}(trgt, steps, scale, min, max, offset, N)
+            (self.target_accpt_rate, self.adapt_every_k_steps, self.scale, self.min, self.max, self.offset,
+             self.N, self.kind) = _raw
+            self.proposed = 0
+            self.accepted = 0
+            return
+        theta = np.atleast_1d(np.asarray(theta, dtype=float))
+        n = theta.size
+        trgt = float(_assure_scalar(kwargs.pop("target_accpt_rate", 0.234)))
+        steps = int(_assure_scalar(kwargs.pop("adapt_every_k_steps", 100)))
+        lengths = {np.atleast_1d(v).size for v in kwargs.values()}
+        assert len(lengths) <= 2
+        scalar = len(lengths) == 0 or max(lengths) == 1
+        vals = []
+        for name, default in _UNIF_DEFAULTS:
+            v = kwargs.get(name, default)
+            if scalar:
+                vals.append(float(np.atleast_1d(v)[0]))
+            else:
+                a = np.atleast_1d(np.asarray(v, dtype=float))
+                if a.size == 1:
+                    a = np.repeat(a, n)
+                assert a.size == n
+                vals.append(a)
+        kind = "scalar" if scalar else ("svector" if static else "vector")
+        self.__init__(_raw=(trgt, steps, *vals, n, kind))
+
+    @classmethod
+    def raw(cls, target_accpt_rate, adapt_every_k_steps, scale, min, max, offset, N, kind="scalar"):
+        return cls(_raw=(target_accpt_rate, adapt_every_k_steps, scale, min, max, offset, N, kind))
+
+    def _fields_equal(self, o, skip=()):
+        if not isinstance(o, AdaptationUnifRW) or self.kind != o.kind:
+            return False
+        for f in self.FIELDS:
+            if f in skip:
+                continue
+            a, b = getattr(self, f), getattr(o, f)
+            if not np.array_equal(np.atleast_1d(a), np.atleast_1d(b)) or np.shape(a) != np.shape(b):
+                return False
+        return True
+
+    def __eq__(self, o):
+        return self._fields_equal(o)
+
+    def isequal_except(self, o, *args):
+        """adaptation.jl:223-235"""
+        return self._fields_equal(o, skip=args)
+
+    # host restatement of the scalar recipes (used by tests and by the device
+    # readjust kernel's parity checks)
+    def acceptance_rate(self):
+        return 0.0 if self.proposed == 0 else self.accepted / self.proposed
+
+    def compute_delta(self, mcmc_iter):
+        """compute_δ (adaptation.jl:312-319)"""
+        return np.asarray(self.scale) / np.sqrt(np.maximum(1.0, mcmc_iter / self.adapt_every_k_steps
+                                                          - np.asarray(self.offset)))
+
+
+def isequal_except(a, b, *args):
+    return a.isequal_except(b, *args)
+
+
+class HaarioTypeAdaptation(Adaptation):
+    """``HaarioTypeAdaptation(state; adapt_every_k_steps=100, scale=2.38^2, f=(x,y,z)->x)``
+    (adaptation.jl:372-397)."""
+
+    def __init__(self, state, adapt_every_k_steps=100, scale=2.38 ** 2, f: Optional[Callable] = None):
+        s = np.atleast_1d(np.asarray(state, dtype=float))
+        self.mean = np.zeros_like(s)
+        self.cov = np.zeros((s.size, s.size))
+        self.adapt_every_k_steps = int(adapt_every_k_steps)
+        self.scale = float(scale)
+        self.N = 1
+        self.M = 0
+        self.f = f if f is not None else (lambda x, y, z: x)
+
+
+# ---------------------------------------------------------------------------
+# updates (src/updates.jl)
+@dataclass
+class RandomWalkUpdate(MCMCParamUpdate):
+    """``RandomWalkUpdate(rw, idx_of_global; prior=ImproperPrior(), adpt=NoAdaptation())``
+    (updates.jl:163-183).  ``coords`` are 1-based global indices, as in the reference."""
+
+    rw: RandomWalk
+    coords: Sequence[int]
+    prior: Prior = field(default_factory=ImproperPrior)
+    adpt: Adaptation = field(default_factory=NoAdaptation)
+
+    def __post_init__(self):
+        self.coords = [int(c) for c in np.atleast_1d(self.coords)]
+        self.invcoords = {c: i + 1 for i, c in enumerate(self.coords)}
+
+    def to_device(self, engine):
+        """Register this update with the engine (emcmc_add_update)."""
+        coords0 = np.asarray(self.coords, dtype=np.int64) - 1
+        if isinstance(self.prior, ImproperPrior):
+            prior = L.PRIOR_IMPROPER
+        else:
+            raise UnsupportedPlugin(f"prior {type(self.prior).__name__} has no device plugin yet")
+        if isinstance(self.adpt, NoAdaptation):
+            adpt = L.ADPT_NONE
+        else:
+            raise UnsupportedPlugin(f"adaptation {type(self.adpt).__name__} has no device plugin yet")
+        if isinstance(self.rw, GaussianRandomWalk):
+            if np.any(self.rw.pos):
+                raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin yet")
+            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior, adaptation=adpt)
+        else:
+            raise UnsupportedPlugin(f"transition kernel {type(self.rw).__name__} has no device plugin yet")
+
+
+class MALAUpdate(MCMCGradientBasedUpdate):
+    """Stub in the reference (updates.jl:216-218)."""
+
+
+class HamiltonianMCUpdate(MCMCGradientBasedUpdate):
+    """Stub in the reference (updates.jl:220-222)."""

@@ -1,0 +1,44 @@
+"""Target laws (reference src/example/gsn_target.jl).
+
+``GsnTargetLaw(μ, Σ)`` keeps the reference's parameter vector θ = [μ; vec(Σ)]
+(gsn_target.jl:1-13).  Device plugin: ``set_parameters!(P, coords, θ)`` +
+``loglikelihood(P, obs)`` run inside the fused step kernel with coords ⊆ μ.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+class GsnTargetLaw:
+    def __init__(self, mu, Sigma=None):
+        mu = np.atleast_1d(np.asarray(mu, dtype=float))
+        d = mu.size
+        S = np.eye(d) if Sigma is None else np.asarray(Sigma, dtype=float).reshape(d, d)
+        self.d = d
+        self.theta = np.zeros(d * (d + 1))
+        self.theta[:d] = mu
+        self.theta[d:] = S.ravel(order="F")  # vec(Σ), column-major
+
+    @property
+    def mu(self):
+        return self.theta[: self.d]
+
+    @property
+    def Sigma(self):
+        # set_parameters! rebuilds Symmetric(triu(Σ)) (gsn_target.jl:17-20): upper triangle wins
+        S = self.theta[self.d :].reshape(self.d, self.d, order="F")
+        U = np.triu(S)
+        return U + np.triu(U, 1).T
+
+    def set_parameters(self, loc2glob_idx, theta):
+        """set_parameters!(P, idx, θ) (gsn_target.jl:15-21), 1-based indices."""
+        idx = np.asarray(loc2glob_idx, dtype=int) - 1
+        self.theta[idx] = theta
+
+    def to_device(self, engine, ll_mode, obs):
+        engine.set_gsn_target(self.mu, self.Sigma, obs, ll_mode=ll_mode)
+
+
+def make_data(P, obs):
+    """The ``data = (P = …, obs = …)`` NamedTuple of the reference (basic_use.md:112)."""
+    return {"P": P, "obs": np.asarray(obs, dtype=float)}

@@ -1,0 +1,250 @@
+/*
+ * emcmc.h — C ABI of the MI355X many-chain MCMC engine (libemcmc.so).
+ *
+ * This is the drop-in boundary for the hot path of ExtensibleMCMC.jl
+ * (reference: JuliaDiffusionBayes/ExtensibleMCMC.jl, mounted read-only at
+ * /root/reference).  The reference has no FFI of its own: its extension point
+ * is the `MCMCBackend` dispatch (src/types.jl:110-117) together with the
+ * workspace/update plugin surface (src/workspaces.jl:38,280; src/updates.jl:42-93).
+ * A Julia `MI355XBackend <: MCMCBackend` (extensiblemcmc.jl_amd/julia/) binds
+ * these entry points with `ccall`; Python binds them with `ctypes`
+ * (extensiblemcmc.jl_amd/extensible_mcmc/_lib.py).  See INTEGRATION.md.
+ *
+ * Each entry point names the reference function(s) it replaces.
+ *
+ * Conventions
+ *  - Plain C: POD structs, plain pointers + sizes, `emcmc_status` return codes.
+ *    Nothing throws across the ABI.  `emcmc_last_error(h)` gives a message.
+ *  - Indices crossing the ABI are 0-based (coords) except `mcmciter`/`pidx` in
+ *    `emcmc_step`, which are 1-based exactly as `MCMCSchedule` yields them
+ *    (src/schedule.jl:56-66).
+ *  - Matrices Σ are column-major (Julia layout); only the upper triangle is
+ *    read, like `Symmetric(Σ)` (uplo = :U) in src/transition_kernels/random_walk.jl:358
+ *    and src/example/gsn_target.jl:173.
+ *  - Chain state crossing the ABI is row-major [C][D] (chain-major).
+ *  - Ownership: the library owns all device memory; the caller owns host
+ *    buffers and keeps them alive for the duration of the call.
+ *  - Threading: one handle = one host thread + one HIP stream on one device.
+ *    Handles are independent; there is no global mutable state (the RNG is
+ *    counter-based, keyed by (seed, global chain id)).
+ *  - `emcmc_run` is asynchronous (enqueue only); every `emcmc_get_*` call and
+ *    `emcmc_synchronize` wait for it.
+ */
+#ifndef EMCMC_H
+#define EMCMC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EMCMC_ABI_VERSION 1u
+
+typedef enum emcmc_status {
+    EMCMC_OK = 0,
+    EMCMC_INVALID_ARG = 1,        /* reference: @assert / error("…") in constructors */
+    EMCMC_HIP_ERROR = 2,
+    EMCMC_RCCL_ERROR = 3,         /* reserved: collectives run in the host layer */
+    EMCMC_UNSUPPORTED_PLUGIN = 4, /* update/target kind with no device plugin */
+    EMCMC_CHAIN_FAULT = 5,        /* ≥1 chain raised a fault bit (see emcmc_get_faults) */
+    EMCMC_OUT_OF_MEMORY = 6,
+    EMCMC_NO_DEVICE = 7,
+    EMCMC_STATE_ERROR = 8         /* call out of order (e.g. run before set_target) */
+} emcmc_status;
+
+/* Transition kernels — src/transition_kernels/random_walk.jl */
+#define EMCMC_RW_UNIFORM 1u       /* UniformRandomWalk        random_walk.jl:45-94  */
+#define EMCMC_RW_GAUSSIAN 2u      /* GaussianRandomWalk       random_walk.jl:123-171 */
+#define EMCMC_RW_GAUSSIAN_MIX 3u  /* GaussianRandomWalkMix    random_walk.jl:193-232 (reserved) */
+
+/* Priors — src/priors.jl */
+#define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior    priors.jl:18-19 */
+#define EMCMC_PRIOR_IMPROPER_POS 1u /* ImproperPosPrior priors.jl:25-26 (reserved) */
+
+/* Adaptation — src/transition_kernels/adaptation.jl */
+#define EMCMC_ADPT_NONE 0u      /* NoAdaptation          adaptation.jl:26 */
+#define EMCMC_ADPT_UNIF_RW 1u   /* AdaptationUnifRW      adaptation.jl:51-329 (reserved) */
+#define EMCMC_ADPT_HAARIO 2u    /* HaarioTypeAdaptation  adaptation.jl:372-426 (reserved) */
+
+/* Targets — src/example/gsn_target.jl */
+#define EMCMC_TARGET_GSN 1u     /* GsnTargetLaw(μ, Σ) with coords ⊆ μ */
+
+/* How the Gaussian log-likelihood Σ_k logpdf(N(μ,Σ), x_k) is evaluated. */
+#define EMCMC_LL_PER_OBS 0u   /* literal gsn_target.jl:23-29: one sqmahal per observation */
+#define EMCMC_LL_SUFFSTAT 1u  /* same quantity via Σ_k‖L⁻¹(x_k−x̄)‖² + n‖L⁻¹(x̄−μ)‖² */
+
+/* History retention — src/workspaces.jl:157-192, 413-476 */
+#define EMCMC_HIST_FULL 0u         /* state, proposal, ll and accept histories */
+#define EMCMC_HIST_ACCEPT_ONLY 1u  /* accept bits only (no per-step state streams) */
+
+/* History selectors for emcmc_get_history / emcmc_history_device_ptr */
+#define EMCMC_H_STATE 0u     /* state_history[iter][pidx]          : double [M][P][C][D] */
+#define EMCMC_H_PROPOSAL 1u  /* state_proposal_history[iter][pidx] : double [M][P][C][D] */
+#define EMCMC_H_LL 2u        /* local_wss[pidx].sub_ws.ll_history  : double [M][P][C]    */
+#define EMCMC_H_ACCEPT 3u    /* local_wss[pidx].acceptance_history : bits   [M][P][ceil(C/64)] u64 */
+
+/* Per-chain fault bits (emcmc_get_faults) */
+#define EMCMC_FAULT_NONFINITE_LL 1u  /* proposal log-likelihood NaN/±Inf */
+
+typedef struct emcmc_handle emcmc_handle;
+
+/* Engine configuration.  Mirrors what `init!(mcmc, …)` (src/mcmc.jl:83-109)
+ * and `init_global_workspace` (src/workspaces.jl:215-234) receive. */
+typedef struct emcmc_config {
+    uint32_t abi_version;      /* must be EMCMC_ABI_VERSION */
+    uint32_t dim;              /* D = length(θinit) */
+    uint64_t num_chains;       /* C: chains held by this handle (one shard) */
+    uint64_t first_chain_id;   /* global id of local chain 0 (sharding; RNG key) */
+    uint64_t num_mcmc_steps;   /* M: history length, run.jl:34 `num_mcmc_steps` */
+    uint64_t seed;             /* master seed of the counter-based stream */
+    int32_t device;            /* HIP device ordinal */
+    uint32_t history_mode;     /* EMCMC_HIST_* */
+    uint32_t roll_window;      /* GenericChainStats roll_window (chain_statistics.jl:27); 0 → 100; ≤ 128 */
+    uint32_t lanes_per_chain;  /* 0 = auto; else 1, 2 or 4 (must divide the work layout) */
+    uint32_t steps_per_launch; /* 0 = auto (64) */
+    uint32_t reserved[7];
+} emcmc_config;
+
+/* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183). */
+typedef struct emcmc_update_desc {
+    uint32_t kernel;          /* EMCMC_RW_* */
+    uint32_t prior;           /* EMCMC_PRIOR_* */
+    uint32_t adaptation;      /* EMCMC_ADPT_* */
+    uint32_t num_coords;      /* length(coords) */
+    const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based) */
+    const double *sigma;      /* GaussianRandomWalk Σ: num_coords² column-major */
+    const double *epsilon;    /* UniformRandomWalk ϵ: num_coords (reserved) */
+    const uint8_t *pos;       /* positivity flags or NULL (all false) */
+    const void *reserved_ptr[4];
+    double reserved_f64[4];
+} emcmc_update_desc;
+
+/* `data = (P = GsnTargetLaw(μ, Σ), obs = [x_1, …, x_n])` (src/example/gsn_target.jl:1-29,
+ * docs/src/get_started/basic_use.md:112). */
+typedef struct emcmc_target_desc {
+    uint32_t kind;        /* EMCMC_TARGET_GSN */
+    uint32_t dim;         /* d = length(μ) */
+    const double *mu;     /* μ at construction: P.θ[1:d] */
+    const double *sigma;  /* Σ: d×d column-major (upper triangle read) */
+    uint64_t num_obs;     /* n */
+    const double *obs;    /* n×d row-major: obs[k*d + i] = x_k[i] */
+    uint32_t ll_mode;     /* EMCMC_LL_* */
+    uint32_t reserved;
+} emcmc_target_desc;
+
+/* One element of the `MCMCSchedule` iteration (src/schedule.jl:56-66). */
+typedef struct emcmc_step {
+    uint32_t mcmciter;  /* 1-based */
+    uint32_t pidx;      /* 1-based update index */
+} emcmc_step;
+
+/* Cross-chain moments of θ over an iteration window, for split-R̂
+ * (new functionality; BASELINE cfg 5).  Each field is a sum over the chains
+ * of this handle, so shards combine by summation (allreduce). */
+typedef struct emcmc_moments {
+    uint64_t num_chains;   /* chains summed (×2 halves when split) */
+    uint64_t num_draws;    /* draws per (half-)chain */
+    uint64_t accepted;     /* accepted proposals in the window, all chains */
+    uint64_t proposed;
+} emcmc_moments;
+
+/* ---- lifecycle --------------------------------------------------------- */
+
+/* Number of HIP devices visible (0 with no GPU).  Never fails on a CPU host. */
+emcmc_status emcmc_device_count(int *count);
+
+/* Replaces init_global_workspace(::GenericMCMCBackend, …) (workspaces.jl:215-234)
+ * and create_workspaces (workspaces.jl:362-371): allocates SoA device state and
+ * history buffers for C chains. */
+emcmc_status emcmc_create(emcmc_handle **h, const emcmc_config *cfg);
+
+/* Appends one update (→ pidx = number of updates added so far).  Replaces the
+ * per-update plugin methods proposal!/log_transition_density/log_prior/
+ * set_parameters! (updates.jl:185-214, run.jl:344-385) with device code. */
+emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u);
+
+/* Replaces set_parameters!(P::GsnTargetLaw, …) + loglikelihood(P, obs)
+ * (gsn_target.jl:15-29): uploads observations and the factorised Σ. */
+emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t);
+
+/* θinit for every chain (row-major [C][D]); ll = NULL means the reference's
+ * initial ll = -Inf (workspaces.jl:425), i.e. the first step always accepts.
+ * Also resets the rolling-acceptance statistics (chain_statistics.jl:23-36). */
+emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll);
+
+/* Replaces the body of __run! (run.jl:64-83) for the given schedule steps:
+ * update_workspaces! → update! (proposal!, set_proposal!, compute_ll!,
+ * accept_reject!, update_stats!) → update_adaptation!, fused over all chains.
+ * Asynchronous. */
+emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps);
+
+/* Wait for all queued work; returns EMCMC_CHAIN_FAULT if any chain faulted. */
+emcmc_status emcmc_synchronize(emcmc_handle *h);
+
+void emcmc_destroy(emcmc_handle *h);
+const char *emcmc_last_error(const emcmc_handle *h);
+
+/* ---- state and histories ------------------------------------------------ */
+
+/* Current θ ([C][D]) and ll ([C]) — state(global_ws), ll(local_ws). Either may be NULL. */
+emcmc_status emcmc_get_state(emcmc_handle *h, double *theta, double *ll);
+
+/* Current rolling acceptance (chain_statistics.jl:61-64) and accepted counts, per chain.
+ * Either may be NULL. */
+emcmc_status emcmc_get_chain_stats(emcmc_handle *h, double *rolling_ar, uint64_t *accepted);
+
+/* Per-chain fault bits (EMCMC_FAULT_*), [C] uint32. */
+emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults);
+
+/* Copies iterations [iter_first, iter_first+num_iters) (1-based) of one history
+ * to host.  Layout per EMCMC_H_* above, restricted to the window. */
+emcmc_status emcmc_get_history(emcmc_handle *h, uint32_t which, uint64_t iter_first,
+                               uint64_t num_iters, void *host_out, size_t host_bytes);
+
+/* Same, restricted to chains [chain_first, chain_first+num_chains) (STATE,
+ * PROPOSAL, LL only): out is [num_iters][P][num_chains][D] / [..][num_chains]. */
+emcmc_status emcmc_get_history_chains(emcmc_handle *h, uint32_t which, uint64_t iter_first,
+                                      uint64_t num_iters, uint64_t chain_first, uint64_t num_chains,
+                                      void *host_out, size_t host_bytes);
+
+/* Device pointer + byte size of a whole history buffer (zero-copy interop). */
+emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dptr,
+                                      size_t *bytes);
+
+/* ---- diagnostics (new; BASELINE cfg 5) --------------------------------- */
+
+/* Per-dimension sums over the chains of this handle of the (split) chain means,
+ * squared means and unbiased variances of θ over iterations
+ * [iter_first, iter_first+num_iters).  out3d = [Σ mean | Σ mean² | Σ var], 3·D doubles.
+ * split != 0 treats each chain as two halves (split-R̂). */
+emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t num_iters,
+                                  int split, double *out3d, emcmc_moments *info);
+
+/* ---- timing (bench / roofline) ----------------------------------------- */
+
+/* Enable per-launch HIP-event timing on the handle's stream. */
+emcmc_status emcmc_set_timing(emcmc_handle *h, int enable);
+/* Sum of per-launch kernel durations (ms) and number of step-kernel launches
+ * since the last reset; also returns algorithmic bytes moved by those launches. */
+emcmc_status emcmc_get_timing(emcmc_handle *h, double *total_ms, uint64_t *launches,
+                              double *algorithmic_bytes, int reset);
+
+/* Human-readable name of the kernel variant `emcmc_run` dispatches to. */
+emcmc_status emcmc_kernel_name(emcmc_handle *h, char *buf, size_t buflen);
+
+/* ---- self-test probes (run the device's own math on given inputs) ------- */
+
+/* For each of n (chain, iter) pairs: the dim normals and the Exp(1) accept draw
+ * the step kernels use at (seed, chain, iter, pidx0).  z: [n][dim], E: [n]. */
+emcmc_status emcmc_probe_variates(int device, uint64_t seed, uint32_t pidx0, uint32_t dim, uint64_t n,
+                                  const uint32_t *chains, const uint32_t *iters, double *z, double *E);
+/* y[i] = device log_pos(x[i]) (the hot path's log, x finite normal > 0). */
+emcmc_status emcmc_probe_log(int device, const double *x, double *y, uint64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* EMCMC_H */

@@ -1,0 +1,364 @@
+/*
+ * emcmc_oracle.c — CPU oracle for the many-chain MH hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load liboracle.so.  The product
+ * (extensiblemcmc.jl_amd/) never links or calls it.
+ *
+ * PARITY STATUS: the reference (Julia, /root/reference) cannot run in this
+ * image (no julia; Distributions.jl unvendored and unpinned, Project.toml:9,
+ * 14-15), and its own tests pin no number on the MH arithmetic (SURVEY §4,
+ * §8c).  The MH arithmetic restated below is therefore "parity unpinned"
+ * against the reference itself; it is pinned by (1) the Random123 Philox
+ * known-answer vectors, (2) the reference's schedule and AdaptationUnifRW KATs
+ * (test/runtests.jl:5-85, restated in the host layer and checked in tests/),
+ * (3) an independent numpy restatement of the literal reference formulas
+ * (oracle/literal.py: per-observation MvNormal logpdf via LAPACK Cholesky)
+ * within fp64 tolerance, and (4) the analytic posterior N(x̄, Σ/n).
+ *
+ * What is restated (reference files under /root/reference/src):
+ *   __run! loop, one update, P = 1 ............................ run.jl:64-83
+ *   update_workspaces!: θ copy, ll carry (−Inf at step 1) ....... run.jl:101-112
+ *   proposal!/rand!(GaussianRandomWalk): θ° = θ + L z ........... updates.jl:191-196,
+ *                                                                 random_walk.jl:145-159
+ *   set_proposal!: proposal history = θ with coords ← θ° ........ run.jl:221-240
+ *   compute_ll!: ll° = Σ_k logpdf(MvNormal(θ°, Σ_t), x_k) ....... run.jl:251-260,
+ *                                                                 gsn_target.jl:15-29
+ *   accept_reject!: llr left-assoc, E ~ Exp(1), accept E > −llr . run.jl:268-281
+ *   log_transition_density (both directions) ................... run.jl:344-367,
+ *                                                                 random_walk.jl:161-171
+ *   log_prior (ImproperPrior → 0.0) ............................ run.jl:374-385,
+ *                                                                 priors.jl:18-19
+ *   register_accept_reject_results!, set_chain_param! .......... run.jl:299-335
+ *   update_stats! rolling acceptance (window W, N from 1) ....... chain_statistics.jl:41-65
+ * MvNormal arithmetic (Distributions.jl, third-party, version unpinned by the
+ * reference — Project.toml has no [compat] entry for it):
+ *   logpdf = mvnormal_c0 − sqmahal/2, mvnormal_c0 = −(D·log2π + logdet Σ)/2,
+ *   sqmahal = ‖L⁻¹(x − μ)‖², rand = μ + L z, L = cholesky(Symmetric(Σ)).L,
+ *   logdet(::Cholesky) = dd + dd with dd = Σ log L_ii (LinearAlgebra).
+ * Evaluation order of every sum is the engine's canonical order (DESIGN.md
+ * §Numerics): blocked-8 pairwise for length-D sums, sequential over
+ * observations.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "oracle_math.h"
+
+#define ORC_EXPORT __attribute__((visibility("default")))
+
+/* ---- canonical helpers --------------------------------------------------- */
+
+/* Cholesky of the upper-stored (column-major) symmetric Σ: row-major lower L.
+ * Column-by-column, sums left to right, no fused multiply-add. */
+ORC_EXPORT int orc_cholesky(const double *S, int D, double *L) {
+    memset(L, 0, sizeof(double) * (size_t)D * D);
+    for (int col = 0; col < D; ++col) {
+        double diag = S[col + (size_t)col * D];
+        for (int k = 0; k < col; ++k) {
+            double l = L[(size_t)col * D + k];
+            diag = diag - l * l;
+        }
+        if (!(diag > 0.0)) return -1; /* PosDefException in the reference */
+        double ljj = sqrt(diag);
+        L[(size_t)col * D + col] = ljj;
+        for (int row = col + 1; row < D; ++row) {
+            double t = S[col + (size_t)row * D];
+            for (int k = 0; k < col; ++k) t = t - L[(size_t)row * D + k] * L[(size_t)col * D + k];
+            L[(size_t)row * D + col] = t / ljj;
+        }
+    }
+    return 0;
+}
+
+/* Length-D sum in the canonical order. */
+ORC_EXPORT double orc_canon_sum(const double *v, int D) {
+    int blk = (D % 8 == 0 && D >= 16) ? 8 : D;
+    int nb = D / blk;
+    double part[64];
+    for (int b = 0; b < nb; ++b) {
+        double s = v[b * blk];
+        for (int i = 1; i < blk; ++i) s = s + v[b * blk + i];
+        part[b] = s;
+    }
+    int n = nb;
+    while (n > 1) {
+        for (int i = 0; i < n / 2; ++i) part[i] = part[2 * i] + part[2 * i + 1];
+        if (n & 1) part[n / 2] = part[n - 1];
+        n = (n + 1) / 2;
+    }
+    return part[0];
+}
+
+/* ‖L⁻¹ r‖² by forward substitution (PDMats sqmahal via chol.L \ r). */
+static double sqmahal(const double *L, const double *invdiag, const double *r, int D, int diag) {
+    double y[64], sq[64];
+    for (int i = 0; i < D; ++i) {
+        double acc = r[i];
+        if (!diag)
+            for (int j = 0; j < i; ++j) acc = fma(-L[(size_t)i * D + j], y[j], acc);
+        y[i] = acc * invdiag[i];
+        sq[i] = y[i] * y[i];
+    }
+    return orc_canon_sum(sq, D);
+}
+
+static double logdet_chol(const double *L, int D) {
+    double dd = 0.0;
+    for (int i = 0; i < D; ++i) dd = dd + orc_log(L[(size_t)i * D + i]);
+    return dd + dd;
+}
+
+static double mvnormal_c0(int D, double logdet) { return -((double)D * ORC_LOG2PI + logdet) / 2.0; }
+
+static int is_diag_upper(const double *S, int D) {
+    for (int i = 0; i < D; ++i)
+        for (int j = i + 1; j < D; ++j)
+            if (S[i + (size_t)j * D] != 0.0) return 0;
+    return 1;
+}
+
+/* ---- problem constants ----------------------------------------------------- */
+
+typedef struct {
+    int D, diag, ll_mode;
+    uint64_t nobs;
+    const double *obs;
+    double Lrw[64 * 64], iLrw[64], Lt[64 * 64], iLt[64], xbar[64];
+    double rw_c0, t_c0, S_c;
+} orc_gsn;
+
+/* constants: out[0]=rw_c0, out[1]=t_c0, out[2]=S_c, out[3..3+D)=x̄ */
+static int gsn_prepare(orc_gsn *g, int D, const double *rw_sigma, const double *t_sigma, uint64_t nobs,
+                       const double *obs, int ll_mode) {
+    if (D < 1 || D > 64) return -2;
+    g->D = D;
+    g->nobs = nobs;
+    g->obs = obs;
+    g->ll_mode = ll_mode & 0xFF;
+    if (orc_cholesky(rw_sigma, D, g->Lrw)) return -1;
+    if (orc_cholesky(t_sigma, D, g->Lt)) return -1;
+    /* ll_mode bit 8 forces the dense (general Cholesky) formulas even for a
+     * diagonal Σ — used by tests to show both formulas give the same bits. */
+    g->diag = !(ll_mode & 0x100) && is_diag_upper(rw_sigma, D) && is_diag_upper(t_sigma, D);
+    for (int i = 0; i < D; ++i) {
+        g->iLrw[i] = 1.0 / g->Lrw[(size_t)i * D + i];
+        g->iLt[i] = 1.0 / g->Lt[(size_t)i * D + i];
+    }
+    g->rw_c0 = mvnormal_c0(D, logdet_chol(g->Lrw, D));
+    g->t_c0 = mvnormal_c0(D, logdet_chol(g->Lt, D));
+    for (int i = 0; i < D; ++i) {
+        double s = 0.0;
+        for (uint64_t k = 0; k < nobs; ++k) s = s + obs[k * D + i];
+        g->xbar[i] = s / (double)nobs;
+    }
+    double Sc = 0.0;
+    int dense_t = !is_diag_upper(t_sigma, D);
+    for (uint64_t k = 0; k < nobs; ++k) {
+        double r[64];
+        for (int i = 0; i < D; ++i) r[i] = obs[k * D + i] - g->xbar[i];
+        Sc = Sc + sqmahal(g->Lt, g->iLt, r, D, !dense_t);
+    }
+    g->S_c = Sc;
+    return 0;
+}
+
+ORC_EXPORT int orc_gsn_constants(int D, const double *rw_sigma, const double *t_sigma, uint64_t nobs,
+                                 const double *obs, double *out, double *Lrw_out, double *Lt_out) {
+    orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
+    int rc = gsn_prepare(g, D, rw_sigma, t_sigma, nobs, obs, 0);
+    if (rc == 0) {
+        out[0] = g->rw_c0;
+        out[1] = g->t_c0;
+        out[2] = g->S_c;
+        for (int i = 0; i < D; ++i) out[3 + i] = g->xbar[i];
+        if (Lrw_out) memcpy(Lrw_out, g->Lrw, sizeof(double) * (size_t)D * D);
+        if (Lt_out) memcpy(Lt_out, g->Lt, sizeof(double) * (size_t)D * D);
+    }
+    free(g);
+    return rc;
+}
+
+/* ---- one chain, `nsteps` steps of the single joint update ----------------- */
+
+typedef struct {
+    double *theta;  /* [D] in/out */
+    double *ll;     /* in/out */
+    double *ra;     /* in/out */
+    uint64_t *ring; /* [2] in/out */
+    uint32_t *nacc; /* in/out */
+    uint32_t *faults;
+} orc_chain;
+
+static void run_chain(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t key1, uint32_t chain_id,
+                      const uint32_t *iters, uint32_t iter0, uint32_t nsteps, uint64_t N0, uint32_t W,
+                      uint64_t C, uint64_t c, double *hist_theta, double *hist_prop, double *hist_ll,
+                      uint8_t *hist_acc) {
+    const int D = g->D;
+    double th[64], thp[64], z[66];
+    memcpy(th, st.theta, sizeof(double) * D);
+    double ll = *st.ll, ra = *st.ra;
+    uint64_t ring0 = st.ring[0], ring1 = st.ring[1];
+    uint32_t nacc = *st.nacc, faults = *st.faults;
+    const int npairs = (D + 1) / 2;
+
+    for (uint32_t s = 0; s < nsteps; ++s) {
+        const uint32_t iter = iters ? iters[s] : iter0 + s;
+        /* proposal!  θ° = θ + L z  (random_walk.jl:147: rand(MvNormal(θ, Σ))) */
+        for (int j = 0; j < npairs; ++j)
+            orc_box_muller(orc_draw(key0, key1, chain_id, iter, (uint32_t)j, 0, 0), &z[2 * j], &z[2 * j + 1]);
+        for (int i = 0; i < D; ++i) {
+            double lz;
+            if (g->diag) {
+                lz = g->Lrw[(size_t)i * D + i] * z[i];
+            } else {
+                lz = g->Lrw[(size_t)i * D] * z[0];
+                for (int j = 1; j <= i; ++j) lz = fma(g->Lrw[(size_t)i * D + j], z[j], lz);
+            }
+            thp[i] = th[i] + lz;
+        }
+        /* log_transition_density(θ→θ°) and (θ°→θ): MvNormal logpdf of ±(θ°−θ);
+         * the two sqmahal values are bitwise equal (random_walk.jl:161-171). */
+        double r[64];
+        for (int i = 0; i < D; ++i) r[i] = thp[i] - th[i];
+        const double ltd_fwd = g->rw_c0 - sqmahal(g->Lrw, g->iLrw, r, D, g->diag) / 2.0;
+        for (int i = 0; i < D; ++i) r[i] = th[i] - thp[i];
+        const double ltd_rev = g->rw_c0 - sqmahal(g->Lrw, g->iLrw, r, D, g->diag) / 2.0;
+        /* compute_ll!  (gsn_target.jl:23-29: ll = 0.0; for obs: ll += logpdf) */
+        double llp;
+        if (g->ll_mode == 0) {
+            llp = 0.0;
+            for (uint64_t k = 0; k < g->nobs; ++k) {
+                for (int i = 0; i < D; ++i) r[i] = g->obs[k * D + i] - thp[i];
+                llp = llp + (g->t_c0 - sqmahal(g->Lt, g->iLt, r, D, g->diag) / 2.0);
+            }
+        } else {
+            for (int i = 0; i < D; ++i) r[i] = g->xbar[i] - thp[i];
+            const double qv = sqmahal(g->Lt, g->iLt, r, D, g->diag);
+            llp = (double)g->nobs * g->t_c0 - (g->S_c + (double)g->nobs * qv) * 0.5;
+        }
+        if (!isfinite(llp)) faults |= 1u;
+        /* accept_reject!  (run.jl:271-278) — ImproperPrior: log_prior = 0.0 */
+        const double lp_prop = 0.0, lp_prev = 0.0;
+        const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + lp_prop) - lp_prev;
+        const double E = orc_exp1(orc_draw(key0, key1, chain_id, iter, ORC_BLOCK_ACCEPT, 0, 0));
+        const int acc = E > -llr;
+        const uint64_t slot = (uint64_t)(s);
+        if (hist_prop) memcpy(hist_prop + (slot * C + c) * D, thp, sizeof(double) * D);
+        if (acc) {
+            memcpy(th, thp, sizeof(double) * D);
+            ll = llp;
+            nacc += 1;
+        }
+        if (hist_theta) memcpy(hist_theta + (slot * C + c) * D, th, sizeof(double) * D);
+        if (hist_ll) hist_ll[slot * C + c] = ll;
+        if (hist_acc) hist_acc[slot * C + c] = (uint8_t)acc;
+        /* update_stats! rolling acceptance (chain_statistics.jl:53-65) */
+        const uint64_t N = N0 + s;
+        int outside = 0;
+        if (iter > W) {
+            uint32_t j = (iter - W) & 127u;
+            outside = (int)((((j & 64u) ? ring1 : ring0) >> (j & 63u)) & 1u);
+        }
+        const uint64_t mn = N < (uint64_t)W ? N : (uint64_t)W;
+        ra = (ra * (double)W + (double)(acc - outside)) / (double)mn;
+        {
+            uint32_t j = iter & 127u;
+            uint64_t bit = 1ull << (j & 63u);
+            if (j & 64u) ring1 = acc ? (ring1 | bit) : (ring1 & ~bit);
+            else ring0 = acc ? (ring0 | bit) : (ring0 & ~bit);
+        }
+    }
+    memcpy(st.theta, th, sizeof(double) * D);
+    *st.ll = ll;
+    *st.ra = ra;
+    st.ring[0] = ring0;
+    st.ring[1] = ring1;
+    *st.nacc = nacc;
+    *st.faults = faults;
+}
+
+/*
+ * Run `nsteps` iterations (P = 1) for chains [0, C) of a shard whose first
+ * global chain id is chain0.  State arrays are in/out.  History outputs are
+ * optional (NULL) and indexed by step s in [0, nsteps): hist_theta/hist_prop
+ * [nsteps][C][D], hist_ll [nsteps][C], hist_acc [nsteps][C] (0/1 bytes).
+ * Returns 0, or <0 on invalid input.
+ */
+ORC_EXPORT int orc_run_gsn(int D, uint64_t C, uint32_t chain0, uint64_t seed, const double *rw_sigma,
+                           const double *t_sigma, uint64_t nobs, const double *obs, int ll_mode, uint32_t W,
+                           const uint32_t *iters, uint32_t iter0, uint32_t nsteps, uint64_t N0, double *theta,
+                           double *ll, double *ra, uint64_t *ring, uint32_t *nacc, uint32_t *faults,
+                           double *hist_theta, double *hist_prop, double *hist_ll, uint8_t *hist_acc,
+                           int nthreads) {
+    orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
+    if (!g) return -3;
+    int rc = gsn_prepare(g, D, rw_sigma, t_sigma, nobs, obs, ll_mode);
+    if (rc) {
+        free(g);
+        return rc;
+    }
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t c = 0; c < (int64_t)C; ++c) {
+        orc_chain st = {theta + (uint64_t)c * D, ll + c, ra + c, ring + 2 * (uint64_t)c, nacc + c, faults + c};
+        run_chain(g, st, k0, k1, chain0 + (uint32_t)c, iters, iter0, nsteps, N0, W, C, (uint64_t)c, hist_theta,
+                  hist_prop, hist_ll, hist_acc);
+    }
+    (void)nthreads;
+    free(g);
+    return 0;
+}
+
+/* ---- stream probes for tests ---------------------------------------------- */
+
+ORC_EXPORT void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    orc_u32x4 c = {{ctr[0], ctr[1], ctr[2], ctr[3]}};
+    orc_u32x4 r = orc_philox4x32_10(c, key[0], key[1]);
+    memcpy(out, r.v, sizeof r.v);
+}
+
+/* The D normals and the Exp(1) draw of (chain, iter, pidx0). */
+ORC_EXPORT void orc_step_variates(uint64_t seed, uint32_t chain, uint32_t iter, uint32_t pidx0, int D, double *z,
+                                  double *E, double *u_radius, double *turn) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    for (int j = 0; j < (D + 1) / 2; ++j) {
+        orc_u32x4 r = orc_draw(k0, k1, chain, iter, (uint32_t)j, pidx0, 0);
+        double a, b;
+        orc_box_muller(r, &a, &b);
+        z[2 * j] = a;
+        if (2 * j + 1 < D) z[2 * j + 1] = b;
+        if (u_radius) u_radius[j] = orc_u01_open0(r.v[0], r.v[1]);
+        if (turn) turn[j] = (double)orc_bits53(r.v[2], r.v[3]) * 0x1p-53;
+    }
+    *E = orc_exp1(orc_draw(k0, k1, chain, iter, ORC_BLOCK_ACCEPT, pidx0, 0));
+}
+
+ORC_EXPORT void orc_log_vec(const double *x, double *y, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) y[i] = orc_log(x[i]);
+}
+
+ORC_EXPORT void orc_sincos_turn_vec(const uint64_t *turn53, double *c, double *s, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) {
+        uint32_t hi = (uint32_t)(turn53[i] >> 21);
+        uint32_t lo = (uint32_t)((turn53[i] & ((1u << 21) - 1u)) << 11);
+        uint64_t turn = orc_bits53(hi, lo);
+        uint32_t quadrant = (uint32_t)(turn >> 51);
+        uint64_t rem = turn & ((1ull << 51) - 1u);
+        int folded = rem >= (1ull << 50);
+        uint64_t rr = folded ? ((1ull << 51) - rem) : rem;
+        double x = (double)rr * 0x1.921fb54442d18p-51;
+        double sk = orc_sin_k(x), ck = orc_cos_k(x);
+        double sp = folded ? ck : sk, cp = folded ? sk : ck;
+        switch (quadrant) {
+        case 0: c[i] = cp; s[i] = sp; break;
+        case 1: c[i] = -sp; s[i] = cp; break;
+        case 2: c[i] = -cp; s[i] = -sp; break;
+        default: c[i] = sp; s[i] = -cp; break;
+        }
+    }
+}

@@ -1,0 +1,178 @@
+"""ctypes wrapper of oracle/lib/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import
+this module.  See oracle/emcmc_oracle.c for what is restated and the parity
+status ("parity unpinned" against the Julia reference itself; pinned by the
+Random123 KATs, the reference's own schedule/adaptation KATs, the numpy
+literal restatement in oracle/literal.py and the analytic posterior).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import subprocess
+from pathlib import Path
+
+import numpy as np
+
+ORACLE_DIR = Path(__file__).resolve().parent
+LIB_PATH = ORACLE_DIR / "lib" / "liboracle.so"
+
+_lib = None
+
+
+def build(force: bool = False) -> Path:
+    if force or not LIB_PATH.exists():
+        subprocess.run(["make", "-C", str(ORACLE_DIR)], check=True, capture_output=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(str(LIB_PATH))
+        dp = C.POINTER(C.c_double)
+        u32p = C.POINTER(C.c_uint32)
+        u64p = C.POINTER(C.c_uint64)
+        u8p = C.POINTER(C.c_uint8)
+        L.orc_run_gsn.restype = C.c_int
+        L.orc_run_gsn.argtypes = [
+            C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32,
+            u32p, C.c_uint32, C.c_uint32, C.c_uint64, dp, dp, dp, u64p, u32p, u32p, dp, dp, dp, u8p, C.c_int,
+        ]
+        L.orc_cholesky.restype = C.c_int
+        L.orc_cholesky.argtypes = [dp, C.c_int, dp]
+        L.orc_canon_sum.restype = C.c_double
+        L.orc_canon_sum.argtypes = [dp, C.c_int]
+        L.orc_gsn_constants.restype = C.c_int
+        L.orc_gsn_constants.argtypes = [C.c_int, dp, dp, C.c_uint64, dp, dp, dp, dp]
+        L.orc_philox.restype = None
+        L.orc_philox.argtypes = [u32p, u32p, u32p]
+        L.orc_step_variates.restype = None
+        L.orc_step_variates.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, dp, dp, dp, dp]
+        L.orc_log_vec.restype = None
+        L.orc_log_vec.argtypes = [dp, dp, C.c_uint64]
+        L.orc_sincos_turn_vec.restype = None
+        L.orc_sincos_turn_vec.argtypes = [u64p, dp, dp, C.c_uint64]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _colmajor(S, D):
+    return np.ascontiguousarray(np.asarray(S, dtype=np.float64).reshape(D, D).ravel(order="F"))
+
+
+class OracleState:
+    """Carried per-chain state (mirrors the engine's SoA state)."""
+
+    def __init__(self, theta, ll=None):
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        self.C, self.D = theta.shape
+        self.theta = theta.copy()
+        self.ll = np.full(self.C, -np.inf) if ll is None else np.ascontiguousarray(ll, dtype=np.float64).copy()
+        self.ra = np.zeros(self.C)
+        self.ring = np.zeros((self.C, 2), dtype=np.uint64)
+        self.nacc = np.zeros(self.C, dtype=np.uint32)
+        self.faults = np.zeros(self.C, dtype=np.uint32)
+        self.N = 1  # GenericChainStats.N
+
+
+def alloc_history(C, D, nsteps):
+    return {"theta": np.empty((nsteps, C, D)), "prop": np.empty((nsteps, C, D)), "ll": np.empty((nsteps, C)),
+            "acc": np.empty((nsteps, C), dtype=np.uint8)}
+
+
+def run_gsn(state: OracleState, *, seed, rw_sigma, t_sigma, obs, iter0, nsteps, chain0=0, ll_mode=0, W=100,
+            iters=None, history=True, nthreads=1, hist=None):
+    """Advance `state` by `nsteps` iterations of the single joint GaussianRW update.
+    `hist` may be a preallocated alloc_history(C, D, nsteps) dict (reused buffers)."""
+    L = lib()
+    Cn, D = state.C, state.D
+    X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
+    reuse = hist is not None
+    if not reuse:
+        hist = alloc_history(Cn, D, nsteps) if history else {}
+    history = bool(hist)
+    it = None
+    if iters is not None:
+        it = np.ascontiguousarray(iters, dtype=np.uint32)
+    rc = L.orc_run_gsn(
+        D, Cn, chain0, seed & 0xFFFFFFFFFFFFFFFF, _d(_colmajor(rw_sigma, D)), _d(_colmajor(t_sigma, D)), X.shape[0],
+        _d(X), ll_mode, W, None if it is None else it.ctypes.data_as(C.POINTER(C.c_uint32)), iter0, nsteps,
+        state.N, _d(state.theta), _d(state.ll), _d(state.ra), state.ring.ctypes.data_as(C.POINTER(C.c_uint64)),
+        state.nacc.ctypes.data_as(C.POINTER(C.c_uint32)), state.faults.ctypes.data_as(C.POINTER(C.c_uint32)),
+        _d(hist.get("theta")), _d(hist.get("prop")), _d(hist.get("ll")),
+        None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads,
+    )
+    if rc != 0:
+        raise ValueError(f"orc_run_gsn failed: {rc}")
+    state.N += nsteps
+    if history and not reuse:
+        hist["acc"] = hist["acc"].astype(bool)
+    return hist
+
+
+def cholesky(S):
+    S = np.asarray(S, dtype=np.float64)
+    D = S.shape[0]
+    Lm = np.zeros(D * D)
+    if lib().orc_cholesky(_d(_colmajor(S, D)), D, _d(Lm)) != 0:
+        raise np.linalg.LinAlgError("not positive definite")
+    return Lm.reshape(D, D)
+
+
+def canon_sum(v):
+    v = np.ascontiguousarray(v, dtype=np.float64)
+    return lib().orc_canon_sum(_d(v), v.shape[0])
+
+
+def gsn_constants(rw_sigma, t_sigma, obs):
+    D = np.asarray(rw_sigma).shape[0]
+    X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
+    out = np.zeros(3 + D)
+    Lr = np.zeros(D * D)
+    Lt = np.zeros(D * D)
+    rc = lib().orc_gsn_constants(D, _d(_colmajor(rw_sigma, D)), _d(_colmajor(t_sigma, D)), X.shape[0], _d(X),
+                                 _d(out), _d(Lr), _d(Lt))
+    if rc:
+        raise ValueError(rc)
+    return {"rw_c0": out[0], "t_c0": out[1], "S_c": out[2], "xbar": out[3:], "L_rw": Lr.reshape(D, D),
+            "L_t": Lt.reshape(D, D)}
+
+
+def philox(ctr, key):
+    c = np.ascontiguousarray(ctr, dtype=np.uint32)
+    k = np.ascontiguousarray(key, dtype=np.uint32)
+    out = np.zeros(4, dtype=np.uint32)
+    p = C.POINTER(C.c_uint32)
+    lib().orc_philox(c.ctypes.data_as(p), k.ctypes.data_as(p), out.ctypes.data_as(p))
+    return out
+
+
+def step_variates(seed, chain, it, D, pidx0=0):
+    z = np.zeros(D + 1)
+    E = np.zeros(1)
+    npair = (D + 1) // 2
+    u = np.zeros(npair)
+    t = np.zeros(npair)
+    lib().orc_step_variates(seed & 0xFFFFFFFFFFFFFFFF, chain, it, pidx0, D, _d(z), _d(E), _d(u), _d(t))
+    return z[:D], float(E[0]), u, t
+
+
+def log_vec(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_log_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def sincos_turn(turn53):
+    t = np.ascontiguousarray(turn53, dtype=np.uint64)
+    c = np.empty(t.size)
+    s = np.empty(t.size)
+    lib().orc_sincos_turn_vec(t.ctypes.data_as(C.POINTER(C.c_uint64)), _d(c), _d(s), t.size)
+    return c, s

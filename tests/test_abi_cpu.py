@@ -1,0 +1,83 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every
+symbol include/emcmc.h declares, the ctypes struct layouts match the header's
+C layout, and on a GPU-less host the engine refuses to run (no CPU fallback)."""
+import ctypes as C
+import re
+import subprocess
+import textwrap
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "emcmc.h"
+
+
+def declared_functions():
+    txt = HEADER.read_text()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(emcmc_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_and_binding_agree():
+    assert declared_functions() == sorted(L.SIGNATURES)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = L.lib()
+    out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (emcmc_\w+)", out))
+    for name in declared_functions():
+        assert name in exported, name
+        assert getattr(lib, name) is not None
+
+
+def test_struct_layout_matches_header(tmp_path):
+    src = textwrap.dedent(
+        """
+        #include <stdio.h>
+        #include <stddef.h>
+        #include "emcmc.h"
+        int main(void) {
+          printf("%zu %zu %zu %zu %zu\\n", sizeof(emcmc_config), sizeof(emcmc_update_desc),
+                 sizeof(emcmc_target_desc), sizeof(emcmc_step), sizeof(emcmc_moments));
+          printf("%zu %zu %zu\\n", offsetof(emcmc_config, device), offsetof(emcmc_update_desc, pos),
+                 offsetof(emcmc_target_desc, ll_mode));
+          return 0;
+        }
+        """
+    )
+    c = tmp_path / "layout.c"
+    c.write_text(src)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", str(HEADER.parent), str(c), "-o", str(exe)], check=True)
+    sizes, offs = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")[:2]
+    assert [int(x) for x in sizes.split()] == [C.sizeof(L.EmcmcConfig), C.sizeof(L.EmcmcUpdateDesc),
+                                               C.sizeof(L.EmcmcTargetDesc), C.sizeof(L.EmcmcStep),
+                                               C.sizeof(L.EmcmcMoments)]
+    assert [int(x) for x in offs.split()] == [L.EmcmcConfig.device.offset, L.EmcmcUpdateDesc.pos.offset,
+                                              L.EmcmcTargetDesc.ll_mode.offset]
+
+
+def test_no_device_means_no_run():
+    """With no GPU the engine refuses (EMCMC_NO_DEVICE) instead of computing on the CPU."""
+    if L.device_count() > 0:
+        pytest.skip("a GPU is visible; covered by the gpu tests")
+    from extensible_mcmc import Engine, EngineConfig
+
+    with pytest.raises(L.EMCMCError) as e:
+        Engine(EngineConfig(dim=2, num_chains=4, num_mcmc_steps=10))
+    assert e.value.status == L.NO_DEVICE
+
+
+def test_invalid_config_rejected_without_device():
+    cfg = L.EmcmcConfig()
+    cfg.abi_version = 999
+    h = C.c_void_p()
+    assert L.lib().emcmc_create(C.byref(h), C.byref(cfg)) == L.INVALID_ARG
+    n = C.c_int(-1)
+    assert L.lib().emcmc_device_count(C.byref(n)) == L.OK and n.value >= 0

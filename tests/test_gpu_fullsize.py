@@ -1,0 +1,76 @@
+"""Headline workload at full size (BASELINE cfg 2: 65,536 chains × 1,000
+iterations, D = 32, full histories in HBM).  The oracle is too slow to replay
+every chain here, so full size is checked through size-independent properties
+plus a bitwise replay of a random sample of chains (each chain is independent
+and keyed by its global id, so the oracle replays it alone)."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc import rhat_from_sums
+from extensible_mcmc import workloads as W
+
+from helpers import run_engine
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def full_run(require_gpu):
+    w = W.cfg2(65536)
+    e = run_engine(w, 65536, 1000, fetch=False)
+    return w, e
+
+
+def test_sampled_chains_bitwise(oracle, full_run):
+    w, e = full_run
+    eng = e["engine"]
+    rng = np.random.default_rng(11)
+    picks = np.sort(rng.choice(65536, 24, replace=False))
+    acc_all = eng.get_history(L.H_ACCEPT, 1, 1000)[:, 0]
+    for c in picks:
+        st = oracle.OracleState(np.zeros((1, 32)))
+        h = oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1,
+                           nsteps=1000, chain0=int(c))
+        assert np.array_equal(acc_all[:, c], h["acc"][:, 0])
+        th = eng.get_history_chains(L.H_STATE, 1, 1000, int(c), 1)[:, 0, 0]
+        assert np.array_equal(th, h["theta"][:, 0])
+        ll = eng.get_history_chains(L.H_LL, 1, 1000, int(c), 1)[:, 0, 0]
+        assert np.array_equal(ll, h["ll"][:, 0])
+        assert np.array_equal(e["theta"][c], st.theta[0])
+
+
+def test_acceptance_and_first_step(full_run):
+    w, e = full_run
+    acc = e["engine"].get_history(L.H_ACCEPT, 1, 1000)[:, 0]
+    assert acc[0].all()  # ll = −Inf before step 1 ⇒ always accept (workspaces.jl:425, run.jl:109)
+    rate = acc[200:].mean()
+    assert 0.20 < rate < 0.30, rate  # σ = 2.38/√(D·n): optimal-scaling acceptance ≈ 0.23–0.26
+    assert e["nacc"].sum() == acc.sum()
+    assert (e["faults"] == 0).all()
+
+
+def test_posterior_matches_analytic(full_run):
+    """ImproperPrior on μ of GsnTargetLaw(μ, I): posterior N(x̄, I/n) exactly."""
+    w, e = full_run
+    eng = e["engine"]
+    m = eng.moments_window(501, 500, split=True)
+    r = rhat_from_sums(m)
+    xbar = w.obs.mean(axis=0)
+    assert np.abs(r["mean"] - xbar).max() < 0.01
+    post_var = r["W"] + r["B"] / m["num_draws"]
+    assert np.abs(post_var / (1.0 / w.nobs) - 1.0).max() < 0.05
+    assert np.abs(r["rhat"] - 1.0).max() < 0.01
+    assert 0.20 < r["accept_rate"] < 0.30
+
+
+def test_timing_reports_launches(full_run):
+    w, _ = full_run
+    e = run_engine(w, 65536, 128, fetch=False, hist=L.HIST_FULL, spl=64)
+    eng = e["engine"]
+    eng.set_timing(True)
+    eng.run_iters(1, 128)
+    eng.synchronize()
+    ms, n, b = eng.get_timing()
+    assert n == 2 and ms > 0
+    assert b == pytest.approx(65536 * (128 * (16 * 32 + 8.125) + 2 * (16 * 32 + 80)))

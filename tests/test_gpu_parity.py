@@ -1,0 +1,120 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle on the
+same seeds and chain ids.  Bar: bit-exact accept/reject stream, θ, θ°, ll,
+rolling acceptance and accept counts (integer and fp64 alike — both sides use
+the same IEEE operation sequence)."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc import workloads as W
+
+from helpers import assert_bitwise, run_engine, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu(require_gpu):
+    pass
+
+
+def test_device_log_matches_oracle(oracle):
+    rng = np.random.default_rng(7)
+    x = np.concatenate([rng.uniform(2.0 ** -53, 1.0, 500_000), 2.0 ** -np.arange(0, 54),
+                        np.exp(rng.uniform(-700, 700, 100_000)), [1.0, 0.5, 2.0]])
+    assert np.array_equal(L.probe_log(x), oracle.log_vec(x))
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 32])
+def test_device_variates_match_oracle(oracle, D):
+    rng = np.random.default_rng(D)
+    n = 4096
+    chains = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    iters = rng.integers(1, 2 ** 31, n, dtype=np.uint64).astype(np.uint32)
+    z, E = L.probe_variates(W.SEED, chains, iters, D)
+    for i in range(0, n, 97):
+        zo, Eo, _, _ = oracle.step_variates(W.SEED, int(chains[i]), int(iters[i]), D)
+        assert np.array_equal(z[i], zo)
+        assert E[i] == Eo
+
+
+@pytest.mark.parametrize("lpc", [1, 2, 4])
+@pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
+def test_d32_headline_shape(oracle, lpc, ll_mode):
+    w = W.cfg2(2048)
+    e = run_engine(w, 2048, 150, lpc=lpc, ll_mode=ll_mode)
+    assert f"LPC={lpc}" in e["kernel"]
+    o = run_oracle(oracle, w, 2048, 150, ll_mode=ll_mode)
+    assert_bitwise(e, o)
+
+
+def test_d32_accept_only_and_launch_splits(oracle):
+    w = W.cfg2(1000)  # 1000 chains: partial last wave at every LPC
+    o = run_oracle(oracle, w, 1000, 130)
+    for spl in (1, 7, 64):
+        e = run_engine(w, 1000, 130, lpc=4, hist=L.HIST_ACCEPT_ONLY, spl=spl)
+        assert "ACCEPT_ONLY" in e["kernel"]
+        assert_bitwise(e, o, full=False)
+
+
+@pytest.mark.parametrize("which", ["ref_test", "iso"])
+def test_d2_reference_test_target(oracle, which):
+    w = W.ref_test() if which == "ref_test" else W.cfg1(True)
+    e = run_engine(w, 777, 300)
+    assert ("dense" in e["kernel"]) == (which == "ref_test")
+    o = run_oracle(oracle, w, 777, 300)
+    assert_bitwise(e, o)
+
+
+@pytest.mark.parametrize("D,lpc", [(16, 2), (64, 4), (8, 1), (3, 1)])
+def test_other_dims(oracle, D, lpc):
+    w = W.cfg2(512, D=D)
+    e = run_engine(w, 512, 80, lpc=lpc)
+    o = run_oracle(oracle, w, 512, 80)
+    assert_bitwise(e, o)
+
+
+def test_dense_correlated_d4(oracle):
+    rng = np.random.default_rng(4)
+    A = rng.standard_normal((4, 4))
+    S = A @ A.T / 4 + np.eye(4)
+    B = rng.standard_normal((4, 4))
+    R = 0.1 * (B @ B.T / 4 + np.eye(4))
+    obs = rng.multivariate_normal(np.ones(4), S, size=9)
+    w = W.GsnWorkload("d4", 4, 300, np.ones(4), S, R, obs, np.zeros(4))
+    for ll_mode in (0, 1):
+        e = run_engine(w, 300, 120, ll_mode=ll_mode)
+        assert "dense" in e["kernel"]
+        assert_bitwise(e, run_oracle(oracle, w, 300, 120, ll_mode=ll_mode))
+
+
+def test_shard_offsets_reproduce_unsharded_chains(oracle):
+    """Chains keyed by global id: two shards == one run (the 8-GPU invariant)."""
+    w = W.cfg5(4096)
+    full = run_engine(w, 4096, 60, theta0=w.theta_init[:4096])
+    a = run_engine(w, 2048, 60, chain0=0, theta0=w.theta_init[:2048])
+    b = run_engine(w, 2048, 60, chain0=2048, theta0=w.theta_init[2048:4096])
+    assert np.array_equal(np.concatenate([a["theta"], b["theta"]]), full["theta"])
+    assert np.array_equal(np.concatenate([a["acc"], b["acc"]], axis=1), full["acc"])
+    o = run_oracle(oracle, w, 256, 60, chain0=2048, theta0=w.theta_init[2048:2304])
+    assert np.array_equal(b["theta"][:256], o["state"].theta)
+
+
+def test_resume_across_runs(oracle):
+    w = W.cfg2(640)
+    e = run_engine(w, 640, 50, M=120, fetch=False)
+    eng = e["engine"]
+    eng.run_iters(51, 70)
+    eng.synchronize()
+    th, ll = eng.get_state()
+    o = run_oracle(oracle, w, 640, 120, history=False)
+    assert np.array_equal(th, o["state"].theta)
+    assert np.array_equal(ll, o["state"].ll)
+
+
+def test_nonfinite_target_sets_fault_bit():
+    w = W.cfg2(64, D=2)
+    w.obs = np.full_like(w.obs, 1e300)  # (x − μ)² overflows → ll° = −Inf
+    e = run_engine(w, 64, 5, fetch=False)
+    assert (e["faults"] & L.FAULT_NONFINITE_LL).all()
+    assert not e["engine"].synchronize(allow_faults=True)

@@ -1,0 +1,120 @@
+"""Oracle self-checks (CPU): the shared variate stream and canonical arithmetic.
+
+Pins: Random123 Philox KATs (tests/golden/philox_kat.json); accuracy of the
+restated log / sin / cos against numpy; Box–Muller normality; the canonical
+Cholesky and summation against LAPACK / math.fsum; and the claim the kernels
+rely on that the dense (general-L) formulas give the same bits as the diagonal
+ones when Σ is diagonal.
+"""
+import json
+import math
+
+import numpy as np
+import pytest
+
+from extensible_mcmc import workloads as W
+
+
+def test_philox_kat(oracle, golden_dir):
+    for v in json.loads((golden_dir / "philox_kat.json").read_text()):
+        assert [int(x) for x in oracle.philox(v["ctr"], v["key"])] == v["out"]
+
+
+def test_log_accuracy(oracle):
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(2.0 ** -53, 1.0, 200_000), 2.0 ** -np.arange(0, 54),
+                        rng.uniform(0.5, 2.0, 50_000), np.exp(rng.uniform(-700, 700, 50_000)), [1.0]])
+    y = oracle.log_vec(x)
+    ref = np.log(x)
+    nz = ref != 0
+    ulp = np.abs(y[nz] - ref[nz]) / np.spacing(np.abs(ref[nz]))
+    assert ulp.max() <= 1.0
+    assert y[x == 1.0][0] == 0.0
+
+
+def test_sincos_accuracy(oracle):
+    rng = np.random.default_rng(1)
+    t = rng.integers(0, 2 ** 53, 200_000, dtype=np.uint64)
+    t = np.concatenate([t, np.array([0, 2 ** 50, 2 ** 51, 3 * 2 ** 51, 2 ** 53 - 1], dtype=np.uint64)])
+    c, s = oracle.sincos_turn(t)
+    # exact angle in long double-free form: use the folded representation
+    ang = 2 * np.pi * (t.astype(np.float64) / 2.0 ** 53)
+    assert np.abs(c - np.cos(ang)).max() < 2e-15
+    assert np.abs(s - np.sin(ang)).max() < 2e-15
+    assert np.allclose(c * c + s * s, 1.0, atol=4e-16)
+
+
+def test_box_muller_normal(oracle):
+    from scipy import stats
+
+    zs = np.concatenate([oracle.step_variates(W.SEED, c, it, 32)[0] for c in range(40) for it in range(1, 51)])
+    assert zs.size == 40 * 50 * 32
+    assert abs(zs.mean()) < 0.02 and abs(zs.std() - 1.0) < 0.02
+    assert stats.kstest(zs, "norm").pvalue > 1e-3
+    Es = np.array([oracle.step_variates(W.SEED, c, 1, 2)[1] for c in range(20_000)])
+    assert abs(Es.mean() - 1.0) < 0.03
+    assert stats.kstest(Es, "expon").pvalue > 1e-3
+
+
+def test_variates_depend_on_counter(oracle):
+    a = oracle.step_variates(W.SEED, 3, 7, 4)
+    b = oracle.step_variates(W.SEED, 3, 7, 4)
+    c = oracle.step_variates(W.SEED, 4, 7, 4)
+    d = oracle.step_variates(W.SEED + 1, 3, 7, 4)
+    e = oracle.step_variates(W.SEED, 3, 7, 4, pidx0=1)
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1]
+    for other in (c, d, e):
+        assert not np.array_equal(a[0], other[0])
+
+
+def test_cholesky_matches_lapack(oracle):
+    rng = np.random.default_rng(2)
+    for D in (1, 2, 5, 32):
+        A = rng.standard_normal((D, D))
+        S = A @ A.T + D * np.eye(D)
+        L = oracle.cholesky(S)
+        assert np.allclose(L, np.linalg.cholesky(S), rtol=1e-13, atol=1e-13)
+        # only the upper triangle is read (Symmetric(Σ), uplo = :U)
+        S2 = np.triu(S) + np.tril(rng.standard_normal((D, D)), -1)
+        assert np.array_equal(oracle.cholesky(S2), L)
+    with pytest.raises(np.linalg.LinAlgError):
+        oracle.cholesky(np.array([[1.0, 2.0], [2.0, 1.0]]))
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 8, 16, 24, 32, 64])
+def test_canonical_sum(oracle, D):
+    rng = np.random.default_rng(D)
+    v = rng.uniform(0, 1, D)
+    s = oracle.canon_sum(v)
+    assert abs(s - math.fsum(v)) <= 4 * D * np.spacing(s)
+    blk = 8 if (D % 8 == 0 and D >= 16) else D
+    parts = [sum_seq(v[i:i + blk]) for i in range(0, D, blk)]
+    while len(parts) > 1:
+        nxt = [parts[2 * i] + parts[2 * i + 1] for i in range(len(parts) // 2)]
+        if len(parts) % 2:
+            nxt.append(parts[-1])
+        parts = nxt
+    assert s == parts[0]
+
+
+def sum_seq(v):
+    s = v[0]
+    for x in v[1:]:
+        s = s + x
+    return s
+
+
+@pytest.mark.parametrize("ll_mode", [0, 1])
+def test_dense_formulas_equal_diagonal_bits(oracle, ll_mode):
+    w = W.cfg2(16)
+    runs = []
+    for force_dense in (0, 0x100):
+        st = oracle.OracleState(np.zeros((16, w.D)))
+        h = oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1,
+                           nsteps=60, ll_mode=ll_mode | force_dense)
+        runs.append((st, h))
+    (a, ha), (b, hb) = runs
+    assert np.array_equal(ha["acc"], hb["acc"])
+    assert np.array_equal(ha["ll"], hb["ll"])
+    assert np.array_equal(ha["theta"], hb["theta"])
+    assert np.array_equal(a.ra, b.ra)

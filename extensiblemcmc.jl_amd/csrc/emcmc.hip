@@ -67,14 +67,14 @@ double logdet_chol(const std::vector<double> &L, int D) {
 // Distributions.mvnormal_c0: −(D·log2π + logdet)/2
 double mvnormal_c0(int D, double logdet) { return -((double)D * kLog2Pi + logdet) / 2.0; }
 
-// host restatement of the canonical blocked sum (used for S_c)
-double canon_sum_host(const double *v, int D) {
+// host restatement of the canonical blocked sum of squares (used for S_c)
+double canon_sumsq_host(const double *y, int D) {
     const int BLK = (D % 8 == 0 && D >= 16) ? 8 : D;
     const int NB = D / BLK;
     std::vector<double> b(NB);
     for (int k = 0; k < NB; ++k) {
-        double s = v[k * BLK];
-        for (int i = 1; i < BLK; ++i) s = s + v[k * BLK + i];
+        double s = y[k * BLK] * y[k * BLK];
+        for (int i = 1; i < BLK; ++i) s = std::fma(y[k * BLK + i], y[k * BLK + i], s);
         b[k] = s;
     }
     int n = NB;
@@ -108,6 +108,8 @@ struct Variant {
     KernelFn fn = nullptr;
     int lpc = 1;
     bool dense = false;
+    bool unit = false;
+    int occ = 0;
     std::string name;
 };
 
@@ -128,10 +130,10 @@ struct emcmc_handle {
     double *d_hist_theta = nullptr, *d_hist_prop = nullptr, *d_hist_ll = nullptr;
     uint8_t *d_hist_acc = nullptr;
     double *d_consts = nullptr, *d_obs = nullptr;
-    uint32_t *d_iters = nullptr;
-    size_t iters_cap = 0;
     double *d_scratch = nullptr;  // diagnostics
     size_t scratch_bytes = 0;
+    double *d_gather = nullptr;   // history layout conversion
+    size_t gather_bytes = 0;
     uint64_t row_bytes = 0;
     // dispatch
     Variant var;
@@ -170,24 +172,32 @@ emcmc_status fail(emcmc_handle *h, emcmc_status st, const char *fmt, ...) {
 
 // ---- kernel table -----------------------------------------------------------
 struct Key {
-    int D, lpc, full, ll, dense;
+    int D, lpc, full, ll, dense, unit, occ;
 };
 
-template <int D, int LPC, bool FULL, int LL>
+template <int D, int LPC, bool FULL, int LL, bool UNIT, int MINW = 1>
 KernelFn diag_fn() {
-    return &rwm_gsn_diag_kernel<D, LPC, FULL, LL>;
+    return &rwm_gsn_diag_kernel<D, LPC, FULL, LL, UNIT, MINW>;
 }
 template <int D, bool FULL, int LL>
 KernelFn dense_fn() {
     return &rwm_gsn_dense_kernel<D, FULL, LL>;
 }
 
-#define DIAG4(D, LPC)                                                                  \
-    {{D, LPC, 1, 0, 0}, diag_fn<D, LPC, true, 0>()}, {{D, LPC, 1, 1, 0}, diag_fn<D, LPC, true, 1>()}, \
-        {{D, LPC, 0, 0, 0}, diag_fn<D, LPC, false, 0>()}, {{D, LPC, 0, 1, 0}, diag_fn<D, LPC, false, 1>()}
-#define DENSE4(D)                                                                        \
-    {{D, 1, 1, 0, 1}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1}, dense_fn<D, true, 1>()},   \
-        {{D, 1, 0, 0, 1}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1}, dense_fn<D, false, 1>()}
+#define DIAGU(D, LPC, U)                                                                          \
+    {{D, LPC, 1, 0, 0, U, 0}, diag_fn<D, LPC, true, 0, U>()},                                        \
+        {{D, LPC, 1, 1, 0, U, 0}, diag_fn<D, LPC, true, 1, U>()},                                    \
+        {{D, LPC, 0, 0, 0, U, 0}, diag_fn<D, LPC, false, 0, U>()},                                   \
+        {{D, LPC, 0, 1, 0, U, 0}, diag_fn<D, LPC, false, 1, U>()}
+#define DIAG4(D, LPC) DIAGU(D, LPC, false), DIAGU(D, LPC, true)
+#define DIAGO(D, LPC, U)                                                                          \
+    {{D, LPC, 1, 0, 0, U, 4}, diag_fn<D, LPC, true, 0, U, 4>()},                                     \
+        {{D, LPC, 1, 1, 0, U, 4}, diag_fn<D, LPC, true, 1, U, 4>()},                                 \
+        {{D, LPC, 0, 0, 0, U, 4}, diag_fn<D, LPC, false, 0, U, 4>()},                                \
+        {{D, LPC, 0, 1, 0, U, 4}, diag_fn<D, LPC, false, 1, U, 4>()}
+#define DENSE4(D)                                                                                    \
+    {{D, 1, 1, 0, 1, 0, 0}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1, 0, 0}, dense_fn<D, true, 1>()},   \
+        {{D, 1, 0, 0, 1, 0, 0}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1, 0, 0}, dense_fn<D, false, 1>()}
 
 struct Entry {
     Key k;
@@ -198,15 +208,17 @@ const std::vector<Entry> &kernel_table() {
     static const std::vector<Entry> t = {
         DIAG4(1, 1),  DIAG4(2, 1),  DIAG4(3, 1),  DIAG4(4, 1),  DIAG4(8, 1),
         DIAG4(16, 1), DIAG4(16, 2), DIAG4(32, 1), DIAG4(32, 2), DIAG4(32, 4),
-        DIAG4(64, 2), DIAG4(64, 4), DENSE4(1),    DENSE4(2),    DENSE4(3),
+        DIAG4(64, 2), DIAG4(64, 4), DIAGO(32, 4, true), DIAGO(32, 4, false), DIAGO(32, 2, true),
+        DENSE4(1),    DENSE4(2),    DENSE4(3),
         DENSE4(4),    DENSE4(8),
     };
     return t;
 }
 
-KernelFn lookup(int D, int lpc, bool full, int ll, bool dense) {
+KernelFn lookup(int D, int lpc, bool full, int ll, bool dense, bool unit, int occ = 0) {
     for (const auto &e : kernel_table())
-        if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == (int)dense)
+        if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == (int)dense &&
+            e.k.unit == (int)unit && e.k.occ == occ)
             return e.fn;
     return nullptr;
 }
@@ -250,15 +262,24 @@ emcmc_status select_variant(emcmc_handle *h) {
     Variant v;
     if (diag) {
         int lpc = h->cfg.lanes_per_chain ? (int)h->cfg.lanes_per_chain : auto_lpc(D);
-        v.fn = lookup(D, lpc, full, ll, false);
+        bool unit = true;
+        for (int i = 0; i < D; ++i) unit = unit && h->target.invdiag[i] == 1.0;
+        v.unit = unit;
+        const int occ = (h->cfg.kernel_variant & EMCMC_VARIANT_HIGH_OCCUPANCY) ? 4 : 0;
+        v.fn = lookup(D, lpc, full, ll, false, unit, occ);
+        v.occ = occ;
+        if (!v.fn && occ) {
+            v.fn = lookup(D, lpc, full, ll, false, unit, 0);
+            v.occ = 0;
+        }
         if (!v.fn && !h->cfg.lanes_per_chain) {
             lpc = 1;
-            v.fn = lookup(D, 1, full, ll, false);
+            v.fn = lookup(D, 1, full, ll, false, unit);
         }
         v.lpc = lpc;
         v.dense = false;
     } else {
-        v.fn = lookup(D, 1, full, ll, true);
+        v.fn = lookup(D, 1, full, ll, true, false);
         v.lpc = 1;
         v.dense = true;
     }
@@ -268,8 +289,9 @@ emcmc_status select_variant(emcmc_handle *h) {
                     "dense D∈{1,2,3,4,8}",
                     D, diag ? "diagonal" : "dense", h->cfg.lanes_per_chain);
     char nm[160];
-    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s>", v.dense ? "dense" : "diag", D, v.lpc,
-             full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
+    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>", v.dense ? "dense" : "diag", D, v.lpc,
+             full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
+             v.occ ? ",MINW=4" : "");
     v.name = nm;
     // constants for this variant
     std::vector<double> c;
@@ -455,15 +477,14 @@ emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t) {
         th.xbar[i] = s / (double)th.nobs;
     }
     double Sc = 0.0;
-    std::vector<double> y(d), v(d);
+    std::vector<double> y(d);
     for (uint64_t k = 0; k < th.nobs; ++k) {
         for (uint32_t i = 0; i < d; ++i) {
             double acc = th.obs[k * d + i] - th.xbar[i];
             for (uint32_t j = 0; j < i; ++j) acc = std::fma(-th.L[(size_t)i * d + j], y[j], acc);
             y[i] = acc * th.invdiag[i];
-            v[i] = y[i] * y[i];
         }
-        Sc = Sc + canon_sum_host(v.data(), (int)d);
+        Sc = Sc + canon_sumsq_host(y.data(), (int)d);
     }
     th.S_c = Sc;
     h->target = std::move(th);
@@ -476,7 +497,11 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
     emcmc_status st = ensure_alloc(h);
     if (st) return st;
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
-    HIPCHK(h, hipMemcpyAsync(h->d_theta, theta, C * D * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    // host row-major [C][D] → device state_pos layout
+    std::vector<double> soa(C * D);
+    for (uint64_t c = 0; c < C; ++c)
+        for (uint64_t d = 0; d < D; ++d) soa[state_pos(d, c, C, (uint32_t)D)] = theta[c * D + d];
+    HIPCHK(h, hipMemcpyAsync(h->d_theta, soa.data(), C * D * sizeof(double), hipMemcpyHostToDevice, h->stream));
     std::vector<double> l(C, -INFINITY);
     if (ll) std::copy(ll, ll + C, l.begin());
     HIPCHK(h, hipMemcpyAsync(h->d_ll, l.data(), C * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -535,32 +560,16 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     const uint64_t K = h->cfg.steps_per_launch;
     uint64_t i = 0;
     while (i < num_steps) {
-        // maximal run of ≤ K steps of the same update
+        // maximal run of ≤ K consecutive iterations of the same update
         uint64_t j = i + 1;
-        bool consecutive = true;
-        while (j < num_steps && j - i < K && steps[j].pidx == steps[i].pidx) {
-            if (steps[j].mcmciter != steps[j - 1].mcmciter + 1) consecutive = false;
+        while (j < num_steps && j - i < K && steps[j].pidx == steps[i].pidx &&
+               steps[j].mcmciter == steps[j - 1].mcmciter + 1)
             ++j;
-        }
         const uint64_t n = j - i;
         p.pidx0 = steps[i].pidx - 1;
         p.iter0 = steps[i].mcmciter;
         p.nsteps = (uint32_t)n;
         p.N0 = h->stats_N;
-        p.iters = nullptr;
-        if (!consecutive) {
-            if (h->iters_cap < n) {
-                HIPCHK(h, hipStreamSynchronize(h->stream));
-                if (h->d_iters) (void)hipFree(h->d_iters);
-                HIPCHK(h, hipMalloc(&h->d_iters, n * sizeof(uint32_t)));
-                h->iters_cap = n;
-            }
-            std::vector<uint32_t> its(n);
-            for (uint64_t q = 0; q < n; ++q) its[q] = steps[i + q].mcmciter;
-            HIPCHK(h, hipStreamSynchronize(h->stream));
-            HIPCHK(h, hipMemcpy(h->d_iters, its.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
-            p.iters = h->d_iters;
-        }
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->timing) {
             e0 = get_event(h);
@@ -603,7 +612,7 @@ void emcmc_destroy(emcmc_handle *h) {
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     void *bufs[] = {h->d_theta,     h->d_ll,        h->d_ra,      h->d_ring,     h->d_nacc,  h->d_faults,
                     h->d_hist_theta, h->d_hist_prop, h->d_hist_ll, h->d_hist_acc, h->d_consts, h->d_obs,
-                    h->d_iters,     h->d_scratch};
+                    h->d_scratch,   h->d_gather};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -617,7 +626,12 @@ emcmc_status emcmc_get_state(emcmc_handle *h, double *theta, double *ll) {
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
-    if (theta) HIPCHK(h, hipMemcpy(theta, h->d_theta, C * D * sizeof(double), hipMemcpyDeviceToHost));
+    if (theta) {  // device state_pos layout → host [C][D]
+        std::vector<double> soa(C * D);
+        HIPCHK(h, hipMemcpy(soa.data(), h->d_theta, C * D * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (uint64_t d = 0; d < D; ++d) theta[c * D + d] = soa[state_pos(d, c, C, (uint32_t)D)];
+    }
     if (ll) HIPCHK(h, hipMemcpy(ll, h->d_ll, C * sizeof(double), hipMemcpyDeviceToHost));
     return EMCMC_OK;
 }
@@ -657,6 +671,34 @@ static emcmc_status hist_geometry(emcmc_handle *h, uint32_t which, void **base, 
     return EMCMC_OK;
 }
 
+// STATE/PROPOSAL slots [slot0, slot0+nslots) for chains [c0, c0+nc): device
+// state_pos layout → host [slot][nc][D], staged through a bounded scratch.
+static emcmc_status copy_state_slots(emcmc_handle *h, const double *base, uint64_t slot0, uint64_t nslots,
+                                     uint64_t c0, uint64_t nc, double *host_out) {
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    const uint64_t per_slot = nc * D;
+    const uint64_t cap_elems = std::max<uint64_t>(per_slot, (256ull << 20) / sizeof(double));
+    const uint64_t slots_per_chunk = std::max<uint64_t>(1, cap_elems / per_slot);
+    const uint64_t need = std::min(nslots, slots_per_chunk) * per_slot * sizeof(double);
+    if (h->gather_bytes < need) {
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        if (h->d_gather) (void)hipFree(h->d_gather);
+        HIPCHK(h, hipMalloc(&h->d_gather, need));
+        h->gather_bytes = need;
+    }
+    for (uint64_t s0 = 0; s0 < nslots; s0 += slots_per_chunk) {
+        const uint64_t ns = std::min(slots_per_chunk, nslots - s0);
+        const uint64_t n = ns * per_slot;
+        hipLaunchKernelGGL(gather_hist_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->stream, base, C,
+                           (uint32_t)D, slot0 + s0, ns, c0, nc, h->d_gather);
+        HIPCHK(h, hipGetLastError());
+        HIPCHK(h, hipMemcpyAsync(host_out + s0 * per_slot, h->d_gather, n * sizeof(double), hipMemcpyDeviceToHost,
+                                 h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    return EMCMC_OK;
+}
+
 emcmc_status emcmc_get_history(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
                                void *host_out, size_t host_bytes) {
     if (!h || !host_out) return EMCMC_INVALID_ARG;
@@ -669,6 +711,11 @@ emcmc_status emcmc_get_history(emcmc_handle *h, uint32_t which, uint64_t iter_fi
     if (st) return st;
     if (host_bytes < row * num_iters) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (which == EMCMC_H_STATE || which == EMCMC_H_PROPOSAL) {
+        const uint64_t P = h->updates.size();
+        return copy_state_slots(h, (const double *)base, (iter_first - 1) * P, num_iters * P, 0,
+                                h->cfg.num_chains, (double *)host_out);
+    }
     HIPCHK(h, hipMemcpy(host_out, (const uint8_t *)base + (iter_first - 1) * row, row * num_iters,
                         hipMemcpyDeviceToHost));
     return EMCMC_OK;
@@ -688,10 +735,13 @@ emcmc_status emcmc_get_history_chains(emcmc_handle *h, uint32_t which, uint64_t 
     emcmc_status st = hist_geometry(h, which, &base, &row);
     if (st) return st;
     const size_t per_chain = (which == EMCMC_H_LL) ? sizeof(double) : h->cfg.dim * sizeof(double);
-    const size_t width = num_chains * per_chain, spitch = C * per_chain;
     const size_t height = num_iters * P;
-    if (host_bytes < width * height) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
+    if (host_bytes < num_chains * per_chain * height) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (which != EMCMC_H_LL)
+        return copy_state_slots(h, (const double *)base, (iter_first - 1) * P, height, chain_first, num_chains,
+                                (double *)host_out);
+    const size_t width = num_chains * per_chain, spitch = C * per_chain;
     const uint8_t *src = (const uint8_t *)base + (iter_first - 1) * row + chain_first * per_chain;
     HIPCHK(h, hipMemcpy2D(host_out, width, src, spitch, width, height, hipMemcpyDeviceToHost));
     return EMCMC_OK;

@@ -2,7 +2,10 @@
 //
 // One launch runs `nsteps` consecutive schedule steps of ONE update for all
 // chains; θ, ll and the rolling-acceptance state stay in VGPRs across those
-// steps and only the per-step history streams leave the CU.  Each chain is
+// steps and only the per-step history streams leave the CU.  The step loop
+// issues no vector-memory loads: on gfx950 loads and stores share vmcnt, so a
+// load inside the loop would make every step wait for the previous step's
+// history stores to drain.  Each chain is
 // owned by LPC ∈ {1,2,4} adjacent lanes of a wave (a "quad" for LPC=4), each
 // lane holding D/LPC coordinates; per-chain sums combine across those lanes
 // with DPP quad permutes.
@@ -47,7 +50,6 @@ struct StepParams {
     // device constants (see DeviceConsts layout in emcmc.hip)
     const double *consts;
     const double *obs;    // [nobs][D]
-    const uint32_t *iters;  // [nsteps] mcmciter per step, or nullptr → iter0 + s
     uint64_t C;
     uint64_t row_bytes;   // bytes per accept-bit row (= Cw*8)
     uint32_t chain0;      // global id of local chain 0
@@ -73,6 +75,16 @@ struct StepParams {
 //                  | [D²+D, 2D²+D) L_t | [2D²+D, 2D²+2D) 1/diag(L_t) | [2D²+2D, 2D²+3D) x̄
 constexpr int LL_PER_OBS = 0;
 constexpr int LL_SUFFSTAT = 1;
+
+// HBM layout of θ state and θ/θ° histories (per history slot): pair-interleaved
+// SoA, element (d, c) at ((d/2)·C + c)·2 + d%2 when D is even, so lane c stores
+// the Box–Muller pair (2j, 2j+1) as one 16-byte word and a wave's store covers
+// contiguous 1 KiB (LPC = 1) or 4 × 256 B (LPC = 4).  Odd D: plain SoA d·C + c.
+__host__ __device__ __forceinline__ uint64_t state_pos(uint64_t d, uint64_t c, uint64_t C, uint32_t D) {
+    return (D % 2 == 0) ? (((d >> 1) * C + c) << 1) + (d & 1) : d * C + c;
+}
+
+typedef double d2v __attribute__((ext_vector_type(2)));
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers (DPP quad permutes; 64-bit values move as two dwords)
@@ -113,16 +125,19 @@ __device__ __forceinline__ double tree_inplace(double (&b)[N]) {
     return b[0];
 }
 
+// Σ y_i² over the chain's D coordinates in the canonical order: blocks of BLK
+// accumulated s = y0·y0, s = fma(y_i, y_i, s); blocks combine pairwise, first
+// inside the lane, then across the chain's LPC lanes.
 template <int D, int LPC, int NV>
-__device__ __forceinline__ double canon_sum(const double (&v)[NV]) {
+__device__ __forceinline__ double canon_sumsq(const double (&y)[NV]) {
     constexpr int BLK = SumShape<D>::BLK;
     constexpr int BPL = NV / BLK;
     double b[BPL];
 #pragma unroll
     for (int k = 0; k < BPL; ++k) {
-        double s = v[k * BLK];
+        double s = y[k * BLK] * y[k * BLK];
 #pragma unroll
-        for (int i = 1; i < BLK; ++i) s = s + v[k * BLK + i];
+        for (int i = 1; i < BLK; ++i) s = fma(y[k * BLK + i], y[k * BLK + i], s);
         b[k] = s;
     }
     double s = tree_inplace<BPL>(b);
@@ -183,8 +198,50 @@ __device__ __forceinline__ double rolling_update(double ra, uint64_t &r0, uint64
 // Diagonal Gaussian RW proposal + diagonal Gaussian target (cfg 2 fast path).
 // GaussianRandomWalk(Σ_rw) with Σ_rw diagonal, GsnTargetLaw(μ, Σ_t) with Σ_t
 // diagonal, coords = 1:D, ImproperPrior, P = 1 schedule slot per step.
-template <int D, int LPC, bool FULL, int LLMODE>
-__global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
+// UNIT_T: Σ_t = I, so L_t⁻¹ = I and the solve y = (x − μ)·1 is skipped (the
+// product by 1.0 is exact: same bits).
+// Store / load the lane's N coordinates [d0, d0+N) of chain c in state_pos
+// layout; base points at the slot start.  Even D: 16-byte words.
+template <int D, int N>
+__device__ __forceinline__ void store_state(double *base, uint64_t C, uint64_t c, int d0, const double (&v)[N],
+                                            bool nt) {
+    if constexpr (D % 2 == 0) {
+        static_assert(N % 2 == 0, "pairs");
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            d2v x = {v[2 * j], v[2 * j + 1]};
+            d2v *p = reinterpret_cast<d2v *>(base) + ((uint64_t)(d0 / 2 + j) * C + c);
+            if (nt) __builtin_nontemporal_store(x, p);
+            else *p = x;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            double *p = base + (uint64_t)(d0 + i) * C + c;
+            if (nt) __builtin_nontemporal_store(v[i], p);
+            else *p = v[i];
+        }
+    }
+}
+template <int D, int N>
+__device__ __forceinline__ void load_state(const double *base, uint64_t C, uint64_t c, int d0, double (&v)[N]) {
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            const d2v x = reinterpret_cast<const d2v *>(base)[(uint64_t)(d0 / 2 + j) * C + c];
+            v[2 * j] = x.x;
+            v[2 * j + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = base[(uint64_t)(d0 + i) * C + c];
+    }
+}
+
+// MINW = minimum waves per SIMD the register allocation must allow
+// (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
+template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1>
+__global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParams a) {
     static_assert(D % LPC == 0, "D must split evenly over the chain's lanes");
     constexpr int DPL = D / LPC;  // coordinates per lane
     static_assert(LPC == 1 || DPL % 8 == 0, "multi-lane chains need whole 8-blocks");
@@ -211,12 +268,9 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
     const int d0 = sub * DPL;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
 
+    const uint64_t C = a.C;
     double th[DPL];
-    {
-        const double *src = a.theta + chain * D + d0;
-#pragma unroll
-        for (int i = 0; i < DPL; ++i) th[i] = src[i];
-    }
+    load_state<D>(a.theta, C, chain, d0, th);
     double ll = a.ll[chain];
     double ra = a.ra[chain];
     uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
@@ -224,7 +278,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
     uint32_t faults = a.faults[chain];
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
-        const uint32_t iter = a.iters ? a.iters[s] : a.iter0 + s;
+        const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
         // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151)
         double thp[DPL];
@@ -240,13 +294,10 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
         double ltd;
         {
-            double v[DPL];
+            double y[DPL];
 #pragma unroll
-            for (int i = 0; i < DPL; ++i) {
-                const double y = (thp[i] - th[i]) * iLrw[d0 + i];
-                v[i] = y * y;
-            }
-            ltd = a.rw_c0 - canon_sum<D, LPC>(v) / 2.0;
+            for (int i = 0; i < DPL; ++i) y[i] = (thp[i] - th[i]) * iLrw[d0 + i];
+            ltd = a.rw_c0 - canon_sumsq<D, LPC>(y) / 2.0;
         }
         // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
         double llp;
@@ -254,22 +305,22 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
             llp = 0.0;
             for (uint32_t k = 0; k < nobs; ++k) {
                 const double *xk = X + (size_t)k * D + d0;
-                double v[DPL];
+                double y[DPL];
 #pragma unroll
                 for (int i = 0; i < DPL; ++i) {
-                    const double y = (xk[i] - thp[i]) * iLt[d0 + i];
-                    v[i] = y * y;
+                    y[i] = xk[i] - thp[i];
+                    if constexpr (!UNIT_T) y[i] = y[i] * iLt[d0 + i];
                 }
-                llp = llp + (a.t_c0 - canon_sum<D, LPC>(v) / 2.0);
+                llp = llp + (a.t_c0 - canon_sumsq<D, LPC>(y) / 2.0);
             }
         } else {
-            double v[DPL];
+            double y[DPL];
 #pragma unroll
             for (int i = 0; i < DPL; ++i) {
-                const double y = (xbar[d0 + i] - thp[i]) * iLt[d0 + i];
-                v[i] = y * y;
+                y[i] = xbar[d0 + i] - thp[i];
+                if constexpr (!UNIT_T) y[i] = y[i] * iLt[d0 + i];
             }
-            const double qv = canon_sum<D, LPC>(v);
+            const double qv = canon_sumsq<D, LPC>(y);
             llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
         }
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
@@ -278,20 +329,14 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
         const double E = exp1(draw(a.key0, a.key1, gid, iter, kBlockAccept, a.pidx0, 0));
         const bool acc = E > -llr;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
-        if constexpr (FULL) {
-            double *dst = a.hist_prop + (slot * a.C + chain) * D + d0;
-#pragma unroll
-            for (int i = 0; i < DPL; ++i) __builtin_nontemporal_store(thp[i], dst + i);
-        }
+        if constexpr (FULL) store_state<D>(a.hist_prop + slot * D * C, C, chain, d0, thp, true);
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)
 #pragma unroll
         for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {
-            double *dst = a.hist_theta + (slot * a.C + chain) * D + d0;
-#pragma unroll
-            for (int i = 0; i < DPL; ++i) __builtin_nontemporal_store(th[i], dst + i);
+            store_state<D>(a.hist_theta + slot * D * C, C, chain, d0, th, true);
             if (sub == 0) __builtin_nontemporal_store(ll, a.hist_ll + slot * a.C + chain);
         }
         {
@@ -311,11 +356,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_kernel(const StepParams a) {
         a.nacc[chain] = nacc;
         a.faults[chain] = faults;
     }
-    {
-        double *dst = a.theta + chain * D + d0;
-#pragma unroll
-        for (int i = 0; i < DPL; ++i) dst[i] = th[i];
-    }
+    store_state<D>(a.theta, C, chain, d0, th, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -343,9 +384,9 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     if (chain >= a.C) return;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
 
+    const uint64_t C = a.C;
     double th[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) th[i] = a.theta[chain * D + i];
+    load_state<D>(a.theta, C, chain, 0, th);
     double ll = a.ll[chain];
     double ra = a.ra[chain];
     uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
@@ -353,7 +394,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     uint32_t faults = a.faults[chain];
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
-        const uint32_t iter = a.iters ? a.iters[s] : a.iter0 + s;
+        const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
         double z[2 * PP];
 #pragma unroll
@@ -371,64 +412,55 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
         }
         double ltd;
         {
-            double y[D], v[D];
+            double y[D];
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 double acc = thp[i] - th[i];
 #pragma unroll
                 for (int j = 0; j < i; ++j) acc = fma(-Lrw[i * D + j], y[j], acc);
                 y[i] = acc * iLrw[i];
-                v[i] = y[i] * y[i];
             }
-            ltd = a.rw_c0 - canon_sum<D, 1>(v) / 2.0;
+            ltd = a.rw_c0 - canon_sumsq<D, 1>(y) / 2.0;
         }
         double llp;
         if constexpr (LLMODE == LL_PER_OBS) {
             llp = 0.0;
             for (uint32_t k = 0; k < nobs; ++k) {
                 const double *xk = X + (size_t)k * D;
-                double y[D], v[D];
+                double y[D];
 #pragma unroll
                 for (int i = 0; i < D; ++i) {
                     double acc = xk[i] - thp[i];
 #pragma unroll
                     for (int j = 0; j < i; ++j) acc = fma(-Lt[i * D + j], y[j], acc);
                     y[i] = acc * iLt[i];
-                    v[i] = y[i] * y[i];
                 }
-                llp = llp + (a.t_c0 - canon_sum<D, 1>(v) / 2.0);
+                llp = llp + (a.t_c0 - canon_sumsq<D, 1>(y) / 2.0);
             }
         } else {
-            double y[D], v[D];
+            double y[D];
 #pragma unroll
             for (int i = 0; i < D; ++i) {
                 double acc = xbar[i] - thp[i];
 #pragma unroll
                 for (int j = 0; j < i; ++j) acc = fma(-Lt[i * D + j], y[j], acc);
                 y[i] = acc * iLt[i];
-                v[i] = y[i] * y[i];
             }
-            const double qv = canon_sum<D, 1>(v);
+            const double qv = canon_sumsq<D, 1>(y);
             llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
         }
         if (!(llp - llp == 0.0)) faults |= 1u;
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
         const double E = exp1(draw(a.key0, a.key1, gid, iter, kBlockAccept, a.pidx0, 0));
         const bool acc = E > -llr;
-        if constexpr (FULL) {
-            double *dst = a.hist_prop + (slot * a.C + chain) * D;
-#pragma unroll
-            for (int i = 0; i < D; ++i) __builtin_nontemporal_store(thp[i], dst + i);
-        }
+        if constexpr (FULL) store_state<D>(a.hist_prop + slot * D * C, C, chain, 0, thp, true);
 #pragma unroll
         for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {
-            double *dst = a.hist_theta + (slot * a.C + chain) * D;
-#pragma unroll
-            for (int i = 0; i < D; ++i) __builtin_nontemporal_store(th[i], dst + i);
-            __builtin_nontemporal_store(ll, a.hist_ll + slot * a.C + chain);
+            store_state<D>(a.hist_theta + slot * D * C, C, chain, 0, th, true);
+            __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
         }
         {
             const uint64_t m = __ballot(acc);
@@ -442,8 +474,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     a.ring[2 * chain + 1] = r1;
     a.nacc[chain] = nacc;
     a.faults[chain] = faults;
-#pragma unroll
-    for (int i = 0; i < D; ++i) a.theta[chain * D + i] = th[i];
+    store_state<D>(a.theta, C, chain, 0, th, false);
 }
 
 // ---------------------------------------------------------------------------
@@ -453,7 +484,8 @@ __global__ void __launch_bounds__(256)
 chain_moments_kernel(const double *__restrict__ hist, uint64_t C, uint32_t D, uint64_t slot0,
                      uint32_t slot_stride, uint32_t n, uint32_t halves, double *__restrict__ mean_out,
                      double *__restrict__ var_out) {
-    // one thread per (chain, dim, half)
+    // one thread per (half, element position within a slot): consecutive
+    // threads read consecutive addresses; the reduce step maps (d, c) → position
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t total = C * D * halves;
     if (t >= total) return;
@@ -484,7 +516,7 @@ moments_reduce_kernel(const double *__restrict__ mean_in, const double *__restri
     const uint64_t rows = C * halves;
     for (uint64_t r = threadIdx.x; r < rows; r += blockDim.x) {
         const uint64_t h = r / C, ch = r % C;
-        const uint64_t idx = h * C * D + ch * D + d;
+        const uint64_t idx = h * C * D + state_pos(d, ch, C, D);
         const double m = mean_in[idx];
         a = a + m;
         b = b + m * m;
@@ -517,6 +549,17 @@ popcount_kernel(const uint64_t *__restrict__ bits, uint64_t words, unsigned long
          i += (uint64_t)gridDim.x * blockDim.x)
         acc += (uint64_t)__popcll(bits[i]);
     if (acc) atomicAdd(out, (unsigned long long)acc);
+}
+
+// device state_pos layout → [slot][nc][D] (host layout) for chains [c0, c0+nc)
+__global__ void __launch_bounds__(256)
+gather_hist_kernel(const double *__restrict__ src, uint64_t C, uint32_t D, uint64_t slot0, uint64_t nslots,
+                   uint64_t c0, uint64_t nc, double *__restrict__ dst) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nslots * nc * D) return;
+    const uint64_t s = t / (nc * D), r = t % (nc * D);
+    const uint64_t c = r / D, d = r % D;
+    dst[t] = src[(slot0 + s) * D * C + state_pos(d, c0 + c, C, D)];
 }
 
 // self-test probes

@@ -39,26 +39,19 @@ struct u32x4 {
     uint32_t x, y, z, w;
 };
 
-EMCMC_HD uint32_t mulhi32(uint32_t a, uint32_t b) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    return __umulhi(a, b);
-#else
-    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
-#endif
-}
-
 EMCMC_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
-        const uint32_t hi0 = mulhi32(M0, c.x), lo0 = M0 * c.x;
-        const uint32_t hi1 = mulhi32(M1, c.z), lo1 = M1 * c.z;
+        // full 32×32→64 products: one v_mad_u64_u32 each on gfx950
+        const uint64_t p0 = (uint64_t)M0 * (uint64_t)c.x;
+        const uint64_t p1 = (uint64_t)M1 * (uint64_t)c.z;
         u32x4 n;
-        n.x = hi1 ^ c.y ^ k0;
-        n.y = lo1;
-        n.z = hi0 ^ c.w ^ k1;
-        n.w = lo0;
+        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.y = (uint32_t)p1;
+        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.w = (uint32_t)p0;
         c = n;
         k0 += W0;
         k1 += W1;
@@ -94,9 +87,9 @@ EMCMC_HD double u01_closed0(uint32_t hi, uint32_t lo) {
     return (double)bits53(hi, lo) * 0x1p-53;
 }
 
-// ---- natural log (restates the fdlibm e_log.c reduction, single branch) -----
+// ---- natural log (fdlibm e_log.c reduction; Lg1..Lg7 polynomial by fma Horner)
 // Valid for finite normal x > 0, which covers u ∈ [2^-53, 1] and every
-// positive normal argument used on the hot path.
+// positive normal argument used on the hot path.  ≤ 1 ulp (tests/).
 EMCMC_HD double log_pos(double x) {
     const double ln2_hi = 6.93147180369123816490e-01;
     const double ln2_lo = 1.90821492927058770002e-10;
@@ -118,34 +111,41 @@ EMCMC_HD double log_pos(double x) {
     const double dk = (double)k;
     const double z = s * s;
     const double w = z * z;
-    const double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    const double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    const double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+    const double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
     const double R = t2 + t1;
     const double hfsq = 0.5 * f * f;
-    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    return dk * ln2_hi - ((hfsq - fma(s, hfsq + R, dk * ln2_lo)) - f);
 }
 
-// ---- sin/cos kernels on [0, π/4] (FreeBSD msun k_sin.c / k_cos.c, y = 0) ----
+// ---- sin/cos kernels on [0, π/4] (FreeBSD msun k_sin.c / k_cos.c
+// coefficients, y = 0, fma Horner) ---------------------------------------------
 EMCMC_HD double ksin(double x) {
     const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
                  S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
                  S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
     const double z = x * x;
-    const double w = z * z;
-    const double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
-    const double v = z * x;
-    return x + v * (S1 + z * r);
+    double p = fma(z, S6, S5);
+    p = fma(z, p, S4);
+    p = fma(z, p, S3);
+    p = fma(z, p, S2);
+    p = fma(z, p, S1);
+    return fma(z * x, p, x);
 }
 EMCMC_HD double kcos(double x) {
     const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
                  C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
                  C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
     const double z = x * x;
-    double w = z * z;
-    const double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    double p = fma(z, C6, C5);
+    p = fma(z, p, C4);
+    p = fma(z, p, C3);
+    p = fma(z, p, C2);
+    p = fma(z, p, C1);
+    const double r = z * p;
     const double hz = 0.5 * z;
-    w = 1.0 - hz;
-    return w + (((1.0 - w) - hz) + (z * r));
+    const double w = 1.0 - hz;
+    return w + fma(z, r, (1.0 - w) - hz);
 }
 
 // ---- Box–Muller pair from one Philox block ----------------------------------
@@ -158,17 +158,19 @@ EMCMC_HD void box_muller(u32x4 r, double &z0, double &z1) {
     const uint64_t b = bits53(r.z, r.w);
     const uint32_t q = (uint32_t)(b >> 51);
     const uint64_t rem = b & ((1ull << 51) - 1ull);
-    const bool sw = rem >= (1ull << 50);
-    const uint64_t rr = sw ? ((1ull << 51) - rem) : rem;
+    const bool fold = rem >= (1ull << 50);
+    const uint64_t rr = fold ? ((1ull << 51) - rem) : rem;
     const double x = (double)rr * 0x1.921fb54442d18p-51;  // rr · (π/2)·2^-51 ∈ [0, π/4]
     const double s = ksin(x), c = kcos(x);
-    const double sp = sw ? c : s;  // sin φ
-    const double cp = sw ? s : c;  // cos φ
-    // rotate by q·π/2
-    const double cq = (q == 0) ? cp : (q == 1) ? -sp : (q == 2) ? -cp : sp;
-    const double sq = (q == 0) ? sp : (q == 1) ? cp : (q == 2) ? -sp : -cp;
-    z0 = rad * cq;
-    z1 = rad * sq;
+    // angle = q·π/2 + φ, φ = fold ? π/2 − x : x.  Branch-free: pick magnitudes,
+    // then flip sign bits (exact negation).
+    const bool t = ((q & 1u) != 0) != fold;
+    const double mc = t ? s : c;
+    const double ms = t ? c : s;
+    const uint64_t negc = (uint64_t)(((q >> 1) ^ q) & 1u) << 63;
+    const uint64_t negs = (uint64_t)((q >> 1) & 1u) << 63;
+    z0 = rad * u2d(d2u(mc) ^ negc);
+    z1 = rad * u2d(d2u(ms) ^ negs);
 }
 
 // Exponential(1) draw for accept_reject! (run.jl:278): E = −log(u), u ∈ (0,1].

@@ -45,6 +45,7 @@ LL_PER_OBS, LL_SUFFSTAT = 0, 1
 HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
 H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
 FAULT_NONFINITE_LL = 1
+VARIANT_HIGH_OCCUPANCY = 1
 
 
 class EmcmcConfig(C.Structure):
@@ -60,7 +61,8 @@ class EmcmcConfig(C.Structure):
         ("roll_window", C.c_uint32),
         ("lanes_per_chain", C.c_uint32),
         ("steps_per_launch", C.c_uint32),
-        ("reserved", C.c_uint32 * 7),
+        ("kernel_variant", C.c_uint32),
+        ("reserved", C.c_uint32 * 6),
     ]
 
 

@@ -25,6 +25,7 @@ class EngineConfig:
     roll_window: int = 100
     lanes_per_chain: int = 0
     steps_per_launch: int = 0
+    kernel_variant: int = 0
 
 
 class Engine:
@@ -43,6 +44,7 @@ class Engine:
         c.roll_window = cfg.roll_window
         c.lanes_per_chain = cfg.lanes_per_chain
         c.steps_per_launch = cfg.steps_per_launch
+        c.kernel_variant = cfg.kernel_variant
         h = C.c_void_p()
         st = self._lib.emcmc_create(C.byref(h), C.byref(c))
         if st != L.OK:

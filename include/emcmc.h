@@ -79,7 +79,11 @@ typedef enum emcmc_status {
 #define EMCMC_HIST_FULL 0u         /* state, proposal, ll and accept histories */
 #define EMCMC_HIST_ACCEPT_ONLY 1u  /* accept bits only (no per-step state streams) */
 
-/* History selectors for emcmc_get_history / emcmc_history_device_ptr */
+/* History selectors for emcmc_get_history / emcmc_history_device_ptr.
+ * Host copies (emcmc_get_history*) use the layouts below.  In HBM the STATE and
+ * PROPOSAL histories are pair-interleaved SoA per slot: element (d, c) of slot
+ * s at s·D·C + ((d/2)·C + c)·2 + d%2 for even D (s·D·C + d·C + c for odd D),
+ * which is what emcmc_history_device_ptr exposes. */
 #define EMCMC_H_STATE 0u     /* state_history[iter][pidx]          : double [M][P][C][D] */
 #define EMCMC_H_PROPOSAL 1u  /* state_proposal_history[iter][pidx] : double [M][P][C][D] */
 #define EMCMC_H_LL 2u        /* local_wss[pidx].sub_ws.ll_history  : double [M][P][C]    */
@@ -104,8 +108,12 @@ typedef struct emcmc_config {
     uint32_t roll_window;      /* GenericChainStats roll_window (chain_statistics.jl:27); 0 → 100; ≤ 128 */
     uint32_t lanes_per_chain;  /* 0 = auto; else 1, 2 or 4 (must divide the work layout) */
     uint32_t steps_per_launch; /* 0 = auto (64) */
-    uint32_t reserved[7];
+    uint32_t kernel_variant;   /* 0 = auto; EMCMC_VARIANT_* tuning flags (results are identical) */
+    uint32_t reserved[6];
 } emcmc_config;
+
+/* kernel_variant flags: performance-only choices, bit-identical results */
+#define EMCMC_VARIANT_HIGH_OCCUPANCY 1u  /* cap registers for 4 waves/SIMD where instantiated */
 
 /* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183). */
 typedef struct emcmc_update_desc {

@@ -92,17 +92,38 @@ ORC_EXPORT double orc_canon_sum(const double *v, int D) {
     return part[0];
 }
 
-/* ‖L⁻¹ r‖² by forward substitution (PDMats sqmahal via chol.L \ r). */
+/* Σ y_i² in the canonical order: same blocks and tree as orc_canon_sum, each
+ * block accumulated as s = y0·y0, s = fma(y_i, y_i, s). */
+ORC_EXPORT double orc_canon_sumsq(const double *y, int D) {
+    int blk = (D % 8 == 0 && D >= 16) ? 8 : D;
+    int nb = D / blk;
+    double part[64];
+    for (int b = 0; b < nb; ++b) {
+        const double *yb = y + b * blk;
+        double s = yb[0] * yb[0];
+        for (int i = 1; i < blk; ++i) s = fma(yb[i], yb[i], s);
+        part[b] = s;
+    }
+    int n = nb;
+    while (n > 1) {
+        for (int i = 0; i < n / 2; ++i) part[i] = part[2 * i] + part[2 * i + 1];
+        if (n & 1) part[n / 2] = part[n - 1];
+        n = (n + 1) / 2;
+    }
+    return part[0];
+}
+
+/* ‖L⁻¹ r‖² by forward substitution (PDMats sqmahal via chol.L \ r).  A unit
+ * diagonal (Σ = I ⇒ L = I) makes y = r exactly, with or without the multiply. */
 static double sqmahal(const double *L, const double *invdiag, const double *r, int D, int diag) {
-    double y[64], sq[64];
+    double y[64];
     for (int i = 0; i < D; ++i) {
         double acc = r[i];
         if (!diag)
             for (int j = 0; j < i; ++j) acc = fma(-L[(size_t)i * D + j], y[j], acc);
         y[i] = acc * invdiag[i];
-        sq[i] = y[i] * y[i];
     }
-    return orc_canon_sum(sq, D);
+    return orc_canon_sumsq(y, D);
 }
 
 static double logdet_chol(const double *L, int D) {
@@ -343,22 +364,5 @@ ORC_EXPORT void orc_log_vec(const double *x, double *y, uint64_t n) {
 }
 
 ORC_EXPORT void orc_sincos_turn_vec(const uint64_t *turn53, double *c, double *s, uint64_t n) {
-    for (uint64_t i = 0; i < n; ++i) {
-        uint32_t hi = (uint32_t)(turn53[i] >> 21);
-        uint32_t lo = (uint32_t)((turn53[i] & ((1u << 21) - 1u)) << 11);
-        uint64_t turn = orc_bits53(hi, lo);
-        uint32_t quadrant = (uint32_t)(turn >> 51);
-        uint64_t rem = turn & ((1ull << 51) - 1u);
-        int folded = rem >= (1ull << 50);
-        uint64_t rr = folded ? ((1ull << 51) - rem) : rem;
-        double x = (double)rr * 0x1.921fb54442d18p-51;
-        double sk = orc_sin_k(x), ck = orc_cos_k(x);
-        double sp = folded ? ck : sk, cp = folded ? sk : ck;
-        switch (quadrant) {
-        case 0: c[i] = cp; s[i] = sp; break;
-        case 1: c[i] = -sp; s[i] = cp; break;
-        case 2: c[i] = -cp; s[i] = -sp; break;
-        default: c[i] = sp; s[i] = -cp; break;
-        }
-    }
+    for (uint64_t i = 0; i < n; ++i) orc_sincos_turn(turn53[i], &c[i], &s[i]);
 }

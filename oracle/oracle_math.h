@@ -85,7 +85,8 @@ static inline double orc_u01_closed0(uint32_t hi, uint32_t lo) {
     return (double)orc_bits53(hi, lo) * 0x1p-53;
 }
 
-/* log for finite normal x > 0 (fdlibm e_log.c, main-branch formula). */
+/* log for finite normal x > 0: fdlibm e_log.c reduction, main-branch formula,
+ * Lg polynomial in fma Horner form. */
 static inline double orc_log(double x) {
     static const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10,
                         Lg1 = 6.666666666666735130e-01, Lg2 = 3.999999999940941908e-01,
@@ -105,39 +106,41 @@ static inline double orc_log(double x) {
     double dk = (double)k;
     double z = s * s;
     double w = z * z;
-    double t1 = w * (Lg2 + w * (Lg4 + w * Lg6));
-    double t2 = z * (Lg1 + w * (Lg3 + w * (Lg5 + w * Lg7)));
+    double t1 = w * fma(w, fma(w, Lg6, Lg4), Lg2);
+    double t2 = z * fma(w, fma(w, fma(w, Lg7, Lg5), Lg3), Lg1);
     double R = t2 + t1;
     double hfsq = 0.5 * f * f;
-    return dk * ln2_hi - ((hfsq - (s * (hfsq + R) + dk * ln2_lo)) - f);
+    return dk * ln2_hi - ((hfsq - fma(s, hfsq + R, dk * ln2_lo)) - f);
 }
 
+/* sin on [0, π/4]: x + x³·P(x²), FreeBSD k_sin.c coefficients S1..S6. */
 static inline double orc_sin_k(double x) {
-    static const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                        S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                        S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    double z = x * x, w = z * z;
-    double r = S2 + z * (S3 + z * S4) + z * w * (S5 + z * S6);
-    double v = z * x;
-    return x + v * (S1 + z * r);
+    static const double S[6] = {-1.66666666666666324348e-01, 8.33333333332248946124e-03,
+                                -1.98412698298579493134e-04, 2.75573137070700676789e-06,
+                                -2.50507602534068634195e-08, 1.58969099521155010221e-10};
+    double z = x * x;
+    double p = fma(z, S[5], S[4]);
+    for (int j = 3; j >= 0; --j) p = fma(z, p, S[j]);
+    return fma(z * x, p, x);
 }
 
+/* cos on [0, π/4]: 1 − z/2 + z²·P(z), FreeBSD k_cos.c coefficients C1..C6,
+ * with the compensated 1 − z/2 step. */
 static inline double orc_cos_k(double x) {
-    static const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                        C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                        C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    double z = x * x, w = z * z;
-    double r = z * (C1 + z * (C2 + z * C3)) + w * w * (C4 + z * (C5 + z * C6));
+    static const double Cc[6] = {4.16666666666666019037e-02, -1.38888888888741095749e-03,
+                                 2.48015872894767294178e-05, -2.75573143513906633035e-07,
+                                 2.08757232129817482790e-09, -1.13596475577881948265e-11};
+    double z = x * x;
+    double p = fma(z, Cc[5], Cc[4]);
+    for (int j = 3; j >= 0; --j) p = fma(z, p, Cc[j]);
+    double r = z * p;
     double hz = 0.5 * z;
     double one_minus = 1.0 - hz;
-    return one_minus + (((1.0 - one_minus) - hz) + (z * r));
+    return one_minus + fma(z, r, (1.0 - one_minus) - hz);
 }
 
-/* Two independent N(0,1) variates from one Philox block. */
-static inline void orc_box_muller(orc_u32x4 r, double *z0, double *z1) {
-    double u = orc_u01_open0(r.v[0], r.v[1]);
-    double radius = sqrt(-2.0 * orc_log(u));
-    uint64_t turn = orc_bits53(r.v[2], r.v[3]);
+/* cos and sin of a 53-bit turn fraction (angle = 2π·turn/2^53). */
+static inline void orc_sincos_turn(uint64_t turn, double *cz, double *sz) {
     uint32_t quadrant = (uint32_t)(turn >> 51);
     uint64_t rem = turn & ((1ull << 51) - 1u);
     int folded = rem >= (1ull << 50);
@@ -146,13 +149,20 @@ static inline void orc_box_muller(orc_u32x4 r, double *z0, double *z1) {
     double s = orc_sin_k(x), c = orc_cos_k(x);
     double sin_phi = folded ? c : s;
     double cos_phi = folded ? s : c;
-    double cz, sz;
     switch (quadrant) {
-    case 0: cz = cos_phi; sz = sin_phi; break;
-    case 1: cz = -sin_phi; sz = cos_phi; break;
-    case 2: cz = -cos_phi; sz = -sin_phi; break;
-    default: cz = sin_phi; sz = -cos_phi; break;
+    case 0: *cz = cos_phi; *sz = sin_phi; break;
+    case 1: *cz = -sin_phi; *sz = cos_phi; break;
+    case 2: *cz = -cos_phi; *sz = -sin_phi; break;
+    default: *cz = sin_phi; *sz = -cos_phi; break;
     }
+}
+
+/* Two independent N(0,1) variates from one Philox block. */
+static inline void orc_box_muller(orc_u32x4 r, double *z0, double *z1) {
+    double u = orc_u01_open0(r.v[0], r.v[1]);
+    double radius = sqrt(-2.0 * orc_log(u));
+    double cz, sz;
+    orc_sincos_turn(orc_bits53(r.v[2], r.v[3]), &cz, &sz);
     *z0 = radius * cz;
     *z1 = radius * sz;
 }

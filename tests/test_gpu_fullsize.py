@@ -50,17 +50,23 @@ def test_acceptance_and_first_step(full_run):
     assert (e["faults"] == 0).all()
 
 
-def test_posterior_matches_analytic(full_run):
-    """ImproperPrior on μ of GsnTargetLaw(μ, I): posterior N(x̄, I/n) exactly."""
-    w, e = full_run
+def test_posterior_matches_analytic(require_gpu):
+    """ImproperPrior on μ of GsnTargetLaw(μ, I): posterior N(x̄, I/n) exactly.
+    From θinit = 0 the chains need ~1,000 iterations of burn-in at D = 32
+    (autocorrelation time of optimally scaled RWM ≈ 3·D), so this uses 8,192
+    chains × 4,000 iterations and the second half for the moments."""
+    w = W.cfg2(8192)
+    e = run_engine(w, 8192, 4000, fetch=False)
     eng = e["engine"]
-    m = eng.moments_window(501, 500, split=True)
+    m = eng.moments_window(2001, 2000, split=True)
     r = rhat_from_sums(m)
     xbar = w.obs.mean(axis=0)
     assert np.abs(r["mean"] - xbar).max() < 0.01
     post_var = r["W"] + r["B"] / m["num_draws"]
     assert np.abs(post_var / (1.0 / w.nobs) - 1.0).max() < 0.05
-    assert np.abs(r["rhat"] - 1.0).max() < 0.01
+    # converged chains still give R̂ ≈ sqrt(1 + (τ−1)/n) with τ the integrated
+    # autocorrelation time (≈ 100 here) and n = 1,000 draws per half-chain
+    assert r["rhat"].max() < 1.1
     assert 0.20 < r["accept_rate"] < 0.30
 
 

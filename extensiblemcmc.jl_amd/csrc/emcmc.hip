@@ -130,6 +130,7 @@ struct emcmc_handle {
     double *d_hist_theta = nullptr, *d_hist_prop = nullptr, *d_hist_ll = nullptr;
     uint8_t *d_hist_acc = nullptr;
     double *d_consts = nullptr, *d_obs = nullptr;
+    Ziggurat *d_zig = nullptr;
     double *d_scratch = nullptr;  // diagnostics
     size_t scratch_bytes = 0;
     double *d_gather = nullptr;   // history layout conversion
@@ -240,6 +241,12 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
     HIPCHK(h, hipMalloc(&h->d_ring, 2 * C * sizeof(uint64_t)));
     HIPCHK(h, hipMalloc(&h->d_nacc, C * sizeof(uint32_t)));
     HIPCHK(h, hipMalloc(&h->d_faults, C * sizeof(uint32_t)));
+    {
+        Ziggurat zt;
+        build_ziggurat(zt);
+        HIPCHK(h, hipMalloc(&h->d_zig, sizeof(Ziggurat)));
+        HIPCHK(h, hipMemcpy(h->d_zig, &zt, sizeof(Ziggurat), hipMemcpyHostToDevice));
+    }
     h->row_bytes = ((C + 63) / 64) * 8;
     HIPCHK(h, hipMalloc(&h->d_hist_acc, M * P * h->row_bytes));
     HIPCHK(h, hipMemsetAsync(h->d_hist_acc, 0, M * P * h->row_bytes, h->stream));
@@ -314,7 +321,7 @@ emcmc_status select_variant(emcmc_handle *h) {
         std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     }
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    const size_t lds = (c.size() + obs_doubles) * sizeof(double);
+    const size_t lds = sizeof(Ziggurat) + (c.size() + obs_doubles) * sizeof(double);
     if (lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu",
@@ -519,6 +526,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
     if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
     if (!h->var.fn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
+    if (!h->d_zig) return fail(h, EMCMC_STATE_ERROR, "state not allocated");
     const uint32_t P = (uint32_t)h->updates.size();
     for (uint64_t i = 0; i < num_steps; ++i) {
         if (steps[i].pidx < 1 || steps[i].pidx > P) return fail(h, EMCMC_INVALID_ARG, "step %llu: pidx", (unsigned long long)i);
@@ -542,6 +550,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     p.hist_prop = h->d_hist_prop;
     p.hist_ll = h->d_hist_ll;
     p.hist_acc = h->d_hist_acc;
+    p.zig = h->d_zig;
     p.consts = h->d_consts;
     p.obs = h->d_obs;
     p.C = C;
@@ -612,7 +621,7 @@ void emcmc_destroy(emcmc_handle *h) {
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     void *bufs[] = {h->d_theta,     h->d_ll,        h->d_ra,      h->d_ring,     h->d_nacc,  h->d_faults,
                     h->d_hist_theta, h->d_hist_prop, h->d_hist_ll, h->d_hist_acc, h->d_consts, h->d_obs,
-                    h->d_scratch,   h->d_gather};
+                    h->d_scratch,   h->d_gather, h->d_zig};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -839,14 +848,19 @@ emcmc_status emcmc_probe_variates(int device, uint64_t seed, uint32_t pidx0, uin
     if (n == 0) return EMCMC_OK;
     uint32_t *dc = nullptr, *di = nullptr;
     double *dz = nullptr, *dE = nullptr;
+    Ziggurat *dzig = nullptr;
+    Ziggurat zt;
+    build_ziggurat(zt);
     emcmc_status st = EMCMC_OK;
-    if (hipMalloc(&dc, n * 4) || hipMalloc(&di, n * 4) || hipMalloc(&dz, n * dim * 8) || hipMalloc(&dE, n * 8)) {
+    if (hipMalloc(&dc, n * 4) || hipMalloc(&di, n * 4) || hipMalloc(&dz, n * dim * 8) || hipMalloc(&dE, n * 8) ||
+        hipMalloc(&dzig, sizeof(Ziggurat))) {
         st = EMCMC_OUT_OF_MEMORY;
     } else if (hipMemcpy(dc, chains, n * 4, hipMemcpyHostToDevice) ||
-               hipMemcpy(di, iters, n * 4, hipMemcpyHostToDevice)) {
+               hipMemcpy(di, iters, n * 4, hipMemcpyHostToDevice) ||
+               hipMemcpy(dzig, &zt, sizeof(Ziggurat), hipMemcpyHostToDevice)) {
         st = EMCMC_HIP_ERROR;
     } else {
-        hipLaunchKernelGGL(probe_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0,
+        hipLaunchKernelGGL(probe_variates_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, dzig,
                            (uint32_t)seed, (uint32_t)(seed >> 32), pidx0, dim, n, dc, di, dz, dE);
         if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess ||
             hipMemcpy(z, dz, n * dim * 8, hipMemcpyDeviceToHost) || hipMemcpy(E, dE, n * 8, hipMemcpyDeviceToHost))
@@ -856,6 +870,7 @@ emcmc_status emcmc_probe_variates(int device, uint64_t seed, uint32_t pidx0, uin
     (void)hipFree(di);
     (void)hipFree(dz);
     (void)hipFree(dE);
+    (void)hipFree(dzig);
     return st;
 }
 

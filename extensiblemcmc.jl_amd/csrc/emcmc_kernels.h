@@ -48,6 +48,7 @@ struct StepParams {
     double *hist_ll;     // [M*P][C]
     uint8_t *hist_acc;   // [M*P][Cw*8] bytes, bit c of row = chain c
     // device constants (see DeviceConsts layout in emcmc.hip)
+    const Ziggurat *zig;  // N(0,1) / Exp(1) ziggurat tables (host-built)
     const double *consts;
     const double *obs;    // [nobs][D]
     uint64_t C;
@@ -85,6 +86,102 @@ __host__ __device__ __forceinline__ uint64_t state_pos(uint64_t d, uint64_t c, u
 }
 
 typedef double d2v __attribute__((ext_vector_type(2)));
+
+// Stage the ziggurat tables (12 KiB, 16-byte aligned at LDS offset 0) and then
+// `nconst` constants and `nobs_d` observation doubles behind them.
+constexpr int kZigLdsDoubles = (int)(sizeof(Ziggurat) / sizeof(double));
+__device__ __forceinline__ void stage_lds(double *lds, const Ziggurat *zig, const double *consts, int nconst,
+                                          const double *obs, int nobs_d) {
+    const double *zsrc = reinterpret_cast<const double *>(zig);
+    const int total = kZigLdsDoubles + nconst + nobs_d;
+    for (int i = threadIdx.x; i < total; i += blockDim.x) {
+        double v;
+        if (i < kZigLdsDoubles) v = zsrc[i];
+        else if (i < kZigLdsDoubles + nconst) v = consts[i - kZigLdsDoubles];
+        else v = obs[i - kZigLdsDoubles - nconst];
+        lds[i] = v;
+    }
+    __syncthreads();
+}
+
+#ifndef EMCMC_SERIAL_PAIRS
+#define EMCMC_SERIAL_PAIRS 1
+#endif
+// 1: keep the scheduler from interleaving the Philox blocks of different
+// pairs (register pressure → occupancy; the waves of a SIMD supply the ILP)
+constexpr bool kSerialPairs = EMCMC_SERIAL_PAIRS != 0;
+
+// N normals of (chain, iter, pidx0) with lane-local index i ↔ global normal
+// index g0 + i, written as out[i] = base[i] + scale[i]·z (the diagonal
+// proposal θ° = θ + L z, random_walk.jl:147).  Fast pass over all pairs, then
+// a wave-uniform loop resolves the ≈1% wedge/tail draws one per lane per trip.
+template <int N>
+__device__ __forceinline__ void propose_diag(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+                                             uint32_t iter, uint32_t pidx0, uint32_t g0, const double (&base)[N],
+                                             const double *scale, double (&out)[N], uint32_t &faults) {
+    constexpr int NP = (N + 1) / 2;
+    uint64_t pend = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        if constexpr (kSerialPairs) __builtin_amdgcn_sched_barrier(0);
+        const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
+        double z0, z1;
+        const bool ok0 = zig_normal_fast(zig_split(r.x, r.y), zt.n, z0);
+        out[2 * j] = base[2 * j] + scale[2 * j] * z0;
+        if (!ok0) pend |= 1ull << (2 * j);
+        if (2 * j + 1 < N) {
+            const bool ok1 = zig_normal_fast(zig_split(r.z, r.w), zt.n, z1);
+            out[2 * j + 1] = base[2 * j + 1] + scale[2 * j + 1] * z1;
+            if (!ok1) pend |= 1ull << (2 * j + 1);
+        }
+    }
+    while (__ballot(pend != 0) != 0) {
+        if (pend != 0) {
+            const int i = __builtin_ctzll(pend);
+            pend &= pend - 1;
+            const double z = normal_draw(zt, key0, key1, chain, iter, pidx0, g0 + (uint32_t)i, faults);
+#pragma unroll
+            for (int q = 0; q < N; ++q)
+                if (q == i) out[q] = base[q] + scale[q] * z;
+        }
+    }
+}
+
+// The N standard normals themselves (dense-L proposals).
+template <int N>
+__device__ __forceinline__ void normals(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+                                        uint32_t iter, uint32_t pidx0, double (&z)[N], uint32_t &faults) {
+    constexpr int NP = (N + 1) / 2;
+    uint64_t pend = 0;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+        const u32x4 r = draw(key0, key1, chain, iter, j, pidx0, 0);
+        if (!zig_normal_fast(zig_split(r.x, r.y), zt.n, z[2 * j])) pend |= 1ull << (2 * j);
+        if (2 * j + 1 < N)
+            if (!zig_normal_fast(zig_split(r.z, r.w), zt.n, z[2 * j + 1])) pend |= 1ull << (2 * j + 1);
+    }
+    while (__ballot(pend != 0) != 0) {
+        if (pend != 0) {
+            const int i = __builtin_ctzll(pend);
+            pend &= pend - 1;
+            const double v = normal_draw(zt, key0, key1, chain, iter, pidx0, (uint32_t)i, faults);
+#pragma unroll
+            for (int q = 0; q < N; ++q)
+                if (q == i) z[q] = v;
+        }
+    }
+}
+
+// Exp(1) draw of the accept test (run.jl:278).
+__device__ __forceinline__ double accept_exp(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+                                             uint32_t iter, uint32_t pidx0, uint32_t &faults) {
+    const u32x4 r = draw(key0, key1, chain, iter, kBlockAccept, pidx0, 0);
+    const ZigDraw d = zig_split(r.x, r.y);
+    double e;
+    if (!zig_exp_fast(d, zt.e, e))
+        e = zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
+    return e;
+}
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers (DPP quad permutes; 64-bit values move as two dwords)
@@ -246,20 +343,18 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
     constexpr int DPL = D / LPC;  // coordinates per lane
     static_assert(LPC == 1 || DPL % 8 == 0, "multi-lane chains need whole 8-blocks");
     static_assert(LPC == 1 || DPL % 2 == 0, "normal pairs must not straddle lanes");
-    constexpr int PPL = (DPL + 1) / 2;
 
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 4 * D;
-    const int nload = (LLMODE == LL_PER_OBS) ? nconst + (int)nobs * D : nconst;
-    for (int i = threadIdx.x; i < nload; i += blockDim.x)
-        lds[i] = (i < nconst) ? a.consts[i] : a.obs[i - nconst];
-    __syncthreads();
-    const double *Lrw = lds;
-    const double *iLrw = lds + D;
-    const double *iLt = lds + 2 * D;
-    const double *xbar = lds + 3 * D;
-    const double *X = lds + 4 * D;
+    stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
+    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
+    const double *cst = lds + kZigLdsDoubles;
+    const double *Lrw = cst;
+    const double *iLrw = cst + D;
+    const double *iLt = cst + 2 * D;
+    const double *xbar = cst + 3 * D;
+    const double *X = cst + 4 * D;
 
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t chain = tid / LPC;
@@ -282,14 +377,7 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
         // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151)
         double thp[DPL];
-#pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-            const u32x4 r = draw(a.key0, a.key1, gid, iter, (uint32_t)(d0 / 2 + j), a.pidx0, 0);
-            double z0, z1;
-            box_muller(r, z0, z1);
-            thp[2 * j] = th[2 * j] + Lrw[d0 + 2 * j] * z0;
-            if (2 * j + 1 < DPL) thp[2 * j + 1] = th[2 * j + 1] + Lrw[d0 + 2 * j + 1] * z1;
-        }
+        propose_diag<DPL>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults);
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
         double ltd;
@@ -326,7 +414,7 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
         // ---- accept_reject! (run.jl:271-278), left-associative as written
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
-        const double E = exp1(draw(a.key0, a.key1, gid, iter, kBlockAccept, a.pidx0, 0));
+        const double E = accept_exp(zt, a.key0, a.key1, gid, iter, a.pidx0, faults);
         const bool acc = E > -llr;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
         if constexpr (FULL) store_state<D>(a.hist_prop + slot * D * C, C, chain, d0, thp, true);
@@ -365,20 +453,18 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
 // (cfg 1: GsnTargetLaw([1,2], [1 .5; .5 1])).  One lane per chain.
 template <int D, bool FULL, int LLMODE>
 __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) {
-    constexpr int PP = (D + 1) / 2;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 2 * D * D + 3 * D;
-    const int nload = (LLMODE == LL_PER_OBS) ? nconst + (int)nobs * D : nconst;
-    for (int i = threadIdx.x; i < nload; i += blockDim.x)
-        lds[i] = (i < nconst) ? a.consts[i] : a.obs[i - nconst];
-    __syncthreads();
-    const double *Lrw = lds;
-    const double *iLrw = lds + D * D;
-    const double *Lt = lds + D * D + D;
-    const double *iLt = lds + 2 * D * D + D;
-    const double *xbar = lds + 2 * D * D + 2 * D;
-    const double *X = lds + 2 * D * D + 3 * D;
+    stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
+    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
+    const double *cst = lds + kZigLdsDoubles;
+    const double *Lrw = cst;
+    const double *iLrw = cst + D * D;
+    const double *Lt = cst + D * D + D;
+    const double *iLt = cst + 2 * D * D + D;
+    const double *xbar = cst + 2 * D * D + 2 * D;
+    const double *X = cst + 2 * D * D + 3 * D;
 
     const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
@@ -396,12 +482,8 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
-        double z[2 * PP];
-#pragma unroll
-        for (int j = 0; j < PP; ++j) {
-            const u32x4 r = draw(a.key0, a.key1, gid, iter, (uint32_t)j, a.pidx0, 0);
-            box_muller(r, z[2 * j], z[2 * j + 1]);
-        }
+        double z[D];
+        normals<D>(zt, a.key0, a.key1, gid, iter, a.pidx0, z, faults);
         double thp[D];
 #pragma unroll
         for (int i = 0; i < D; ++i) {
@@ -451,7 +533,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
         }
         if (!(llp - llp == 0.0)) faults |= 1u;
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
-        const double E = exp1(draw(a.key0, a.key1, gid, iter, kBlockAccept, a.pidx0, 0));
+        const double E = accept_exp(zt, a.key0, a.key1, gid, iter, a.pidx0, faults);
         const bool acc = E > -llr;
         if constexpr (FULL) store_state<D>(a.hist_prop + slot * D * C, C, chain, 0, thp, true);
 #pragma unroll
@@ -564,18 +646,14 @@ gather_hist_kernel(const double *__restrict__ src, uint64_t C, uint32_t D, uint6
 
 // self-test probes
 __global__ void __launch_bounds__(256)
-probe_variates_kernel(uint32_t key0, uint32_t key1, uint32_t pidx0, uint32_t D, uint64_t n,
-                      const uint32_t *__restrict__ chains, const uint32_t *__restrict__ iters, double *__restrict__ z,
-                      double *__restrict__ E) {
+probe_variates_kernel(const Ziggurat *__restrict__ zig, uint32_t key0, uint32_t key1, uint32_t pidx0, uint32_t D,
+                      uint64_t n, const uint32_t *__restrict__ chains, const uint32_t *__restrict__ iters,
+                      double *__restrict__ z, double *__restrict__ E) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    for (uint32_t j = 0; j < (D + 1) / 2; ++j) {
-        double a, b;
-        box_muller(draw(key0, key1, chains[t], iters[t], j, pidx0, 0), a, b);
-        z[t * D + 2 * j] = a;
-        if (2 * j + 1 < D) z[t * D + 2 * j + 1] = b;
-    }
-    E[t] = exp1(draw(key0, key1, chains[t], iters[t], kBlockAccept, pidx0, 0));
+    uint32_t faults = 0;
+    for (uint32_t j = 0; j < D; ++j) z[t * D + j] = normal_draw(*zig, key0, key1, chains[t], iters[t], pidx0, j, faults);
+    E[t] = exp_draw(*zig, key0, key1, chains[t], iters[t], pidx0, faults);
 }
 
 __global__ void __launch_bounds__(256) probe_log_kernel(const double *__restrict__ x, double *__restrict__ y,

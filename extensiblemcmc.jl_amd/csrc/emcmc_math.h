@@ -3,10 +3,11 @@
 //
 // Why this exists: parity with the CPU oracle is defined bit-for-bit on the
 // accept/reject stream (BASELINE.json north_star).  Device libm (ocml) and
-// host glibc disagree in the last ulp for log/sin/cos, so every
-// transcendental on the hot path is built here from IEEE basic operations
-// (+ − × ÷ and sqrt, all correctly rounded on both sides) and compiled with
-// -ffp-contract=off.  The variate stream itself is counter-based
+// host glibc disagree in the last ulp for log/exp, so every transcendental is
+// built here from IEEE basic operations (+ − × ÷, fma, sqrt, rint — all
+// correctly rounded on both sides) and compiled with -ffp-contract=off.
+// Normal and exponential variates come from a 256-layer ziggurat whose fast
+// path is integer work plus one multiply (see below).  The variate stream itself is counter-based
 // (Philox4x32-10), keyed by the master seed and indexed by
 // (global chain id, mcmciter, block, pidx/attempt), so any chain on any shard
 // can be replayed independently.
@@ -39,7 +40,15 @@ struct u32x4 {
     uint32_t x, y, z, w;
 };
 
+#ifndef EMCMC_ABLATE
+#define EMCMC_ABLATE 0  // timing-only builds (make ablate): 1 = Philox replaced by a cheap hash
+#endif
+
 EMCMC_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#if EMCMC_ABLATE & 1
+    u32x4 o = {c.x * 0x9E3779B9u ^ k0, c.y * 0x85EBCA6Bu ^ c.x, c.z * 0xC2B2AE35u ^ k1, c.w ^ c.y * 0x27D4EB2Fu};
+    return o;
+#endif
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
@@ -118,63 +127,192 @@ EMCMC_HD double log_pos(double x) {
     return dk * ln2_hi - ((hfsq - fma(s, hfsq + R, dk * ln2_lo)) - f);
 }
 
-// ---- sin/cos kernels on [0, π/4] (FreeBSD msun k_sin.c / k_cos.c
-// coefficients, y = 0, fma Horner) ---------------------------------------------
-EMCMC_HD double ksin(double x) {
-    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
-                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
-                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
-    const double z = x * x;
-    double p = fma(z, S6, S5);
-    p = fma(z, p, S4);
-    p = fma(z, p, S3);
-    p = fma(z, p, S2);
-    p = fma(z, p, S1);
-    return fma(z * x, p, x);
-}
-EMCMC_HD double kcos(double x) {
-    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
-                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
-                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
-    const double z = x * x;
-    double p = fma(z, C6, C5);
-    p = fma(z, p, C4);
-    p = fma(z, p, C3);
-    p = fma(z, p, C2);
-    p = fma(z, p, C1);
-    const double r = z * p;
-    const double hz = 0.5 * z;
-    const double w = 1.0 - hz;
-    return w + fma(z, r, (1.0 - w) - hz);
+// ---- exp on [−700, 0] (rare paths and table construction) ------------------
+// x = k·ln2 + r, |r| ≤ ln2/2, e^r by its degree-13 Taylor polynomial in fma
+// Horner form (truncation < 5e-18), 2^k applied through the exponent bits.
+EMCMC_HD double exp_nonpos(double x) {
+    const double invln2 = 1.44269504088896338700e+00;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double kd = rint(x * invln2);
+    double r = fma(-kd, ln2_hi, x);
+    r = fma(-kd, ln2_lo, r);
+    double p = 1.0 / 6227020800.0;  // 1/13!
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    const int k = (int)kd;
+    return p * u2d((uint64_t)(1023 + k) << 52);
 }
 
-// ---- Box–Muller pair from one Philox block ----------------------------------
-// radius from (x,y): r = sqrt(-2 log u), u ∈ (0,1]
-// angle from (z,w): a 53-bit turn fraction; quadrant = top 2 bits, the
-// remaining 51 bits are folded to [0, π/4] exactly in integer arithmetic.
-EMCMC_HD void box_muller(u32x4 r, double &z0, double &z1) {
-    const double u = u01_open0(r.x, r.y);
-    const double rad = sqrt(-2.0 * log_pos(u));
-    const uint64_t b = bits53(r.z, r.w);
-    const uint32_t q = (uint32_t)(b >> 51);
-    const uint64_t rem = b & ((1ull << 51) - 1ull);
-    const bool fold = rem >= (1ull << 50);
-    const uint64_t rr = fold ? ((1ull << 51) - rem) : rem;
-    const double x = (double)rr * 0x1.921fb54442d18p-51;  // rr · (π/2)·2^-51 ∈ [0, π/4]
-    const double s = ksin(x), c = kcos(x);
-    // angle = q·π/2 + φ, φ = fold ? π/2 − x : x.  Branch-free: pick magnitudes,
-    // then flip sign bits (exact negation).
-    const bool t = ((q & 1u) != 0) != fold;
-    const double mc = t ? s : c;
-    const double ms = t ? c : s;
-    const uint64_t negc = (uint64_t)(((q >> 1) ^ q) & 1u) << 63;
-    const uint64_t negs = (uint64_t)((q >> 1) & 1u) << 63;
-    z0 = rad * u2d(d2u(mc) ^ negc);
-    z1 = rad * u2d(d2u(ms) ^ negs);
+// ---- Marsaglia–Tsang ziggurat, 256 layers (J. Stat. Softw. 5(8), 2000) ------
+// The same sampler family as Julia's randn/randexp (Random stdlib), fed by the
+// Philox stream: one 64-bit word pair per draw → layer index (8 bits), sign
+// (1 bit), 52-bit magnitude.  ≈ 99% of draws take the fast path (integer
+// compare + one table read + one multiply); wedge/tail draws use the portable
+// log/exp above with fresh counter blocks.  Tables are built on the host by
+// build_ziggurat() (oracle/ restates the same construction).
+constexpr double kZigNR = 3.6541528853610088;       // normal: rightmost layer edge r
+constexpr double kZigNV = 4.92867323399e-3;         // normal: area per layer v
+constexpr double kZigNInvR = 1.0 / 3.6541528853610088;
+constexpr double kZigER = 7.69711747013104972;      // exponential: r
+constexpr double kZigEV = 3.949659822581572e-3;     // exponential: v
+
+struct ZigEntry {
+    uint64_t k;  // fast-accept threshold on the 52-bit magnitude
+    double w;    // magnitude → x scale (x_i / 2^52)
+};
+struct Ziggurat {
+    ZigEntry n[256];
+    double nf[256];  // exp(−x_i²/2)
+    ZigEntry e[256];
+    double ef[256];  // exp(−x_i)
+};
+
+inline void build_ziggurat(Ziggurat &z) {
+    const double m = 0x1p52;
+    {  // N(0,1), f(x) = exp(−x²/2)
+        double dn = kZigNR, tn = dn;
+        const double q = kZigNV / exp_nonpos(-0.5 * (dn * dn));
+        z.n[0].k = (uint64_t)((dn / q) * m);
+        z.n[1].k = 0;
+        z.n[0].w = q / m;
+        z.n[255].w = dn / m;
+        z.nf[0] = 1.0;
+        z.nf[255] = exp_nonpos(-0.5 * (dn * dn));
+        for (int i = 254; i >= 1; --i) {
+            dn = sqrt(-2.0 * log_pos(kZigNV / dn + exp_nonpos(-0.5 * (dn * dn))));
+            z.n[i + 1].k = (uint64_t)((dn / tn) * m);
+            tn = dn;
+            z.nf[i] = exp_nonpos(-0.5 * (dn * dn));
+            z.n[i].w = dn / m;
+        }
+    }
+    {  // Exp(1), f(x) = exp(−x)
+        double de = kZigER, te = de;
+        const double q = kZigEV / exp_nonpos(-de);
+        z.e[0].k = (uint64_t)((de / q) * m);
+        z.e[1].k = 0;
+        z.e[0].w = q / m;
+        z.e[255].w = de / m;
+        z.ef[0] = 1.0;
+        z.ef[255] = exp_nonpos(-de);
+        for (int i = 254; i >= 1; --i) {
+            de = -log_pos(kZigEV / de + exp_nonpos(-de));
+            z.e[i + 1].k = (uint64_t)((de / te) * m);
+            te = de;
+            z.ef[i] = exp_nonpos(-de);
+            z.e[i].w = de / m;
+        }
+    }
 }
 
-// Exponential(1) draw for accept_reject! (run.jl:278): E = −log(u), u ∈ (0,1].
-EMCMC_HD double exp1(u32x4 r) { return -log_pos(u01_open0(r.x, r.y)); }
+struct ZigDraw {
+    uint32_t idx, sign;
+    uint64_t mag;  // 52 bits
+};
+EMCMC_HD ZigDraw zig_split(uint32_t hi, uint32_t lo) {
+    ZigDraw d;
+    d.idx = lo & 255u;
+    d.sign = (lo >> 8) & 1u;
+    d.mag = ((uint64_t)hi << 20) | (uint64_t)(lo >> 12);
+    return d;
+}
+// exact (double)mag for mag < 2^52 through the exponent bits
+EMCMC_HD double mag_to_double(uint64_t mag) { return u2d(0x4330000000000000ull | mag) - 0x1p52; }
+EMCMC_HD double with_sign(double x, uint32_t s) { return u2d(d2u(x) ^ ((uint64_t)s << 63)); }
+
+constexpr uint32_t kFaultRngRetries = 2u;  // EMCMC_FAULT_RNG_RETRIES
+constexpr uint32_t kMaxAttempt = 0xFFFFu;
+
+EMCMC_HD bool zig_normal_fast(ZigDraw d, const ZigEntry *tab, double &z) {
+    const ZigEntry t = tab[d.idx];
+    z = with_sign(mag_to_double(d.mag) * t.w, d.sign);
+    return d.mag < t.k;
+}
+
+// Rare path of normal number `gj` of (chain, iter, pidx0) whose attempt-0
+// draw `d` failed the fast test.  Slow step k uses the counter block
+// (pair = gj/2, attempt = 1 + 2k + gj%2), so the two normals of a pair never
+// share a block.
+EMCMC_HD double zig_normal_slow(ZigDraw d, const ZigEntry *tab, const double *f, uint32_t key0, uint32_t key1,
+                                uint32_t chain, uint32_t iter, uint32_t pidx0, uint32_t gj, uint32_t &faults) {
+    const uint32_t pair = gj >> 1, h = gj & 1u;
+    for (uint32_t k = 0;; ++k) {
+        const uint32_t attempt = 1u + 2u * k + h;
+        if (attempt > kMaxAttempt) {
+            faults |= kFaultRngRetries;
+            return 0.0;
+        }
+        const u32x4 b = draw(key0, key1, chain, iter, pair, pidx0, attempt);
+        if (d.idx == 0) {  // base strip beyond the rectangle: tail x > r
+            const double xx = -log_pos(u01_open0(b.x, b.y)) * kZigNInvR;
+            const double yy = -log_pos(u01_open0(b.z, b.w));
+            if (yy + yy > xx * xx) return with_sign(kZigNR + xx, d.sign);
+        } else {  // wedge test, else a fresh draw
+            const double x = mag_to_double(d.mag) * tab[d.idx].w;
+            const double u = u01_closed0(b.x, b.y);
+            if (fma(u, f[d.idx - 1] - f[d.idx], f[d.idx]) < exp_nonpos(-0.5 * (x * x))) return with_sign(x, d.sign);
+            d = zig_split(b.z, b.w);
+            double z;
+            if (zig_normal_fast(d, tab, z)) return z;
+        }
+    }
+}
+
+EMCMC_HD bool zig_exp_fast(ZigDraw d, const ZigEntry *tab, double &e) {
+    const ZigEntry t = tab[d.idx];
+    e = mag_to_double(d.mag) * t.w;
+    return d.mag < t.k;
+}
+
+// Rare path of the Exp(1) draw of block `block`: slow step k uses attempt 1 + k.
+EMCMC_HD double zig_exp_slow(ZigDraw d, const ZigEntry *tab, const double *f, uint32_t key0, uint32_t key1,
+                             uint32_t chain, uint32_t iter, uint32_t block, uint32_t pidx0, uint32_t &faults) {
+    for (uint32_t k = 0;; ++k) {
+        const uint32_t attempt = 1u + k;
+        if (attempt > kMaxAttempt) {
+            faults |= kFaultRngRetries;
+            return 0.0;
+        }
+        const u32x4 b = draw(key0, key1, chain, iter, block, pidx0, attempt);
+        if (d.idx == 0) return kZigER - log_pos(u01_open0(b.x, b.y));
+        const double x = mag_to_double(d.mag) * tab[d.idx].w;
+        const double u = u01_closed0(b.x, b.y);
+        if (fma(u, f[d.idx - 1] - f[d.idx], f[d.idx]) < exp_nonpos(-x)) return x;
+        d = zig_split(b.z, b.w);
+        double e;
+        if (zig_exp_fast(d, tab, e)) return e;
+    }
+}
+
+// Scalar reference forms (probes, host code): the full draw of normal gj and
+// of the accept exponential.
+EMCMC_HD double normal_draw(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
+                            uint32_t pidx0, uint32_t gj, uint32_t &faults) {
+    const u32x4 r = draw(key0, key1, chain, iter, gj >> 1, pidx0, 0);
+    const ZigDraw d = (gj & 1u) ? zig_split(r.z, r.w) : zig_split(r.x, r.y);
+    double z;
+    if (zig_normal_fast(d, zt.n, z)) return z;
+    return zig_normal_slow(d, zt.n, zt.nf, key0, key1, chain, iter, pidx0, gj, faults);
+}
+EMCMC_HD double exp_draw(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
+                         uint32_t pidx0, uint32_t &faults) {
+    const u32x4 r = draw(key0, key1, chain, iter, kBlockAccept, pidx0, 0);
+    const ZigDraw d = zig_split(r.x, r.y);
+    double e;
+    if (zig_exp_fast(d, zt.e, e)) return e;
+    return zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
+}
 
 // log(2π) rounded to double, Float64(log2π) in Distributions' mvnormal_c0.
 constexpr double kLog2Pi = 1.8378770664093454835606594728112;

@@ -45,6 +45,7 @@ LL_PER_OBS, LL_SUFFSTAT = 0, 1
 HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
 H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
 FAULT_NONFINITE_LL = 1
+FAULT_RNG_RETRIES = 2
 VARIANT_HIGH_OCCUPANCY = 1
 
 

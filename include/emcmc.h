@@ -91,6 +91,7 @@ typedef enum emcmc_status {
 
 /* Per-chain fault bits (emcmc_get_faults) */
 #define EMCMC_FAULT_NONFINITE_LL 1u  /* proposal log-likelihood NaN/±Inf */
+#define EMCMC_FAULT_RNG_RETRIES 2u   /* a ziggurat draw exhausted its 65,535 attempt counters */
 
 typedef struct emcmc_handle emcmc_handle;
 

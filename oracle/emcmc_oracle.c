@@ -49,6 +49,16 @@
 
 #define ORC_EXPORT __attribute__((visibility("default")))
 
+static orc_zig_tables g_zig;
+static int g_zig_ready = 0;
+static const orc_zig_tables *zig(void) {
+    if (!g_zig_ready) { /* first call happens outside any parallel region */
+        orc_zig_build(&g_zig);
+        g_zig_ready = 1;
+    }
+    return &g_zig;
+}
+
 /* ---- canonical helpers --------------------------------------------------- */
 
 /* Cholesky of the upper-stored (column-major) symmetric Σ: row-major lower L.
@@ -218,18 +228,17 @@ static void run_chain(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t ke
                       uint64_t C, uint64_t c, double *hist_theta, double *hist_prop, double *hist_ll,
                       uint8_t *hist_acc) {
     const int D = g->D;
-    double th[64], thp[64], z[66];
+    const orc_zig_tables *zt = zig();
+    double th[64], thp[64], z[64];
     memcpy(th, st.theta, sizeof(double) * D);
     double ll = *st.ll, ra = *st.ra;
     uint64_t ring0 = st.ring[0], ring1 = st.ring[1];
     uint32_t nacc = *st.nacc, faults = *st.faults;
-    const int npairs = (D + 1) / 2;
 
     for (uint32_t s = 0; s < nsteps; ++s) {
         const uint32_t iter = iters ? iters[s] : iter0 + s;
         /* proposal!  θ° = θ + L z  (random_walk.jl:147: rand(MvNormal(θ, Σ))) */
-        for (int j = 0; j < npairs; ++j)
-            orc_box_muller(orc_draw(key0, key1, chain_id, iter, (uint32_t)j, 0, 0), &z[2 * j], &z[2 * j + 1]);
+        for (int j = 0; j < D; ++j) z[j] = orc_normal(zt, key0, key1, chain_id, iter, 0, (uint32_t)j, &faults);
         for (int i = 0; i < D; ++i) {
             double lz;
             if (g->diag) {
@@ -264,7 +273,7 @@ static void run_chain(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t ke
         /* accept_reject!  (run.jl:271-278) — ImproperPrior: log_prior = 0.0 */
         const double lp_prop = 0.0, lp_prev = 0.0;
         const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + lp_prop) - lp_prev;
-        const double E = orc_exp1(orc_draw(key0, key1, chain_id, iter, ORC_BLOCK_ACCEPT, 0, 0));
+        const double E = orc_exponential(zt, key0, key1, chain_id, iter, 0, &faults);
         const int acc = E > -llr;
         const uint64_t slot = (uint64_t)(s);
         if (hist_prop) memcpy(hist_prop + (slot * C + c) * D, thp, sizeof(double) * D);
@@ -316,6 +325,7 @@ ORC_EXPORT int orc_run_gsn(int D, uint64_t C, uint32_t chain0, uint64_t seed, co
                            int nthreads) {
     orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
     if (!g) return -3;
+    (void)zig();
     int rc = gsn_prepare(g, D, rw_sigma, t_sigma, nobs, obs, ll_mode);
     if (rc) {
         free(g);
@@ -344,25 +354,44 @@ ORC_EXPORT void orc_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_
 }
 
 /* The D normals and the Exp(1) draw of (chain, iter, pidx0). */
-ORC_EXPORT void orc_step_variates(uint64_t seed, uint32_t chain, uint32_t iter, uint32_t pidx0, int D, double *z,
-                                  double *E, double *u_radius, double *turn) {
+ORC_EXPORT uint32_t orc_step_variates(uint64_t seed, uint32_t chain, uint32_t iter, uint32_t pidx0, int D, double *z,
+                                      double *E) {
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
-    for (int j = 0; j < (D + 1) / 2; ++j) {
-        orc_u32x4 r = orc_draw(k0, k1, chain, iter, (uint32_t)j, pidx0, 0);
-        double a, b;
-        orc_box_muller(r, &a, &b);
-        z[2 * j] = a;
-        if (2 * j + 1 < D) z[2 * j + 1] = b;
-        if (u_radius) u_radius[j] = orc_u01_open0(r.v[0], r.v[1]);
-        if (turn) turn[j] = (double)orc_bits53(r.v[2], r.v[3]) * 0x1p-53;
-    }
-    *E = orc_exp1(orc_draw(k0, k1, chain, iter, ORC_BLOCK_ACCEPT, pidx0, 0));
+    uint32_t faults = 0;
+    for (int j = 0; j < D; ++j) z[j] = orc_normal(zig(), k0, k1, chain, iter, pidx0, (uint32_t)j, &faults);
+    *E = orc_exponential(zig(), k0, k1, chain, iter, pidx0, &faults);
+    return faults;
+}
+
+/* Bulk draws for distribution tests: n normals / exponentials from the stream. */
+ORC_EXPORT void orc_normal_vec(uint64_t seed, uint32_t chain, uint32_t iter0, uint64_t n, double *out) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t faults = 0;
+    for (uint64_t i = 0; i < n; ++i)
+        out[i] = orc_normal(zig(), k0, k1, chain, iter0 + (uint32_t)(i >> 6), 0, (uint32_t)(i & 63u), &faults);
+}
+ORC_EXPORT void orc_exp_vec(uint64_t seed, uint32_t chain, uint32_t iter0, uint64_t n, double *out) {
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    uint32_t faults = 0;
+    for (uint64_t i = 0; i < n; ++i) out[i] = orc_exponential(zig(), k0, k1, chain + (uint32_t)i, iter0, 0, &faults);
+}
+
+ORC_EXPORT void orc_exp_nonpos_vec(const double *x, double *y, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) y[i] = orc_exp_nonpos(x[i]);
+}
+
+/* Ziggurat tables: kn, wn, fn, ke, we, fe (256 each). */
+ORC_EXPORT void orc_zig_tables_copy(uint64_t *kn, double *wn, double *fn, uint64_t *ke, double *we, double *fe) {
+    const orc_zig_tables *t = zig();
+    memcpy(kn, t->kn, sizeof t->kn);
+    memcpy(wn, t->wn, sizeof t->wn);
+    memcpy(fn, t->fn, sizeof t->fn);
+    memcpy(ke, t->ke, sizeof t->ke);
+    memcpy(we, t->we, sizeof t->we);
+    memcpy(fe, t->fe, sizeof t->fe);
 }
 
 ORC_EXPORT void orc_log_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_log(x[i]);
 }
 
-ORC_EXPORT void orc_sincos_turn_vec(const uint64_t *turn53, double *c, double *s, uint64_t n) {
-    for (uint64_t i = 0; i < n; ++i) orc_sincos_turn(turn53[i], &c[i], &s[i]);
-}

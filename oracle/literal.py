@@ -51,7 +51,7 @@ def run_chain(seed, chain, theta0, rw_sigma, t_sigma, obs, nsteps, iter0=1, W=10
     N = 1
     for s in range(nsteps):
         it = iter0 + s
-        z, E, _, _ = _oracle.step_variates(seed, chain, it, D)
+        z, E, _ = _oracle.step_variates(seed, chain, it, D)
         thp = th + Lrw @ z
         llp = 0.0
         for x in obs:

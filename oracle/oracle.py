@@ -48,12 +48,18 @@ def lib():
         L.orc_gsn_constants.argtypes = [C.c_int, dp, dp, C.c_uint64, dp, dp, dp, dp]
         L.orc_philox.restype = None
         L.orc_philox.argtypes = [u32p, u32p, u32p]
-        L.orc_step_variates.restype = None
-        L.orc_step_variates.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, dp, dp, dp, dp]
+        L.orc_step_variates.restype = C.c_uint32
+        L.orc_step_variates.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, dp, dp]
         L.orc_log_vec.restype = None
         L.orc_log_vec.argtypes = [dp, dp, C.c_uint64]
-        L.orc_sincos_turn_vec.restype = None
-        L.orc_sincos_turn_vec.argtypes = [u64p, dp, dp, C.c_uint64]
+        L.orc_exp_nonpos_vec.restype = None
+        L.orc_exp_nonpos_vec.argtypes = [dp, dp, C.c_uint64]
+        L.orc_normal_vec.restype = None
+        L.orc_normal_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
+        L.orc_exp_vec.restype = None
+        L.orc_exp_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
+        L.orc_zig_tables_copy.restype = None
+        L.orc_zig_tables_copy.argtypes = [u64p, dp, dp, u64p, dp, dp]
         _lib = L
     return _lib
 
@@ -154,13 +160,11 @@ def philox(ctr, key):
 
 
 def step_variates(seed, chain, it, D, pidx0=0):
-    z = np.zeros(D + 1)
+    """The D proposal normals and the accept Exp(1) draw of one (chain, iter)."""
+    z = np.zeros(D)
     E = np.zeros(1)
-    npair = (D + 1) // 2
-    u = np.zeros(npair)
-    t = np.zeros(npair)
-    lib().orc_step_variates(seed & 0xFFFFFFFFFFFFFFFF, chain, it, pidx0, D, _d(z), _d(E), _d(u), _d(t))
-    return z[:D], float(E[0]), u, t
+    faults = lib().orc_step_variates(seed & 0xFFFFFFFFFFFFFFFF, chain, it, pidx0, D, _d(z), _d(E))
+    return z, float(E[0]), int(faults)
 
 
 def log_vec(x):
@@ -170,9 +174,29 @@ def log_vec(x):
     return y
 
 
-def sincos_turn(turn53):
-    t = np.ascontiguousarray(turn53, dtype=np.uint64)
-    c = np.empty(t.size)
-    s = np.empty(t.size)
-    lib().orc_sincos_turn_vec(t.ctypes.data_as(C.POINTER(C.c_uint64)), _d(c), _d(s), t.size)
-    return c, s
+def exp_nonpos_vec(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_exp_nonpos_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def normals(seed, n, chain=0, iter0=1):
+    out = np.empty(n)
+    lib().orc_normal_vec(seed & 0xFFFFFFFFFFFFFFFF, chain, iter0, n, _d(out))
+    return out
+
+
+def exponentials(seed, n, chain0=0, it=1):
+    out = np.empty(n)
+    lib().orc_exp_vec(seed & 0xFFFFFFFFFFFFFFFF, chain0, it, n, _d(out))
+    return out
+
+
+def zig_tables():
+    kn = np.empty(256, dtype=np.uint64)
+    ke = np.empty(256, dtype=np.uint64)
+    wn, fn, we, fe = (np.empty(256) for _ in range(4))
+    u64 = C.POINTER(C.c_uint64)
+    lib().orc_zig_tables_copy(kn.ctypes.data_as(u64), _d(wn), _d(fn), ke.ctypes.data_as(u64), _d(we), _d(fe))
+    return {"kn": kn, "wn": wn, "fn": fn, "ke": ke, "we": we, "fe": fe}

@@ -12,9 +12,10 @@
  *    vectors in tests/golden/philox_kat.json.
  *  - natural log: fdlibm e_log.c argument reduction + Lg1..Lg7 polynomial,
  *    evaluated with the single formula of its main branch.
- *  - sin/cos on [0, π/4]: FreeBSD msun k_sin.c / k_cos.c (y = 0).
- *  - Box–Muller transform (radius from one 53-bit uniform in (0,1], angle from
- *    a 53-bit turn fraction folded to [0, π/4] in integer arithmetic).
+ *  - exp on [-700, 0]: ln2 range reduction + degree-13 Taylor polynomial.
+ *  - Marsaglia & Tsang's ziggurat, 256 strips (J. Stat. Softw. 5(8), 2000),
+ *    for N(0,1) and Exp(1) — the sampler family Julia's randn/randexp use —
+ *    with 52-bit magnitudes drawn from the Philox stream.
  *
  * The reference (Julia) draws from Random.GLOBAL_RNG via Distributions
  * (src/transition_kernels/random_walk.jl:147, src/run.jl:278); that stream
@@ -67,7 +68,6 @@ static inline orc_u32x4 orc_philox4x32_10(orc_u32x4 ctr, uint32_t key0, uint32_t
 }
 
 /* Counter layout: (chain id, mcmciter, block, (pidx0 << 16) | attempt). */
-#define ORC_BLOCK_ACCEPT 0xFFFFFFFFu
 
 static inline orc_u32x4 orc_draw(uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
                                  uint32_t block, uint32_t pidx0, uint32_t attempt) {
@@ -113,62 +113,139 @@ static inline double orc_log(double x) {
     return dk * ln2_hi - ((hfsq - fma(s, hfsq + R, dk * ln2_lo)) - f);
 }
 
-/* sin on [0, π/4]: x + x³·P(x²), FreeBSD k_sin.c coefficients S1..S6. */
-static inline double orc_sin_k(double x) {
-    static const double S[6] = {-1.66666666666666324348e-01, 8.33333333332248946124e-03,
-                                -1.98412698298579493134e-04, 2.75573137070700676789e-06,
-                                -2.50507602534068634195e-08, 1.58969099521155010221e-10};
-    double z = x * x;
-    double p = fma(z, S[5], S[4]);
-    for (int j = 3; j >= 0; --j) p = fma(z, p, S[j]);
-    return fma(z * x, p, x);
+/* exp(x) for x in [-700, 0]: x = k ln2 + r, e^r by the degree-13 Taylor
+ * polynomial (fma Horner), 2^k through the exponent field. */
+static inline double orc_exp_nonpos(double x) {
+    const double invln2 = 1.44269504088896338700e+00;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    double kd = rint(x * invln2);
+    double r = fma(-kd, ln2_hi, x);
+    r = fma(-kd, ln2_lo, r);
+    static const double inv_fact[14] = {1.0, 1.0, 0.5, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+                                        1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+                                        1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0};
+    double p = inv_fact[13];
+    for (int n = 12; n >= 0; --n) p = fma(p, r, inv_fact[n]);
+    int k = (int)kd;
+    return p * orc_u2d((uint64_t)(1023 + k) << 52);
 }
 
-/* cos on [0, π/4]: 1 − z/2 + z²·P(z), FreeBSD k_cos.c coefficients C1..C6,
- * with the compensated 1 − z/2 step. */
-static inline double orc_cos_k(double x) {
-    static const double Cc[6] = {4.16666666666666019037e-02, -1.38888888888741095749e-03,
-                                 2.48015872894767294178e-05, -2.75573143513906633035e-07,
-                                 2.08757232129817482790e-09, -1.13596475577881948265e-11};
-    double z = x * x;
-    double p = fma(z, Cc[5], Cc[4]);
-    for (int j = 3; j >= 0; --j) p = fma(z, p, Cc[j]);
-    double r = z * p;
-    double hz = 0.5 * z;
-    double one_minus = 1.0 - hz;
-    return one_minus + fma(z, r, (1.0 - one_minus) - hz);
-}
+/* ---- 256-layer Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---- */
+#define ORC_ZN_R 3.6541528853610088
+#define ORC_ZN_V 4.92867323399e-3
+#define ORC_ZE_R 7.69711747013104972
+#define ORC_ZE_V 3.949659822581572e-3
 
-/* cos and sin of a 53-bit turn fraction (angle = 2π·turn/2^53). */
-static inline void orc_sincos_turn(uint64_t turn, double *cz, double *sz) {
-    uint32_t quadrant = (uint32_t)(turn >> 51);
-    uint64_t rem = turn & ((1ull << 51) - 1u);
-    int folded = rem >= (1ull << 50);
-    uint64_t rr = folded ? ((1ull << 51) - rem) : rem;
-    double x = (double)rr * 0x1.921fb54442d18p-51;
-    double s = orc_sin_k(x), c = orc_cos_k(x);
-    double sin_phi = folded ? c : s;
-    double cos_phi = folded ? s : c;
-    switch (quadrant) {
-    case 0: *cz = cos_phi; *sz = sin_phi; break;
-    case 1: *cz = -sin_phi; *sz = cos_phi; break;
-    case 2: *cz = -cos_phi; *sz = -sin_phi; break;
-    default: *cz = sin_phi; *sz = -cos_phi; break;
+typedef struct {
+    uint64_t kn[256];
+    double wn[256], fn[256];
+    uint64_t ke[256];
+    double we[256], fe[256];
+} orc_zig_tables;
+
+/* zigset (M&T Fig. 1) for 256 strips and 52-bit magnitudes */
+static inline void orc_zig_build(orc_zig_tables *t) {
+    const double m = 4503599627370496.0; /* 2^52 */
+    double dn = ORC_ZN_R, tn = dn;
+    double q = ORC_ZN_V / orc_exp_nonpos(-0.5 * (dn * dn));
+    t->kn[0] = (uint64_t)((dn / q) * m);
+    t->kn[1] = 0;
+    t->wn[0] = q / m;
+    t->wn[255] = dn / m;
+    t->fn[0] = 1.0;
+    t->fn[255] = orc_exp_nonpos(-0.5 * (dn * dn));
+    for (int i = 254; i >= 1; --i) {
+        dn = sqrt(-2.0 * orc_log(ORC_ZN_V / dn + orc_exp_nonpos(-0.5 * (dn * dn))));
+        t->kn[i + 1] = (uint64_t)((dn / tn) * m);
+        tn = dn;
+        t->fn[i] = orc_exp_nonpos(-0.5 * (dn * dn));
+        t->wn[i] = dn / m;
+    }
+    double de = ORC_ZE_R, te = de;
+    q = ORC_ZE_V / orc_exp_nonpos(-de);
+    t->ke[0] = (uint64_t)((de / q) * m);
+    t->ke[1] = 0;
+    t->we[0] = q / m;
+    t->we[255] = de / m;
+    t->fe[0] = 1.0;
+    t->fe[255] = orc_exp_nonpos(-de);
+    for (int i = 254; i >= 1; --i) {
+        de = -orc_log(ORC_ZE_V / de + orc_exp_nonpos(-de));
+        t->ke[i + 1] = (uint64_t)((de / te) * m);
+        te = de;
+        t->fe[i] = orc_exp_nonpos(-de);
+        t->we[i] = de / m;
     }
 }
 
-/* Two independent N(0,1) variates from one Philox block. */
-static inline void orc_box_muller(orc_u32x4 r, double *z0, double *z1) {
-    double u = orc_u01_open0(r.v[0], r.v[1]);
-    double radius = sqrt(-2.0 * orc_log(u));
-    double cz, sz;
-    orc_sincos_turn(orc_bits53(r.v[2], r.v[3]), &cz, &sz);
-    *z0 = radius * cz;
-    *z1 = radius * sz;
+/* one 64-bit draw: layer = lo[7:0], sign = lo[8], magnitude = hi:lo[31:12] (52 bits) */
+typedef struct {
+    uint32_t layer, negative;
+    uint64_t mag;
+} orc_zdraw;
+
+static inline orc_zdraw orc_zsplit(uint32_t hi, uint32_t lo) {
+    orc_zdraw d = {lo & 255u, (lo >> 8) & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
+    return d;
 }
 
-/* rand(Exponential(1.0)) of run.jl:278 restated as −log(u), u ∈ (0,1]. */
-static inline double orc_exp1(orc_u32x4 r) { return -orc_log(orc_u01_open0(r.v[0], r.v[1])); }
+static inline double orc_signed(double x, uint32_t negative) { return negative ? -x : x; }
+
+#define ORC_FAULT_RNG 2u
+#define ORC_MAX_ATTEMPT 0xFFFFu
+
+/* Normal number g of (chain, iter, pidx0): attempt 0 from word pair g%2 of
+ * block (g/2, 0); the k-th rare-path step uses block (g/2, 1 + 2k + g%2). */
+static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k1, uint32_t chain, uint32_t iter,
+                                uint32_t pidx0, uint32_t g, uint32_t *faults) {
+    orc_u32x4 r0 = orc_draw(k0, k1, chain, iter, g >> 1, pidx0, 0);
+    orc_zdraw d = (g & 1u) ? orc_zsplit(r0.v[2], r0.v[3]) : orc_zsplit(r0.v[0], r0.v[1]);
+    if (d.mag < t->kn[d.layer]) return orc_signed((double)d.mag * t->wn[d.layer], d.negative);
+    for (uint32_t step = 0;; ++step) {
+        uint32_t attempt = 1u + 2u * step + (g & 1u);
+        if (attempt > ORC_MAX_ATTEMPT) {
+            *faults |= ORC_FAULT_RNG;
+            return 0.0;
+        }
+        orc_u32x4 b = orc_draw(k0, k1, chain, iter, g >> 1, pidx0, attempt);
+        if (d.layer == 0) { /* tail beyond r */
+            double xx = -orc_log(orc_u01_open0(b.v[0], b.v[1])) * (1.0 / ORC_ZN_R);
+            double yy = -orc_log(orc_u01_open0(b.v[2], b.v[3]));
+            if (yy + yy > xx * xx) return orc_signed(ORC_ZN_R + xx, d.negative);
+        } else {
+            double x = (double)d.mag * t->wn[d.layer];
+            double u = orc_u01_closed0(b.v[0], b.v[1]);
+            if (fma(u, t->fn[d.layer - 1] - t->fn[d.layer], t->fn[d.layer]) < orc_exp_nonpos(-0.5 * (x * x)))
+                return orc_signed(x, d.negative);
+            d = orc_zsplit(b.v[2], b.v[3]);
+            if (d.mag < t->kn[d.layer]) return orc_signed((double)d.mag * t->wn[d.layer], d.negative);
+        }
+    }
+}
+
+/* rand(Exponential(1.0)) of run.jl:278: block (ORC_BLOCK_ACCEPT, 0), then
+ * rare-path step k on attempt 1 + k. */
+#define ORC_BLOCK_ACCEPT 0xFFFFFFFFu
+static inline double orc_exponential(const orc_zig_tables *t, uint32_t k0, uint32_t k1, uint32_t chain,
+                                     uint32_t iter, uint32_t pidx0, uint32_t *faults) {
+    orc_u32x4 r0 = orc_draw(k0, k1, chain, iter, ORC_BLOCK_ACCEPT, pidx0, 0);
+    orc_zdraw d = orc_zsplit(r0.v[0], r0.v[1]);
+    if (d.mag < t->ke[d.layer]) return (double)d.mag * t->we[d.layer];
+    for (uint32_t step = 0;; ++step) {
+        uint32_t attempt = 1u + step;
+        if (attempt > ORC_MAX_ATTEMPT) {
+            *faults |= ORC_FAULT_RNG;
+            return 0.0;
+        }
+        orc_u32x4 b = orc_draw(k0, k1, chain, iter, ORC_BLOCK_ACCEPT, pidx0, attempt);
+        if (d.layer == 0) return ORC_ZE_R - orc_log(orc_u01_open0(b.v[0], b.v[1]));
+        double x = (double)d.mag * t->we[d.layer];
+        double u = orc_u01_closed0(b.v[0], b.v[1]);
+        if (fma(u, t->fe[d.layer - 1] - t->fe[d.layer], t->fe[d.layer]) < orc_exp_nonpos(-x)) return x;
+        d = orc_zsplit(b.v[2], b.v[3]);
+        if (d.mag < t->ke[d.layer]) return (double)d.mag * t->we[d.layer];
+    }
+}
 
 #define ORC_LOG2PI 1.8378770664093454835606594728112
 

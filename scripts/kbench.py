@@ -37,7 +37,8 @@ def main():
     grid = []
     for hist in (L.HIST_FULL, L.HIST_ACCEPT_ONLY):
         for ll in (L.LL_PER_OBS, L.LL_SUFFSTAT):
-            lv = ((1, 0), (2, 0), (4, 0)) if a.variants == "all" else ((1, 0), (4, 0))
+            lv = {"all": ((1, 0), (2, 0), (4, 0), (4, 1)), "lpc14": ((1, 0), (4, 0)),
+                  "lpc4": ((4, 0), (4, 1))}[a.variants]
             for lpc, var in lv:
                 grid.append((lpc, var, ll, hist, 100))
     S = 100 + a.steps * a.rounds

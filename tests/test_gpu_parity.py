@@ -32,8 +32,8 @@ def test_device_variates_match_oracle(oracle, D):
     chains = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
     iters = rng.integers(1, 2 ** 31, n, dtype=np.uint64).astype(np.uint32)
     z, E = L.probe_variates(W.SEED, chains, iters, D)
-    for i in range(0, n, 97):
-        zo, Eo, _, _ = oracle.step_variates(W.SEED, int(chains[i]), int(iters[i]), D)
+    for i in range(0, n, 7):
+        zo, Eo, _ = oracle.step_variates(W.SEED, int(chains[i]), int(iters[i]), D)
         assert np.array_equal(z[i], zo)
         assert E[i] == Eo
 

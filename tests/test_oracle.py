@@ -1,7 +1,8 @@
 """Oracle self-checks (CPU): the shared variate stream and canonical arithmetic.
 
 Pins: Random123 Philox KATs (tests/golden/philox_kat.json); accuracy of the
-restated log / sin / cos against numpy; Box–Muller normality; the canonical
+restated log / exp against numpy; the 256-strip ziggurat tables (equal strip
+areas) and the N(0,1) / Exp(1) distributions they produce; the canonical
 Cholesky and summation against LAPACK / math.fsum; and the claim the kernels
 rely on that the dense (general-L) formulas give the same bits as the diagonal
 ones when Σ is diagonal.
@@ -32,28 +33,48 @@ def test_log_accuracy(oracle):
     assert y[x == 1.0][0] == 0.0
 
 
-def test_sincos_accuracy(oracle):
-    rng = np.random.default_rng(1)
-    t = rng.integers(0, 2 ** 53, 200_000, dtype=np.uint64)
-    t = np.concatenate([t, np.array([0, 2 ** 50, 2 ** 51, 3 * 2 ** 51, 2 ** 53 - 1], dtype=np.uint64)])
-    c, s = oracle.sincos_turn(t)
-    # exact angle in long double-free form: use the folded representation
-    ang = 2 * np.pi * (t.astype(np.float64) / 2.0 ** 53)
-    assert np.abs(c - np.cos(ang)).max() < 2e-15
-    assert np.abs(s - np.sin(ang)).max() < 2e-15
-    assert np.allclose(c * c + s * s, 1.0, atol=4e-16)
+def test_exp_accuracy(oracle):
+    rng = np.random.default_rng(3)
+    x = np.concatenate([-rng.uniform(0, 8, 200_000), -rng.uniform(0, 700, 50_000), [0.0, -1e-300, -0.5, -700.0]])
+    y = oracle.exp_nonpos_vec(x)
+    ref = np.exp(x)
+    assert (np.abs(y - ref) / ref).max() < 4e-16
+    assert y[x == 0.0][0] == 1.0
 
 
-def test_box_muller_normal(oracle):
+def test_ziggurat_tables(oracle):
+    """256 strips of equal area v (M&T construction): x_255 = r, top strip
+    reaches x_0 ≈ 0, thresholds below 2^52 and increasing towards the base."""
+    t = oracle.zig_tables()
+    m = 2.0 ** 52
+    for k, w, f, r, v, fx in ((t["kn"], t["wn"], t["fn"], 3.6541528853610088, 4.92867323399e-3,
+                               lambda x: np.exp(-0.5 * x * x)),
+                              (t["ke"], t["we"], t["fe"], 7.69711747013104972, 3.949659822581572e-3,
+                               lambda x: np.exp(-x))):
+        x = w * m  # x_i for i ≥ 1; base strip width for i = 0
+        assert x[255] == pytest.approx(r, rel=1e-15)
+        assert np.all(np.diff(x[1:]) > 0)
+        assert np.allclose(f[1:], fx(x[1:]), rtol=1e-14)
+        areas = x[1:] * (f[:-1] - f[1:])  # strip i spans f(x_i)..f(x_{i-1})
+        assert np.allclose(areas, v, rtol=1e-9)
+        assert x[0] * fx(r) == pytest.approx(v, rel=1e-12)  # base rectangle width q
+        assert k[1] == 0 and np.all(k < 2 ** 52)
+        assert np.allclose(k[2:] / m, x[1:-1] / x[2:], rtol=1e-15, atol=2.0 ** -52)
+
+
+def test_ziggurat_distributions(oracle):
     from scipy import stats
 
-    zs = np.concatenate([oracle.step_variates(W.SEED, c, it, 32)[0] for c in range(40) for it in range(1, 51)])
-    assert zs.size == 40 * 50 * 32
-    assert abs(zs.mean()) < 0.02 and abs(zs.std() - 1.0) < 0.02
-    assert stats.kstest(zs, "norm").pvalue > 1e-3
-    Es = np.array([oracle.step_variates(W.SEED, c, 1, 2)[1] for c in range(20_000)])
-    assert abs(Es.mean() - 1.0) < 0.03
-    assert stats.kstest(Es, "expon").pvalue > 1e-3
+    z = oracle.normals(W.SEED, 400_000)
+    assert abs(z.mean()) < 0.006 and abs(z.std() - 1.0) < 0.006
+    assert stats.kstest(z, "norm").pvalue > 1e-3
+    # tail beyond r = 3.654 is reached through the rare path and has the right mass
+    tail = (np.abs(z) > 3.6541528853610088).mean()
+    assert abs(tail - 2 * stats.norm.sf(3.6541528853610088)) < 3e-4
+    e = oracle.exponentials(W.SEED, 200_000)
+    assert abs(e.mean() - 1.0) < 0.01
+    assert stats.kstest(e, "expon").pvalue > 1e-3
+    assert (e > 7.69711747013104972).sum() > 0
 
 
 def test_variates_depend_on_counter(oracle):

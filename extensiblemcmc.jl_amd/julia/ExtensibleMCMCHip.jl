@@ -1,0 +1,231 @@
+#===============================================================================
+    ExtensibleMCMCHip.jl — MI355X backend for ExtensibleMCMC.jl over libemcmc.so
+
+    Adds `MI355XBackend <: MCMCBackend` (the extension point of
+    src/types.jl:110-117) with the global/local workspace constructors the
+    reference dispatches on (src/workspaces.jl:38, :280) and a `run!` method
+    for `MCMC` objects built with this backend.  The hot loop (__run!,
+    src/run.jl:64-83) executes on the GPU through the C ABI declared in
+    include/emcmc.h; the schedule (src/schedule.jl) stays in Julia and is
+    handed over as a list of (mcmciter, pidx) steps.
+
+    Not executed in this repository's CI (no Julia in the build image); the
+    Python twin (extensible_mcmc/_lib.py) exercises the same entry points.
+===============================================================================#
+module ExtensibleMCMCHip
+
+using ExtensibleMCMC
+const eMCMC = ExtensibleMCMC
+
+const LIB = get(ENV, "EMCMC_LIB", joinpath(@__DIR__, "..", "lib", "libemcmc.so"))
+const ABI_VERSION = UInt32(1)
+
+# ---- C structs (include/emcmc.h) ---------------------------------------------
+struct EmcmcConfig
+    abi_version::UInt32
+    dim::UInt32
+    num_chains::UInt64
+    first_chain_id::UInt64
+    num_mcmc_steps::UInt64
+    seed::UInt64
+    device::Int32
+    history_mode::UInt32
+    roll_window::UInt32
+    lanes_per_chain::UInt32
+    steps_per_launch::UInt32
+    kernel_variant::UInt32
+    reserved::NTuple{6,UInt32}
+end
+
+struct EmcmcUpdateDesc
+    kernel::UInt32
+    prior::UInt32
+    adaptation::UInt32
+    num_coords::UInt32
+    coords::Ptr{UInt32}
+    sigma::Ptr{Float64}
+    epsilon::Ptr{Float64}
+    pos::Ptr{UInt8}
+    reserved_ptr::NTuple{4,Ptr{Cvoid}}
+    reserved_f64::NTuple{4,Float64}
+end
+
+struct EmcmcTargetDesc
+    kind::UInt32
+    dim::UInt32
+    mu::Ptr{Float64}
+    sigma::Ptr{Float64}
+    num_obs::UInt64
+    obs::Ptr{Float64}
+    ll_mode::UInt32
+    reserved::UInt32
+end
+
+struct EmcmcStep
+    mcmciter::UInt32
+    pidx::UInt32
+end
+
+const RW_GAUSSIAN = UInt32(2)
+const PRIOR_IMPROPER = UInt32(0)
+const ADPT_NONE = UInt32(0)
+const TARGET_GSN = UInt32(1)
+const H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
+
+function check(st, h, where)
+    st == 0 && return nothing
+    msg = h == C_NULL ? "" : unsafe_string(ccall((:emcmc_last_error, LIB), Cstring, (Ptr{Cvoid},), h))
+    error("$where failed with emcmc_status $st: $msg")
+end
+
+# ---- backend -------------------------------------------------------------------
+"""
+    MI355XBackend(; num_chains=1, seed=0, first_chain_id=0, device=0,
+                  history=:full, ll_mode=:per_obs)
+
+Many-chain GPU backend: each of the `num_chains` chains is an independent
+replica of the reference's single-chain sampler, keyed by its global id.
+"""
+Base.@kwdef struct MI355XBackend <: eMCMC.MCMCBackend
+    num_chains::Int = 1
+    seed::UInt64 = 0
+    first_chain_id::Int = 0
+    device::Int = 0
+    history::Symbol = :full
+    ll_mode::Symbol = :per_obs
+end
+
+mutable struct MI355XGlobalWorkspace{T} <: eMCMC.GlobalWorkspace{T}
+    handle::Ptr{Cvoid}
+    backend::MI355XBackend
+    num_mcmc_steps::Int
+    dim::Int
+    num_updates::Int
+    num_locals::Int
+end
+
+struct MI355XLocalWorkspace{T} <: eMCMC.LocalWorkspace{T}
+    gws::MI355XGlobalWorkspace{T}
+    pidx::Int
+end
+
+function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
+    updt.rw isa eMCMC.GaussianRandomWalk || error("no device plugin for $(typeof(updt.rw))")
+    updt.prior isa eMCMC.ImproperPrior || error("no device plugin for $(typeof(updt.prior))")
+    updt.adpt isa eMCMC.NoAdaptation || error("no device plugin for $(typeof(updt.adpt))")
+    coords = UInt32.(collect(updt.coords) .- 1)                 # 0-based across the ABI
+    Σ = Matrix{Float64}(updt.rw.Σ)                             # column-major already
+    push!(keep, coords, Σ)
+    EmcmcUpdateDesc(RW_GAUSSIAN, PRIOR_IMPROPER, ADPT_NONE, UInt32(length(coords)),
+                    pointer(coords), pointer(Σ), C_NULL, C_NULL,
+                    (C_NULL, C_NULL, C_NULL, C_NULL), (0.0, 0.0, 0.0, 0.0))
+end
+
+# workspaces.jl:38 — init_global_workspace(::MCMCBackend, …)
+function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
+                                     updates::Vector{<:eMCMC.MCMCUpdate}, data, θinit::Vector{T};
+                                     kwargs...) where T
+    D = length(θinit)
+    cfg = Ref(EmcmcConfig(ABI_VERSION, UInt32(D), UInt64(be.num_chains), UInt64(be.first_chain_id),
+                          UInt64(num_mcmc_steps), be.seed, Int32(be.device),
+                          be.history === :full ? UInt32(0) : UInt32(1), UInt32(100), UInt32(0),
+                          UInt32(0), UInt32(0), ntuple(_ -> UInt32(0), 6)))
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:emcmc_create, LIB), Cint, (Ref{Ptr{Cvoid}}, Ref{EmcmcConfig}), h, cfg), C_NULL, "emcmc_create")
+    keep = Any[]
+    GC.@preserve keep begin
+        for u in updates
+            desc = Ref(_update_desc(u, keep))
+            check(ccall((:emcmc_add_update, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcUpdateDesc}), h[], desc),
+                  h[], "emcmc_add_update")
+        end
+    end
+    P = data.P
+    d = length(P.θ) == 0 ? 0 : Int(round((sqrt(1 + 4length(P.θ)) - 1) / 2))  # θ = [μ; vec Σ]
+    μ = P.θ[1:d]
+    Σ = reshape(P.θ[(d+1):end], d, d)
+    X = reduce(vcat, permutedims.(data.obs))                     # n×d
+    Xrm = permutedims(X)                                           # row-major view for the ABI
+    GC.@preserve μ Σ Xrm begin
+        t = Ref(EmcmcTargetDesc(TARGET_GSN, UInt32(d), pointer(μ), pointer(Σ), UInt64(size(X, 1)),
+                                pointer(Xrm), be.ll_mode === :per_obs ? UInt32(0) : UInt32(1), UInt32(0)))
+        check(ccall((:emcmc_set_target, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcTargetDesc}), h[], t),
+              h[], "emcmc_set_target")
+    end
+    θ0 = repeat(Float64.(θinit), be.num_chains)                     # [C][D] row-major
+    check(ccall((:emcmc_set_state, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), h[], θ0, C_NULL),
+          h[], "emcmc_set_state")
+    ws = MI355XGlobalWorkspace{T}(h[], be, num_mcmc_steps, D, length(updates), 0)
+    finalizer(w -> ccall((:emcmc_destroy, LIB), Cvoid, (Ptr{Cvoid},), w.handle), ws)
+    ws
+end
+
+# workspaces.jl:280 — create_workspace(::MCMCBackend, mcmcupdate, global_ws, num_mcmc_steps);
+# the per-update state lives on the device, the local workspace only names it.
+function eMCMC.create_workspace(::MI355XBackend, updt, gws::MI355XGlobalWorkspace{T},
+                                num_mcmc_steps) where T
+    gws.num_locals += 1
+    MI355XLocalWorkspace{T}(gws, gws.num_locals)
+end
+
+# run.jl:64-83 — __run!(global_ws, local_wss, updates, schedule, callbacks).
+# run!() (run.jl:34) dispatches here through the workspace type: the schedule is
+# walked in Julia, cut at callback boundaries, and each slice runs on the GPU.
+function eMCMC.__run!(gws::MI355XGlobalWorkspace, local_wss, updates, schedule, callbacks)
+    h = gws.handle
+    steps = EmcmcStep[]
+    flush!() = begin
+        if !isempty(steps)
+            check(ccall((:emcmc_run, LIB), Cint, (Ptr{Cvoid}, Ptr{EmcmcStep}, UInt64), h, steps,
+                        length(steps)), h, "emcmc_run")
+            empty!(steps)
+        end
+        check(ccall((:emcmc_synchronize, LIB), Cint, (Ptr{Cvoid},), h), h, "emcmc_synchronize")
+    end
+    pre, post = eMCMC.PreMCMCStep(), eMCMC.PostMCMCStep()
+    wants(step, flag) = any(cb -> eMCMC.check_if_execute(cb, step, flag), callbacks)
+    for step in schedule
+        # callbacks observe device state only at the steps they ask for
+        # (callbacks.jl:33-45); everything between two such steps is one slice
+        if wants(step, pre)
+            flush!()
+            eMCMC.update_callbacks!(callbacks, gws, local_wss, step, pre)
+        end
+        push!(steps, EmcmcStep(UInt32(step.mcmciter), UInt32(step.pidx)))   # both 1-based across the ABI
+        if wants(step, post)
+            flush!()
+            eMCMC.update_callbacks!(callbacks, gws, local_wss, step, post)
+        end
+    end
+    flush!()
+    nothing
+end
+
+"""
+    state(gws::MI355XGlobalWorkspace) -> Matrix{Float64} (C × D)
+
+Current θ of every chain (`state(global_ws)` of the reference, per chain).
+"""
+function eMCMC.state(gws::MI355XGlobalWorkspace)
+    out = Matrix{Float64}(undef, gws.dim, gws.backend.num_chains)      # column-major = row-major [C][D]
+    check(ccall((:emcmc_get_state, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), gws.handle, out, C_NULL),
+          gws.handle, "emcmc_get_state")
+    permutedims(out)
+end
+
+"""
+    state_history(gws, iter_first, n) -> Array{Float64,4} (D, C, P, n)
+
+`state_history[iter][pidx]` of every chain for iterations iter_first:iter_first+n-1.
+"""
+function state_history(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integer)
+    out = Array{Float64}(undef, gws.dim, gws.backend.num_chains, gws.num_updates, n)
+    check(ccall((:emcmc_get_history, LIB), Cint,
+                (Ptr{Cvoid}, UInt32, UInt64, UInt64, Ptr{Cvoid}, Csize_t),
+                gws.handle, H_STATE, iter_first, n, out, sizeof(out)), gws.handle, "emcmc_get_history")
+    out
+end
+
+export MI355XBackend, state_history
+
+end # module

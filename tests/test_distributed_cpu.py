@@ -1,0 +1,91 @@
+"""Multi-process chain sharding on CPU (torch.distributed gloo, world_size 2).
+
+The N>1 path of bench.py/extensible_mcmc shards chains by global id with no
+data-path collective and all-reduces the cross-chain diagnostics once.  Here
+each rank advances its shard with the oracle (the GPU engine is exercised by
+the gpu tests), reduces its shard's split-chain moments and all-reduces them
+through extensible_mcmc.diagnostics.allreduce_sums; the result must equal the
+single-process reduction, and per-chain states must equal the unsharded run
+(RNG keyed by global chain id)."""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def shard_moments(hist_theta, split=True):
+    """Per-(half-)chain mean/var over the window, summed over chains — the
+    host restatement of chain_moments_kernel + moments_reduce_kernel."""
+    S, C, D = hist_theta.shape
+    halves = 2 if split else 1
+    ln = S // halves
+    parts = [hist_theta[h * ln:(h + 1) * ln] for h in range(halves)]
+    means = np.concatenate([p.mean(axis=0) for p in parts])  # [halves*C][D]
+    vars_ = np.concatenate([p.var(axis=0, ddof=1) for p in parts])
+    return {"sum_mean": means.sum(0), "sum_mean_sq": (means * means).sum(0), "sum_var": vars_.sum(0),
+            "num_chains": C * halves, "num_draws": ln, "accepted": 0, "proposed": 0}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir):
+    sys.path[:0] = [str(ROOT), str(ROOT / "extensiblemcmc.jl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from extensible_mcmc import diagnostics as DG
+    from extensible_mcmc import workloads as W
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = W.cfg5(256, D=8)
+    per = 256 // world
+    lo = rank * per
+    st = O.OracleState(w.theta_init[lo:lo + per])
+    h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=120,
+                  chain0=lo)
+    m = shard_moments(h["theta"][20:])
+    m["accepted"] = int(h["acc"][20:].sum())
+    m["proposed"] = int(h["acc"][20:].size)
+    tot = DG.allreduce_sums(m, w.D)
+    np.save(os.path.join(out_dir, f"theta_{rank}.npy"), st.theta)
+    if rank == 0:
+        np.save(os.path.join(out_dir, "reduced.npy"), DG.pack(tot))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_sharding_and_diagnostics(tmp_path, oracle):
+    import torch.multiprocessing as mp
+
+    from extensible_mcmc import diagnostics as DG
+    from extensible_mcmc import workloads as W
+
+    mp.spawn(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    w = W.cfg5(256, D=8)
+    st = oracle.OracleState(w.theta_init[:256])
+    h = oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=120)
+    # per-chain results do not depend on the sharding
+    sharded = np.concatenate([np.load(tmp_path / "theta_0.npy"), np.load(tmp_path / "theta_1.npy")])
+    assert np.array_equal(sharded, st.theta)
+    # the all-reduced diagnostics equal the single-process reduction
+    ref = shard_moments(h["theta"][20:])
+    ref["accepted"], ref["proposed"] = int(h["acc"][20:].sum()), int(h["acc"][20:].size)
+    got = DG.unpack(np.load(tmp_path / "reduced.npy"), w.D, ref["num_draws"])
+    for k in ("sum_mean", "sum_mean_sq", "sum_var"):
+        np.testing.assert_allclose(got[k], ref[k], rtol=1e-12)
+    assert got["num_chains"] == ref["num_chains"] and got["accepted"] == ref["accepted"]
+    r_got, r_ref = DG.rhat_from_sums(got), DG.rhat_from_sums(ref)
+    np.testing.assert_allclose(r_got["rhat"], r_ref["rhat"], rtol=1e-10)
+    assert r_got["accept_rate"] == r_ref["accept_rate"]

@@ -196,6 +196,11 @@ KernelFn dense_fn() {
         {{D, LPC, 1, 1, 0, U, 4}, diag_fn<D, LPC, true, 1, U, 4>()},                                 \
         {{D, LPC, 0, 0, 0, U, 4}, diag_fn<D, LPC, false, 0, U, 4>()},                                \
         {{D, LPC, 0, 1, 0, U, 4}, diag_fn<D, LPC, false, 1, U, 4>()}
+#define DIAGO3(D, LPC, U)                                                                         \
+    {{D, LPC, 1, 0, 0, U, 3}, diag_fn<D, LPC, true, 0, U, 3>()},                                     \
+        {{D, LPC, 1, 1, 0, U, 3}, diag_fn<D, LPC, true, 1, U, 3>()},                                 \
+        {{D, LPC, 0, 0, 0, U, 3}, diag_fn<D, LPC, false, 0, U, 3>()},                                \
+        {{D, LPC, 0, 1, 0, U, 3}, diag_fn<D, LPC, false, 1, U, 3>()}
 #define DENSE4(D)                                                                                    \
     {{D, 1, 1, 0, 1, 0, 0}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1, 0, 0}, dense_fn<D, true, 1>()},   \
         {{D, 1, 0, 0, 1, 0, 0}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1, 0, 0}, dense_fn<D, false, 1>()}
@@ -210,6 +215,7 @@ const std::vector<Entry> &kernel_table() {
         DIAG4(1, 1),  DIAG4(2, 1),  DIAG4(3, 1),  DIAG4(4, 1),  DIAG4(8, 1),
         DIAG4(16, 1), DIAG4(16, 2), DIAG4(32, 1), DIAG4(32, 2), DIAG4(32, 4),
         DIAG4(64, 2), DIAG4(64, 4), DIAGO(32, 4, true), DIAGO(32, 4, false), DIAGO(32, 2, true),
+        DIAGO3(32, 2, true), DIAGO3(32, 4, true), DIAGO3(32, 1, true),
         DENSE4(1),    DENSE4(2),    DENSE4(3),
         DENSE4(4),    DENSE4(8),
     };
@@ -224,8 +230,10 @@ KernelFn lookup(int D, int lpc, bool full, int ll, bool dense, bool unit, int oc
     return nullptr;
 }
 
+// lanes per chain: 16 coordinates per lane where D allows (measured best at
+// D=32: fewer duplicated per-chain scalar ops than LPC=4, 2 waves/SIMD)
 int auto_lpc(int D) {
-    if (D % 32 == 0) return 4;
+    if (D % 16 == 0 && D >= 32) return D / 16 <= 4 ? D / 16 : 4;
     if (D % 16 == 0) return 2;
     return 1;
 }
@@ -272,7 +280,9 @@ emcmc_status select_variant(emcmc_handle *h) {
         bool unit = true;
         for (int i = 0; i < D; ++i) unit = unit && h->target.invdiag[i] == 1.0;
         v.unit = unit;
-        const int occ = (h->cfg.kernel_variant & EMCMC_VARIANT_HIGH_OCCUPANCY) ? 4 : 0;
+        const int occ = (h->cfg.kernel_variant & EMCMC_VARIANT_HIGH_OCCUPANCY) ? 4
+                        : (h->cfg.kernel_variant & EMCMC_VARIANT_OCCUPANCY3)   ? 3
+                                                                               : 0;
         v.fn = lookup(D, lpc, full, ll, false, unit, occ);
         v.occ = occ;
         if (!v.fn && occ) {
@@ -298,7 +308,7 @@ emcmc_status select_variant(emcmc_handle *h) {
     char nm[160];
     snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>", v.dense ? "dense" : "diag", D, v.lpc,
              full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
-             v.occ ? ",MINW=4" : "");
+             v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : "");
     v.name = nm;
     // constants for this variant
     std::vector<double> c;
@@ -321,7 +331,8 @@ emcmc_status select_variant(emcmc_handle *h) {
         std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     }
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    const size_t lds = sizeof(Ziggurat) + (c.size() + obs_doubles) * sizeof(double);
+    size_t lds = sizeof(Ziggurat) + (c.size() + obs_doubles) * sizeof(double);
+    if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc);
     if (lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu",
@@ -396,6 +407,9 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
     if (cfg->num_mcmc_steps >= (1ull << 32)) return EMCMC_INVALID_ARG;
     if (cfg->history_mode > EMCMC_HIST_ACCEPT_ONLY) return EMCMC_INVALID_ARG;
     if (cfg->roll_window > 128) return EMCMC_INVALID_ARG;
+    // history stores address a slot with a 32-bit byte offset (SlotOffsets)
+    if (cfg->history_mode == EMCMC_HIST_FULL && cfg->num_chains * cfg->dim * sizeof(double) > 0xFFFFFFFFull)
+        return EMCMC_INVALID_ARG;
     if (cfg->lanes_per_chain != 0 && cfg->lanes_per_chain != 1 && cfg->lanes_per_chain != 2 &&
         cfg->lanes_per_chain != 4)
         return EMCMC_INVALID_ARG;
@@ -566,6 +580,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     p.n_tc0 = (double)t.nobs * t.c0;
     p.S_c = t.S_c;
     p.nobs_d = (double)t.nobs;
+    p.rcp_W = 1.0 / (double)h->cfg.roll_window;
     const uint64_t K = h->cfg.steps_per_launch;
     uint64_t i = 0;
     while (i < num_steps) {

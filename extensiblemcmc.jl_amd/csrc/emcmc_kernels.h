@@ -68,6 +68,7 @@ struct StepParams {
     double n_tc0;         // nobs · t_c0     (SUFFSTAT)
     double S_c;           // Σ_k ‖L_t⁻¹(x_k − x̄)‖²  (SUFFSTAT)
     double nobs_d;        // (double) nobs
+    double rcp_W;         // RN(1/W) for the rolling-acceptance quotient
 };
 
 // constants layout (offsets in doubles), D = dimension
@@ -114,37 +115,197 @@ constexpr bool kSerialPairs = EMCMC_SERIAL_PAIRS != 0;
 // N normals of (chain, iter, pidx0) with lane-local index i ↔ global normal
 // index g0 + i, written as out[i] = base[i] + scale[i]·z (the diagonal
 // proposal θ° = θ + L z, random_walk.jl:147).  Fast pass over all pairs, then
-// a wave-uniform loop resolves the ≈1% wedge/tail draws one per lane per trip.
+// a wave-uniform loop resolves the ≈1% wedge/tail draws one per lane per trip
+// (with 64 lanes × N draws per wave most steps take one trip, so the trip only
+// fixes z[i]; the proposal arithmetic runs once, after it).
 template <int N>
 __device__ __forceinline__ void propose_diag(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
                                              uint32_t iter, uint32_t pidx0, uint32_t g0, const double (&base)[N],
                                              const double *scale, double (&out)[N], uint32_t &faults) {
     constexpr int NP = (N + 1) / 2;
-    uint64_t pend = 0;
+    uint32_t pend = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         if constexpr (kSerialPairs) __builtin_amdgcn_sched_barrier(0);
         const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
-        double z0, z1;
-        const bool ok0 = zig_normal_fast(zig_split(r.x, r.y), zt.n, z0);
-        out[2 * j] = base[2 * j] + scale[2 * j] * z0;
-        if (!ok0) pend |= 1ull << (2 * j);
-        if (2 * j + 1 < N) {
-            const bool ok1 = zig_normal_fast(zig_split(r.z, r.w), zt.n, z1);
-            out[2 * j + 1] = base[2 * j + 1] + scale[2 * j + 1] * z1;
-            if (!ok1) pend |= 1ull << (2 * j + 1);
-        }
+        if (!zig_normal_fast(zig_split(r.x, r.y), zt.n, out[2 * j])) pend |= 1u << (2 * j);
+        if (2 * j + 1 < N)
+            if (!zig_normal_fast(zig_split(r.z, r.w), zt.n, out[2 * j + 1])) pend |= 1u << (2 * j + 1);
     }
+    if constexpr ((EMCMC_ABLATE & 2) != 0) pend = 0;  // timing-only build: no rare paths
     while (__ballot(pend != 0) != 0) {
         if (pend != 0) {
-            const int i = __builtin_ctzll(pend);
+            const int i = __builtin_ctz(pend);
             pend &= pend - 1;
             const double z = normal_draw(zt, key0, key1, chain, iter, pidx0, g0 + (uint32_t)i, faults);
 #pragma unroll
             for (int q = 0; q < N; ++q)
-                if (q == i) out[q] = base[q] + scale[q] * z;
+                if (q == i) out[q] = z;
         }
     }
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = base[i] + scale[i] * out[i];
+}
+
+// ---------------------------------------------------------------------------
+// Wave-batched rare paths (diag kernels).  Per wave the LDS holds
+//   zs[64][N]  this step's normals, lane-major (N = coordinates per lane)
+//   q[64]      rare-path work queue: (owner lane << 8) | lane-local index
+//   fl[64]     fault bits raised by resolvers on behalf of each owner lane
+// Every lane writes its fast-path normals to zs; a draw that fails the fast
+// test is queued; then the wave's active lanes resolve up to 64 queued draws
+// at once (one rare-path pass per wave-step, however the failures spread over
+// lanes) and write the values into the owner's zs slots; each lane reads its
+// N normals back.  No lane-dynamic register indexing, no per-lane retry loop.
+#ifndef EMCMC_BATCH_MODE
+#define EMCMC_BATCH_MODE 2  // 1: all normals round-trip through LDS; 2: compact results + selects
+#endif
+template <int N>
+struct WaveScratch {
+    static constexpr int kZs = (EMCMC_BATCH_MODE == 1) ? 64 * N * 8 : 64 * 8;
+    static constexpr int kBytes = kZs + 64 * 4 + 64 * 4;
+    double *zs;  // mode 1: [64][N] normals; mode 2: [64] resolved values by queue position
+    uint32_t *q;
+    uint32_t *fl;
+    __device__ __forceinline__ explicit WaveScratch(char *base) {
+        zs = reinterpret_cast<double *>(base);
+        q = reinterpret_cast<uint32_t *>(base + kZs);
+        fl = q + 64;
+    }
+};
+
+// LDS bytes of the per-wave scratch of a diag kernel (4 waves per block); the
+// scratch starts 16-byte aligned after the tables, constants and observations.
+// (batched only for ≤ 16 coordinates per lane: 4 waves × 64 lanes × 16 × 8 B
+// = 32 KiB of normals per block keeps the block within 64 KiB of LDS)
+#ifndef EMCMC_BATCHED
+#define EMCMC_BATCHED 1
+#endif
+constexpr bool diag_batched(int D, int LPC) { return EMCMC_BATCHED && (D / LPC) % 2 == 0 && D / LPC <= 16; }
+constexpr size_t diag_scratch_bytes(int D, int LPC) {
+    return diag_batched(D, LPC) ? 4 * (size_t)(((EMCMC_BATCH_MODE == 1) ? 64 * (D / LPC) * 8 : 64 * 8) + 64 * 4 + 64 * 4)
+                                : 0;
+}
+__host__ __device__ constexpr size_t lds_align16(size_t b) { return (b + 15) & ~(size_t)15; }
+
+__device__ __forceinline__ void wave_lds_sync() {
+    // LDS ops of one wave execute in order; this only stops the compiler from
+    // moving LDS accesses across the phase boundary
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// θ° = base + scale·z for the lane's N coordinates (lane-local index i ↔
+// normal g0 + i of chain `chain`); LPC lanes per chain, so lane L of the wave
+// owns chain gid0 + L/LPC and normals (L % LPC)·N + i.
+template <int N, int LPC>
+__device__ __forceinline__ void propose_diag_batched(const Ziggurat &zt, const WaveScratch<N> &ws, uint32_t key0,
+                                                     uint32_t key1, uint32_t chain, uint32_t wave_gid0,
+                                                     uint32_t iter, uint32_t pidx0, uint32_t g0,
+                                                     const double (&base)[N], const double *scale,
+                                                     double (&out)[N]) {
+    static_assert(N % 2 == 0, "pairs");
+    const uint32_t lane = __lane_id();
+    uint32_t pend = 0;
+    // software-pipelined fast pass: pair j's Philox block and table reads are
+    // issued before pair j−1 is consumed, so the LDS latency of the lookups
+    // hides behind the next block's integer work
+    ZigDraw pa, pb;
+    ZigEntry ta, tb;
+#pragma unroll
+    for (int j = 0; j <= N / 2; ++j) {
+        ZigDraw na, nb;
+        ZigEntry sa, sb;
+        if (j < N / 2) {
+            __builtin_amdgcn_sched_barrier(0);
+            const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
+            na = zig_split(r.x, r.y);
+            nb = zig_split(r.z, r.w);
+            sa = zig_entry(zt.n, na);
+            sb = zig_entry(zt.n, nb);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        if (j > 0) {
+            const int k = j - 1;
+            out[2 * k] = zig_scale(pa.v, with_sign(ta.w, pa.sbit));
+            out[2 * k + 1] = zig_scale(pb.v, with_sign(tb.w, pb.sbit));
+            if (!(pa.v < ta.kv)) pend |= 1u << (2 * k);
+            if (!(pb.v < tb.kv)) pend |= 1u << (2 * k + 1);
+            if constexpr (EMCMC_BATCH_MODE == 1)
+                reinterpret_cast<d2v *>(ws.zs + lane * N)[k] = d2v{out[2 * k], out[2 * k + 1]};
+        }
+        if (j < N / 2) {
+            pa = na;
+            pb = nb;
+            ta = sa;
+            tb = sb;
+        }
+    }
+    if constexpr ((EMCMC_ABLATE & 2) != 0) pend = 0;  // timing-only build: no rare paths
+    if (__ballot(pend != 0) != 0) {
+        const uint32_t rank = lane_rank(__ballot(true));  // resolver slot among active lanes
+        uint32_t rem = pend;
+        while (__ballot(rem != 0) != 0) {
+            const uint32_t rem0 = rem;
+            uint32_t qn = 0;  // wave-uniform queue fill
+            for (;;) {
+                const uint64_t m = __ballot(rem != 0);
+                if (m == 0 || qn >= 64) break;
+                const uint32_t pos = qn + lane_rank(m);
+                if (rem != 0 && pos < 64) {
+                    ws.q[pos] = (lane << 8) | (uint32_t)__builtin_ctz(rem);
+                    rem &= rem - 1;
+                }
+                const uint32_t c = (uint32_t)__popcll(m);
+                qn = (qn + c > 64) ? 64 : qn + c;
+            }
+            wave_lds_sync();
+            if (rank < qn) {
+                const uint32_t e = ws.q[rank];
+                const uint32_t ol = e >> 8, i = e & 0xFFu;
+                uint32_t f = 0;
+                const double z = normal_draw(zt, key0, key1, wave_gid0 + ol / LPC, iter, pidx0,
+                                             (ol % LPC) * N + i, f);
+                if constexpr (EMCMC_BATCH_MODE == 1) ws.zs[ol * N + i] = z;
+                else ws.zs[rank] = z;
+                if (f) atomicOr(ws.fl + ol, f);
+            }
+            wave_lds_sync();
+            if constexpr (EMCMC_BATCH_MODE == 2) {
+                // replay the queue order to find this lane's results
+                uint32_t rr = rem0, qb = 0;
+                for (;;) {
+                    const uint64_t m = __ballot(rr != 0);
+                    if (m == 0 || qb >= 64) break;
+                    const uint32_t pos = qb + lane_rank(m);
+                    const bool take = rr != 0 && pos < 64;
+                    const uint32_t i = take ? (uint32_t)__builtin_ctz(rr) : 0xFFu;
+                    const double z = ws.zs[take ? pos : 0];
+#pragma unroll
+                    for (int qq = 0; qq < N; ++qq) out[qq] = (i == (uint32_t)qq) ? z : out[qq];
+                    if (take) rr &= rr - 1;
+                    const uint32_t c = (uint32_t)__popcll(m);
+                    qb = (qb + c > 64) ? 64 : qb + c;
+                }
+                wave_lds_sync();
+            }
+        }
+    }
+    if constexpr (EMCMC_BATCH_MODE == 1) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            const d2v z = reinterpret_cast<const d2v *>(ws.zs + lane * N)[j];
+            out[2 * j] = z.x;
+            out[2 * j + 1] = z.y;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = base[i] + scale[i] * out[i];
 }
 
 // The N standard normals themselves (dense-L proposals).
@@ -172,16 +333,20 @@ __device__ __forceinline__ void normals(const Ziggurat &zt, uint32_t key0, uint3
     }
 }
 
-// Exp(1) draw of the accept test (run.jl:278).
-__device__ __forceinline__ double accept_exp(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
-                                             uint32_t iter, uint32_t pidx0, uint32_t &faults) {
-    const u32x4 r = draw(key0, key1, chain, iter, kBlockAccept, pidx0, 0);
-    const ZigDraw d = zig_split(r.x, r.y);
-    double e;
-    if (!zig_exp_fast(d, zt.e, e))
-        e = zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
-    return e;
-}
+// Exp(1) draws of the accept test (run.jl:278) for consecutive iterations: one
+// Philox block serves iterations 2m and 2m+1 (kBlockAccept), so a launch pays
+// half a block per step.  `first` forces the block at the launch's first step.
+struct AcceptStream {
+    u32x4 r;
+    __device__ __forceinline__ double next(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+                                           uint32_t iter, uint32_t pidx0, bool first, uint32_t &faults) {
+        if (first || (iter & 1u) == 0) r = draw(key0, key1, chain, iter >> 1, kBlockAccept, pidx0, 0);
+        const ZigDraw d = accept_split(r, iter);
+        double e;
+        if (!zig_exp_fast(d, zt.e, e) && (EMCMC_ABLATE & 2) == 0) e = zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
+        return e;
+    }
+};
 
 // ---------------------------------------------------------------------------
 // cross-lane helpers (DPP quad permutes; 64-bit values move as two dwords)
@@ -222,23 +387,39 @@ __device__ __forceinline__ double tree_inplace(double (&b)[N]) {
     return b[0];
 }
 
-// Σ y_i² over the chain's D coordinates in the canonical order: blocks of BLK
-// accumulated s = y0·y0, s = fma(y_i, y_i, s); blocks combine pairwise, first
-// inside the lane, then across the chain's LPC lanes.
-template <int D, int LPC, int NV>
-__device__ __forceinline__ double canon_sumsq(const double (&y)[NV]) {
+#ifndef EMCMC_SUMSQ_BARRIER
+#define EMCMC_SUMSQ_BARRIER 1
+#endif
+// Σ y_i² in the canonical order with y_i = yf(i) produced on the fly, one
+// block at a time (sched barriers keep the scheduler from materialising all
+// NV values — e.g. a whole observation row — at once).
+template <int D, int LPC, int NV, typename YF>
+__device__ __forceinline__ double canon_sumsq_f(YF yf) {
     constexpr int BLK = SumShape<D>::BLK;
     constexpr int BPL = NV / BLK;
     double b[BPL];
 #pragma unroll
     for (int k = 0; k < BPL; ++k) {
-        double s = y[k * BLK] * y[k * BLK];
+        if constexpr (BPL > 1 && EMCMC_SUMSQ_BARRIER) __builtin_amdgcn_sched_barrier(0);
+        const double y0 = yf(k * BLK);
+        double s = y0 * y0;
 #pragma unroll
-        for (int i = 1; i < BLK; ++i) s = fma(y[k * BLK + i], y[k * BLK + i], s);
+        for (int i = 1; i < BLK; ++i) {
+            const double yi = yf(k * BLK + i);
+            s = fma(yi, yi, s);
+        }
         b[k] = s;
     }
     double s = tree_inplace<BPL>(b);
     return lane_tree<LPC>(s);
+}
+
+// Σ y_i² over the chain's D coordinates in the canonical order: blocks of BLK
+// accumulated s = y0·y0, s = fma(y_i, y_i, s); blocks combine pairwise, first
+// inside the lane, then across the chain's LPC lanes.
+template <int D, int LPC, int NV>
+__device__ __forceinline__ double canon_sumsq(const double (&y)[NV]) {
+    return canon_sumsq_f<D, LPC, NV>([&](int i) { return y[i]; });
 }
 
 // compact one accept bit per chain out of a 64-lane ballot (LPC lanes/chain)
@@ -273,17 +454,28 @@ __device__ __forceinline__ void store_acc_bits(uint8_t *row, uint64_t chain_firs
     else *reinterpret_cast<uint16_t *>(p) = (uint16_t)bits;
 }
 
-// rolling acceptance, chain_statistics.jl:53-65 (N = cs.N before increment)
+// x / b for b = W with q = RN(x·y), y = RN(1/b): Markstein's correction
+// q + (x − b·q)·y rounds to the IEEE quotient (tests/test_oracle.py checks it)
+__device__ __forceinline__ double div_markstein(double x, double b, double y) {
+    const double q = x * y;
+    const double r = fma(-q, b, x);
+    return fma(r, y, q);
+}
+
+// rolling acceptance, chain_statistics.jl:53-65 (N = cs.N before increment;
+// N is the same for every chain, so the divisor branch is wave-uniform)
 __device__ __forceinline__ double rolling_update(double ra, uint64_t &r0, uint64_t &r1, uint32_t iter,
-                                                 uint32_t W, uint64_t N, bool acc) {
+                                                 uint32_t W, uint64_t N, double rcpW, bool acc) {
     int out = 0;
     if (iter > W) {
         const uint32_t j = (iter - W) & 127u;
         const uint64_t w = (j & 64u) ? r1 : r0;
         out = (int)((w >> (j & 63u)) & 1ull);
     }
-    const uint64_t mn = (N < (uint64_t)W) ? N : (uint64_t)W;
-    const double nra = (ra * (double)W + (double)((int)acc - out)) / (double)mn;
+    const double num = ra * (double)W + (double)((int)acc - out);
+    double nra;
+    if (N >= (uint64_t)W) nra = div_markstein(num, (double)W, rcpW);
+    else nra = num / (double)N;
     const uint32_t jw = iter & 127u;
     const uint64_t bit = 1ull << (jw & 63u);
     if (jw & 64u) r1 = acc ? (r1 | bit) : (r1 & ~bit);
@@ -335,6 +527,73 @@ __device__ __forceinline__ void load_state(const double *base, uint64_t C, uint6
     }
 }
 
+// A history slot is written as (wave-uniform slot base + j·stride) + one
+// per-lane 32-bit byte offset: the base and the per-word stride live in
+// SGPRs, so a store needs no per-step VALU address math (global_store with
+// saddr).  The host guarantees a slot is < 4 GiB (EMCMC_INVALID_ARG otherwise).
+template <int D>
+struct SlotOffset {
+    uint32_t o;       // lane's first word: pair d0/2 (even D) or coordinate d0 (odd D) of chain c
+    uint64_t stride;  // bytes between consecutive words of one chain (uniform)
+    __device__ __forceinline__ SlotOffset(uint64_t C, uint64_t c, int d0) {
+        if constexpr (D % 2 == 0) {
+            o = (uint32_t)((((uint64_t)(d0 / 2)) * C + c) * 16u);
+            stride = C * 16u;
+        } else {
+            o = (uint32_t)((((uint64_t)d0) * C + c) * 8u);
+            stride = C * 8u;
+        }
+    }
+};
+template <int D, int N>
+__device__ __forceinline__ void store_slot(double *slot_base, const SlotOffset<D> &off, const double (&v)[N]) {
+    char *b = reinterpret_cast<char *>(slot_base);
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            d2v x = {v[2 * j], v[2 * j + 1]};
+            __builtin_nontemporal_store(x, reinterpret_cast<d2v *>(b + (uint64_t)j * off.stride + off.o));
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i)
+            __builtin_nontemporal_store(v[i], reinterpret_cast<double *>(b + (uint64_t)i * off.stride + off.o));
+    }
+}
+
+template <int D, int N>
+__device__ __forceinline__ void load_slot(const double *slot_base, const SlotOffset<D> &off, double (&v)[N]) {
+    const char *b = reinterpret_cast<const char *>(slot_base);
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            const d2v x = *reinterpret_cast<const d2v *>(b + (uint64_t)j * off.stride + off.o);
+            v[2 * j] = x.x;
+            v[2 * j + 1] = x.y;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) v[i] = *reinterpret_cast<const double *>(b + (uint64_t)i * off.stride + off.o);
+    }
+}
+template <int D, int N>
+__device__ __forceinline__ void store_slot_cached(double *slot_base, const SlotOffset<D> &off, const double (&v)[N]) {
+    char *b = reinterpret_cast<char *>(slot_base);
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j)
+            *reinterpret_cast<d2v *>(b + (uint64_t)j * off.stride + off.o) = d2v{v[2 * j], v[2 * j + 1]};
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) *reinterpret_cast<double *>(b + (uint64_t)i * off.stride + off.o) = v[i];
+    }
+}
+// element `c` of a per-chain array through a 32-bit byte offset (saddr form)
+template <typename T>
+__device__ __forceinline__ T &chain_elem(T *base, uint32_t c) {
+    return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + c * (uint32_t)sizeof(T));
+}
+
 // MINW = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
 template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1>
@@ -349,12 +608,7 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
     const int nconst = 4 * D;
     stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
     const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
-    const double *cst = lds + kZigLdsDoubles;
-    const double *Lrw = cst;
-    const double *iLrw = cst + D;
-    const double *iLt = cst + 2 * D;
-    const double *xbar = cst + 3 * D;
-    const double *X = cst + 4 * D;
+    const double *cst0 = lds + kZigLdsDoubles;
 
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t chain = tid / LPC;
@@ -364,68 +618,116 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
     const uint32_t gid = a.chain0 + (uint32_t)chain;
 
     const uint64_t C = a.C;
+    const SlotOffset<D> soff(C, chain, d0);
+    const uint32_t c32 = (uint32_t)chain;  // C < 2^32 (emcmc_create)
     double th[DPL];
-    load_state<D>(a.theta, C, chain, d0, th);
-    double ll = a.ll[chain];
-    double ra = a.ra[chain];
-    uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
-    uint32_t nacc = a.nacc[chain];
-    uint32_t faults = a.faults[chain];
+    load_slot<D>(a.theta, soff, th);
+    double ll = chain_elem(a.ll, c32);
+    double ra = chain_elem(a.ra, c32);
+    uint64_t r0 = chain_elem(a.ring, 2 * c32), r1 = chain_elem(a.ring, 2 * c32 + 1);
+    uint32_t nacc = chain_elem(a.nacc, c32);
+    uint32_t faults = chain_elem(a.faults, c32);
+    constexpr bool kBatched = diag_batched(D, LPC);
+    const size_t used = lds_align16(sizeof(Ziggurat) + sizeof(double) * (size_t)(nconst + ((LLMODE == LL_PER_OBS) ? (int)nobs * D : 0)));
+    const WaveScratch<DPL> ws(reinterpret_cast<char *>(lds) + used +
+                              (threadIdx.x >> 6) * (size_t)WaveScratch<DPL>::kBytes);
+    const uint32_t wave_gid0 = a.chain0 + (uint32_t)((tid & ~(uint64_t)63) / LPC);
+    if constexpr (kBatched) ws.fl[__lane_id()] = 0;
+    AcceptStream accs;
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
+        const double *cst = cst0;
+        const double *Lrw = cst;
+        const double *iLrw = cst + D;
+        const double *iLt = cst + 2 * D;
+        const double *xbar = cst + 3 * D;
+        const double *X = cst + 4 * D;
         // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151)
         double thp[DPL];
-        propose_diag<DPL>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults);
+        if constexpr (kBatched)
+            propose_diag_batched<DPL, LPC>(zt, ws, a.key0, a.key1, gid, wave_gid0, iter, a.pidx0, (uint32_t)d0, th,
+                                           Lrw + d0, thp);
+        else
+            propose_diag<DPL>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults);
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
-        double ltd;
-        {
-            double y[DPL];
-#pragma unroll
-            for (int i = 0; i < DPL; ++i) y[i] = (thp[i] - th[i]) * iLrw[d0 + i];
-            ltd = a.rw_c0 - canon_sumsq<D, LPC>(y) / 2.0;
-        }
+        const double ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
+                               a.rw_c0);  // = c0 − q/2 (q/2 exact)
         // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
         double llp;
         if constexpr (LLMODE == LL_PER_OBS) {
             llp = 0.0;
+            // observation rows are read one canonical block ahead of use
+          constexpr int BLK = SumShape<D>::BLK, BPL = DPL / BLK;
+          if constexpr (BLK % 2 == 0) {
+            d2v cur[BLK / 2];
+            const d2v *xrow = reinterpret_cast<const d2v *>(X + d0);
+#pragma unroll
+            for (int i = 0; i < BLK / 2; ++i) cur[i] = xrow[i];
+            for (uint32_t k = 0; k < nobs; ++k) {
+                double b[BPL];
+#pragma unroll
+                for (int blk = 0; blk < BPL; ++blk) {
+                    // next block: same row's next block, else the next row's first
+                    // (past the last row: row 0 again, a harmless read)
+                    const uint32_t nk = (blk + 1 < BPL) ? k : ((k + 1 < nobs) ? k + 1 : 0u);
+                    const int nb = (blk + 1 < BPL) ? blk + 1 : 0;
+                    const d2v *xn = reinterpret_cast<const d2v *>(X + (size_t)nk * D + d0 + nb * BLK);
+                    d2v nxt[BLK / 2];
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int i = 0; i < BLK / 2; ++i) nxt[i] = xn[i];
+                    __builtin_amdgcn_sched_barrier(0);
+                    const int c0 = blk * BLK;
+                    auto y = [&](int i) {
+                        const double xv = (i & 1) ? cur[i >> 1].y : cur[i >> 1].x;
+                        const double yv = xv - thp[c0 + i];
+                        return UNIT_T ? yv : yv * iLt[d0 + c0 + i];
+                    };
+                    double acc = y(0) * y(0);
+#pragma unroll
+                    for (int i = 1; i < BLK; ++i) acc = fma(y(i), y(i), acc);
+                    b[blk] = acc;
+#pragma unroll
+                    for (int i = 0; i < BLK / 2; ++i) cur[i] = nxt[i];
+                }
+                const double q = lane_tree<LPC>(tree_inplace<BPL>(b));
+                llp = llp + fma(-0.5, q, a.t_c0);
+            }
+          } else {
             for (uint32_t k = 0; k < nobs; ++k) {
                 const double *xk = X + (size_t)k * D + d0;
-                double y[DPL];
-#pragma unroll
-                for (int i = 0; i < DPL; ++i) {
-                    y[i] = xk[i] - thp[i];
-                    if constexpr (!UNIT_T) y[i] = y[i] * iLt[d0 + i];
-                }
-                llp = llp + (a.t_c0 - canon_sumsq<D, LPC>(y) / 2.0);
+                const double q = canon_sumsq_f<D, LPC, DPL>([&](int i) {
+                    const double y = xk[i] - thp[i];
+                    return UNIT_T ? y : y * iLt[d0 + i];
+                });
+                llp = llp + fma(-0.5, q, a.t_c0);
             }
+          }
         } else {
-            double y[DPL];
-#pragma unroll
-            for (int i = 0; i < DPL; ++i) {
-                y[i] = xbar[d0 + i] - thp[i];
-                if constexpr (!UNIT_T) y[i] = y[i] * iLt[d0 + i];
-            }
-            const double qv = canon_sumsq<D, LPC>(y);
+            const double qv = canon_sumsq_f<D, LPC, DPL>([&](int i) {
+                const double y = xbar[d0 + i] - thp[i];
+                return UNIT_T ? y : y * iLt[d0 + i];
+            });
             llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
         }
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
         // ---- accept_reject! (run.jl:271-278), left-associative as written
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
-        const double E = accept_exp(zt, a.key0, a.key1, gid, iter, a.pidx0, faults);
+        const double E = accs.next(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults);
         const bool acc = E > -llr;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
-        if constexpr (FULL) store_state<D>(a.hist_prop + slot * D * C, C, chain, d0, thp, true);
+        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)
 #pragma unroll
         for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {
-            store_state<D>(a.hist_theta + slot * D * C, C, chain, d0, th, true);
-            if (sub == 0) __builtin_nontemporal_store(ll, a.hist_ll + slot * a.C + chain);
+            store_slot<D>(a.hist_theta + slot * D * C, soff, th);
+            if (sub == 0) __builtin_nontemporal_store(ll, &chain_elem(a.hist_ll + slot * a.C, c32));
         }
         {
             const uint64_t m = compact_ballot<LPC>(__ballot(acc));
@@ -433,18 +735,25 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
                 store_acc_bits<LPC>(a.hist_acc + slot * a.row_bytes, chain, m);
         }
         // ---- update_stats! rolling acceptance (chain_statistics.jl:53-65)
-        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, acc);
+        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
     }
 
-    if (sub == 0) {
-        a.ll[chain] = ll;
-        a.ra[chain] = ra;
-        a.ring[2 * chain] = r0;
-        a.ring[2 * chain + 1] = r1;
-        a.nacc[chain] = nacc;
-        a.faults[chain] = faults;
+    if constexpr (kBatched) {
+        wave_lds_sync();
+        faults |= ws.fl[__lane_id()];
+        // the chain's lanes may hold different resolver fault bits
+        if constexpr (LPC >= 2) faults |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)faults, 0xB1, 0xF, 0xF, false);
+        if constexpr (LPC >= 4) faults |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)faults, 0x4E, 0xF, 0xF, false);
     }
-    store_state<D>(a.theta, C, chain, d0, th, false);
+    if (sub == 0) {
+        chain_elem(a.ll, c32) = ll;
+        chain_elem(a.ra, c32) = ra;
+        chain_elem(a.ring, 2 * c32) = r0;
+        chain_elem(a.ring, 2 * c32 + 1) = r1;
+        chain_elem(a.nacc, c32) = nacc;
+        chain_elem(a.faults, c32) = faults;
+    }
+    store_slot_cached<D>(a.theta, soff, th);
 }
 
 // ---------------------------------------------------------------------------
@@ -478,6 +787,8 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
     uint32_t nacc = a.nacc[chain];
     uint32_t faults = a.faults[chain];
+    const SlotOffset<D> soff(C, chain, 0);
+    AcceptStream accs;
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
@@ -502,7 +813,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
                 for (int j = 0; j < i; ++j) acc = fma(-Lrw[i * D + j], y[j], acc);
                 y[i] = acc * iLrw[i];
             }
-            ltd = a.rw_c0 - canon_sumsq<D, 1>(y) / 2.0;
+            ltd = fma(-0.5, canon_sumsq<D, 1>(y), a.rw_c0);  // = c0 − q/2 (q/2 exact)
         }
         double llp;
         if constexpr (LLMODE == LL_PER_OBS) {
@@ -517,7 +828,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
                     for (int j = 0; j < i; ++j) acc = fma(-Lt[i * D + j], y[j], acc);
                     y[i] = acc * iLt[i];
                 }
-                llp = llp + (a.t_c0 - canon_sumsq<D, 1>(y) / 2.0);
+                llp = llp + fma(-0.5, canon_sumsq<D, 1>(y), a.t_c0);
             }
         } else {
             double y[D];
@@ -533,22 +844,22 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
         }
         if (!(llp - llp == 0.0)) faults |= 1u;
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
-        const double E = accept_exp(zt, a.key0, a.key1, gid, iter, a.pidx0, faults);
+        const double E = accs.next(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults);
         const bool acc = E > -llr;
-        if constexpr (FULL) store_state<D>(a.hist_prop + slot * D * C, C, chain, 0, thp, true);
+        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
 #pragma unroll
         for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {
-            store_state<D>(a.hist_theta + slot * D * C, C, chain, 0, th, true);
+            store_slot<D>(a.hist_theta + slot * D * C, soff, th);
             __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
         }
         {
             const uint64_t m = __ballot(acc);
             if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
         }
-        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, acc);
+        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
     }
     a.ll[chain] = ll;
     a.ra[chain] = ra;

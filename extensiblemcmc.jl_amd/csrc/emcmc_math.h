@@ -44,7 +44,41 @@ struct u32x4 {
 #define EMCMC_ABLATE 0  // timing-only builds (make ablate): 1 = Philox replaced by a cheap hash
 #endif
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// a ^ b ^ k in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); k is a
+// round key derived from the seed, wave-uniform, so it sits in an SGPR
+__device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
+    return r;
+}
+#else
+static inline uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) { return a ^ b ^ k; }
+#endif
+
+#if defined(__HIP_DEVICE_COMPILE__)
+// The key words re-materialised through an opaque SALU move: the ten round
+// keys of each Philox call are then derived inside the call (s_add per round)
+// instead of being hoisted out of the step loop as 20 live SGPRs (which the
+// register allocator spills into VGPR lanes and reloads with v_readlane).
+__device__ __forceinline__ uint32_t key_local(uint32_t k) {
+    uint32_t r;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(r) : "s"(k));
+    return r;
+}
+#else
+static inline uint32_t key_local(uint32_t k) { return k; }
+#endif
+
+#ifndef EMCMC_KEY_LOCAL
+#define EMCMC_KEY_LOCAL 1
+#endif
+
 EMCMC_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+    if (EMCMC_KEY_LOCAL) {
+        k0 = key_local(k0);
+        k1 = key_local(k1);
+    }
 #if EMCMC_ABLATE & 1
     u32x4 o = {c.x * 0x9E3779B9u ^ k0, c.y * 0x85EBCA6Bu ^ c.x, c.z * 0xC2B2AE35u ^ k1, c.w ^ c.y * 0x27D4EB2Fu};
     return o;
@@ -57,9 +91,9 @@ EMCMC_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
         const uint64_t p0 = (uint64_t)M0 * (uint64_t)c.x;
         const uint64_t p1 = (uint64_t)M1 * (uint64_t)c.z;
         u32x4 n;
-        n.x = (uint32_t)(p1 >> 32) ^ c.y ^ k0;
+        n.x = xor3_key((uint32_t)(p1 >> 32), c.y, k0);
         n.y = (uint32_t)p1;
-        n.z = (uint32_t)(p0 >> 32) ^ c.w ^ k1;
+        n.z = xor3_key((uint32_t)(p0 >> 32), c.w, k1);
         n.w = (uint32_t)p0;
         c = n;
         k0 += W0;
@@ -70,7 +104,10 @@ EMCMC_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
 
 // Counter layout of the shared stream:
 //   x = global chain id, y = mcmciter (1-based), z = block, w = (pidx << 16) | attempt
-// Blocks: normal pair j → z = j; accept uniform → z = kBlockAccept.
+// Blocks: normal pair j → z = j; accept draws → z = kBlockAccept.  The fast
+// (attempt 0) accept draws of iterations 2m and 2m+1 share one block, indexed
+// by y = m: words (x,y) serve the even iteration, (z,w) the odd one.  Their
+// rare-path blocks use y = mcmciter and attempt ≥ 1, so they never collide.
 constexpr uint32_t kBlockAccept = 0xFFFFFFFFu;
 
 EMCMC_HD u32x4 draw(uint32_t k0, uint32_t k1, uint32_t chain, uint32_t iter, uint32_t block,
@@ -156,9 +193,14 @@ EMCMC_HD double exp_nonpos(double x) {
 
 // ---- Marsaglia–Tsang ziggurat, 256 layers (J. Stat. Softw. 5(8), 2000) ------
 // The same sampler family as Julia's randn/randexp (Random stdlib), fed by the
-// Philox stream: one 64-bit word pair per draw → layer index (8 bits), sign
-// (1 bit), 52-bit magnitude.  ≈ 99% of draws take the fast path (integer
-// compare + one table read + one multiply); wedge/tail draws use the portable
+// Philox stream.  One 64-bit draw (hi:lo) per variate:
+//   layer = lo[11:4]   sign = lo[0]   magnitude u = (hi:lo)[63:12] / 2^52
+// Bits lo[3:1] are unused.  The layout is chosen for gfx950: the LDS byte
+// address of the 16-byte table entry is lo & 0xFF0, and v = 1 + u is built
+// directly as a double from two v_alignbit_b32, so the fast path is
+//   x = fma(v, W, −W) = u·W (one rounding, the bits of (double)mag · W/2^52),
+//   accepted iff v < 1 + k/2^52 (the integer test mag < k, exactly).
+// ≈ 99% of draws take the fast path; wedge/tail draws use the portable
 // log/exp above with fresh counter blocks.  Tables are built on the host by
 // build_ziggurat() (oracle/ restates the same construction).
 constexpr double kZigNR = 3.6541528853610088;       // normal: rightmost layer edge r
@@ -168,8 +210,8 @@ constexpr double kZigER = 7.69711747013104972;      // exponential: r
 constexpr double kZigEV = 3.949659822581572e-3;     // exponential: v
 
 struct ZigEntry {
-    uint64_t k;  // fast-accept threshold on the 52-bit magnitude
-    double w;    // magnitude → x scale (x_i / 2^52)
+    double kv;  // 1 + k/2^52: fast-accept bound on v = 1 + u
+    double w;   // layer width x_i (base layer: q = v/f(r))
 };
 struct Ziggurat {
     ZigEntry n[256];
@@ -180,64 +222,78 @@ struct Ziggurat {
 
 inline void build_ziggurat(Ziggurat &z) {
     const double m = 0x1p52;
+    auto kv = [](uint64_t k) { return u2d(0x3FF0000000000000ull | k); };
     {  // N(0,1), f(x) = exp(−x²/2)
         double dn = kZigNR, tn = dn;
         const double q = kZigNV / exp_nonpos(-0.5 * (dn * dn));
-        z.n[0].k = (uint64_t)((dn / q) * m);
-        z.n[1].k = 0;
-        z.n[0].w = q / m;
-        z.n[255].w = dn / m;
+        z.n[0].kv = kv((uint64_t)((dn / q) * m));
+        z.n[1].kv = kv(0);
+        z.n[0].w = q;
+        z.n[255].w = dn;
         z.nf[0] = 1.0;
         z.nf[255] = exp_nonpos(-0.5 * (dn * dn));
         for (int i = 254; i >= 1; --i) {
             dn = sqrt(-2.0 * log_pos(kZigNV / dn + exp_nonpos(-0.5 * (dn * dn))));
-            z.n[i + 1].k = (uint64_t)((dn / tn) * m);
+            z.n[i + 1].kv = kv((uint64_t)((dn / tn) * m));
             tn = dn;
             z.nf[i] = exp_nonpos(-0.5 * (dn * dn));
-            z.n[i].w = dn / m;
+            z.n[i].w = dn;
         }
     }
     {  // Exp(1), f(x) = exp(−x)
         double de = kZigER, te = de;
         const double q = kZigEV / exp_nonpos(-de);
-        z.e[0].k = (uint64_t)((de / q) * m);
-        z.e[1].k = 0;
-        z.e[0].w = q / m;
-        z.e[255].w = de / m;
+        z.e[0].kv = kv((uint64_t)((de / q) * m));
+        z.e[1].kv = kv(0);
+        z.e[0].w = q;
+        z.e[255].w = de;
         z.ef[0] = 1.0;
         z.ef[255] = exp_nonpos(-de);
         for (int i = 254; i >= 1; --i) {
             de = -log_pos(kZigEV / de + exp_nonpos(-de));
-            z.e[i + 1].k = (uint64_t)((de / te) * m);
+            z.e[i + 1].kv = kv((uint64_t)((de / te) * m));
             te = de;
             z.ef[i] = exp_nonpos(-de);
-            z.e[i].w = de / m;
+            z.e[i].w = de;
         }
     }
 }
 
 struct ZigDraw {
-    uint32_t idx, sign;
-    uint64_t mag;  // 52 bits
+    uint32_t off;   // byte offset of the layer's ZigEntry (layer · 16)
+    uint32_t sbit;  // sign in bit 31
+    double v;       // 1 + u, u = 52-bit magnitude / 2^52
 };
 EMCMC_HD ZigDraw zig_split(uint32_t hi, uint32_t lo) {
     ZigDraw d;
-    d.idx = lo & 255u;
-    d.sign = (lo >> 8) & 1u;
-    d.mag = ((uint64_t)hi << 20) | (uint64_t)(lo >> 12);
+    d.off = lo & 0xFF0u;
+    d.sbit = lo << 31;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t vlo = __builtin_amdgcn_alignbit(hi, lo, 12);
+    const uint32_t vhi = __builtin_amdgcn_alignbit(0x3FFu, hi, 12);
+#else
+    const uint32_t vlo = (hi << 20) | (lo >> 12);
+    const uint32_t vhi = 0x3FF00000u | (hi >> 12);
+#endif
+    d.v = u2d(((uint64_t)vhi << 32) | vlo);
     return d;
 }
-// exact (double)mag for mag < 2^52 through the exponent bits
-EMCMC_HD double mag_to_double(uint64_t mag) { return u2d(0x4330000000000000ull | mag) - 0x1p52; }
-EMCMC_HD double with_sign(double x, uint32_t s) { return u2d(d2u(x) ^ ((uint64_t)s << 63)); }
+EMCMC_HD uint32_t zig_layer(const ZigDraw &d) { return d.off >> 4; }
+EMCMC_HD const ZigEntry &zig_entry(const ZigEntry *tab, const ZigDraw &d) {
+    return *reinterpret_cast<const ZigEntry *>(reinterpret_cast<const char *>(tab) + d.off);
+}
+EMCMC_HD double with_sign(double x, uint32_t sbit) { return u2d(d2u(x) | ((uint64_t)sbit << 32)); }
+// u·W with one rounding (v = 1 + u exactly)
+EMCMC_HD double zig_scale(double v, double w) { return fma(v, w, -w); }
 
 constexpr uint32_t kFaultRngRetries = 2u;  // EMCMC_FAULT_RNG_RETRIES
 constexpr uint32_t kMaxAttempt = 0xFFFFu;
 
 EMCMC_HD bool zig_normal_fast(ZigDraw d, const ZigEntry *tab, double &z) {
-    const ZigEntry t = tab[d.idx];
-    z = with_sign(mag_to_double(d.mag) * t.w, d.sign);
-    return d.mag < t.k;
+    const ZigEntry t = zig_entry(tab, d);
+    const double ws = with_sign(t.w, d.sbit);
+    z = zig_scale(d.v, ws);
+    return d.v < t.kv;
 }
 
 // Rare path of normal number `gj` of (chain, iter, pidx0) whose attempt-0
@@ -254,14 +310,15 @@ EMCMC_HD double zig_normal_slow(ZigDraw d, const ZigEntry *tab, const double *f,
             return 0.0;
         }
         const u32x4 b = draw(key0, key1, chain, iter, pair, pidx0, attempt);
-        if (d.idx == 0) {  // base strip beyond the rectangle: tail x > r
+        const uint32_t L = zig_layer(d);
+        if (L == 0) {  // base strip beyond the rectangle: tail x > r
             const double xx = -log_pos(u01_open0(b.x, b.y)) * kZigNInvR;
             const double yy = -log_pos(u01_open0(b.z, b.w));
-            if (yy + yy > xx * xx) return with_sign(kZigNR + xx, d.sign);
+            if (yy + yy > xx * xx) return with_sign(kZigNR + xx, d.sbit);
         } else {  // wedge test, else a fresh draw
-            const double x = mag_to_double(d.mag) * tab[d.idx].w;
+            const double x = zig_scale(d.v, tab[L].w);
             const double u = u01_closed0(b.x, b.y);
-            if (fma(u, f[d.idx - 1] - f[d.idx], f[d.idx]) < exp_nonpos(-0.5 * (x * x))) return with_sign(x, d.sign);
+            if (fma(u, f[L - 1] - f[L], f[L]) < exp_nonpos(-0.5 * (x * x))) return with_sign(x, d.sbit);
             d = zig_split(b.z, b.w);
             double z;
             if (zig_normal_fast(d, tab, z)) return z;
@@ -270,12 +327,12 @@ EMCMC_HD double zig_normal_slow(ZigDraw d, const ZigEntry *tab, const double *f,
 }
 
 EMCMC_HD bool zig_exp_fast(ZigDraw d, const ZigEntry *tab, double &e) {
-    const ZigEntry t = tab[d.idx];
-    e = mag_to_double(d.mag) * t.w;
-    return d.mag < t.k;
+    const ZigEntry t = zig_entry(tab, d);
+    e = zig_scale(d.v, t.w);
+    return d.v < t.kv;
 }
 
-// Rare path of the Exp(1) draw of block `block`: slow step k uses attempt 1 + k.
+// Rare path of an Exp(1) draw: slow step k uses the block (mcmciter, attempt 1 + k).
 EMCMC_HD double zig_exp_slow(ZigDraw d, const ZigEntry *tab, const double *f, uint32_t key0, uint32_t key1,
                              uint32_t chain, uint32_t iter, uint32_t block, uint32_t pidx0, uint32_t &faults) {
     for (uint32_t k = 0;; ++k) {
@@ -285,14 +342,21 @@ EMCMC_HD double zig_exp_slow(ZigDraw d, const ZigEntry *tab, const double *f, ui
             return 0.0;
         }
         const u32x4 b = draw(key0, key1, chain, iter, block, pidx0, attempt);
-        if (d.idx == 0) return kZigER - log_pos(u01_open0(b.x, b.y));
-        const double x = mag_to_double(d.mag) * tab[d.idx].w;
+        const uint32_t L = zig_layer(d);
+        if (L == 0) return kZigER - log_pos(u01_open0(b.x, b.y));
+        const double x = zig_scale(d.v, tab[L].w);
         const double u = u01_closed0(b.x, b.y);
-        if (fma(u, f[d.idx - 1] - f[d.idx], f[d.idx]) < exp_nonpos(-x)) return x;
+        if (fma(u, f[L - 1] - f[L], f[L]) < exp_nonpos(-x)) return x;
         d = zig_split(b.z, b.w);
         double e;
         if (zig_exp_fast(d, tab, e)) return e;
     }
+}
+
+// The attempt-0 draw of the accept exponential of `iter` (shared block, see
+// kBlockAccept).
+EMCMC_HD ZigDraw accept_split(const u32x4 &r, uint32_t iter) {
+    return (iter & 1u) ? zig_split(r.z, r.w) : zig_split(r.x, r.y);
 }
 
 // Scalar reference forms (probes, host code): the full draw of normal gj and
@@ -307,8 +371,8 @@ EMCMC_HD double normal_draw(const Ziggurat &zt, uint32_t key0, uint32_t key1, ui
 }
 EMCMC_HD double exp_draw(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
                          uint32_t pidx0, uint32_t &faults) {
-    const u32x4 r = draw(key0, key1, chain, iter, kBlockAccept, pidx0, 0);
-    const ZigDraw d = zig_split(r.x, r.y);
+    const u32x4 r = draw(key0, key1, chain, iter >> 1, kBlockAccept, pidx0, 0);
+    const ZigDraw d = accept_split(r, iter);
     double e;
     if (zig_exp_fast(d, zt.e, e)) return e;
     return zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);

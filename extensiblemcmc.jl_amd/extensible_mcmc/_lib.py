@@ -47,6 +47,7 @@ H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
 FAULT_NONFINITE_LL = 1
 FAULT_RNG_RETRIES = 2
 VARIANT_HIGH_OCCUPANCY = 1
+VARIANT_OCCUPANCY3 = 2
 
 
 class EmcmcConfig(C.Structure):

@@ -115,6 +115,7 @@ typedef struct emcmc_config {
 
 /* kernel_variant flags: performance-only choices, bit-identical results */
 #define EMCMC_VARIANT_HIGH_OCCUPANCY 1u  /* cap registers for 4 waves/SIMD where instantiated */
+#define EMCMC_VARIANT_OCCUPANCY3 2u      /* cap registers for 3 waves/SIMD where instantiated */
 
 /* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183). */
 typedef struct emcmc_update_desc {

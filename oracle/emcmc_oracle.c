@@ -395,3 +395,19 @@ ORC_EXPORT void orc_log_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_log(x[i]);
 }
 
+
+/* Checker for the device's rolling-acceptance quotient (emcmc_kernels.h
+ * div_markstein): q = RN(x·y), y = RN(1/b), q' = RN(q + RN_exact(x − b·q)·y)
+ * must equal the IEEE quotient x / b.  Returns the number of mismatches. */
+ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t n) {
+    const double y = 1.0 / b;
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const double q = x[i] * y;
+        const double r = fma(-q, b, x[i]);
+        const double q1 = fma(r, y, q);
+        const double ref = x[i] / b;
+        if (orc_d2u(q1) != orc_d2u(ref)) ++bad;
+    }
+    return bad;
+}

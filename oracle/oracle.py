@@ -58,6 +58,8 @@ def lib():
         L.orc_normal_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
         L.orc_exp_vec.restype = None
         L.orc_exp_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
+        L.orc_markstein_mismatches.restype = C.c_uint64
+        L.orc_markstein_mismatches.argtypes = [C.c_double, dp, C.c_uint64]
         L.orc_zig_tables_copy.restype = None
         L.orc_zig_tables_copy.argtypes = [u64p, dp, dp, u64p, dp, dp]
         _lib = L
@@ -200,3 +202,9 @@ def zig_tables():
     u64 = C.POINTER(C.c_uint64)
     lib().orc_zig_tables_copy(kn.ctypes.data_as(u64), _d(wn), _d(fn), ke.ctypes.data_as(u64), _d(we), _d(fe))
     return {"kn": kn, "wn": wn, "fn": fn, "ke": ke, "we": we, "fe": fe}
+
+
+def markstein_mismatches(b, x):
+    """Count of x where the device's Markstein quotient differs from IEEE x / b."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    return int(lib().orc_markstein_mismatches(float(b), _d(x), x.size))

@@ -178,14 +178,14 @@ static inline void orc_zig_build(orc_zig_tables *t) {
     }
 }
 
-/* one 64-bit draw: layer = lo[7:0], sign = lo[8], magnitude = hi:lo[31:12] (52 bits) */
+/* one 64-bit draw: layer = lo[11:4], sign = lo[0], magnitude = hi:lo[31:12] (52 bits) */
 typedef struct {
     uint32_t layer, negative;
     uint64_t mag;
 } orc_zdraw;
 
 static inline orc_zdraw orc_zsplit(uint32_t hi, uint32_t lo) {
-    orc_zdraw d = {lo & 255u, (lo >> 8) & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
+    orc_zdraw d = {(lo >> 4) & 255u, lo & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
     return d;
 }
 
@@ -223,13 +223,15 @@ static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k
     }
 }
 
-/* rand(Exponential(1.0)) of run.jl:278: block (ORC_BLOCK_ACCEPT, 0), then
- * rare-path step k on attempt 1 + k. */
+/* rand(Exponential(1.0)) of run.jl:278.  Attempt 0 of iterations 2m and
+ * 2m+1 shares the block (counter y = m, ORC_BLOCK_ACCEPT, attempt 0): word
+ * pair 0 for the even iteration, pair 1 for the odd one.  Rare-path step k
+ * uses (y = iter, ORC_BLOCK_ACCEPT, attempt 1 + k). */
 #define ORC_BLOCK_ACCEPT 0xFFFFFFFFu
 static inline double orc_exponential(const orc_zig_tables *t, uint32_t k0, uint32_t k1, uint32_t chain,
                                      uint32_t iter, uint32_t pidx0, uint32_t *faults) {
-    orc_u32x4 r0 = orc_draw(k0, k1, chain, iter, ORC_BLOCK_ACCEPT, pidx0, 0);
-    orc_zdraw d = orc_zsplit(r0.v[0], r0.v[1]);
+    orc_u32x4 r0 = orc_draw(k0, k1, chain, iter >> 1, ORC_BLOCK_ACCEPT, pidx0, 0);
+    orc_zdraw d = (iter & 1u) ? orc_zsplit(r0.v[2], r0.v[3]) : orc_zsplit(r0.v[0], r0.v[1]);
     if (d.mag < t->ke[d.layer]) return (double)d.mag * t->we[d.layer];
     for (uint32_t step = 0;; ++step) {
         uint32_t attempt = 1u + step;

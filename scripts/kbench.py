@@ -32,13 +32,21 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variants", default="all")
+    ap.add_argument("--grid", default="", help="lpc:variant,... (overrides --variants)")
+    ap.add_argument("--hist", default="full,accept_only")
+    ap.add_argument("--ll", default="per_obs,suffstat")
     a = ap.parse_args()
     w = W.cfg2(a.chains)
     grid = []
-    for hist in (L.HIST_FULL, L.HIST_ACCEPT_ONLY):
-        for ll in (L.LL_PER_OBS, L.LL_SUFFSTAT):
-            lv = {"all": ((1, 0), (2, 0), (4, 0), (4, 1)), "lpc14": ((1, 0), (4, 0)),
-                  "lpc4": ((4, 0), (4, 1))}[a.variants]
+    hists = [{"full": L.HIST_FULL, "accept_only": L.HIST_ACCEPT_ONLY}[h] for h in a.hist.split(",")]
+    lls = [{"per_obs": L.LL_PER_OBS, "suffstat": L.LL_SUFFSTAT}[x] for x in a.ll.split(",")]
+    if a.grid:
+        lv = tuple(tuple(int(v) for v in g.split(":")) for g in a.grid.split(","))
+    else:
+        lv = {"all": ((1, 0), (2, 0), (4, 0), (4, 1)), "lpc14": ((1, 0), (4, 0)),
+              "lpc4": ((4, 0), (4, 1))}[a.variants]
+    for hist in hists:
+        for ll in lls:
             for lpc, var in lv:
                 grid.append((lpc, var, ll, hist, 100))
     S = 100 + a.steps * a.rounds

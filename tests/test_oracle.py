@@ -139,3 +139,17 @@ def test_dense_formulas_equal_diagonal_bits(oracle, ll_mode):
     assert np.array_equal(ha["ll"], hb["ll"])
     assert np.array_equal(ha["theta"], hb["theta"])
     assert np.array_equal(a.ra, b.ra)
+
+
+def test_markstein_quotient_is_ieee_division(oracle):
+    """The kernels divide the rolling-acceptance numerator by W (N ≥ W) with
+    Markstein's correction from RN(1/W); it must round like IEEE division."""
+    rng = np.random.default_rng(11)
+    n = 400_000
+    x = np.ldexp(1.0 + rng.integers(0, 2 ** 52, n) * 2.0 ** -52, rng.integers(-60, 200, n))
+    x[rng.random(n) < 0.5] *= -1
+    ints = rng.integers(-1_000_000, 1_000_001, n // 4).astype(np.float64)
+    halves = rng.integers(-256, 257, n // 4) / 2.0
+    xs = np.concatenate([x, ints, halves])
+    for b in list(range(1, 129)):
+        assert oracle.markstein_mismatches(b, xs if b in (1, 7, 100, 127, 128) else xs[::16]) == 0

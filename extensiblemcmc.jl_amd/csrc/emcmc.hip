@@ -20,6 +20,7 @@
 
 #include "../../include/emcmc.h"
 #include "emcmc_kernels.h"
+#include "emcmc_mwg.h"
 
 using namespace emcmc;
 
@@ -89,7 +90,9 @@ double canon_sumsq_host(const double *y, int D) {
 struct UpdateHost {
     uint32_t kernel = 0, prior = 0, adaptation = 0;
     std::vector<uint32_t> coords;
-    std::vector<double> sigma, L, invdiag;
+    std::vector<double> sigma, L, invdiag;  // GaussianRandomWalk
+    std::vector<double> eps;                // UniformRandomWalk ϵ
+    emcmc_unifrw_adaptation adpt{};         // AdaptationUnifRW (scalar form)
     bool diag = false;
     double c0 = 0.0;
 };
@@ -103,9 +106,11 @@ struct TargetHost {
 };
 
 using KernelFn = void (*)(StepParams);
+using MwgFn = void (*)(MwgParams);
 
 struct Variant {
     KernelFn fn = nullptr;
+    MwgFn mfn = nullptr;  // general schedule kernel (mwg_gsn_kernel) when set
     int lpc = 1;
     bool dense = false;
     bool unit = false;
@@ -136,6 +141,13 @@ struct emcmc_handle {
     double *d_gather = nullptr;   // history layout conversion
     size_t gather_bytes = 0;
     uint64_t row_bytes = 0;
+    // general schedule path (mwg_gsn_kernel)
+    double *d_mu_p = nullptr, *d_eps = nullptr, *d_tL = nullptr, *d_tiL = nullptr, *d_xbar = nullptr;
+    uint32_t *d_aprop = nullptr, *d_aacc = nullptr, *d_steps = nullptr;
+    MwgUpdate *d_mwg = nullptr;
+    std::vector<uint32_t> last_iter;                    // per update: last iteration it ran (uniform)
+    std::vector<std::vector<uint32_t>> steps_staging;   // host step lists alive until synchronize
+    uint64_t steps_used = 0;
     // dispatch
     Variant var;
     size_t lds_bytes = 0;
@@ -238,6 +250,16 @@ int auto_lpc(int D) {
     return 1;
 }
 
+// P°.θ[1:d] ← μ for every chain (workspaces.jl:225-233: P° = deepcopy(data.P))
+emcmc_status reset_mu_p(emcmc_handle *h) {
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    std::vector<double> m(C * D);
+    for (uint64_t c = 0; c < C; ++c)
+        for (uint64_t d = 0; d < D; ++d) m[state_pos(d, c, C, (uint32_t)D)] = h->target.mu[d];
+    HIPCHK(h, hipMemcpy(h->d_mu_p, m.data(), m.size() * sizeof(double), hipMemcpyHostToDevice));
+    return EMCMC_OK;
+}
+
 emcmc_status ensure_alloc(emcmc_handle *h) {
     if (h->allocated) return EMCMC_OK;
     if (h->updates.empty()) return fail(h, EMCMC_STATE_ERROR, "no update added (emcmc_add_update)");
@@ -245,10 +267,17 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
     const uint64_t P = h->updates.size();
     HIPCHK(h, hipMalloc(&h->d_theta, C * D * sizeof(double)));
     HIPCHK(h, hipMalloc(&h->d_ll, C * sizeof(double)));
-    HIPCHK(h, hipMalloc(&h->d_ra, C * sizeof(double)));
-    HIPCHK(h, hipMalloc(&h->d_ring, 2 * C * sizeof(uint64_t)));
-    HIPCHK(h, hipMalloc(&h->d_nacc, C * sizeof(uint32_t)));
+    // per-update chain statistics [P][C] (the fused kernels use update 0)
+    HIPCHK(h, hipMalloc(&h->d_ra, P * C * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_ring, 2 * P * C * sizeof(uint64_t)));
+    HIPCHK(h, hipMalloc(&h->d_nacc, P * C * sizeof(uint32_t)));
     HIPCHK(h, hipMalloc(&h->d_faults, C * sizeof(uint32_t)));
+    // general schedule path: P° mean, AdaptationUnifRW state, step lists
+    HIPCHK(h, hipMalloc(&h->d_mu_p, C * D * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_aprop, P * C * sizeof(uint32_t)));
+    HIPCHK(h, hipMalloc(&h->d_aacc, P * C * sizeof(uint32_t)));
+    HIPCHK(h, hipMalloc(&h->d_eps, P * kMwgMaxD * C * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_steps, M * P * 4 * sizeof(uint32_t)));
     {
         Ziggurat zt;
         build_ziggurat(zt);
@@ -267,8 +296,101 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
+// ---- general schedule kernel table ----------------------------------------
+template <int D, bool FULL, int LL>
+MwgFn mwg_fn() {
+    return &mwg_gsn_kernel<D, FULL, LL>;
+}
+#define MWG4(D) \
+    {D, mwg_fn<D, true, 0>(), mwg_fn<D, true, 1>(), mwg_fn<D, false, 0>(), mwg_fn<D, false, 1>()}
+struct MwgEntry {
+    int D;
+    MwgFn full_perobs, full_suff, acc_perobs, acc_suff;
+};
+const std::vector<MwgEntry> &mwg_table() {
+    static const std::vector<MwgEntry> t = {MWG4(1), MWG4(2), MWG4(3), MWG4(4), MWG4(8), MWG4(16)};
+    return t;
+}
+
+// Every schedule but one joint GaussianRandomWalk update on coords 1:D runs on
+// mwg_gsn_kernel: per-update constants as MwgUpdate records (scalar loads),
+// target factor / x̄ / observations in plain global memory.
+emcmc_status select_mwg(emcmc_handle *h) {
+    const int D = (int)h->cfg.dim;
+    const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
+    const int ll = (int)h->target.ll_mode;
+    Variant v;
+    for (const auto &e : mwg_table())
+        if (e.D == D) v.mfn = full ? (ll == LL_PER_OBS ? e.full_perobs : e.full_suff)
+                                   : (ll == LL_PER_OBS ? e.acc_perobs : e.acc_suff);
+    if (!v.mfn)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "no general-schedule device kernel for D=%d (instantiated: D ∈ {1,2,3,4,8,16})", D);
+    std::vector<MwgUpdate> tab(h->updates.size());
+    for (size_t p = 0; p < h->updates.size(); ++p) {
+        const UpdateHost &u = h->updates[p];
+        MwgUpdate &m = tab[p];
+        std::memset(&m, 0, sizeof m);
+        m.kind = u.kernel;
+        m.nc = (uint32_t)u.coords.size();
+        m.adapt = u.adaptation;
+        for (uint32_t j = 0; j < m.nc; ++j) m.coords[j] = u.coords[j];
+        if (u.kernel == EMCMC_RW_UNIFORM) {
+            for (uint32_t j = 0; j < m.nc; ++j) m.eps0[j] = u.eps[j];
+            if (u.adaptation == EMCMC_ADPT_UNIF_RW) {
+                m.k = u.adpt.adapt_every_k_steps;
+                m.target = u.adpt.target_accpt_rate;
+                m.scale = u.adpt.scale;
+                m.amin = u.adpt.min;
+                m.amax = u.adpt.max;
+                m.offset = u.adpt.offset;
+            }
+        } else {
+            const int n = (int)m.nc;
+            for (int i = 0; i < n; ++i)
+                for (int j = 0; j <= i; ++j) m.L[i * kMwgMaxD + j] = u.L[(size_t)i * n + j];
+            for (int i = 0; i < n; ++i) m.iL[i] = u.invdiag[i];
+            m.c0 = u.c0;
+            m.diag = u.diag ? 1u : 0u;
+        }
+    }
+    if (h->d_mwg) (void)hipFree(h->d_mwg);
+    HIPCHK(h, hipMalloc(&h->d_mwg, tab.size() * sizeof(MwgUpdate)));
+    HIPCHK(h, hipMemcpy(h->d_mwg, tab.data(), tab.size() * sizeof(MwgUpdate), hipMemcpyHostToDevice));
+    const TargetHost &t = h->target;
+    auto upload = [&](double *&dst, const std::vector<double> &src) -> emcmc_status {
+        if (dst) (void)hipFree(dst);
+        dst = nullptr;
+        HIPCHK(h, hipMalloc(&dst, std::max<size_t>(1, src.size()) * sizeof(double)));
+        if (!src.empty()) HIPCHK(h, hipMemcpy(dst, src.data(), src.size() * sizeof(double), hipMemcpyHostToDevice));
+        return EMCMC_OK;
+    };
+    emcmc_status st;
+    if ((st = upload(h->d_tL, t.L)) || (st = upload(h->d_tiL, t.invdiag)) || (st = upload(h->d_xbar, t.xbar)) ||
+        (st = upload(h->d_obs, t.obs)))
+        return st;
+    char nm[160];
+    snprintf(nm, sizeof nm, "mwg_gsn_kernel<D=%d,P=%zu,%s,%s>", D, h->updates.size(), full ? "FULL" : "ACCEPT_ONLY",
+             ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
+    v.name = nm;
+    h->lds_bytes = sizeof(Ziggurat);
+    h->var = v;
+    return EMCMC_OK;
+}
+
+bool fused_eligible(const emcmc_handle *h) {
+    if (h->updates.size() != 1) return false;
+    const UpdateHost &u = h->updates[0];
+    if (u.kernel != EMCMC_RW_GAUSSIAN || u.adaptation != EMCMC_ADPT_NONE) return false;
+    if (u.coords.size() != h->cfg.dim) return false;
+    for (uint32_t i = 0; i < h->cfg.dim; ++i)
+        if (u.coords[i] != i) return false;
+    return true;
+}
+
 emcmc_status select_variant(emcmc_handle *h) {
     if (!h->target_set || h->updates.empty()) return EMCMC_OK;
+    if (!fused_eligible(h)) return select_mwg(h);
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
@@ -385,6 +507,88 @@ emcmc_status drain_timing(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
+// General schedule: the step list goes to HBM (4 u32 per step, read by the
+// kernel with scalar loads) and runs in launches of ≤ K steps in schedule order.
+emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps) {
+    const uint64_t C = h->cfg.num_chains, P = h->updates.size();
+    const uint64_t cap = h->cfg.num_mcmc_steps * P;
+    if (num_steps == 0) return EMCMC_OK;
+    if (num_steps > cap) return fail(h, EMCMC_INVALID_ARG, "more steps than M·P in one call");
+    std::vector<uint32_t> st(4 * num_steps);
+    for (uint64_t i = 0; i < num_steps; ++i) {
+        const uint32_t it = steps[i].mcmciter, q = steps[i].pidx - 1;
+        st[4 * i] = it;
+        st[4 * i + 1] = steps[i].pidx;
+        st[4 * i + 2] = (it > 1 && h->last_iter[q] == it - 1) ? 1u : 0u;  // rolling_ar[it−1][q] was written
+        st[4 * i + 3] = 0;
+        h->last_iter[q] = it;
+    }
+    if (h->steps_used + num_steps > cap) h->steps_used = 0;  // earlier lists were consumed in stream order
+    uint32_t *dst = h->d_steps + 4 * h->steps_used;
+    HIPCHK(h, hipMemcpyAsync(dst, st.data(), st.size() * sizeof(uint32_t), hipMemcpyHostToDevice, h->stream));
+    h->steps_staging.push_back(std::move(st));  // alive until emcmc_synchronize
+    h->steps_used += num_steps;
+    const TargetHost &t = h->target;
+    MwgParams a{};
+    a.theta = h->d_theta;
+    a.mu_p = h->d_mu_p;
+    a.ll = h->d_ll;
+    a.ra = h->d_ra;
+    a.ring = h->d_ring;
+    a.nacc = h->d_nacc;
+    a.aprop = h->d_aprop;
+    a.aacc = h->d_aacc;
+    a.eps = h->d_eps;
+    a.faults = h->d_faults;
+    a.hist_theta = h->d_hist_theta;
+    a.hist_prop = h->d_hist_prop;
+    a.hist_ll = h->d_hist_ll;
+    a.hist_acc = h->d_hist_acc;
+    a.zig = h->d_zig;
+    a.updates = h->d_mwg;
+    a.Lt = h->d_tL;
+    a.iLt = h->d_tiL;
+    a.xbar = h->d_xbar;
+    a.obs = h->d_obs;
+    a.C = C;
+    a.row_bytes = h->row_bytes;
+    a.chain0 = (uint32_t)h->cfg.first_chain_id;
+    a.key0 = (uint32_t)h->cfg.seed;
+    a.key1 = (uint32_t)(h->cfg.seed >> 32);
+    a.P = (uint32_t)P;
+    a.W = h->cfg.roll_window;
+    a.nobs = (uint32_t)t.nobs;
+    a.tdiag = t.diag ? 1u : 0u;
+    a.t_c0 = t.c0;
+    a.n_tc0 = (double)t.nobs * t.c0;
+    a.S_c = t.S_c;
+    a.nobs_d = (double)t.nobs;
+    const dim3 block(256), grid((unsigned)((C + 255) / 256));
+    const uint64_t K = h->cfg.steps_per_launch;
+    for (uint64_t i = 0; i < num_steps; i += K) {
+        const uint64_t n = std::min<uint64_t>(K, num_steps - i);
+        a.steps = dst + 4 * i;
+        a.nsteps = (uint32_t)n;
+        a.N0 = h->stats_N;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->timing) {
+            e0 = get_event(h);
+            e1 = get_event(h);
+            HIPCHK(h, hipEventRecord(e0, h->stream));
+        }
+        void *args[] = {&a};
+        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mfn), grid, block, args, h->lds_bytes,
+                                  h->stream));
+        if (h->timing) {
+            HIPCHK(h, hipEventRecord(e1, h->stream));
+            h->ev.emplace_back(e0, e1);
+            h->pending_bytes += bytes_per_launch(h, n);
+        }
+        h->stats_N += n;
+    }
+    return EMCMC_OK;
+}
+
 }  // namespace
 
 // ============================================================================
@@ -434,36 +638,51 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     if (h->allocated) return fail(h, EMCMC_STATE_ERROR, "updates must be added before set_state/run");
     const uint32_t D = h->cfg.dim;
     if (u->num_coords == 0 || !u->coords) return fail(h, EMCMC_INVALID_ARG, "update needs coords");
-    for (uint32_t i = 0; i < u->num_coords; ++i)
+    if (u->num_coords > D) return fail(h, EMCMC_INVALID_ARG, "more coords than D");
+    for (uint32_t i = 0; i < u->num_coords; ++i) {
         if (u->coords[i] >= D) return fail(h, EMCMC_INVALID_ARG, "coord %u out of range (D=%u)", u->coords[i], D);
-    if (u->kernel != EMCMC_RW_GAUSSIAN)
+        for (uint32_t j = 0; j < i; ++j)
+            if (u->coords[j] == u->coords[i]) return fail(h, EMCMC_INVALID_ARG, "repeated coord %u", u->coords[i]);
+    }
+    if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "transition kernel %u has no device plugin yet", u->kernel);
     if (u->prior != EMCMC_PRIOR_IMPROPER)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin yet", u->prior);
-    if (u->adaptation != EMCMC_ADPT_NONE)
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "adaptation %u has no device plugin yet", u->adaptation);
+    if (u->adaptation != EMCMC_ADPT_NONE &&
+        !(u->adaptation == EMCMC_ADPT_UNIF_RW && u->kernel == EMCMC_RW_UNIFORM))
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "adaptation %u has no device plugin for kernel %u yet",
+                    u->adaptation, u->kernel);
     if (u->pos)
         for (uint32_t i = 0; i < u->num_coords; ++i)
             if (u->pos[i]) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "positivity-restricted coordinates not on device yet");
-    if (!h->updates.empty())
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "multi-update (Metropolis-within-Gibbs) schedules not on device yet");
-    if (u->num_coords != D) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device path updates all coordinates jointly");
-    for (uint32_t i = 0; i < D; ++i)
-        if (u->coords[i] != i) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device path needs coords = 1:D in order");
-    if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");
+    if (h->updates.size() >= 64) return fail(h, EMCMC_INVALID_ARG, "at most 64 updates");
     UpdateHost uh;
     uh.kernel = u->kernel;
     uh.prior = u->prior;
     uh.adaptation = u->adaptation;
     uh.coords.assign(u->coords, u->coords + u->num_coords);
     const int n = (int)u->num_coords;
-    uh.sigma.assign(u->sigma, u->sigma + (size_t)n * n);
-    if (!cholesky_upper_colmajor(uh.sigma.data(), n, uh.L))
-        return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk Σ is not positive definite");
-    uh.invdiag.resize(n);
-    for (int i = 0; i < n; ++i) uh.invdiag[i] = 1.0 / uh.L[(size_t)i * n + i];
-    uh.diag = is_diag_upper(uh.sigma.data(), n);
-    uh.c0 = mvnormal_c0(n, logdet_chol(uh.L, n));
+    if (u->kernel == EMCMC_RW_GAUSSIAN) {
+        if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");
+        uh.sigma.assign(u->sigma, u->sigma + (size_t)n * n);
+        if (!cholesky_upper_colmajor(uh.sigma.data(), n, uh.L))
+            return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk Σ is not positive definite");
+        uh.invdiag.resize(n);
+        for (int i = 0; i < n; ++i) uh.invdiag[i] = 1.0 / uh.L[(size_t)i * n + i];
+        uh.diag = is_diag_upper(uh.sigma.data(), n);
+        uh.c0 = mvnormal_c0(n, logdet_chol(uh.L, n));
+    } else {
+        if (!u->epsilon) return fail(h, EMCMC_INVALID_ARG, "UniformRandomWalk needs ϵ");
+        uh.eps.assign(u->epsilon, u->epsilon + n);
+        for (double e : uh.eps)  // UniformRandomWalk: @assert all(ϵ .> 0.0) (random_walk.jl:50)
+            if (!(e > 0.0)) return fail(h, EMCMC_INVALID_ARG, "UniformRandomWalk ϵ must be > 0");
+        if (u->adaptation == EMCMC_ADPT_UNIF_RW) {
+            const auto *ad = static_cast<const emcmc_unifrw_adaptation *>(u->reserved_ptr[0]);
+            if (!ad) return fail(h, EMCMC_INVALID_ARG, "AdaptationUnifRW parameters missing (reserved_ptr[0])");
+            if (ad->adapt_every_k_steps == 0) return fail(h, EMCMC_INVALID_ARG, "adapt_every_k_steps must be ≥ 1");
+            uh.adpt = *ad;
+        }
+    }
     h->updates.push_back(std::move(uh));
     return select_variant(h);
 }
@@ -510,6 +729,10 @@ emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t) {
     th.S_c = Sc;
     h->target = std::move(th);
     h->target_set = true;
+    if (h->allocated) {  // P° = deepcopy(data.P): every chain's P° mean starts at μ
+        emcmc_status st = reset_mu_p(h);
+        if (st) return st;
+    }
     return select_variant(h);
 }
 
@@ -526,12 +749,27 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
     std::vector<double> l(C, -INFINITY);
     if (ll) std::copy(ll, ll + C, l.begin());
     HIPCHK(h, hipMemcpyAsync(h->d_ll, l.data(), C * sizeof(double), hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
-    HIPCHK(h, hipMemsetAsync(h->d_ring, 0, 2 * C * sizeof(uint64_t), h->stream));
-    HIPCHK(h, hipMemsetAsync(h->d_nacc, 0, C * sizeof(uint32_t), h->stream));
+    const uint64_t P = h->updates.size();
+    HIPCHK(h, hipMemsetAsync(h->d_ra, 0, P * C * sizeof(double), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_ring, 0, 2 * P * C * sizeof(uint64_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_nacc, 0, P * C * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_faults, 0, C * sizeof(uint32_t), h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));  // host vector l goes out of scope
+    HIPCHK(h, hipMemsetAsync(h->d_aprop, 0, P * C * sizeof(uint32_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_aacc, 0, P * C * sizeof(uint32_t), h->stream));
+    {  // per-chain ϵ of every update starts at the update's ϵ
+        std::vector<double> e(P * kMwgMaxD * C, 0.0);
+        for (uint64_t q = 0; q < P; ++q)
+            for (size_t j = 0; j < h->updates[q].eps.size(); ++j)
+                std::fill_n(e.begin() + (q * kMwgMaxD + j) * C, C, h->updates[q].eps[j]);
+        HIPCHK(h, hipMemcpyAsync(h->d_eps, e.data(), e.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+        if (h->target_set) {
+            st = reset_mu_p(h);
+            if (st) return st;
+        }
+        HIPCHK(h, hipStreamSynchronize(h->stream));  // host vectors go out of scope
+    }
     h->stats_N = 1;
+    h->last_iter.assign(P, 0u);
     return EMCMC_OK;
 }
 
@@ -539,7 +777,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     if (!h || (!steps && num_steps)) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
     if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
-    if (!h->var.fn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
+    if (!h->var.fn && !h->var.mfn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
     if (!h->d_zig) return fail(h, EMCMC_STATE_ERROR, "state not allocated");
     const uint32_t P = (uint32_t)h->updates.size();
     for (uint64_t i = 0; i < num_steps; ++i) {
@@ -548,6 +786,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
             return fail(h, EMCMC_INVALID_ARG, "step %llu: mcmciter %u outside 1..M", (unsigned long long)i,
                         steps[i].mcmciter);
     }
+    if (h->var.mfn) return run_mwg(h, steps, num_steps);
     const uint64_t C = h->cfg.num_chains;
     const int lpc = h->var.lpc;
     const uint64_t threads = C * (uint64_t)lpc;
@@ -594,6 +833,11 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
         p.iter0 = steps[i].mcmciter;
         p.nsteps = (uint32_t)n;
         p.N0 = h->stats_N;
+        // rolling_ar[iter−1][p] of an iteration that did not run is 0.0
+        // (chain_statistics.jl:57 reads a never-written slot)
+        if (p.iter0 > 1 && h->last_iter[p.pidx0] != p.iter0 - 1)
+            HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
+        h->last_iter[p.pidx0] = steps[j - 1].mcmciter;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->timing) {
             e0 = get_event(h);
@@ -617,6 +861,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
 emcmc_status emcmc_synchronize(emcmc_handle *h) {
     if (!h) return EMCMC_INVALID_ARG;
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->steps_staging.clear();
     if (!h->allocated) return EMCMC_OK;
     std::vector<uint32_t> f(h->cfg.num_chains);
     HIPCHK(h, hipMemcpy(f.data(), h->d_faults, f.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -636,7 +881,8 @@ void emcmc_destroy(emcmc_handle *h) {
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     void *bufs[] = {h->d_theta,     h->d_ll,        h->d_ra,      h->d_ring,     h->d_nacc,  h->d_faults,
                     h->d_hist_theta, h->d_hist_prop, h->d_hist_ll, h->d_hist_acc, h->d_consts, h->d_obs,
-                    h->d_scratch,   h->d_gather, h->d_zig};
+                    h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
+                    h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -664,13 +910,34 @@ emcmc_status emcmc_get_chain_stats(emcmc_handle *h, double *rolling_ar, uint64_t
     if (!h) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    const uint64_t C = h->cfg.num_chains;
-    if (rolling_ar) HIPCHK(h, hipMemcpy(rolling_ar, h->d_ra, C * sizeof(double), hipMemcpyDeviceToHost));
+    const uint64_t PC = h->cfg.num_chains * h->updates.size();
+    if (rolling_ar) HIPCHK(h, hipMemcpy(rolling_ar, h->d_ra, PC * sizeof(double), hipMemcpyDeviceToHost));
     if (accepted) {
-        std::vector<uint32_t> a(C);
-        HIPCHK(h, hipMemcpy(a.data(), h->d_nacc, C * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        for (uint64_t c = 0; c < C; ++c) accepted[c] = a[c];
+        std::vector<uint32_t> a(PC);
+        HIPCHK(h, hipMemcpy(a.data(), h->d_nacc, PC * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        for (uint64_t i = 0; i < PC; ++i) accepted[i] = a[i];
     }
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_update_state(emcmc_handle *h, uint32_t pidx, double *epsilon, uint32_t *proposed,
+                                    uint32_t *accepted) {
+    if (!h) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (pidx < 1 || pidx > h->updates.size()) return fail(h, EMCMC_INVALID_ARG, "pidx %u", pidx);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t C = h->cfg.num_chains, q = pidx - 1;
+    const UpdateHost &u = h->updates[q];
+    if (epsilon) {
+        const size_t nc = u.coords.size();
+        if (u.kernel != EMCMC_RW_UNIFORM) return fail(h, EMCMC_INVALID_ARG, "update %u has no ϵ", pidx);
+        std::vector<double> e(nc * C);
+        HIPCHK(h, hipMemcpy(e.data(), h->d_eps + q * kMwgMaxD * C, e.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (size_t j = 0; j < nc; ++j) epsilon[c * nc + j] = e[j * C + c];
+    }
+    if (proposed) HIPCHK(h, hipMemcpy(proposed, h->d_aprop + q * C, C * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (accepted) HIPCHK(h, hipMemcpy(accepted, h->d_aacc + q * C, C * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return EMCMC_OK;
 }
 

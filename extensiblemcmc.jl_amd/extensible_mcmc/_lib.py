@@ -83,6 +83,19 @@ class EmcmcUpdateDesc(C.Structure):
     ]
 
 
+class EmcmcUnifRWAdaptation(C.Structure):
+    """AdaptationUnifRW parameters (include/emcmc.h emcmc_unifrw_adaptation)."""
+    _fields_ = [
+        ("adapt_every_k_steps", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("target_accpt_rate", C.c_double),
+        ("scale", C.c_double),
+        ("min", C.c_double),
+        ("max", C.c_double),
+        ("offset", C.c_double),
+    ]
+
+
 class EmcmcTargetDesc(C.Structure):
     _fields_ = [
         ("kind", C.c_uint32),
@@ -124,6 +137,9 @@ SIGNATURES = {
     "emcmc_last_error": (C.c_char_p, [_H]),
     "emcmc_get_state": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_get_chain_stats": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
+    "emcmc_get_update_state": (
+        _ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    ),
     "emcmc_get_faults": (_ST, [_H, C.POINTER(C.c_uint32)]),
     "emcmc_get_history": (_ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]),
     "emcmc_get_history_chains": (

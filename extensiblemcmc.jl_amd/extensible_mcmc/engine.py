@@ -87,6 +87,29 @@ class Engine:
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
 
+    def add_uniform_rw_update(self, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None):
+        """UniformRandomWalk(ϵ) on coords0 (0-based); adapt: None or a dict with
+        AdaptationUnifRW's k, target, scale, min, max, offset."""
+        coords = np.ascontiguousarray(coords0, dtype=np.uint32)
+        e = np.ascontiguousarray(np.broadcast_to(np.asarray(eps, dtype=np.float64), (len(coords),)))
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.RW_UNIFORM
+        u.prior = prior
+        u.num_coords = len(coords)
+        u.coords = L.u32ptr(coords)
+        u.epsilon = L.dptr(e)
+        ad = None
+        if adapt is not None:
+            ad = L.EmcmcUnifRWAdaptation(int(adapt["k"]), 0, float(adapt["target"]), float(adapt["scale"]),
+                                         float(adapt["min"]), float(adapt["max"]), float(adapt["offset"]))
+            u.adaptation = L.ADPT_UNIF_RW
+            u.reserved_ptr[0] = C.cast(C.pointer(ad), C.c_void_p)
+        if pos is not None:
+            p = np.ascontiguousarray(pos, dtype=np.uint8)
+            u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
+        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
+        self.num_updates += 1
+
     def add_update_desc(self, u: L.EmcmcUpdateDesc, keepalive=()):
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
@@ -144,13 +167,25 @@ class Engine:
         return th, ll
 
     def get_chain_stats(self):
-        ra = np.empty(self.cfg.num_chains, dtype=np.float64)
-        acc = np.empty(self.cfg.num_chains, dtype=np.uint64)
+        """Rolling acceptance and accepted counts, [P][C] each."""
+        P = max(1, self.num_updates)
+        ra = np.empty((P, self.cfg.num_chains), dtype=np.float64)
+        acc = np.empty((P, self.cfg.num_chains), dtype=np.uint64)
         self._check(
             self._lib.emcmc_get_chain_stats(self._h, L.dptr(ra), acc.ctypes.data_as(C.POINTER(C.c_uint64))),
             "emcmc_get_chain_stats",
         )
         return ra, acc
+
+    def get_update_state(self, pidx: int, nc: int = 0):
+        """(ϵ [C][nc] or None, proposed [C], accepted [C]) of update pidx (1-based)."""
+        Cn = self.cfg.num_chains
+        eps = np.empty((Cn, nc), dtype=np.float64) if nc else None
+        pr = np.empty(Cn, dtype=np.uint32)
+        ac = np.empty(Cn, dtype=np.uint32)
+        self._check(self._lib.emcmc_get_update_state(self._h, pidx, None if eps is None else L.dptr(eps), L.u32ptr(pr),
+                                                     L.u32ptr(ac)), "emcmc_get_update_state")
+        return eps, pr, ac
 
     def get_faults(self):
         f = np.empty(self.cfg.num_chains, dtype=np.uint32)

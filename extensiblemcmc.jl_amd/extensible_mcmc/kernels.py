@@ -330,16 +330,36 @@ class RandomWalkUpdate(MCMCParamUpdate):
             prior = L.PRIOR_IMPROPER
         else:
             raise UnsupportedPlugin(f"prior {type(self.prior).__name__} has no device plugin yet")
+        adapt = None
         if isinstance(self.adpt, NoAdaptation):
-            adpt = L.ADPT_NONE
+            pass
+        elif isinstance(self.adpt, AdaptationUnifRW) and isinstance(self.rw, UniformRandomWalk):
+            if self.adpt.kind != "scalar":
+                raise UnsupportedPlugin("AdaptationUnifRW with per-coordinate parameters has no device plugin yet")
+            a = self.adpt
+            adapt = {"k": a.adapt_every_k_steps, "target": a.target_accpt_rate, "scale": a.scale, "min": a.min,
+                     "max": a.max, "offset": a.offset}
         else:
-            raise UnsupportedPlugin(f"adaptation {type(self.adpt).__name__} has no device plugin yet")
+            raise UnsupportedPlugin(f"adaptation {type(self.adpt).__name__} has no device plugin for "
+                                    f"{type(self.rw).__name__} yet")
+        if np.any(getattr(self.rw, "pos", False)):
+            raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin yet")
         if isinstance(self.rw, GaussianRandomWalk):
-            if np.any(self.rw.pos):
-                raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin yet")
-            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior, adaptation=adpt)
+            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior)
+        elif isinstance(self.rw, UniformRandomWalk):
+            engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior)
         else:
             raise UnsupportedPlugin(f"transition kernel {type(self.rw).__name__} has no device plugin yet")
+
+    def pull_device_state(self, engine, pidx):
+        """After a run: the reference mutates updt.rw.ϵ and updt.adpt in place
+        (adaptation.jl:273-279); with many chains each chain has its own, so
+        ``self.rw.eps_chains`` / ``self.adpt.proposed_chains`` etc. hold [C] arrays."""
+        if isinstance(self.rw, UniformRandomWalk):
+            eps, pr, ac = engine.get_update_state(pidx, len(self.rw.eps))
+            self.rw.eps_chains = eps
+            if isinstance(self.adpt, AdaptationUnifRW):
+                self.adpt.proposed_chains, self.adpt.accepted_chains = pr, ac
 
 
 class MALAUpdate(MCMCGradientBasedUpdate):

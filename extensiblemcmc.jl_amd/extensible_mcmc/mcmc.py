@@ -234,6 +234,9 @@ def run(mcmc: MCMC, num_mcmc_steps: int, data, theta_init, callbacks=(), **kwarg
     for cb in callbacks:
         cb.init(mcmc.workspace)
     _run_loop(mcmc.workspace, local_wss, mcmc.updates, mcmc.schedule, list(callbacks))
+    for i, u in enumerate(mcmc.updates):  # adapted ϵ / counters, as the reference mutates them
+        if hasattr(u, "pull_device_state"):
+            u.pull_device_state(mcmc.workspace.engine, i + 1)
     for cb in callbacks:
         cb.cleanup(mcmc.workspace, local_wss, Step(None, None, num_mcmc_steps, 1))
     return mcmc.workspace, local_wss

@@ -65,7 +65,7 @@ typedef enum emcmc_status {
 
 /* Adaptation — src/transition_kernels/adaptation.jl */
 #define EMCMC_ADPT_NONE 0u      /* NoAdaptation          adaptation.jl:26 */
-#define EMCMC_ADPT_UNIF_RW 1u   /* AdaptationUnifRW      adaptation.jl:51-329 (reserved) */
+#define EMCMC_ADPT_UNIF_RW 1u   /* AdaptationUnifRW      adaptation.jl:51-329 */
 #define EMCMC_ADPT_HAARIO 2u    /* HaarioTypeAdaptation  adaptation.jl:372-426 (reserved) */
 
 /* Targets — src/example/gsn_target.jl */
@@ -117,17 +117,35 @@ typedef struct emcmc_config {
 #define EMCMC_VARIANT_HIGH_OCCUPANCY 1u  /* cap registers for 4 waves/SIMD where instantiated */
 #define EMCMC_VARIANT_OCCUPANCY3 2u      /* cap registers for 3 waves/SIMD where instantiated */
 
-/* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183). */
+/* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
+ * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,
+ * defaults 100, 0.234, 1.0, 1e-12, 1e7, 1e2).  Passed as
+ * emcmc_update_desc.reserved_ptr[0] when adaptation == EMCMC_ADPT_UNIF_RW. */
+typedef struct emcmc_unifrw_adaptation {
+    uint32_t adapt_every_k_steps;
+    uint32_t reserved;
+    double target_accpt_rate;
+    double scale;
+    double min;
+    double max;
+    double offset;
+} emcmc_unifrw_adaptation;
+
+/* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183).
+ * Any number of updates, each on any coordinate subset (Metropolis-within-Gibbs,
+ * BASELINE cfg 1 and the reference's own test, test/runtests.jl:87-114).  A single
+ * GaussianRandomWalk update on coords 1:D without adaptation runs on the fused
+ * kernels; every other schedule runs on the general schedule kernel (D ≤ 16). */
 typedef struct emcmc_update_desc {
-    uint32_t kernel;          /* EMCMC_RW_* */
-    uint32_t prior;           /* EMCMC_PRIOR_* */
-    uint32_t adaptation;      /* EMCMC_ADPT_* */
+    uint32_t kernel;          /* EMCMC_RW_UNIFORM or EMCMC_RW_GAUSSIAN */
+    uint32_t prior;           /* EMCMC_PRIOR_IMPROPER */
+    uint32_t adaptation;      /* EMCMC_ADPT_NONE, or EMCMC_ADPT_UNIF_RW (UniformRandomWalk only) */
     uint32_t num_coords;      /* length(coords) */
-    const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based) */
+    const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based), any order */
     const double *sigma;      /* GaussianRandomWalk Σ: num_coords² column-major */
-    const double *epsilon;    /* UniformRandomWalk ϵ: num_coords (reserved) */
-    const uint8_t *pos;       /* positivity flags or NULL (all false) */
-    const void *reserved_ptr[4];
+    const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
+    const uint8_t *pos;       /* positivity flags or NULL (all false; true is not on device yet) */
+    const void *reserved_ptr[4]; /* [0]: const emcmc_unifrw_adaptation* for EMCMC_ADPT_UNIF_RW */
     double reserved_f64[4];
 } emcmc_update_desc;
 
@@ -201,9 +219,16 @@ const char *emcmc_last_error(const emcmc_handle *h);
 /* Current θ ([C][D]) and ll ([C]) — state(global_ws), ll(local_ws). Either may be NULL. */
 emcmc_status emcmc_get_state(emcmc_handle *h, double *theta, double *ll);
 
-/* Current rolling acceptance (chain_statistics.jl:61-64) and accepted counts, per chain.
- * Either may be NULL. */
+/* Current rolling acceptance (chain_statistics.jl:61-64: the value of
+ * rolling_ar[last iteration][pidx]) and accepted counts, per update and chain:
+ * [P][C] each.  Either may be NULL. */
 emcmc_status emcmc_get_chain_stats(emcmc_handle *h, double *rolling_ar, uint64_t *accepted);
+
+/* Adaptation state of update `pidx` (1-based), per chain: the UniformRandomWalk
+ * ϵ as adapted (updt.rw.ϵ; [C][num_coords]) and AdaptationUnifRW's `proposed` /
+ * `accepted` counters ([C] each) (adaptation.jl:51-70).  Any pointer may be NULL. */
+emcmc_status emcmc_get_update_state(emcmc_handle *h, uint32_t pidx, double *epsilon, uint32_t *proposed,
+                                    uint32_t *accepted);
 
 /* Per-chain fault bits (EMCMC_FAULT_*), [C] uint32. */
 emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults);

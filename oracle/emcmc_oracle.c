@@ -411,3 +411,244 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
     }
     return bad;
 }
+
+/* ==========================================================================
+ * General schedule path: P ≥ 1 RandomWalkUpdates over coordinate subsets
+ * (Metropolis-within-Gibbs), UniformRandomWalk or GaussianRandomWalk,
+ * NoAdaptation or AdaptationUnifRW, ImproperPrior, GsnTargetLaw target.
+ *
+ * Restated (reference files under /root/reference/src):
+ *   schedule order, first step has no prev_ws ........... schedule.jl:56-89, run.jl:64-83
+ *   update_workspaces!: θ_local ← θ[coords]; ll ← ll of the previous step's
+ *     local workspace at its iteration (−Inf before the first step) .. run.jl:101-112
+ *   UniformRandomWalk rand: U = a + (b − a)·u, a = −ϵ, b = ϵ (Distributions'
+ *     Uniform), θ° = θ·(e^U·pos + 1·!pos) + U·!pos; pos = false ⇒ θ + U
+ *                                                           random_walk.jl:63-73
+ *   UniformRandomWalk logpdf (pos = false) = 0.0 ......... random_walk.jl:88-94
+ *   GaussianRandomWalk over the update's coordinates ..... random_walk.jl:145-171
+ *   set_parameters!(::Proposal): P°.θ[coords] ← θ°; P° persists across updates
+ *     and starts as deepcopy(data.P) — the target's μ, not θinit
+ *                                         updates.jl:198-205, workspaces.jl:225-233
+ *   loglikelihood(ws, ::Proposal) = loglikelihood(P°, obs) ... workspaces.jl:236-238
+ *   proposal history = θ with coords ← θ°; state history = θ after accept
+ *                                                         run.jl:231-240, 312-320
+ *   update_stats!: N counts every update step (from 1); ra_prev =
+ *     rolling_ar[max(1, iter−1)][pidx], 0.0 when (iter−1, pidx) did not run
+ *                                                         chain_statistics.jl:42-66
+ *   AdaptationUnifRW on its own turn: accepted += a, proposed += 1; when
+ *     proposed ≥ k: δ = scale/√max(1, iter/k − offset), a_r = accepted/proposed
+ *     (counters reset), ϵ ← clamp(ϵ + (a_r > target ? δ : −δ), min, max)
+ *                                              run.jl:136-178, adaptation.jl:273-329
+ * Variates: uniform j of update p at iter from block (j/2, attempt 0) with
+ * counter w = (p << 16): words (x,y) for even j, (z,w) for odd j, u ∈ [0,1)
+ * from 53 bits; Gaussian normals as in the single-update path (index j local
+ * to the update); the accept exponential as orc_exponential with pidx0 = p.
+ * ========================================================================== */
+
+#define ORC_MWG_MAXD 16
+typedef struct {
+    uint32_t kind; /* 1 uniform, 2 gaussian */
+    uint32_t nc;
+    uint32_t coords[ORC_MWG_MAXD];
+    double eps0[ORC_MWG_MAXD];
+    double L[ORC_MWG_MAXD * ORC_MWG_MAXD], iL[ORC_MWG_MAXD], c0;
+    int diag;
+    uint32_t adapt, k;
+    double target, scale, amin, amax, offset;
+} orc_mwg_update;
+
+/* table layout from Python (per update p, 64 doubles of params + 16 coords):
+ *   kind[P], nc[P], coords[P*16], eps[P*16], sigma[P*256] (nc×nc column-major),
+ *   adapt[P], k[P], aparams[P*5] = (target, scale, min, max, offset) */
+ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, uint32_t P, const uint32_t *kind,
+                           const uint32_t *nc, const uint32_t *coords, const double *eps, const double *sigma,
+                           const uint32_t *adapt, const uint32_t *adapt_k, const double *aparams,
+                           const double *t_sigma, uint64_t nobs, const double *obs, int ll_mode,
+                           uint32_t W, uint32_t nsteps, const uint32_t *step_iter, const uint32_t *step_pidx,
+                           uint64_t *N_io, uint32_t *last_iter_io, double *theta, double *mu_p, double *ll,
+                           double *ra, uint64_t *ring, uint32_t *nacc, uint32_t *aprop, uint32_t *aacc,
+                           double *eps_state, uint32_t *faults, double *hist_theta, double *hist_prop,
+                           double *hist_ll, uint8_t *hist_acc, int nthreads) {
+    if (D < 1 || D > ORC_MWG_MAXD || P < 1 || P > 64) return -2;
+    (void)zig();
+    orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
+    orc_mwg_update *U = (orc_mwg_update *)calloc(P, sizeof(orc_mwg_update));
+    if (!g || !U) return -3;
+    /* target constants (the rw Σ argument is unused here: pass Σ_t twice) */
+    int rc = gsn_prepare(g, D, t_sigma, t_sigma, nobs, obs, ll_mode | 0x100);
+    if (rc) {
+        free(g);
+        free(U);
+        return rc;
+    }
+    const int tdiag = is_diag_upper(t_sigma, D);
+    for (uint32_t p = 0; p < P; ++p) {
+        orc_mwg_update *u = &U[p];
+        u->kind = kind[p];
+        u->nc = nc[p];
+        if (u->nc < 1 || u->nc > ORC_MWG_MAXD) {
+            free(g);
+            free(U);
+            return -2;
+        }
+        for (uint32_t j = 0; j < u->nc; ++j) {
+            u->coords[j] = coords[p * ORC_MWG_MAXD + j];
+            u->eps0[j] = eps[p * ORC_MWG_MAXD + j];
+            if (u->coords[j] >= (uint32_t)D) {
+                free(g);
+                free(U);
+                return -2;
+            }
+        }
+        if (u->kind == 2) {
+            const int n = (int)u->nc;
+            if (orc_cholesky(sigma + (size_t)p * 256, n, u->L)) {
+                free(g);
+                free(U);
+                return -1;
+            }
+            for (int i = 0; i < n; ++i) u->iL[i] = 1.0 / u->L[(size_t)i * n + i];
+            u->c0 = mvnormal_c0(n, logdet_chol(u->L, n));
+            u->diag = is_diag_upper(sigma + (size_t)p * 256, n);
+        }
+        u->adapt = adapt[p];
+        u->k = adapt_k[p];
+        u->target = aparams[p * 5 + 0];
+        u->scale = aparams[p * 5 + 1];
+        u->amin = aparams[p * 5 + 2];
+        u->amax = aparams[p * 5 + 3];
+        u->offset = aparams[p * 5 + 4];
+    }
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const orc_zig_tables *zt = zig();
+    const uint64_t N_start = *N_io;
+    uint32_t last0[64];
+    for (uint32_t p = 0; p < P; ++p) last0[p] = last_iter_io[p];
+#pragma omp parallel for num_threads(nthreads > 0 ? nthreads : 1) schedule(static)
+    for (int64_t ci = 0; ci < (int64_t)C; ++ci) {
+        const uint64_t c = (uint64_t)ci;
+        const uint32_t chain_id = chain0 + (uint32_t)c;
+        double th[ORC_MWG_MAXD], mp[ORC_MWG_MAXD];
+        memcpy(th, theta + c * D, sizeof(double) * D);
+        memcpy(mp, mu_p + c * D, sizeof(double) * D);
+        double cll = ll[c];
+        uint32_t f = faults[c];
+        uint32_t last[64];
+        memcpy(last, last0, sizeof(uint32_t) * P);
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            const uint32_t iter = step_iter[s], p = step_pidx[s] - 1;
+            const orc_mwg_update *u = &U[p];
+            const uint32_t n = u->nc;
+            double *ep = eps_state + ((size_t)p * C + c) * ORC_MWG_MAXD;
+            double tl[ORC_MWG_MAXD], tp[ORC_MWG_MAXD];
+            for (uint32_t j = 0; j < n; ++j) tl[j] = th[u->coords[j]];
+            double ltd_fwd = 0.0, ltd_rev = 0.0;
+            if (u->kind == 1) { /* UniformRandomWalk, pos = false */
+                for (uint32_t j = 0; j < n; ++j) {
+                    const orc_u32x4 r = orc_draw(k0, k1, chain_id, iter, j >> 1, p, 0);
+                    const double uu = (j & 1u) ? orc_u01_closed0(r.v[2], r.v[3]) : orc_u01_closed0(r.v[0], r.v[1]);
+                    const double e = ep[j];
+                    const double a = -e, b = e;
+                    const double Uv = a + (b - a) * uu;
+                    tp[j] = tl[j] * 1.0 + Uv;
+                }
+            } else { /* GaussianRandomWalk over the update's coordinates */
+                double z[ORC_MWG_MAXD];
+                for (uint32_t j = 0; j < n; ++j) z[j] = orc_normal(zt, k0, k1, chain_id, iter, p, j, &f);
+                for (uint32_t i = 0; i < n; ++i) {
+                    double lz;
+                    if (u->diag) {
+                        lz = u->L[(size_t)i * n + i] * z[i];
+                    } else {
+                        lz = u->L[(size_t)i * n] * z[0];
+                        for (uint32_t j = 1; j <= i; ++j) lz = fma(u->L[(size_t)i * n + j], z[j], lz);
+                    }
+                    tp[i] = tl[i] + lz;
+                }
+                double r[ORC_MWG_MAXD];
+                for (uint32_t i = 0; i < n; ++i) r[i] = tp[i] - tl[i];
+                ltd_fwd = u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0;
+                for (uint32_t i = 0; i < n; ++i) r[i] = tl[i] - tp[i];
+                ltd_rev = u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0;
+            }
+            /* set_proposal!: history θ with coords ← θ°; P°.θ[coords] ← θ° */
+            double prop[ORC_MWG_MAXD];
+            memcpy(prop, th, sizeof(double) * D);
+            for (uint32_t j = 0; j < n; ++j) {
+                prop[u->coords[j]] = tp[j];
+                mp[u->coords[j]] = tp[j];
+            }
+            /* compute_ll!: loglikelihood(P°, obs) */
+            double llp, r[ORC_MWG_MAXD];
+            if (g->ll_mode == 0) {
+                llp = 0.0;
+                for (uint64_t kk = 0; kk < nobs; ++kk) {
+                    for (int i = 0; i < D; ++i) r[i] = obs[kk * D + i] - mp[i];
+                    llp = llp + (g->t_c0 - sqmahal(g->Lt, g->iLt, r, D, tdiag) / 2.0);
+                }
+            } else {
+                for (int i = 0; i < D; ++i) r[i] = g->xbar[i] - mp[i];
+                const double qv = sqmahal(g->Lt, g->iLt, r, D, tdiag);
+                llp = (double)nobs * g->t_c0 - (g->S_c + (double)nobs * qv) * 0.5;
+            }
+            if (!isfinite(llp)) f |= 1u;
+            const double llr = ((((llp - cll) + ltd_rev) - ltd_fwd) + 0.0) - 0.0;
+            const double E = orc_exponential(zt, k0, k1, chain_id, iter, p, &f);
+            const int acc = E > -llr;
+            if (hist_prop) memcpy(hist_prop + ((uint64_t)s * C + c) * D, prop, sizeof(double) * D);
+            if (acc) {
+                for (uint32_t j = 0; j < n; ++j) th[u->coords[j]] = tp[j];
+                cll = llp;
+                nacc[(size_t)p * C + c] += 1;
+            }
+            if (hist_theta) memcpy(hist_theta + ((uint64_t)s * C + c) * D, th, sizeof(double) * D);
+            if (hist_ll) hist_ll[(uint64_t)s * C + c] = cll;
+            if (hist_acc) hist_acc[(uint64_t)s * C + c] = (uint8_t)acc;
+            /* update_stats! rolling acceptance of update p */
+            {
+                const uint64_t N = N_start + s;
+                uint64_t *rg = ring + ((size_t)p * C + c) * 2;
+                int outside = 0;
+                if (iter > W) {
+                    uint32_t j = (iter - W) & 127u;
+                    outside = (int)((((j & 64u) ? rg[1] : rg[0]) >> (j & 63u)) & 1u);
+                }
+                const double ra_prev = (iter > 1 && last[p] == iter - 1) ? ra[(size_t)p * C + c] : 0.0;
+                const uint64_t mn = N < (uint64_t)W ? N : (uint64_t)W;
+                ra[(size_t)p * C + c] = (ra_prev * (double)W + (double)(acc - outside)) / (double)mn;
+                uint32_t j = iter & 127u;
+                uint64_t bit = 1ull << (j & 63u);
+                if (j & 64u) rg[1] = acc ? (rg[1] | bit) : (rg[1] & ~bit);
+                else rg[0] = acc ? (rg[0] | bit) : (rg[0] & ~bit);
+                last[p] = iter;
+            }
+            /* update_adaptation!: only the update whose turn it is registers */
+            if (u->adapt == 1) {
+                uint32_t *pr = aprop + (size_t)p * C + c, *ac = aacc + (size_t)p * C + c;
+                *ac += (uint32_t)acc;
+                *pr += 1;
+                if (*pr >= u->k) {
+                    const double delta = u->scale / sqrt(fmax(1.0, (double)iter / (double)u->k - u->offset));
+                    const double a_r = (*pr == 0) ? 0.0 : (double)*ac / (double)*pr;
+                    *pr = 0;
+                    *ac = 0;
+                    const double step = (a_r > u->target) ? delta : -delta;
+                    for (uint32_t j = 0; j < n; ++j) {
+                        double e = ep[j] + step;
+                        e = e < u->amax ? e : u->amax;
+                        ep[j] = e > u->amin ? e : u->amin;
+                    }
+                }
+            }
+        }
+        memcpy(theta + c * D, th, sizeof(double) * D);
+        memcpy(mu_p + c * D, mp, sizeof(double) * D);
+        ll[c] = cll;
+        faults[c] = f;
+    }
+    *N_io = N_start + nsteps;
+    for (uint32_t s = 0; s < nsteps; ++s) last_iter_io[step_pidx[s] - 1] = step_iter[s];
+    free(g);
+    free(U);
+    return 0;
+}

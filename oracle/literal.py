@@ -73,3 +73,73 @@ def run_chain(seed, chain, theta0, rw_sigma, t_sigma, obs, nsteps, iter0=1, W=10
         out["acc"].append(acc)
         out["ra"].append(ra)
     return {k: np.array(v) for k, v in out.items()}
+
+
+def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100):
+    """Literal single-chain restatement of the P-update loop (see
+    oracle/emcmc_oracle.c orc_run_mwg for the reference lines): plain Python
+    floats and numpy/LAPACK for the MvNormal logpdf."""
+    Lt = np.linalg.cholesky(np.asarray(t_sigma, dtype=float))
+    obs = np.asarray(obs, dtype=float)
+    th = np.array(theta0, dtype=float)
+    mp = np.array(mu0, dtype=float)           # P°.θ[1:d], starts at the target's μ
+    P = len(updates)
+    eps = [list(u["eps"]) if u["eps"] is not None else None for u in updates]
+    prop_c, acc_c = [0] * P, [0] * P
+    ll = -np.inf
+    N = 1
+    ra = {}                                    # (iter, p) → rolling_ar value
+    acc_hist = {}
+    out = {"theta": [], "prop": [], "ll": [], "acc": [], "ra": [], "eps": []}
+    for it, pidx in steps:
+        p = pidx - 1
+        u = updates[p]
+        cs = u["coords"]
+        tl = th[cs].copy()
+        if u["kind"] == 1:                     # UniformRandomWalk, pos = false
+            tp = np.empty_like(tl)
+            for j in range(len(cs)):
+                a, b = -eps[p][j], eps[p][j]
+                U = a + (b - a) * _oracle.uniform01(seed, chain, it, p, j)
+                tp[j] = tl[j] * (np.exp(U) * False + 1.0 * True) + U * True
+            ltd_fwd = ltd_rev = 0.0
+        else:                                  # GaussianRandomWalk
+            Lr = np.linalg.cholesky(np.asarray(u["sigma"], dtype=float))
+            z, _, _ = _oracle.step_variates(seed, chain, it, len(cs), pidx0=p)
+            tp = tl + Lr @ z
+            ltd_fwd = mvnormal_logpdf(tp, tl, Lr)
+            ltd_rev = mvnormal_logpdf(tl, tp, Lr)
+        prop = th.copy()
+        prop[cs] = tp
+        mp[cs] = tp                            # set_parameters!(P°, coords, θ°)
+        llp = 0.0
+        for x in obs:
+            llp += mvnormal_logpdf(x, mp, Lt)
+        _, E, _ = _oracle.step_variates(seed, chain, it, 1, pidx0=p)
+        llr = llp - ll + ltd_rev - ltd_fwd + 0.0 - 0.0
+        acc = bool(E > -llr)
+        if acc:
+            th[cs] = tp
+            ll = llp
+        acc_hist[(it, p)] = acc
+        prev = ra.get((it - 1, p), 0.0) if it > 1 else 0.0
+        outside = acc_hist.get((it - W, p), False) if it > W else False
+        ra[(it, p)] = (prev * W + (int(acc) - int(outside))) / min(W, N)
+        N += 1
+        if u["adapt"] is not None:             # AdaptationUnifRW, own turn
+            ad = u["adapt"]
+            acc_c[p] += int(acc)
+            prop_c[p] += 1
+            if prop_c[p] >= ad["k"]:
+                delta = ad["scale"] / np.sqrt(max(1.0, it / ad["k"] - ad["offset"]))
+                a_r = 0.0 if prop_c[p] == 0 else acc_c[p] / prop_c[p]
+                prop_c[p] = acc_c[p] = 0
+                eps[p] = [max(min(e + 1.0 * (2 * int(a_r > ad["target"]) - 1) * delta, ad["max"]), ad["min"])
+                          for e in eps[p]]
+        out["theta"].append(th.copy())
+        out["prop"].append(prop)
+        out["ll"].append(ll)
+        out["acc"].append(acc)
+        out["ra"].append(ra[(it, p)])
+        out["eps"].append([list(e) if e is not None else None for e in eps])
+    return out

@@ -208,3 +208,107 @@ def markstein_mismatches(b, x):
     """Count of x where the device's Markstein quotient differs from IEEE x / b."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     return int(lib().orc_markstein_mismatches(float(b), _d(x), x.size))
+
+
+# ---- general schedule path (P ≥ 1 updates, Metropolis-within-Gibbs) ---------
+MWG_MAXD = 16
+KIND_UNIFORM, KIND_GAUSSIAN = 1, 2
+
+
+def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None):
+    """One RandomWalkUpdate for run_mwg.  coords0: 0-based coordinates.
+    adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW)."""
+    return {"kind": kind, "coords": [int(c) for c in coords0], "eps": None if eps is None else list(eps),
+            "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt}
+
+
+class MWGState:
+    def __init__(self, theta, mu0, updates, ll=None):
+        theta = np.ascontiguousarray(theta, dtype=np.float64)
+        self.C, self.D = theta.shape
+        P = len(updates)
+        self.theta = theta.copy()
+        self.mu_p = np.ascontiguousarray(np.broadcast_to(np.asarray(mu0, dtype=np.float64), theta.shape)).copy()
+        self.ll = np.full(self.C, -np.inf) if ll is None else np.asarray(ll, dtype=np.float64).copy()
+        self.ra = np.zeros((P, self.C))
+        self.ring = np.zeros((P, self.C, 2), dtype=np.uint64)
+        self.nacc = np.zeros((P, self.C), dtype=np.uint32)
+        self.aprop = np.zeros((P, self.C), dtype=np.uint32)
+        self.aacc = np.zeros((P, self.C), dtype=np.uint32)
+        self.eps = np.zeros((P, self.C, MWG_MAXD))
+        for p, u in enumerate(updates):
+            if u["eps"] is not None:
+                self.eps[p, :, :len(u["eps"])] = u["eps"]
+        self.faults = np.zeros(self.C, dtype=np.uint32)
+        self.N = np.array([1], dtype=np.uint64)
+        self.last_iter = np.zeros(P, dtype=np.uint32)
+
+
+def _mwg_tables(updates):
+    P = len(updates)
+    kind = np.zeros(P, dtype=np.uint32)
+    nc = np.zeros(P, dtype=np.uint32)
+    coords = np.zeros((P, MWG_MAXD), dtype=np.uint32)
+    eps = np.zeros((P, MWG_MAXD))
+    sigma = np.zeros((P, 256))
+    adapt = np.zeros(P, dtype=np.uint32)
+    ak = np.ones(P, dtype=np.uint32)
+    ap = np.zeros((P, 5))
+    for p, u in enumerate(updates):
+        n = len(u["coords"])
+        kind[p], nc[p] = u["kind"], n
+        coords[p, :n] = u["coords"]
+        if u["eps"] is not None:
+            eps[p, :n] = u["eps"]
+        if u["sigma"] is not None:
+            sigma[p, :n * n] = np.asarray(u["sigma"], dtype=np.float64).reshape(n, n).ravel(order="F")
+        if u["adapt"] is not None:
+            a = u["adapt"]
+            adapt[p], ak[p] = 1, a["k"]
+            ap[p] = (a["target"], a["scale"], a["min"], a["max"], a["offset"])
+    return kind, nc, coords, eps, sigma, adapt, ak, ap
+
+
+def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll_mode=0, W=100, history=True,
+            nthreads=1):
+    """Advance `state` over `steps` [(mcmciter, pidx 1-based), …]; histories per step."""
+    L = lib()
+    if not hasattr(L, "_mwg_ready"):
+        dp, u32p, u64p, u8p = (C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_uint8))
+        L.orc_run_mwg.restype = C.c_int
+        L.orc_run_mwg.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, u32p, u32p, u32p, dp, dp,
+                                  u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
+                                  u64p, u32p, dp, dp, dp, dp, u64p, u32p, u32p, u32p, dp, u32p, dp, dp, dp, u8p,
+                                  C.c_int]
+        L._mwg_ready = True
+    Cn, D = state.C, state.D
+    kind, nc, coords, eps, sigma, adapt, ak, ap = _mwg_tables(updates)
+    steps = np.asarray(steps, dtype=np.uint32).reshape(-1, 2)
+    si = np.ascontiguousarray(steps[:, 0])
+    sp = np.ascontiguousarray(steps[:, 1])
+    n = steps.shape[0]
+    X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
+    hist = {"theta": np.empty((n, Cn, D)), "prop": np.empty((n, Cn, D)), "ll": np.empty((n, Cn)),
+            "acc": np.empty((n, Cn), dtype=np.uint8)} if history else {}
+    u32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))  # noqa: E731
+    u64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
+    rc = L.orc_run_mwg(
+        D, Cn, chain0, seed & 0xFFFFFFFFFFFFFFFF, len(updates), u32(kind), u32(nc), u32(coords), _d(eps), _d(sigma),
+        u32(adapt), u32(ak), _d(ap), _d(_colmajor(t_sigma, D)), X.shape[0], _d(X), ll_mode, W, n, u32(si), u32(sp),
+        u64(state.N), u32(state.last_iter), _d(state.theta), _d(state.mu_p), _d(state.ll), _d(state.ra),
+        u64(state.ring), u32(state.nacc), u32(state.aprop), u32(state.aacc), _d(state.eps), u32(state.faults),
+        _d(hist.get("theta")), _d(hist.get("prop")), _d(hist.get("ll")),
+        None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads)
+    if rc != 0:
+        raise ValueError(f"orc_run_mwg failed: {rc}")
+    if history:
+        hist["acc"] = hist["acc"].astype(bool)
+    return hist
+
+
+def uniform01(seed, chain, it, pidx0, j):
+    """The [0,1) uniform of coordinate j (update-local) of a UniformRandomWalk draw."""
+    r = philox([chain, it, j >> 1, (pidx0 << 16)], [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
+    hi, lo = (int(r[2]), int(r[3])) if j & 1 else (int(r[0]), int(r[1]))
+    return float((hi << 21) | (lo >> 11)) * 2.0 ** -53

@@ -77,6 +77,29 @@ def gsn_fixture(w, nchains, nsteps, ll_mode, seed):
     }
 
 
+def mwg_fixture():
+    """The reference's own test workload (test/runtests.jl:87-114): two single-site
+    UniformRandomWalk([1.0]) updates, 8 chains × 200 iterations, and the
+    tutorial's adaptive variant (ϵ = 0.1, AdaptationUnifRW k = 50, scale = 0.1)."""
+    w = W.ref_test()
+    out = {"obs": np.asarray(w.obs), "t_sigma": np.asarray(w.t_sigma), "mu0": np.array([1.0, 2.0]),
+           "seed": np.uint64(W.SEED)}
+    steps = [(i, p) for i in range(1, 201) for p in (1, 2)]
+    out["steps"] = np.asarray(steps, dtype=np.uint32)
+    for tag, eps, ad in (("plain", 1.0, None),
+                         ("adapt", 0.1, {"k": 50, "target": 0.234, "scale": 0.1, "min": 1e-12, "max": 1e7,
+                                          "offset": 1e2})):
+        ups = [O.mwg_update(1, [0], eps=[eps], adapt=ad), O.mwg_update(1, [1], eps=[eps], adapt=ad)]
+        st = O.MWGState(np.zeros((8, 2)), [1.0, 2.0], ups)
+        h = O.run_mwg(st, ups, seed=W.SEED, t_sigma=w.t_sigma, obs=w.obs, steps=steps)
+        out[f"{tag}_acc"] = h["acc"]
+        out[f"{tag}_theta"] = h["theta"]
+        out[f"{tag}_ll"] = h["ll"]
+        out[f"{tag}_ra"] = st.ra
+        out[f"{tag}_eps"] = st.eps[:, :, 0]
+    return out
+
+
 def main():
     O.build()
     (HERE / "philox_kat.json").write_text(json.dumps(PHILOX_KAT, indent=1))
@@ -86,6 +109,7 @@ def main():
     np.savez_compressed(HERE / "gsn_d2_iso.npz", **gsn_fixture(W.cfg1(True), 8, 200, 0, W.SEED))
     np.savez_compressed(HERE / "gsn_d32_perobs.npz", **gsn_fixture(W.cfg2(8), 8, 200, 0, W.SEED))
     np.savez_compressed(HERE / "gsn_d32_suffstat.npz", **gsn_fixture(W.cfg2(8), 8, 200, 1, W.SEED))
+    np.savez_compressed(HERE / "mwg_d2_reftest.npz", **mwg_fixture())
     print("wrote", sorted(p.name for p in HERE.iterdir()))
 
 

@@ -23,7 +23,8 @@ def run_engine(w, C, S, *, lpc=0, ll_mode=0, hist=L.HIST_FULL, spl=0, chain0=0, 
     eng.synchronize(allow_faults=True)
     out = {"engine": eng, "kernel": eng.kernel_name()}
     out["theta"], out["ll"] = eng.get_state()
-    out["ra"], out["nacc"] = eng.get_chain_stats()
+    ra, nacc = eng.get_chain_stats()
+    out["ra"], out["nacc"] = ra[0], nacc[0]
     out["faults"] = eng.get_faults()
     if fetch:
         out["acc"] = eng.get_history(L.H_ACCEPT, iter_first, S)[:, 0]

@@ -45,8 +45,9 @@ def test_struct_layout_matches_header(tmp_path):
         int main(void) {
           printf("%zu %zu %zu %zu %zu\\n", sizeof(emcmc_config), sizeof(emcmc_update_desc),
                  sizeof(emcmc_target_desc), sizeof(emcmc_step), sizeof(emcmc_moments));
-          printf("%zu %zu %zu\\n", offsetof(emcmc_config, device), offsetof(emcmc_update_desc, pos),
-                 offsetof(emcmc_target_desc, ll_mode));
+          printf("%zu %zu %zu %zu %zu\\n", offsetof(emcmc_config, device), offsetof(emcmc_update_desc, pos),
+                 offsetof(emcmc_target_desc, ll_mode), sizeof(emcmc_unifrw_adaptation),
+                 offsetof(emcmc_unifrw_adaptation, offset));
           return 0;
         }
         """
@@ -60,7 +61,8 @@ def test_struct_layout_matches_header(tmp_path):
                                                C.sizeof(L.EmcmcTargetDesc), C.sizeof(L.EmcmcStep),
                                                C.sizeof(L.EmcmcMoments)]
     assert [int(x) for x in offs.split()] == [L.EmcmcConfig.device.offset, L.EmcmcUpdateDesc.pos.offset,
-                                              L.EmcmcTargetDesc.ll_mode.offset]
+                                              L.EmcmcTargetDesc.ll_mode.offset, C.sizeof(L.EmcmcUnifRWAdaptation),
+                                              L.EmcmcUnifRWAdaptation.offset.offset]
 
 
 def test_no_device_means_no_run():

@@ -40,3 +40,20 @@ def test_sharding_equals_unsharded(oracle, golden_dir):
                        iter0=1, nsteps=200, chain0=5)
     assert np.array_equal(h["acc"], g["acc_hist"][:, 5:8])
     assert np.array_equal(st.theta, g["theta"][5:8])
+
+
+def test_mwg_reference_workload_fixture(oracle, golden_dir):
+    """The general-schedule oracle reproduces the committed reference-test fixture."""
+    g = np.load(golden_dir / "mwg_d2_reftest.npz")
+    steps = [tuple(int(v) for v in s) for s in g["steps"]]
+    for tag, eps, ad in (("plain", 1.0, None),
+                         ("adapt", 0.1, {"k": 50, "target": 0.234, "scale": 0.1, "min": 1e-12, "max": 1e7,
+                                          "offset": 1e2})):
+        ups = [oracle.mwg_update(1, [0], eps=[eps], adapt=ad), oracle.mwg_update(1, [1], eps=[eps], adapt=ad)]
+        st = oracle.MWGState(np.zeros((8, 2)), g["mu0"], ups)
+        h = oracle.run_mwg(st, ups, seed=int(g["seed"]), t_sigma=g["t_sigma"], obs=g["obs"], steps=steps)
+        assert np.array_equal(h["acc"], g[f"{tag}_acc"])
+        assert np.array_equal(h["theta"], g[f"{tag}_theta"])
+        assert np.array_equal(h["ll"], g[f"{tag}_ll"])
+        assert np.array_equal(st.ra, g[f"{tag}_ra"])
+        assert np.array_equal(st.eps[:, :, 0], g[f"{tag}_eps"])

@@ -4,9 +4,9 @@ MI355X backend, mirroring the reference's "mcmc" testset and tutorial
 import numpy as np
 import pytest
 
-from extensible_mcmc import (MCMC, GaussianRandomWalk, GsnTargetLaw, ImproperPrior, MI355XBackend,
-                             RandomWalkUpdate, REPLCallback, SavingCallback, UniformRandomWalk,
-                             UnsupportedPlugin, run)
+from extensible_mcmc import (MCMC, AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMix, GsnTargetLaw,
+                             ImproperPrior, MI355XBackend, RandomWalkUpdate, REPLCallback, SavingCallback,
+                             UniformRandomWalk, UnsupportedPlugin, run)
 from extensible_mcmc import workloads as W
 
 from helpers import run_oracle
@@ -42,7 +42,50 @@ def test_run_bivariate_joint_gaussian_rw(oracle, tmp_path):
 
 def test_unsupported_plugins_raise_not_fallback():
     w = W.ref_test()
-    mcmc = MCMC([RandomWalkUpdate(UniformRandomWalk([1.0]), [1]), RandomWalkUpdate(UniformRandomWalk([1.0]), [2])],
+    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(np.eye(2), 2 * np.eye(2)), [1, 2])],
                 backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
+    mcmc = MCMC([RandomWalkUpdate(UniformRandomWalk([1.0], [True]), [1]),
+                 RandomWalkUpdate(UniformRandomWalk([1.0]), [2])], backend=MI355XBackend(num_chains=8))
+    with pytest.raises(UnsupportedPlugin):  # positivity-restricted coordinates
+        run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
+
+
+def test_reference_mcmc_testset_through_the_api(oracle):
+    """test/runtests.jl:87-114 as written (two single-site UniformRandomWalk([1.0])
+    updates), through MCMC/run with the MI355X backend, against the oracle."""
+    w = W.ref_test()
+    mcmc = MCMC([RandomWalkUpdate(UniformRandomWalk([1.0]), [1]), RandomWalkUpdate(UniformRandomWalk([1.0]), [2])],
+                backend=MI355XBackend(num_chains=300, seed=w.seed))
+    ws, lwss = run(mcmc, 1000, dict(P=GsnTargetLaw([1.0, 2.0], [[1.0, 0.5], [0.5, 1.0]]), obs=w.obs), [0.0, 0.0])
+    ups = [oracle.mwg_update(1, [0], eps=[1.0]), oracle.mwg_update(1, [1], eps=[1.0])]
+    st = oracle.MWGState(np.zeros((300, 2)), [1.0, 2.0], ups)
+    h = oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs,
+                       steps=[(i, p) for i in range(1, 1001) for p in (1, 2)], nthreads=8)
+    assert "mwg_gsn_kernel" in ws.engine.kernel_name()
+    assert np.array_equal(ws.state, st.theta)
+    assert np.array_equal(lwss[0].acceptance_history(1, 1000), h["acc"][0::2])
+    assert np.array_equal(lwss[1].acceptance_history(1, 1000), h["acc"][1::2])
+    assert np.array_equal(ws.state_history(1, 1000)[:, 1], h["theta"][1::2])
+
+
+def test_tutorial_adaptation_through_the_api(oracle):
+    """mean_of_bivariate_gaussian.md: UniformRandomWalk([0.1]) with
+    AdaptationUnifRW([0.0]; adapt_every_k_steps=50, scale=0.1): the adapted ϵ of
+    every chain equals the oracle's."""
+    w = W.ref_test()
+    ups_api = [RandomWalkUpdate(UniformRandomWalk([0.1]), [i], prior=ImproperPrior(),
+                                adpt=AdaptationUnifRW([0.0], adapt_every_k_steps=50, scale=0.1)) for i in (1, 2)]
+    mcmc = MCMC(ups_api, backend=MI355XBackend(num_chains=256, seed=w.seed))
+    ws, lwss = run(mcmc, 1000, dict(P=GsnTargetLaw([0.3, 0.7], [[1.0, 0.5], [0.5, 1.0]]), obs=w.obs), [0.0, 0.0])
+    adapt = {"k": 50, "target": 0.234, "scale": 0.1, "min": 1e-12, "max": 1e7, "offset": 1e2}
+    ups = [oracle.mwg_update(1, [0], eps=[0.1], adapt=adapt), oracle.mwg_update(1, [1], eps=[0.1], adapt=adapt)]
+    st = oracle.MWGState(np.zeros((256, 2)), [0.3, 0.7], ups)
+    oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs,
+                   steps=[(i, p) for i in range(1, 1001) for p in (1, 2)], history=False, nthreads=8)
+    assert np.array_equal(ws.state, st.theta)
+    for p in (0, 1):
+        assert np.array_equal(ups_api[p].rw.eps_chains[:, 0], st.eps[p, :, 0])
+        assert np.array_equal(ups_api[p].adpt.proposed_chains, st.aprop[p])
+        assert np.array_equal(ups_api[p].adpt.accepted_chains, st.aacc[p])

@@ -1,0 +1,140 @@
+"""General schedule kernel (mwg_gsn_kernel) on the GPU against the oracle
+(orc_run_mwg), bit for bit: several updates per iteration over coordinate
+subsets in any order, UniformRandomWalk and GaussianRandomWalk, AdaptationUnifRW,
+exclusion schedules, split runs, both likelihood modes, both history modes."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc import workloads as W
+from extensible_mcmc.engine import Engine, EngineConfig
+from extensible_mcmc.schedule import MCMCSchedule
+
+pytestmark = pytest.mark.gpu
+
+ADAPT = {"k": 50, "target": 0.234, "scale": 0.1, "min": 1e-12, "max": 1e7, "offset": 1e2}
+
+
+@pytest.fixture(autouse=True)
+def _gpu(require_gpu):
+    pass
+
+
+def full_steps(M, P, first=1):
+    return [(i, p) for i in range(first, M + 1) for p in range(1, P + 1)]
+
+
+def make_engine(D, C, M, ups, mu, t_sigma, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL, spl=0, theta0=None):
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
+                              steps_per_launch=spl))
+    for u in ups:
+        if u["kind"] == 1:
+            eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"])
+        else:
+            eng.add_gaussian_rw_update(u["coords"], u["sigma"])
+    eng.set_gsn_target(mu, t_sigma, obs, ll_mode=ll_mode)
+    eng.set_state(np.zeros((C, D)) if theta0 is None else theta0)
+    return eng
+
+
+def check(oracle, eng, st, h, steps, ups, P, full=True):
+    eng.synchronize(allow_faults=True)
+    th, ll = eng.get_state()
+    assert np.array_equal(th, st.theta)
+    assert np.array_equal(ll, st.ll)
+    ra, nacc = eng.get_chain_stats()
+    assert np.array_equal(ra, st.ra)
+    assert np.array_equal(nacc, st.nacc)
+    assert np.array_equal(eng.get_faults(), st.faults)
+    iters = sorted({i for i, _ in steps})
+    i0, n = iters[0], iters[-1] - iters[0] + 1
+    acc = eng.get_history(L.H_ACCEPT, i0, n)
+    hs = eng.get_history(L.H_STATE, i0, n) if full else None
+    hp = eng.get_history(L.H_PROPOSAL, i0, n) if full else None
+    hl = eng.get_history(L.H_LL, i0, n) if full else None
+    for s, (it, p) in enumerate(steps):
+        assert np.array_equal(acc[it - i0, p - 1], h["acc"][s]), f"accepts at step {s} ({it}, {p})"
+        if full:
+            assert np.array_equal(hs[it - i0, p - 1], h["theta"][s])
+            assert np.array_equal(hp[it - i0, p - 1], h["prop"][s])
+            assert np.array_equal(hl[it - i0, p - 1], h["ll"][s])
+    for p, u in enumerate(ups):
+        if u["kind"] == 1:
+            eps, pr, ac = eng.get_update_state(p + 1, len(u["coords"]))
+            assert np.array_equal(eps, st.eps[p, :, :len(u["coords"])])
+            assert np.array_equal(pr, st.aprop[p]) and np.array_equal(ac, st.aacc[p])
+
+
+def run_both(oracle, D, C, M, ups, mu, t_sigma, obs, steps, seed, **kw):
+    eng = make_engine(D, C, M, ups, mu, t_sigma, obs, seed, **kw)
+    eng.run(steps)
+    st = oracle.MWGState(np.zeros((C, D)), mu, ups)
+    h = oracle.run_mwg(st, ups, seed=seed, t_sigma=t_sigma, obs=obs, steps=steps,
+                       ll_mode=kw.get("ll_mode", 0), nthreads=8)
+    return eng, st, h
+
+
+@pytest.mark.parametrize("kind", ["uniform", "gaussian", "adaptive"])
+def test_reference_single_site(oracle, kind):
+    """test/runtests.jl:87-114 and the tutorial variants: D = 2, P = 2."""
+    w = W.ref_test()
+    if kind == "gaussian":
+        ups = [oracle.mwg_update(2, [0], sigma=[[1.0]]), oracle.mwg_update(2, [1], sigma=[[1.0]])]
+    else:
+        eps, ad = (0.1, ADAPT) if kind == "adaptive" else (1.0, None)
+        ups = [oracle.mwg_update(1, [0], eps=[eps], adapt=ad), oracle.mwg_update(1, [1], eps=[eps], adapt=ad)]
+    steps = full_steps(400, 2)
+    eng, st, h = run_both(oracle, 2, 1000, 400, ups, [1.0, 2.0], w.t_sigma, w.obs, steps, w.seed)
+    assert "mwg_gsn_kernel<D=2,P=2" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 2)
+
+
+def test_exclusions_and_split_runs(oracle):
+    """exclude_updates: update 2 off on iterations 5:40; the schedule is run in
+    three calls with 7-step launches."""
+    w = W.ref_test()
+    ups = [oracle.mwg_update(1, [0], eps=[0.5]), oracle.mwg_update(1, [1], eps=[0.5])]
+    steps = [(s.mcmciter, s.pidx) for s in MCMCSchedule(150, 2, [(2, range(5, 41))])]
+    eng = make_engine(2, 333, 150, ups, [1.0, 2.0], w.t_sigma, w.obs, w.seed, spl=7)
+    for a, b in ((0, 50), (50, 51), (51, len(steps))):
+        eng.run(steps[a:b])
+    st = oracle.MWGState(np.zeros((333, 2)), [1.0, 2.0], ups)
+    h = oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs, steps=steps, nthreads=8)
+    check(oracle, eng, st, h, steps, ups, 2)
+
+
+@pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
+@pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
+def test_block_updates_mixed_kernels(oracle, ll_mode, hist):
+    """D = 4: a dense GaussianRandomWalk block on coords (3, 1) and an adaptive
+    UniformRandomWalk block on coords (4, 2) (1-based, out of order)."""
+    w = W.cfg2(64)
+    D = 4
+    rng = np.random.default_rng(5)
+    A = rng.standard_normal((D, D))
+    ts = A @ A.T / D + np.eye(D)
+    obs = rng.standard_normal((12, D)) + 0.5
+    mu = np.array([0.1, -0.2, 0.3, 0.0])
+    ups = [oracle.mwg_update(2, [2, 0], sigma=[[0.09, 0.02], [0.02, 0.04]]),
+           oracle.mwg_update(1, [3, 1], eps=[0.3, 0.2], adapt=dict(ADAPT, k=20))]
+    steps = full_steps(300, 2)
+    eng, st, h = run_both(oracle, D, 900, 300, ups, mu, ts, obs, steps, w.seed, ll_mode=ll_mode, hist=hist)
+    check(oracle, eng, st, h, steps, ups, 2, full=(hist == L.HIST_FULL))
+
+
+@pytest.mark.parametrize("D,split", [(8, (8,)), (16, (8, 8)), (16, (16,)), (3, (1, 2))])
+def test_dimensions_and_canonical_blocks(oracle, D, split):
+    """Updates of 1, 2, 8 and 16 coordinates (the 16-coordinate update sums in
+    two canonical blocks); coords reversed so the general path is taken."""
+    w = W.cfg2(256)
+    obs = np.asarray(w.obs)[:, :D]
+    ts = np.asarray(w.t_sigma)[:D, :D]
+    mu = np.asarray(w.mu_true)[:D]
+    ups, c0 = [], 0
+    for n in split:
+        coords = list(range(c0, c0 + n))[::-1]
+        ups.append(oracle.mwg_update(2, coords, sigma=0.02 * np.eye(n)))
+        c0 += n
+    steps = full_steps(120, len(ups))
+    eng, st, h = run_both(oracle, D, 256, 120, ups, mu, ts, obs, steps, w.seed)
+    check(oracle, eng, st, h, steps, ups, len(ups))

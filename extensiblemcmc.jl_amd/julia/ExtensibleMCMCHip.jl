@@ -109,16 +109,48 @@ struct MI355XLocalWorkspace{T} <: eMCMC.LocalWorkspace{T}
     pidx::Int
 end
 
+struct EmcmcUnifRWAdaptation
+    adapt_every_k_steps::UInt32
+    reserved::UInt32
+    target_accpt_rate::Float64
+    scale::Float64
+    min::Float64
+    max::Float64
+    offset::Float64
+end
+
+const RW_UNIFORM = UInt32(1)
+const ADPT_UNIF_RW = UInt32(1)
+
 function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
-    updt.rw isa eMCMC.GaussianRandomWalk || error("no device plugin for $(typeof(updt.rw))")
     updt.prior isa eMCMC.ImproperPrior || error("no device plugin for $(typeof(updt.prior))")
-    updt.adpt isa eMCMC.NoAdaptation || error("no device plugin for $(typeof(updt.adpt))")
     coords = UInt32.(collect(updt.coords) .- 1)                 # 0-based across the ABI
-    Σ = Matrix{Float64}(updt.rw.Σ)                             # column-major already
-    push!(keep, coords, Σ)
-    EmcmcUpdateDesc(RW_GAUSSIAN, PRIOR_IMPROPER, ADPT_NONE, UInt32(length(coords)),
-                    pointer(coords), pointer(Σ), C_NULL, C_NULL,
-                    (C_NULL, C_NULL, C_NULL, C_NULL), (0.0, 0.0, 0.0, 0.0))
+    push!(keep, coords)
+    adpt, adptp = ADPT_NONE, C_NULL
+    if updt.rw isa eMCMC.GaussianRandomWalk
+        updt.adpt isa eMCMC.NoAdaptation || error("no device plugin for $(typeof(updt.adpt)) with GaussianRandomWalk")
+        any(updt.rw.pos) && error("positivity-restricted coordinates are not on device yet")
+        Σ = Matrix{Float64}(updt.rw.Σ)                         # column-major already
+        push!(keep, Σ)
+        return EmcmcUpdateDesc(RW_GAUSSIAN, PRIOR_IMPROPER, ADPT_NONE, UInt32(length(coords)), pointer(coords),
+                               pointer(Σ), C_NULL, C_NULL, (C_NULL, C_NULL, C_NULL, C_NULL), (0.0, 0.0, 0.0, 0.0))
+    elseif updt.rw isa eMCMC.UniformRandomWalk
+        any(updt.rw.pos) && error("positivity-restricted coordinates are not on device yet")
+        ϵ = Float64.(collect(updt.rw.ϵ))
+        push!(keep, ϵ)
+        if updt.adpt isa eMCMC.AdaptationUnifRW{Float64}      # scalar form (adaptation.jl:162-169)
+            a = updt.adpt
+            p = Ref(EmcmcUnifRWAdaptation(UInt32(a.adapt_every_k_steps), UInt32(0), a.target_accpt_rate, a.scale,
+                                          a.min, a.max, a.offset))
+            push!(keep, p)
+            adpt, adptp = ADPT_UNIF_RW, Base.unsafe_convert(Ptr{Cvoid}, p)
+        elseif !(updt.adpt isa eMCMC.NoAdaptation)
+            error("no device plugin for $(typeof(updt.adpt))")
+        end
+        return EmcmcUpdateDesc(RW_UNIFORM, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords), C_NULL,
+                               pointer(ϵ), C_NULL, (adptp, C_NULL, C_NULL, C_NULL), (0.0, 0.0, 0.0, 0.0))
+    end
+    error("no device plugin for $(typeof(updt.rw))")
 end
 
 # workspaces.jl:38 — init_global_workspace(::MCMCBackend, …)

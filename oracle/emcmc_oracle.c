@@ -293,6 +293,8 @@ static void run_chain(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t ke
             outside = (int)((((j & 64u) ? ring1 : ring0) >> (j & 63u)) & 1u);
         }
         const uint64_t mn = N < (uint64_t)W ? N : (uint64_t)W;
+        /* rolling_ar[iter−1] of an iteration that did not run reads 0.0 */
+        if (s > 0 && iter != (iters ? iters[s - 1] : iter0 + s - 1) + 1) ra = 0.0;
         ra = (ra * (double)W + (double)(acc - outside)) / (double)mn;
         {
             uint32_t j = iter & 127u;

@@ -87,6 +87,7 @@ class OracleState:
         self.nacc = np.zeros(self.C, dtype=np.uint32)
         self.faults = np.zeros(self.C, dtype=np.uint32)
         self.N = 1  # GenericChainStats.N
+        self.last_iter = 0  # last iteration run (rolling_ar[iter−1] reads 0.0 after a gap)
 
 
 def alloc_history(C, D, nsteps):
@@ -108,6 +109,9 @@ def run_gsn(state: OracleState, *, seed, rw_sigma, t_sigma, obs, iter0, nsteps, 
     it = None
     if iters is not None:
         it = np.ascontiguousarray(iters, dtype=np.uint32)
+    first = int(it[0]) if it is not None else int(iter0)
+    if first > 1 and state.last_iter != first - 1:
+        state.ra[:] = 0.0
     rc = L.orc_run_gsn(
         D, Cn, chain0, seed & 0xFFFFFFFFFFFFFFFF, _d(_colmajor(rw_sigma, D)), _d(_colmajor(t_sigma, D)), X.shape[0],
         _d(X), ll_mode, W, None if it is None else it.ctypes.data_as(C.POINTER(C.c_uint32)), iter0, nsteps,
@@ -119,6 +123,7 @@ def run_gsn(state: OracleState, *, seed, rw_sigma, t_sigma, obs, iter0, nsteps, 
     if rc != 0:
         raise ValueError(f"orc_run_gsn failed: {rc}")
     state.N += nsteps
+    state.last_iter = int(it[-1]) if it is not None else int(iter0) + nsteps - 1
     if history and not reuse:
         hist["acc"] = hist["acc"].astype(bool)
     return hist

@@ -7,6 +7,7 @@ import pytest
 
 from extensible_mcmc import _lib as L
 from extensible_mcmc import workloads as W
+from extensible_mcmc.engine import Engine, EngineConfig
 
 from helpers import assert_bitwise, run_engine, run_oracle
 
@@ -118,3 +119,25 @@ def test_nonfinite_target_sets_fault_bit():
     e = run_engine(w, 64, 5, fetch=False)
     assert (e["faults"] & L.FAULT_NONFINITE_LL).all()
     assert not e["engine"].synchronize(allow_faults=True)
+
+
+def test_fused_schedule_gap_restarts_rolling_rate(oracle):
+    """A schedule gap (iterations 41:60 skipped) on the fused single-update
+    kernel: rolling_ar[iter−1] of a skipped iteration reads 0.0
+    (chain_statistics.jl:57), in the engine and in the oracle."""
+    w = W.cfg2(500)
+    eng = Engine(EngineConfig(dim=w.D, num_chains=500, num_mcmc_steps=120, seed=w.seed))
+    eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    eng.set_state(np.zeros((500, w.D)))
+    eng.run_iters(1, 40)
+    eng.run_iters(61, 60)
+    eng.synchronize()
+    st = oracle.OracleState(np.zeros((500, w.D)))
+    iters = np.concatenate([np.arange(1, 41), np.arange(61, 121)]).astype(np.uint32)
+    oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=100,
+                   iters=iters, nthreads=8, history=False)
+    th, ll = eng.get_state()
+    ra, _ = eng.get_chain_stats()
+    assert np.array_equal(th, st.theta) and np.array_equal(ll, st.ll)
+    assert np.array_equal(ra[0], st.ra)

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
 """bench.py — MCMC steps×chains/sec on the D=32 Gaussian target (BASELINE cfg 2).
 
+--workload cfg4 measures BASELINE cfg 4 instead: GaussianRandomWalkMix +
+HaarioTypeAdaptation with the per-chain running mean/cov kept on device
+(131,072 chains by default); same metric and JSON contract.
+
 One "step" = one MCMC iteration of every chain on every GPU: proposal,
 log-prior, log-likelihood, MH accept/reject, rolling acceptance and the full
 per-step histories (θ, θ°, ll, accept bit) written to HBM — the reference's
@@ -35,7 +39,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--chains-per-gpu", type=int, default=65536)
+    ap.add_argument("--workload", choices=["cfg2", "cfg4"], default="cfg2")
+    ap.add_argument("--chains-per-gpu", type=int, default=0, help="0: 65,536 (cfg2) / 131,072 (cfg4)")
+    ap.add_argument("--haario-k", type=int, default=200)
     ap.add_argument("--history", choices=["full", "accept_only"], default="full")
     ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
     ap.add_argument("--lpc", type=int, default=0)
@@ -55,22 +61,33 @@ def cpu_baseline(w, seconds, ll_mode):
     threads = max(1, min(threads, 16))
     C = 256 * threads
     chunk = 50
-    st = O.OracleState(np.zeros((C, w.D)))
-    hist = O.alloc_history(C, w.D, chunk)
+    mix = w.haario_k is not None
+    if mix:
+        st = O.MixState(np.zeros((C, w.D)), sigma_b=w.sigma_b)
+
+        def step(it):
+            O.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
+                      lam=w.lam, haario_k=w.haario_k, ll_mode=ll_mode, nthreads=threads)
+    else:
+        st = O.OracleState(np.zeros((C, w.D)))
+        hist = O.alloc_history(C, w.D, chunk)
+
+        def step(it):
+            O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
+                      ll_mode=ll_mode, nthreads=threads, hist=hist)
     it = 1
-    O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
-              ll_mode=ll_mode, nthreads=threads, hist=hist)  # warm (page faults, caches)
+    step(it)  # warm (page faults, caches)
     it += chunk
     steps = 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
-                  ll_mode=ll_mode, nthreads=threads, hist=hist)
+        step(it)
         it += chunk
         steps += chunk
     dt = time.perf_counter() - t0
+    what = ("GaussianRandomWalkMix + HaarioTypeAdaptation(k=%d) + chain mean/cov" % w.haario_k) if mix else "RWM"
     return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{C} chains x {steps} iterations of the same D=32 workload ({w.nobs} obs, "
+            "sample": f"{C} chains x {steps} iterations of the same D=32 {what} workload ({w.nobs} obs, "
                       f"{'per-observation' if ll_mode == 0 else 'sufficient-statistic'} log-likelihood, "
                       f"full histories), oracle/liboracle.so, {dt:.1f} s"}
 
@@ -93,20 +110,24 @@ def main():
     from extensible_mcmc import workloads as W
     from extensible_mcmc.engine import Engine, EngineConfig
 
-    Cg = a.chains_per_gpu
-    w = W.cfg2(Cg)
+    cfg4 = a.workload == "cfg4"
+    Cg = a.chains_per_gpu or (131072 if cfg4 else 65536)
+    w = W.cfg4(Cg, k=a.haario_k) if cfg4 else W.cfg2(Cg)
     ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
     hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
     M = a.warmup + a.steps * a.reps
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=rank * Cg,
                               device=local, history_mode=hist, lanes_per_chain=a.lpc,
                               steps_per_launch=a.steps_per_launch))
-    eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    if cfg4:
+        eng.add_gaussian_rw_mix_update(np.arange(w.D), w.rw_sigma, w.sigma_b, lam=w.lam, haario_k=w.haario_k)
+    else:
+        eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
     eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
     eng.set_state(np.zeros((Cg, w.D)))
     if a.warmup:
         eng.run_iters(1, a.warmup)
-    eng.synchronize()
+    eng.synchronize(allow_faults=cfg4)  # cfg 4: PosDef faults are counted and reported
 
     def barrier():
         if dist is not None:
@@ -124,7 +145,7 @@ def main():
             torch.cuda.synchronize()
         t0 = time.perf_counter()
         eng.run_iters(it, a.steps)
-        eng.synchronize()
+        eng.synchronize(allow_faults=cfg4)
         if dist is not None:
             torch.cuda.synchronize()
         barrier()
@@ -183,16 +204,21 @@ def main():
         "dtype": "f64",
         "data": "synthetic (GsnTargetLaw(μ*, I32), 10 obs from numpy default_rng(20261015)), θinit = 0",
         "config": {
-            "workload": f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64",
+            "workload": (f"BASELINE cfg 4: {Cg} adaptive RWM chains per GPU (GaussianRandomWalkMix + "
+                         f"HaarioTypeAdaptation, per-chain running mean/cov on device), D=32 Gaussian target, fp64"
+                         if cfg4 else
+                         f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64"),
             "chains_per_gpu": Cg,
             "total_chains": total_chains,
             "dim": w.D,
             "num_obs": w.nobs,
-            "proposal": "GaussianRandomWalk(σ²I32), σ=2.38/√(D·n)",
+            "proposal": (f"GaussianRandomWalkMix(σ²I32, σ²I32, λ={w.lam}) + HaarioTypeAdaptation(k={w.haario_k})"
+                         if cfg4 else "GaussianRandomWalk(σ²I32), σ=2.38/√(D·n)"),
             "prior": "ImproperPrior",
             "history": a.history,
             "ll_mode": a.ll_mode,
-            "chain_stats": "rolling acceptance (chain_statistics.jl:51-65)",
+            "chain_stats": ("rolling acceptance + running mean/cov (chain_statistics.jl:41-66)" if cfg4
+                            else "rolling acceptance (chain_statistics.jl:51-65)"),
             "steps_per_launch": a.steps_per_launch,
             "kernel": kname,
             "parallelism": f"chain-sharded x{world}",
@@ -208,10 +234,12 @@ def main():
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "avg_launch_ms": avg_launch_s * 1e3,
             "launches": launches,
-            "bytes_per_chain_step": (16 * w.D + 8 + 0.125) if hist == L.HIST_FULL else 0.125,
+            "bytes_per_chain_step": bytes_per_launch / (Cg * a.steps / launches),
         },
         "kernel_chain_steps_per_s": Cg * a.steps / (ms / 1e3),
     }
+    if cfg4:
+        out["posdef_faulted_chains"] = int(np.count_nonzero(eng.get_faults() & L.FAULT_POSDEF))
     if diag is not None:
         out["diagnostics"] = {"accept_rate": diag["accept_rate"], "max_split_rhat": float(np.max(diag["rhat"])),
                               "max_abs_mean_minus_xbar": float(np.max(np.abs(diag["mean"] - w.obs.mean(0))))}
@@ -243,9 +271,14 @@ def parity_sample(eng, w, a, ll_mode, n=8):
     theta, ll = eng.get_state()
     ok_acc = ok_th = True
     for c in picks:
-        st = O.OracleState(np.zeros((1, w.D)))
-        h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
-                      chain0=int(c), ll_mode=ll_mode, history=True)
+        if w.haario_k is not None:
+            st = O.MixState(np.zeros((1, w.D)), sigma_b=w.sigma_b)
+            h = O.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
+                          lam=w.lam, haario_k=w.haario_k, chain0=int(c), ll_mode=ll_mode)
+        else:
+            st = O.OracleState(np.zeros((1, w.D)))
+            h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
+                          chain0=int(c), ll_mode=ll_mode, history=True)
         ok_acc &= bool(np.array_equal(acc[:, c], h["acc"][:, 0]))
         ok_th &= bool(np.array_equal(theta[c], st.theta[0]) and ll[c] == st.ll[0])
     return {"chains_replayed": int(n), "iterations": int(S), "accept_stream_bitwise": ok_acc,

@@ -20,6 +20,7 @@
 
 #include "../../include/emcmc.h"
 #include "emcmc_kernels.h"
+#include "emcmc_mix.h"
 #include "emcmc_mwg.h"
 
 using namespace emcmc;
@@ -95,6 +96,10 @@ struct UpdateHost {
     emcmc_unifrw_adaptation adpt{};         // AdaptationUnifRW (scalar form)
     bool diag = false;
     double c0 = 0.0;
+    // GaussianRandomWalkMix: Σ_B, its factor, λ; HaarioTypeAdaptation
+    std::vector<double> sigma_b, LB, invdiagB;
+    double c0B = 0.0, lam = 0.0;
+    emcmc_haario_adaptation haario{};
 };
 
 struct TargetHost {
@@ -107,10 +112,15 @@ struct TargetHost {
 
 using KernelFn = void (*)(StepParams);
 using MwgFn = void (*)(MwgParams);
+using MixFn = void (*)(MixParams);
+using ReadjustFn = void (*)(MixReadjustParams);
 
 struct Variant {
     KernelFn fn = nullptr;
     MwgFn mfn = nullptr;  // general schedule kernel (mwg_gsn_kernel) when set
+    MixFn xfn = nullptr;  // mix / chain-moments kernel (mix_gsn_kernel) when set
+    ReadjustFn rfn = nullptr;  // Haario readjust kernel
+    bool mix = false;
     int lpc = 1;
     bool dense = false;
     bool unit = false;
@@ -148,6 +158,11 @@ struct emcmc_handle {
     std::vector<uint32_t> last_iter;                    // per update: last iteration it ran (uniform)
     std::vector<std::vector<uint32_t>> steps_staging;   // host step lists alive until synchronize
     uint64_t steps_used = 0;
+    // mix / chain-moments path (mix_gsn_kernel): GenericChainStats mean/cov,
+    // per-chain Σ_B factor, Haario M (same for every chain)
+    double *d_mean = nullptr, *d_cov = nullptr, *d_LB = nullptr, *d_iLB = nullptr, *d_c0B = nullptr;
+    double *d_Lnew = nullptr;
+    uint32_t mix_M = 0;
     // dispatch
     Variant var;
     size_t lds_bytes = 0;
@@ -250,6 +265,25 @@ int auto_lpc(int D) {
     return 1;
 }
 
+// one update, joint on coords 1:D in order
+bool joint_all_coords(const emcmc_handle *h) {
+    if (h->updates.size() != 1) return false;
+    const UpdateHost &u = h->updates[0];
+    if (u.coords.size() != h->cfg.dim) return false;
+    for (uint32_t i = 0; i < h->cfg.dim; ++i)
+        if (u.coords[i] != i) return false;
+    return true;
+}
+
+// GaussianRandomWalkMix (± Haario), or GaussianRandomWalk with chain moments:
+// the mix kernels
+bool mix_path(const emcmc_handle *h) {
+    if (!joint_all_coords(h)) return false;
+    const UpdateHost &u = h->updates[0];
+    return u.kernel == EMCMC_RW_GAUSSIAN_MIX ||
+           (u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE && h->cfg.chain_moments);
+}
+
 // P°.θ[1:d] ← μ for every chain (workspaces.jl:225-233: P° = deepcopy(data.P))
 emcmc_status reset_mu_p(emcmc_handle *h) {
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
@@ -283,6 +317,18 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
         build_ziggurat(zt);
         HIPCHK(h, hipMalloc(&h->d_zig, sizeof(Ziggurat)));
         HIPCHK(h, hipMemcpy(h->d_zig, &zt, sizeof(Ziggurat), hipMemcpyHostToDevice));
+    }
+    if (mix_path(h)) {  // GenericChainStats mean/cov; Σ_B factors
+        const uint64_t DP = (uint64_t)packed_n((int)D);
+        const UpdateHost &u = h->updates[0];
+        HIPCHK(h, hipMalloc(&h->d_mean, C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_cov, C * DP * sizeof(double)));
+        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) {
+            HIPCHK(h, hipMalloc(&h->d_LB, C * DP * sizeof(double)));
+            HIPCHK(h, hipMalloc(&h->d_iLB, C * D * sizeof(double)));
+            HIPCHK(h, hipMalloc(&h->d_c0B, C * sizeof(double)));
+        }
+        if (u.adaptation == EMCMC_ADPT_HAARIO) HIPCHK(h, hipMalloc(&h->d_Lnew, C * DP * sizeof(double)));
     }
     h->row_bytes = ((C + 63) / 64) * 8;
     HIPCHK(h, hipMalloc(&h->d_hist_acc, M * P * h->row_bytes));
@@ -379,17 +425,110 @@ emcmc_status select_mwg(emcmc_handle *h) {
 }
 
 bool fused_eligible(const emcmc_handle *h) {
-    if (h->updates.size() != 1) return false;
+    if (!joint_all_coords(h) || h->cfg.chain_moments) return false;
     const UpdateHost &u = h->updates[0];
-    if (u.kernel != EMCMC_RW_GAUSSIAN || u.adaptation != EMCMC_ADPT_NONE) return false;
-    if (u.coords.size() != h->cfg.dim) return false;
-    for (uint32_t i = 0; i < h->cfg.dim; ++i)
-        if (u.coords[i] != i) return false;
-    return true;
+    return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
+}
+
+// ---- mix kernel table -------------------------------------------------------
+template <int D, bool FULL, int LL, bool MIX, bool ADIAG>
+MixFn mix_fn() {
+    return &mix_gsn_kernel<D, FULL, LL, MIX, ADIAG>;
+}
+struct MixEntry {
+    int D, full, ll, mix, adiag;
+    MixFn fn;
+};
+#define MIXV(D, F, L, M, A) {D, F, L, M, A, mix_fn<D, F, L, M, A>()}
+#define MIX8(D, A)                                                                                         \
+    MIXV(D, true, 0, true, A), MIXV(D, true, 1, true, A), MIXV(D, false, 0, true, A),                     \
+        MIXV(D, false, 1, true, A), MIXV(D, true, 0, false, A), MIXV(D, true, 1, false, A),                \
+        MIXV(D, false, 0, false, A), MIXV(D, false, 1, false, A)
+const std::vector<MixEntry> &mix_table() {
+    // dense Σ_A / Σ_t for D ≤ 8; D = 16, 32 take diagonal ones (cfg 4: σ²I, I)
+    static const std::vector<MixEntry> t = {MIX8(1, true),  MIX8(2, true),  MIX8(2, false), MIX8(3, true),
+                                            MIX8(3, false), MIX8(4, true),  MIX8(4, false), MIX8(8, true),
+                                            MIX8(8, false), MIX8(16, true), MIX8(32, true)};
+    return t;
+}
+template <int D>
+ReadjustFn readjust_fn() {
+    return &mix_readjust_kernel<D>;
+}
+ReadjustFn readjust_lookup(int D) {
+    switch (D) {
+    case 1: return readjust_fn<1>();
+    case 2: return readjust_fn<2>();
+    case 3: return readjust_fn<3>();
+    case 4: return readjust_fn<4>();
+    case 8: return readjust_fn<8>();
+    case 16: return readjust_fn<16>();
+    case 32: return readjust_fn<32>();
+    default: return nullptr;
+    }
+}
+
+emcmc_status select_mix(emcmc_handle *h) {
+    const int D = (int)h->cfg.dim;
+    const UpdateHost &u = h->updates[0];
+    const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
+    const int ll = (int)h->target.ll_mode;
+    const bool mix = u.kernel == EMCMC_RW_GAUSSIAN_MIX;
+    const bool adiag = (u.diag && h->target.diag) || D == 1;
+    Variant v;
+    for (const auto &e : mix_table())
+        if (e.D == D && e.full == (int)full && e.ll == ll && e.mix == (int)mix && e.adiag == (int)adiag) v.xfn = e.fn;
+    if (!v.xfn)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "no mix/chain-moments kernel for D=%d with %s Σ_A/Σ_t (instantiated: D ∈ {1,2,3,4,8} any, "
+                    "D ∈ {16,32} diagonal Σ_A and Σ_t)",
+                    D, adiag ? "diagonal" : "dense");
+    if (u.adaptation == EMCMC_ADPT_HAARIO) {
+        v.rfn = readjust_lookup(D);
+        if (!v.rfn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no Haario readjust kernel for D=%d", D);
+    }
+    v.mix = true;
+    char nm[160];
+    snprintf(nm, sizeof nm, "mix_gsn_kernel<D=%d,%s,%s,%s,%s>%s", D, full ? "FULL" : "ACCEPT_ONLY",
+             ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", mix ? "MIX" : "GSN_MOMENTS", adiag ? "DIAG" : "DENSE",
+             v.rfn ? "+mix_readjust_kernel" : "");
+    v.name = nm;
+    const TargetHost &t = h->target;
+    const size_t DD = (size_t)D * D;
+    std::vector<double> c(2 * DD + 3 * (size_t)D);
+    std::copy(u.L.begin(), u.L.end(), c.begin());
+    std::copy(u.invdiag.begin(), u.invdiag.end(), c.begin() + DD);
+    std::copy(t.L.begin(), t.L.end(), c.begin() + DD + D);
+    std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
+    std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
+    const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
+    const size_t lds = sizeof(Ziggurat) + (c.size() + obs_doubles) * sizeof(double);
+    if (lds > kMaxLds)
+        return fail(h, EMCMC_INVALID_ARG,
+                    "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu", lds,
+                    kMaxLds, (unsigned long long)t.nobs);
+    if (h->d_consts) (void)hipFree(h->d_consts);
+    HIPCHK(h, hipMalloc(&h->d_consts, c.size() * sizeof(double)));
+    HIPCHK(h, hipMemcpy(h->d_consts, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (h->d_obs) (void)hipFree(h->d_obs);
+    h->d_obs = nullptr;
+    HIPCHK(h, hipMalloc(&h->d_obs, t.obs.size() * sizeof(double)));
+    HIPCHK(h, hipMemcpy(h->d_obs, t.obs.data(), t.obs.size() * sizeof(double), hipMemcpyHostToDevice));
+    h->lds_bytes = lds;
+    h->var = v;
+    return EMCMC_OK;
 }
 
 emcmc_status select_variant(emcmc_handle *h) {
     if (!h->target_set || h->updates.empty()) return EMCMC_OK;
+    if (mix_path(h)) return select_mix(h);
+    for (const auto &u : h->updates)
+        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX)
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                        "GaussianRandomWalkMix runs on device as the single joint update on coords 1:D");
+    if (h->cfg.chain_moments)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "chain moments on device need a single joint GaussianRandomWalk(Mix) update on coords 1:D");
     if (!fused_eligible(h)) return select_mwg(h);
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
@@ -475,8 +614,16 @@ emcmc_status select_variant(emcmc_handle *h) {
 
 double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps) {
     const double C = (double)h->cfg.num_chains, D = (double)h->cfg.dim;
-    const double per_step = (h->cfg.history_mode == EMCMC_HIST_FULL) ? (16.0 * D + 8.0 + 0.125) : 0.125;
-    const double state = 16.0 * D + 2 * 8 + 2 * 8 + 2 * 16 + 2 * 4 + 2 * 4;  // θ, ll, ra, ring, nacc, faults (R+W)
+    double per_step = (h->cfg.history_mode == EMCMC_HIST_FULL) ? (16.0 * D + 8.0 + 0.125) : 0.125;
+    double state = 16.0 * D + 2 * 8 + 2 * 8 + 2 * 16 + 2 * 4 + 2 * 4;  // θ, ll, ra, ring, nacc, faults (R+W)
+    if (h->var.xfn) {
+        const double DP = D * (D + 1) / 2;
+        per_step += 16.0 * DP + 16.0 * D;  // cov and mean, read + write
+        if (h->updates[0].kernel == EMCMC_RW_GAUSSIAN_MIX) {
+            per_step += 8.0 * DP + 8.0 * D;  // L_B and 1/L_B,ii, read
+            state += 8.0;                    // c0_B
+        }
+    }
     return C * ((double)nsteps * per_step + state);
 }
 
@@ -504,6 +651,103 @@ emcmc_status drain_timing(emcmc_handle *h) {
     h->ev.clear();
     h->timed_bytes += h->pending_bytes;
     h->pending_bytes = 0.0;
+    return EMCMC_OK;
+}
+
+// Mix / chain-moments path: maximal runs of consecutive iterations, cut at
+// K steps and at Haario readjust steps (M reaches k after the run), each
+// followed by the readjust kernel when due.
+emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps) {
+    const uint64_t C = h->cfg.num_chains;
+    const TargetHost &t = h->target;
+    const UpdateHost &u = h->updates[0];
+    const bool haario = u.adaptation == EMCMC_ADPT_HAARIO;
+    const uint32_t k = haario ? u.haario.adapt_every_k_steps : 0;
+    MixParams p{};
+    p.theta = h->d_theta;
+    p.ll = h->d_ll;
+    p.ra = h->d_ra;
+    p.ring = h->d_ring;
+    p.nacc = h->d_nacc;
+    p.faults = h->d_faults;
+    p.mean = h->d_mean;
+    p.cov = h->d_cov;
+    p.LB = h->d_LB;
+    p.iLB = h->d_iLB;
+    p.c0B = h->d_c0B;
+    p.hist_theta = h->d_hist_theta;
+    p.hist_prop = h->d_hist_prop;
+    p.hist_ll = h->d_hist_ll;
+    p.hist_acc = h->d_hist_acc;
+    p.zig = h->d_zig;
+    p.consts = h->d_consts;
+    p.obs = h->d_obs;
+    p.C = C;
+    p.row_bytes = h->row_bytes;
+    p.chain0 = (uint32_t)h->cfg.first_chain_id;
+    p.key0 = (uint32_t)h->cfg.seed;
+    p.key1 = (uint32_t)(h->cfg.seed >> 32);
+    p.W = h->cfg.roll_window;
+    p.nobs = (uint32_t)t.nobs;
+    p.tdiag = t.diag ? 1u : 0u;
+    p.lam = u.lam;
+    p.oml = 1.0 - u.lam;
+    p.c0A = u.c0;
+    p.t_c0 = t.c0;
+    p.n_tc0 = (double)t.nobs * t.c0;
+    p.S_c = t.S_c;
+    p.nobs_d = (double)t.nobs;
+    p.rcp_W = 1.0 / (double)h->cfg.roll_window;
+    MixReadjustParams r{};
+    r.cov = h->d_cov;
+    r.LB = h->d_LB;
+    r.iLB = h->d_iLB;
+    r.c0B = h->d_c0B;
+    r.Lnew = h->d_Lnew;
+    r.faults = h->d_faults;
+    r.C = C;
+    r.sB = (2.38 * 2.38) / (double)h->cfg.dim;  // 2.38^2/length(rw), adaptation.jl:423
+    const dim3 block(256), grid((unsigned)((C + 255) / 256));
+    const uint64_t K = h->cfg.steps_per_launch;
+    uint64_t i = 0;
+    while (i < num_steps) {
+        uint64_t cap = K;
+        if (haario) cap = std::min<uint64_t>(cap, k - h->mix_M);
+        uint64_t j = i + 1;
+        while (j < num_steps && j - i < cap && steps[j].mcmciter == steps[j - 1].mcmciter + 1) ++j;
+        const uint64_t n = j - i;
+        p.iter0 = steps[i].mcmciter;
+        p.nsteps = (uint32_t)n;
+        p.N0 = h->stats_N;
+        if (p.iter0 > 1 && h->last_iter[0] != p.iter0 - 1)  // rolling_ar[iter−1] never written → 0.0
+            HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
+        h->last_iter[0] = steps[j - 1].mcmciter;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->timing) {
+            e0 = get_event(h);
+            e1 = get_event(h);
+            HIPCHK(h, hipEventRecord(e0, h->stream));
+        }
+        void *args[] = {&p};
+        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.xfn), grid, block, args, h->lds_bytes,
+                                  h->stream));
+        if (h->timing) {
+            HIPCHK(h, hipEventRecord(e1, h->stream));
+            h->ev.emplace_back(e0, e1);
+            h->pending_bytes += bytes_per_launch(h, n);
+        }
+        h->stats_N += n;
+        if (haario) {
+            h->mix_M += (uint32_t)n;
+            if (h->mix_M >= k) {  // time_to_update: readjust!, M = 0
+                void *rargs[] = {&r};
+                HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.rfn), grid, block, rargs, 0,
+                                          h->stream));
+                h->mix_M = 0;
+            }
+        }
+        i = j;
+    }
     return EMCMC_OK;
 }
 
@@ -644,12 +888,13 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
         for (uint32_t j = 0; j < i; ++j)
             if (u->coords[j] == u->coords[i]) return fail(h, EMCMC_INVALID_ARG, "repeated coord %u", u->coords[i]);
     }
-    if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM)
+    if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN_MIX)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "transition kernel %u has no device plugin yet", u->kernel);
     if (u->prior != EMCMC_PRIOR_IMPROPER)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin yet", u->prior);
     if (u->adaptation != EMCMC_ADPT_NONE &&
-        !(u->adaptation == EMCMC_ADPT_UNIF_RW && u->kernel == EMCMC_RW_UNIFORM))
+        !(u->adaptation == EMCMC_ADPT_UNIF_RW && u->kernel == EMCMC_RW_UNIFORM) &&
+        !(u->adaptation == EMCMC_ADPT_HAARIO && u->kernel == EMCMC_RW_GAUSSIAN_MIX))
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "adaptation %u has no device plugin for kernel %u yet",
                     u->adaptation, u->kernel);
     if (u->pos)
@@ -662,7 +907,7 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     uh.adaptation = u->adaptation;
     uh.coords.assign(u->coords, u->coords + u->num_coords);
     const int n = (int)u->num_coords;
-    if (u->kernel == EMCMC_RW_GAUSSIAN) {
+    if (u->kernel == EMCMC_RW_GAUSSIAN || u->kernel == EMCMC_RW_GAUSSIAN_MIX) {
         if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");
         uh.sigma.assign(u->sigma, u->sigma + (size_t)n * n);
         if (!cholesky_upper_colmajor(uh.sigma.data(), n, uh.L))
@@ -671,14 +916,32 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
         for (int i = 0; i < n; ++i) uh.invdiag[i] = 1.0 / uh.L[(size_t)i * n + i];
         uh.diag = is_diag_upper(uh.sigma.data(), n);
         uh.c0 = mvnormal_c0(n, logdet_chol(uh.L, n));
+        if (u->kernel == EMCMC_RW_GAUSSIAN_MIX) {  // random_walk.jl:198-206
+            if (!u->sigma_b) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalkMix needs Σ_B (sigma_b)");
+            if (!(u->mix_lambda >= 0.0 && u->mix_lambda <= 1.0))
+                return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalkMix: @assert 0.0 <= λ <= 1.0");
+            uh.lam = u->mix_lambda;
+            uh.sigma_b.assign(u->sigma_b, u->sigma_b + (size_t)n * n);
+            if (!cholesky_upper_colmajor(uh.sigma_b.data(), n, uh.LB))
+                return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalkMix Σ_B is not positive definite");
+            uh.invdiagB.resize(n);
+            for (int i = 0; i < n; ++i) uh.invdiagB[i] = 1.0 / uh.LB[(size_t)i * n + i];
+            uh.c0B = mvnormal_c0(n, logdet_chol(uh.LB, n));
+            if (u->adaptation == EMCMC_ADPT_HAARIO) {
+                const auto *ad = static_cast<const emcmc_haario_adaptation *>(u->adaptation_params);
+                if (!ad) return fail(h, EMCMC_INVALID_ARG, "HaarioTypeAdaptation parameters missing (adaptation_params)");
+                if (ad->adapt_every_k_steps == 0) return fail(h, EMCMC_INVALID_ARG, "adapt_every_k_steps must be ≥ 1");
+                uh.haario = *ad;
+            }
+        }
     } else {
         if (!u->epsilon) return fail(h, EMCMC_INVALID_ARG, "UniformRandomWalk needs ϵ");
         uh.eps.assign(u->epsilon, u->epsilon + n);
         for (double e : uh.eps)  // UniformRandomWalk: @assert all(ϵ .> 0.0) (random_walk.jl:50)
             if (!(e > 0.0)) return fail(h, EMCMC_INVALID_ARG, "UniformRandomWalk ϵ must be > 0");
         if (u->adaptation == EMCMC_ADPT_UNIF_RW) {
-            const auto *ad = static_cast<const emcmc_unifrw_adaptation *>(u->reserved_ptr[0]);
-            if (!ad) return fail(h, EMCMC_INVALID_ARG, "AdaptationUnifRW parameters missing (reserved_ptr[0])");
+            const auto *ad = static_cast<const emcmc_unifrw_adaptation *>(u->adaptation_params);
+            if (!ad) return fail(h, EMCMC_INVALID_ARG, "AdaptationUnifRW parameters missing (adaptation_params)");
             if (ad->adapt_every_k_steps == 0) return fail(h, EMCMC_INVALID_ARG, "adapt_every_k_steps must be ≥ 1");
             uh.adpt = *ad;
         }
@@ -768,6 +1031,26 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
         }
         HIPCHK(h, hipStreamSynchronize(h->stream));  // host vectors go out of scope
     }
+    if (h->d_mean) {  // GenericChainStats: mean = 0, cov = 0, N = 1 (chain_statistics.jl:30-35)
+        const uint64_t DP = (uint64_t)packed_n((int)D);
+        HIPCHK(h, hipMemsetAsync(h->d_mean, 0, C * D * sizeof(double), h->stream));
+        HIPCHK(h, hipMemsetAsync(h->d_cov, 0, C * DP * sizeof(double), h->stream));
+        if (h->d_LB) {  // every chain starts from the user's Σ_B
+            const UpdateHost &u = h->updates[0];
+            std::vector<double> lb(C * DP), il(C * D), c0(C, u.c0B);
+            for (uint64_t c = 0; c < C; ++c) {
+                for (int i = 0; i < (int)D; ++i)
+                    for (int j = 0; j <= i; ++j)
+                        lb[state_pos((uint64_t)lo_idx(i, j), c, C, (uint32_t)DP)] = u.LB[(size_t)i * D + j];
+                for (uint64_t i = 0; i < D; ++i) il[i * C + c] = u.invdiagB[i];
+            }
+            HIPCHK(h, hipMemcpy(h->d_LB, lb.data(), lb.size() * sizeof(double), hipMemcpyHostToDevice));
+            HIPCHK(h, hipMemcpy(h->d_iLB, il.data(), il.size() * sizeof(double), hipMemcpyHostToDevice));
+            HIPCHK(h, hipMemcpy(h->d_c0B, c0.data(), c0.size() * sizeof(double), hipMemcpyHostToDevice));
+        }
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
+    h->mix_M = 0;
     h->stats_N = 1;
     h->last_iter.assign(P, 0u);
     return EMCMC_OK;
@@ -777,7 +1060,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     if (!h || (!steps && num_steps)) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
     if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
-    if (!h->var.fn && !h->var.mfn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
+    if (!h->var.fn && !h->var.mfn && !h->var.xfn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
     if (!h->d_zig) return fail(h, EMCMC_STATE_ERROR, "state not allocated");
     const uint32_t P = (uint32_t)h->updates.size();
     for (uint64_t i = 0; i < num_steps; ++i) {
@@ -787,6 +1070,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
                         steps[i].mcmciter);
     }
     if (h->var.mfn) return run_mwg(h, steps, num_steps);
+    if (h->var.xfn) return run_mix(h, steps, num_steps);
     const uint64_t C = h->cfg.num_chains;
     const int lpc = h->var.lpc;
     const uint64_t threads = C * (uint64_t)lpc;
@@ -882,7 +1166,8 @@ void emcmc_destroy(emcmc_handle *h) {
     void *bufs[] = {h->d_theta,     h->d_ll,        h->d_ra,      h->d_ring,     h->d_nacc,  h->d_faults,
                     h->d_hist_theta, h->d_hist_prop, h->d_hist_ll, h->d_hist_acc, h->d_consts, h->d_obs,
                     h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
-                    h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg};
+                    h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
+                    h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -938,6 +1223,55 @@ emcmc_status emcmc_get_update_state(emcmc_handle *h, uint32_t pidx, double *epsi
     }
     if (proposed) HIPCHK(h, hipMemcpy(proposed, h->d_aprop + q * C, C * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (accepted) HIPCHK(h, hipMemcpy(accepted, h->d_aacc + q * C, C * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_chain_moments(emcmc_handle *h, double *mean, double *cov) {
+    if (!h) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (!h->d_mean)
+        return fail(h, EMCMC_STATE_ERROR,
+                    "chain moments are kept on device only with GaussianRandomWalkMix or emcmc_config.chain_moments");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, DP = (uint64_t)packed_n((int)D);
+    if (mean) {
+        std::vector<double> m(C * D);
+        HIPCHK(h, hipMemcpy(m.data(), h->d_mean, m.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (uint64_t d = 0; d < D; ++d) mean[c * D + d] = m[state_pos(d, c, C, (uint32_t)D)];
+    }
+    if (cov) {
+        std::vector<double> v(C * DP);
+        HIPCHK(h, hipMemcpy(v.data(), h->d_cov, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (int i = 0; i < (int)D; ++i)
+                for (int j = i; j < (int)D; ++j) {
+                    const double x = v[state_pos((uint64_t)up_idx((int)D, i, j), c, C, (uint32_t)DP)];
+                    cov[(c * D + i) * D + j] = x;
+                    cov[(c * D + j) * D + i] = x;
+                }
+    }
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_sigma_b, uint32_t *steps_since_adapt) {
+    if (!h) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (pidx < 1 || pidx > h->updates.size()) return fail(h, EMCMC_INVALID_ARG, "pidx %u", pidx);
+    if (h->updates[pidx - 1].kernel != EMCMC_RW_GAUSSIAN_MIX || !h->d_LB)
+        return fail(h, EMCMC_INVALID_ARG, "update %u is not a GaussianRandomWalkMix", pidx);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, DP = (uint64_t)packed_n((int)D);
+    if (chol_sigma_b) {
+        std::vector<double> v(C * DP);
+        HIPCHK(h, hipMemcpy(v.data(), h->d_LB, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (int i = 0; i < (int)D; ++i)
+                for (int j = 0; j < (int)D; ++j)
+                    chol_sigma_b[(c * D + i) * D + j] =
+                        (j <= i) ? v[state_pos((uint64_t)lo_idx(i, j), c, C, (uint32_t)DP)] : 0.0;
+    }
+    if (steps_since_adapt) *steps_since_adapt = h->mix_M;
     return EMCMC_OK;
 }
 

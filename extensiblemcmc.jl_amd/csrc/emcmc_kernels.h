@@ -316,6 +316,7 @@ __device__ __forceinline__ void normals(const Ziggurat &zt, uint32_t key0, uint3
     uint64_t pend = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
+        if constexpr (N > 8) __builtin_amdgcn_sched_barrier(0);  // one Philox block at a time
         const u32x4 r = draw(key0, key1, chain, iter, j, pidx0, 0);
         if (!zig_normal_fast(zig_split(r.x, r.y), zt.n, z[2 * j])) pend |= 1ull << (2 * j);
         if (2 * j + 1 < N)

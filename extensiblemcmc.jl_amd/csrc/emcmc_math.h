@@ -191,6 +191,49 @@ EMCMC_HD double exp_nonpos(double x) {
     return p * u2d((uint64_t)(1023 + k) << 52);
 }
 
+// ---- exp and log over the whole range (GaussianRandomWalkMix density) ------
+// log((1−λ)·e^{lp_A} + λ·e^{lp_B}) (random_walk.jl:229-232) exponentiates
+// log-densities of either sign.  exp_any: the exp_nonpos reduction and
+// polynomial; 2^k in two exact steps for subnormal results (one rounding) and
+// k = 1024; 0 below −745.13, +Inf above 709.78.  log_any: 0 → −Inf, +Inf →
+// +Inf, NaN → NaN, subnormals scaled by 2^54 first.
+EMCMC_HD double exp_any(double x) {
+    if (x != x) return x;
+    if (x > 709.782712893384) return __builtin_inf();
+    if (x < -745.1332191019412) return 0.0;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const double kd = rint(x * invln2);
+    double r = fma(-kd, ln2_hi, x);
+    r = fma(-kd, ln2_lo, r);
+    double p = 1.0 / 6227020800.0;
+    p = fma(p, r, 1.0 / 479001600.0);
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    const int k = (int)kd;
+    if (k > 1023) return (p * u2d((uint64_t)(1023 + k - 1) << 52)) * 2.0;
+    if (k < -1022) return (p * u2d((uint64_t)(1023 + k + 64) << 52)) * 0x1p-64;
+    return p * u2d((uint64_t)(1023 + k) << 52);
+}
+
+EMCMC_HD double log_any(double x) {
+    if (x != x) return x;
+    if (x == 0.0) return -__builtin_inf();
+    if (x == __builtin_inf()) return x;
+    if (x < 0x1p-1022) return log_pos(x * 0x1p54) - 37.42994775023705;
+    return log_pos(x);
+}
+
 // ---- Marsaglia–Tsang ziggurat, 256 layers (J. Stat. Softw. 5(8), 2000) ------
 // The same sampler family as Julia's randn/randexp (Random stdlib), fed by the
 // Philox stream.  One 64-bit draw (hi:lo) per variate:

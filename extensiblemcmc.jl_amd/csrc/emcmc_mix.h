@@ -1,0 +1,390 @@
+// emcmc_mix.h — GaussianRandomWalkMix + HaarioTypeAdaptation + on-device
+// GenericChainStats mean/cov (BASELINE cfg 4), one lane per chain (gfx950).
+//
+// One joint update (P = 1) on coords 1:D.  Reference semantics (src/ under
+// /root/reference), restated in oracle/emcmc_oracle.c (orc_run_mix) and
+// oracle/literal.py (run_mix_chain):
+//   pick_kernel        B iff rand() ≤ λ (Bernoulli(λ))          random_walk.jl:225-227
+//   rand(gsn_X, θ)     θ° = θ + L_X z                           random_walk.jl:145-151
+//   logpdf(mix)        log((1−λ)·e^{lp_A} + λ·e^{lp_B}); lp_X = MvNormal logpdf
+//                      + logJ (−0.0: identity)                  random_walk.jl:161-171,229-232
+//   update_stats!      running mean/cov of θ after the step (phantom zero
+//                      sample: N = 1, mean 0, cov 0) and rolling acceptance
+//                                                          chain_statistics.jl:41-66
+//   HaarioTypeAdaptation  registers θ with the same recurrence (P = 1: equal to
+//                      the chain-stats mean/cov, kept once); M += 1 per step;
+//                      readjust at M ≥ k: Σ_B = 2.38²/D·cov     adaptation.jl:399-426
+// The readjust runs as its own kernel between step launches (M is the same for
+// every chain, so the host splits launches at readjust steps): a per-chain
+// canonical Cholesky of Σ_B; a non-positive pivot sets EMCMC_FAULT_POSDEF and
+// keeps the previous factor (the reference throws PosDefException at the next
+// MvNormal(θ, Σ_B)).
+//
+// HBM layout (all SoA over chains, state_pos pair-interleaving):
+//   mean  [D]        state_pos(d, c, C, D)
+//   cov   [DP]       packed upper, row-major: (i, j ≥ i) ↦ i·D − i(i−1)/2 + j − i
+//   L_B   [DP]       packed lower, row-major: (i, j ≤ i) ↦ i(i+1)/2 + j
+//   1/L_B,ii [D][C], c0_B [C]
+// DP = D(D+1)/2.  Per chain-step the kernel reads and writes cov and mean and
+// reads L_B: the step is HBM-bound.
+#pragma once
+
+#include "emcmc_kernels.h"
+
+namespace emcmc {
+
+// Philox block of the mixture pick uniform (block ids 0..D/2 are normals,
+// kBlockAccept the accept exponentials).
+constexpr uint32_t kBlockMixPick = 0xFFFFFFFEu;
+
+__host__ __device__ constexpr int packed_n(int D) { return D * (D + 1) / 2; }
+__host__ __device__ constexpr int up_idx(int D, int i, int j) { return i * D - i * (i - 1) / 2 + (j - i); }
+__host__ __device__ constexpr int lo_idx(int i, int j) { return i * (i + 1) / 2 + j; }
+
+struct MixParams {
+    double *theta;   // [D] state_pos
+    double *ll;      // [C]
+    double *ra;      // [C]
+    uint64_t *ring;  // [C][2]
+    uint32_t *nacc;  // [C]
+    uint32_t *faults;
+    double *mean;       // [D] state_pos
+    double *cov;        // [DP] packed upper, state_pos(p, c, C, DP)
+    const double *LB;   // [DP] packed lower, state_pos(q, c, C, DP)
+    const double *iLB;  // [D][C]
+    const double *c0B;  // [C]
+    double *hist_theta, *hist_prop, *hist_ll;
+    uint8_t *hist_acc;
+    const Ziggurat *zig;
+    const double *consts;  // L_A (D×D row-major lower) | 1/L_A,ii | L_t | 1/L_t,ii | x̄
+    const double *obs;     // [nobs][D]
+    uint64_t C;
+    uint64_t row_bytes;
+    uint64_t N0;  // GenericChainStats.N before the first step of the launch
+    uint32_t chain0, key0, key1, iter0, nsteps, W, nobs, tdiag;
+    double lam, oml;  // λ and 1 − λ
+    double c0A, t_c0, n_tc0, S_c, nobs_d, rcp_W;
+};
+
+// Canonical Σ y_i² accumulated as y_i is produced (blocks of 8 when D % 8 == 0
+// and D ≥ 16, then a pairwise tree over the blocks — canon_sumsq's order).
+template <int D>
+struct SumSqAcc {
+    static constexpr int BLK = SumShape<D>::BLK;
+    static constexpr int NB = SumShape<D>::NB;
+    double b[NB];
+    __device__ __forceinline__ void add(int i, double y) {
+        if (i % BLK == 0) b[i / BLK] = y * y;
+        else b[i / BLK] = fma(y, y, b[i / BLK]);
+    }
+    __device__ __forceinline__ double finish() { return tree_inplace(b); }
+};
+
+// Per-chain SoA arrays addressed as (wave-uniform row base) + (32-bit lane
+// offset): the row base is SALU arithmetic on an opaque per-step stride, so the
+// compiler neither hoists hundreds of 64-bit per-element addresses out of the
+// step loop (they would not fit in registers) nor spends VALU on them; loads
+// and stores use the global saddr form.
+struct LaneSoA {
+    uint64_t stride;  // bytes between consecutive words of one chain (uniform)
+    uint32_t off;     // lane's byte offset within a word row
+};
+// pair-interleaved layout (state_pos) of an n-element per-chain vector
+__device__ __forceinline__ LaneSoA lane_soa(uint64_t C, uint64_t chain, int n) {
+    uint64_t stride = (n % 2 == 0) ? C * 16u : C * 8u;
+    asm volatile("" : "+s"(stride));  // opaque: recomputed per step, never hoisted
+    return LaneSoA{stride, (uint32_t)((n % 2 == 0) ? chain * 16u : chain * 8u)};
+}
+template <int NP>
+__device__ __forceinline__ double *soa_ptr(double *base, const LaneSoA &l, int q) {
+    if constexpr (NP % 2 == 0)
+        return reinterpret_cast<double *>(reinterpret_cast<char *>(base) + (uint64_t)(q >> 1) * l.stride + l.off) +
+               (q & 1);
+    else
+        return reinterpret_cast<double *>(reinterpret_cast<char *>(base) + (uint64_t)q * l.stride + l.off);
+}
+template <int NP>
+__device__ __forceinline__ const double *soa_ptr(const double *base, const LaneSoA &l, int q) {
+    return soa_ptr<NP>(const_cast<double *>(base), l, q);
+}
+// plain [n][C] layout (element q of chain c at q·C + c)
+__device__ __forceinline__ LaneSoA lane_plain(uint64_t C, uint64_t chain) {
+    uint64_t stride = C * 8u;
+    asm volatile("" : "+s"(stride));
+    return LaneSoA{stride, (uint32_t)(chain * 8u)};
+}
+__device__ __forceinline__ const double *plain_ptr(const double *base, const LaneSoA &l, int q) {
+    return reinterpret_cast<const double *>(reinterpret_cast<const char *>(base) + (uint64_t)q * l.stride + l.off);
+}
+
+// Keeps a value's computation where it is written: without it LLVM sinks the
+// whole y_B substitution (used only after exp_any's branches) past the row loop,
+// and every L_B element loaded there stays live until then.
+__device__ __forceinline__ void pin(double &x) { asm volatile("" : "+v"(x)); }
+
+// ‖L_t⁻¹ (x − θ°)‖² of the target (factor in LDS).  DIAG: y_i = r_i/L_ii,
+// summed as produced; dense: forward substitution (the dense formulas give the
+// diagonal formulas' bits on a diagonal factor, tests/test_oracle.py).
+template <int D, bool DIAG>
+__device__ __forceinline__ double target_sqmahal(const double *Lt, const double *iLt, const double *x,
+                                                 const double (&thp)[D]) {
+    if constexpr (DIAG) {
+        SumSqAcc<D> q;
+#pragma unroll
+        for (int i = 0; i < D; ++i) q.add(i, (x[i] - thp[i]) * iLt[i]);
+        return q.finish();
+    } else {
+        double y[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            double acc = x[i] - thp[i];
+#pragma unroll
+            for (int j = 0; j < i; ++j) acc = fma(-Lt[i * D + j], y[j], acc);
+            y[i] = acc * iLt[i];
+        }
+        return canon_sumsq<D, 1>(y);
+    }
+}
+
+// DIAG: Σ_A and Σ_t both diagonal (diagonal formulas); otherwise the dense
+// formulas for both.
+template <int D, bool FULL, int LLMODE, bool MIX, bool DIAG>
+__global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
+    constexpr bool ADIAG = DIAG;
+    constexpr int DP = packed_n(D);
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const uint32_t nobs = a.nobs;
+    stage_lds(lds, a.zig, a.consts, 2 * D * D + 3 * D, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
+    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
+
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint64_t C = a.C;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+
+    double th[D];
+    load_state<D>(a.theta, C, chain, 0, th);
+    double ll = a.ll[chain];
+    double ra = a.ra[chain];
+    uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
+    uint32_t nacc = a.nacc[chain];
+    uint32_t faults = a.faults[chain];
+    const double c0B = MIX ? a.c0B[chain] : 0.0;
+    const SlotOffset<D> soff(C, chain, 0);
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
+        const uint64_t N = a.N0 + s;
+        const uint64_t slot = (uint64_t)(iter - 1);
+        // LDS constants through an opaque per-step offset: loop-invariant LDS
+        // loads (up to 2·D² of them) must not be hoisted out of the step loop
+        uint32_t o = 0;
+        asm volatile("" : "+s"(o));
+        const double *LA = lds + kZigLdsDoubles + o;
+        const double *iLA = LA + D * D;
+        const double *Lt = LA + D * D + D;
+        const double *iLt = LA + 2 * D * D + D;
+        const double *xbar = LA + 2 * D * D + 2 * D;
+        const double *X = LA + 2 * D * D + 3 * D;
+        // ---- proposal!: pick the kernel, θ° = θ + L z
+        bool useB = false;
+        if constexpr (MIX) {
+            const u32x4 pr = draw(a.key0, a.key1, gid, iter, kBlockMixPick, 0, 0);
+            useB = u01_closed0(pr.x, pr.y) <= a.lam;
+        }
+        double z[D];
+        normals<D>(zt, a.key0, a.key1, gid, iter, 0, z, faults);
+        // One pass over the rows of L_B: the proposal row (θ°_i) and the forward
+        // substitutions y_A = L_A⁻¹(θ° − θ), y_B = L_B⁻¹(θ° − θ) share each load.
+        // logpdf(θ → θ°) and logpdf(θ° → θ) see ±(θ° − θ): bitwise equal
+        // sqmahal values, so the mixture density is evaluated once.
+        double thp[D];
+        double yA[ADIAG ? 1 : D];
+        double yB[MIX ? D : 1];
+        SumSqAcc<D> qa, qb;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            // one row at a time: without the barrier the scheduler hoists all
+            // DP loads of L_B and spills
+            __builtin_amdgcn_sched_barrier(0);
+            const LaneSoA lb = lane_soa(C, chain, DP);
+            const LaneSoA il = lane_plain(C, chain);
+            double lzA;
+            if constexpr (ADIAG) {
+                lzA = LA[i * D + i] * z[i];
+            } else {
+                lzA = LA[i * D] * z[0];
+#pragma unroll
+                for (int j = 1; j <= i; ++j) lzA = fma(LA[i * D + j], z[j], lzA);
+            }
+            double lz = lzA;
+            double Lr[MIX ? D : 1];
+            if constexpr (MIX) {
+#pragma unroll
+                for (int j = 0; j <= i; ++j) Lr[j] = *soa_ptr<DP>(a.LB, lb, lo_idx(i, j));
+                double lzB = Lr[0] * z[0];
+#pragma unroll
+                for (int j = 1; j <= i; ++j) lzB = fma(Lr[j], z[j], lzB);
+                lz = useB ? lzB : lzA;
+            }
+            thp[i] = th[i] + lz;
+            const double r = thp[i] - th[i];
+            if constexpr (ADIAG) {
+                qa.add(i, r * iLA[i]);
+            } else {
+                double acc = r;
+#pragma unroll
+                for (int j = 0; j < i; ++j) acc = fma(-LA[i * D + j], yA[j], acc);
+                yA[i] = acc * iLA[i];
+                qa.add(i, yA[i]);
+            }
+            if constexpr (MIX) {
+                double acc = r;
+#pragma unroll
+                for (int j = 0; j < i; ++j) acc = fma(-Lr[j], yB[j], acc);
+                yB[i] = acc * *plain_ptr(a.iLB, il, i);
+                pin(yB[i]);
+                qb.add(i, yB[i]);
+            }
+        }
+        const double lpA = fma(-0.5, qa.finish(), a.c0A);  // = c0 − q/2 (q/2 exact)
+        double ltd = lpA;
+        if constexpr (MIX) {
+            const double lpB = fma(-0.5, qb.finish(), c0B);
+            ltd = log_any(a.oml * exp_any(lpA) + a.lam * exp_any(lpB));
+        }
+        // ---- compute_ll!
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            llp = 0.0;
+            for (uint32_t k = 0; k < nobs; ++k)
+                llp = llp + fma(-0.5, target_sqmahal<D, DIAG>(Lt, iLt, X + (size_t)k * D, thp), a.t_c0);
+        } else {
+            const double qv = target_sqmahal<D, DIAG>(Lt, iLt, xbar, thp);
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        // ---- accept_reject!
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double E = exp_draw(zt, a.key0, a.key1, gid, iter, 0, faults);
+        const bool acc = E > -llr;
+        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
+#pragma unroll
+        for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            store_slot<D>(a.hist_theta + slot * D * C, soff, th);
+            __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
+        }
+        {
+            const uint64_t m = __ballot(acc);
+            if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
+        }
+        ra = rolling_update(ra, r0, r1, iter, a.W, N, a.rcp_W, acc);
+        // ---- update_stats!: running mean/cov of θ (chain_statistics.jl:46-49)
+        {
+            const double Nd = (double)N, N1d = (double)(N + 1);
+            const double ca = (double)(N - 1) / Nd;  // (N−1)/N
+            const double cb = Nd / N1d;              // N/(N+1)
+            const double cc = N1d / Nd;              // (N+1)/N
+            const double rN = 1.0 / Nd, rN1 = 1.0 / N1d;
+            const LaneSoA lm = lane_soa(C, chain, D);
+            double mo[D], mn[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) mo[i] = *soa_ptr<D>(a.mean, lm, i);
+#pragma unroll
+            for (int i = 0; i < D; ++i) mn[i] = mo[i] * cb + div_markstein(th[i], N1d, rN1);
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                __builtin_amdgcn_sched_barrier(0);  // one packed row in flight at a time
+                const LaneSoA lc = lane_soa(C, chain, DP);
+#pragma unroll
+                for (int j = i; j < D; ++j) {
+                    double *pc = soa_ptr<DP>(a.cov, lc, up_idx(D, i, j));
+                    const double old_sq = ca * *pc + mo[i] * mo[j];
+                    const double new_sq = old_sq + div_markstein(th[i] * th[j], Nd, rN);
+                    *pc = new_sq - cc * (mn[i] * mn[j]);
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < D; ++i) *soa_ptr<D>(a.mean, lm, i) = mn[i];
+        }
+    }
+    a.ll[chain] = ll;
+    a.ra[chain] = ra;
+    a.ring[2 * chain] = r0;
+    a.ring[2 * chain + 1] = r1;
+    a.nacc[chain] = nacc;
+    a.faults[chain] = faults;
+    store_state<D>(a.theta, C, chain, 0, th, false);
+}
+
+// ---- HaarioTypeAdaptation readjust! (adaptation.jl:422-426) -----------------
+struct MixReadjustParams {
+    const double *cov;  // [DP] packed upper
+    double *LB;         // [DP] packed lower
+    double *iLB;        // [D][C]
+    double *c0B;        // [C]
+    double *Lnew;       // [DP] packed lower scratch
+    uint32_t *faults;
+    uint64_t C;
+    double sB;  // 2.38²/D
+};
+
+// Σ_B = sB·cov; L_B = cholesky(Symmetric(Σ_B)).L in the canonical order of
+// oracle/emcmc_oracle.c orc_cholesky (each element's sum over k ascending, the
+// products rounded before subtraction), computed row by row: the row being
+// built stays in registers, earlier rows are re-read from the scratch copy
+// (volatile loads: program order, no store-to-load forwarding into registers).
+template <int D>
+__global__ void __launch_bounds__(256) mix_readjust_kernel(const MixReadjustParams a) {
+    constexpr int DP = packed_n(D);
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint64_t C = a.C;
+    double dg[D];
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        __builtin_amdgcn_sched_barrier(0);
+        // fresh opaque stride per row: addresses are not CSE'd across rows
+        const LaneSoA lp = lane_soa(C, chain, DP);
+        double row[D];
+#pragma unroll
+        for (int j = 0; j < i; ++j) {
+            double t = a.sB * *soa_ptr<DP>(a.cov, lp, up_idx(D, j, i));
+#pragma unroll
+            for (int k = 0; k < j; ++k)
+                t = t - row[k] * *reinterpret_cast<const volatile double *>(soa_ptr<DP>(a.Lnew, lp, lo_idx(j, k)));
+            row[j] = t / dg[j];
+            pin(row[j]);
+        }
+        double s = a.sB * *soa_ptr<DP>(a.cov, lp, up_idx(D, i, i));
+#pragma unroll
+        for (int k = 0; k < i; ++k) s = s - row[k] * row[k];
+        ok = ok && (s > 0.0);
+        dg[i] = sqrt(s);
+        pin(dg[i]);
+        row[i] = dg[i];
+#pragma unroll
+        for (int j = 0; j <= i; ++j) *soa_ptr<DP>(a.Lnew, lp, lo_idx(i, j)) = row[j];
+    }
+    if (!ok) {
+        a.faults[chain] |= 4u;  // EMCMC_FAULT_POSDEF
+        return;
+    }
+    const LaneSoA lp = lane_soa(C, chain, DP);
+#pragma unroll
+    for (int q = 0; q < DP; ++q)
+        *soa_ptr<DP>(a.LB, lp, q) = *reinterpret_cast<const volatile double *>(soa_ptr<DP>(a.Lnew, lp, q));
+    double dd = 0.0;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        a.iLB[(uint64_t)i * C + chain] = 1.0 / dg[i];
+        dd = dd + log_pos(dg[i]);
+    }
+    a.c0B[chain] = -((double)D * kLog2Pi + (dd + dd)) / 2.0;
+}
+
+}  // namespace emcmc

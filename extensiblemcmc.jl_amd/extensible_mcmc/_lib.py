@@ -46,6 +46,7 @@ HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
 H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
 FAULT_NONFINITE_LL = 1
 FAULT_RNG_RETRIES = 2
+FAULT_POSDEF = 4
 VARIANT_HIGH_OCCUPANCY = 1
 VARIANT_OCCUPANCY3 = 2
 
@@ -64,7 +65,8 @@ class EmcmcConfig(C.Structure):
         ("lanes_per_chain", C.c_uint32),
         ("steps_per_launch", C.c_uint32),
         ("kernel_variant", C.c_uint32),
-        ("reserved", C.c_uint32 * 6),
+        ("chain_moments", C.c_uint32),
+        ("reserved", C.c_uint32 * 5),
     ]
 
 
@@ -78,8 +80,20 @@ class EmcmcUpdateDesc(C.Structure):
         ("sigma", C.POINTER(C.c_double)),
         ("epsilon", C.POINTER(C.c_double)),
         ("pos", C.POINTER(C.c_uint8)),
-        ("reserved_ptr", C.c_void_p * 4),
-        ("reserved_f64", C.c_double * 4),
+        ("adaptation_params", C.c_void_p),
+        ("sigma_b", C.POINTER(C.c_double)),
+        ("reserved_ptr", C.c_void_p * 2),
+        ("mix_lambda", C.c_double),
+        ("reserved_f64", C.c_double * 3),
+    ]
+
+
+class EmcmcHaarioAdaptation(C.Structure):
+    """HaarioTypeAdaptation parameters (include/emcmc.h emcmc_haario_adaptation)."""
+    _fields_ = [
+        ("adapt_every_k_steps", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("scale", C.c_double),
     ]
 
 
@@ -141,6 +155,8 @@ SIGNATURES = {
         _ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     ),
     "emcmc_get_faults": (_ST, [_H, C.POINTER(C.c_uint32)]),
+    "emcmc_get_chain_moments": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "emcmc_get_mix_state": (_ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
     "emcmc_get_history": (_ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]),
     "emcmc_get_history_chains": (
         _ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]

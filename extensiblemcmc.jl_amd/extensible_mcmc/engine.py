@@ -26,6 +26,7 @@ class EngineConfig:
     lanes_per_chain: int = 0
     steps_per_launch: int = 0
     kernel_variant: int = 0
+    chain_moments: bool = False
 
 
 class Engine:
@@ -45,6 +46,7 @@ class Engine:
         c.lanes_per_chain = cfg.lanes_per_chain
         c.steps_per_launch = cfg.steps_per_launch
         c.kernel_variant = cfg.kernel_variant
+        c.chain_moments = int(bool(cfg.chain_moments))
         h = C.c_void_p()
         st = self._lib.emcmc_create(C.byref(h), C.byref(c))
         if st != L.OK:
@@ -103,7 +105,34 @@ class Engine:
             ad = L.EmcmcUnifRWAdaptation(int(adapt["k"]), 0, float(adapt["target"]), float(adapt["scale"]),
                                          float(adapt["min"]), float(adapt["max"]), float(adapt["offset"]))
             u.adaptation = L.ADPT_UNIF_RW
-            u.reserved_ptr[0] = C.cast(C.pointer(ad), C.c_void_p)
+            u.adaptation_params = C.cast(C.pointer(ad), C.c_void_p)
+        if pos is not None:
+            p = np.ascontiguousarray(pos, dtype=np.uint8)
+            u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
+        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
+        self.num_updates += 1
+
+    def add_gaussian_rw_mix_update(self, coords0, sigma_a, sigma_b, lam=0.5, haario_k=None, haario_scale=2.38 ** 2,
+                                   prior=L.PRIOR_IMPROPER, pos=None):
+        """GaussianRandomWalkMix(Σ_A, Σ_B, λ) on coords0 (0-based); haario_k: None
+        or HaarioTypeAdaptation's adapt_every_k_steps."""
+        coords = np.ascontiguousarray(coords0, dtype=np.uint32)
+        n = len(coords)
+        SA = np.ascontiguousarray(np.asarray(sigma_a, dtype=np.float64).reshape(n, n).ravel(order="F"))
+        SB = np.ascontiguousarray(np.asarray(sigma_b, dtype=np.float64).reshape(n, n).ravel(order="F"))
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.RW_GAUSSIAN_MIX
+        u.prior = prior
+        u.num_coords = n
+        u.coords = L.u32ptr(coords)
+        u.sigma = L.dptr(SA)
+        u.sigma_b = L.dptr(SB)
+        u.mix_lambda = float(lam)
+        ad = None
+        if haario_k is not None:
+            ad = L.EmcmcHaarioAdaptation(int(haario_k), 0, float(haario_scale))
+            u.adaptation = L.ADPT_HAARIO
+            u.adaptation_params = C.cast(C.pointer(ad), C.c_void_p)
         if pos is not None:
             p = np.ascontiguousarray(pos, dtype=np.uint8)
             u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
@@ -186,6 +215,22 @@ class Engine:
         self._check(self._lib.emcmc_get_update_state(self._h, pidx, None if eps is None else L.dptr(eps), L.u32ptr(pr),
                                                      L.u32ptr(ac)), "emcmc_get_update_state")
         return eps, pr, ac
+
+    def get_chain_moments(self):
+        """GenericChainStats running (mean [C][D], cov [C][D][D]) kept on device."""
+        Cn, D = self.cfg.num_chains, self.cfg.dim
+        m = np.empty((Cn, D), dtype=np.float64)
+        v = np.empty((Cn, D, D), dtype=np.float64)
+        self._check(self._lib.emcmc_get_chain_moments(self._h, L.dptr(m), L.dptr(v)), "emcmc_get_chain_moments")
+        return m, v
+
+    def get_mix_state(self, pidx: int = 1):
+        """(lower Cholesky factor of each chain's Σ_B [C][D][D], Haario M)."""
+        Cn, D = self.cfg.num_chains, self.cfg.dim
+        Lb = np.empty((Cn, D, D), dtype=np.float64)
+        M = C.c_uint32()
+        self._check(self._lib.emcmc_get_mix_state(self._h, pidx, L.dptr(Lb), C.byref(M)), "emcmc_get_mix_state")
+        return Lb, int(M.value)
 
     def get_faults(self):
         f = np.empty(self.cfg.num_chains, dtype=np.uint32)

@@ -304,6 +304,7 @@ class HaarioTypeAdaptation(Adaptation):
         self.scale = float(scale)
         self.N = 1
         self.M = 0
+        self.identity_f = f is None
         self.f = f if f is not None else (lambda x, y, z: x)
 
 
@@ -333,6 +334,10 @@ class RandomWalkUpdate(MCMCParamUpdate):
         adapt = None
         if isinstance(self.adpt, NoAdaptation):
             pass
+        elif isinstance(self.adpt, HaarioTypeAdaptation) and isinstance(self.rw, GaussianRandomWalkMix):
+            if not self.adpt.identity_f:
+                raise UnsupportedPlugin("HaarioTypeAdaptation with a custom fλ has no device plugin (λ is fixed)")
+            adapt = {"k": self.adpt.adapt_every_k_steps, "scale": self.adpt.scale}
         elif isinstance(self.adpt, AdaptationUnifRW) and isinstance(self.rw, UniformRandomWalk):
             if self.adpt.kind != "scalar":
                 raise UnsupportedPlugin("AdaptationUnifRW with per-coordinate parameters has no device plugin yet")
@@ -342,9 +347,17 @@ class RandomWalkUpdate(MCMCParamUpdate):
         else:
             raise UnsupportedPlugin(f"adaptation {type(self.adpt).__name__} has no device plugin for "
                                     f"{type(self.rw).__name__} yet")
-        if np.any(getattr(self.rw, "pos", False)):
+        pos = getattr(self.rw, "pos", None)
+        if isinstance(self.rw, GaussianRandomWalkMix):
+            pos = np.concatenate([self.rw.gsn_A.pos, self.rw.gsn_B.pos])
+        if np.any(pos if pos is not None else False):
             raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin yet")
-        if isinstance(self.rw, GaussianRandomWalk):
+        if isinstance(self.rw, GaussianRandomWalkMix):
+            engine.add_gaussian_rw_mix_update(coords0, self.rw.gsn_A.Sigma, self.rw.gsn_B.Sigma, lam=self.rw.lam,
+                                              haario_k=None if adapt is None else adapt["k"],
+                                              haario_scale=2.38 ** 2 if adapt is None else adapt["scale"],
+                                              prior=prior)
+        elif isinstance(self.rw, GaussianRandomWalk):
             engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior)
         elif isinstance(self.rw, UniformRandomWalk):
             engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior)
@@ -355,6 +368,14 @@ class RandomWalkUpdate(MCMCParamUpdate):
         """After a run: the reference mutates updt.rw.ϵ and updt.adpt in place
         (adaptation.jl:273-279); with many chains each chain has its own, so
         ``self.rw.eps_chains`` / ``self.adpt.proposed_chains`` etc. hold [C] arrays."""
+        if isinstance(self.rw, GaussianRandomWalkMix):
+            # per chain: the lower factor of gsn_B.Σ and, with Haario, its
+            # mean/cov (= GenericChainStats mean/cov for a single update) and M
+            Lb, M = engine.get_mix_state(pidx)
+            self.rw.gsn_B.chol_chains = Lb
+            if isinstance(self.adpt, HaarioTypeAdaptation):
+                self.adpt.mean_chains, self.adpt.cov_chains = engine.get_chain_moments()
+                self.adpt.M = M
         if isinstance(self.rw, UniformRandomWalk):
             eps, pr, ac = engine.get_update_state(pidx, len(self.rw.eps))
             self.rw.eps_chains = eps

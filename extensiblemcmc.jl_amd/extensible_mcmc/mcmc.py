@@ -39,6 +39,8 @@ class MI355XBackend(MCMCBackend):
     history         "full" (state/proposal/ll/accept histories, the reference's
                     outputs) or "accept_only"
     ll_mode         "per_obs" (literal gsn_target.jl loop) or "suffstat"
+    chain_moments   keep GenericChainStats' running mean/cov on device
+                    (chain_statistics.jl:46-49; always on with GaussianRandomWalkMix)
     """
 
     num_chains: int = 1
@@ -50,6 +52,7 @@ class MI355XBackend(MCMCBackend):
     roll_window: int = 100
     lanes_per_chain: int = 0
     steps_per_launch: int = 0
+    chain_moments: bool = False  # GenericChainStats mean/cov on device (single joint GaussianRandomWalk)
 
 
 class GenericMCMCBackend(MCMCBackend):
@@ -92,7 +95,13 @@ class MI355XGlobalWorkspace:
     def chain_stats(self):
         """rolling_ar (current value, chain_statistics.jl:61-64) and accept counts."""
         ra, acc = self.engine.get_chain_stats()
-        return {"rolling_ar": ra, "accepted": acc}
+        out = {"rolling_ar": ra, "accepted": acc}
+        try:  # GenericChainStats mean/cov, when kept on device
+            out["mean"], out["cov"] = self.engine.get_chain_moments()
+        except L.EMCMCError as e:
+            if e.status != L.STATE_ERROR:
+                raise
+        return out
 
     def summary(self, init=False):
         """workspaces.jl:244-262 (over chains)."""
@@ -169,11 +178,17 @@ def init_global_workspace(backend: MCMCBackend, num_mcmc_steps: int, updates, da
     cfg = EngineConfig(dim=D, num_chains=C, num_mcmc_steps=num_mcmc_steps, seed=backend.seed,
                        first_chain_id=backend.first_chain_id, device=backend.device,
                        history_mode=_HIST[backend.history], roll_window=backend.roll_window,
-                       lanes_per_chain=backend.lanes_per_chain, steps_per_launch=backend.steps_per_launch)
+                       lanes_per_chain=backend.lanes_per_chain, steps_per_launch=backend.steps_per_launch,
+                       chain_moments=backend.chain_moments)
     eng = Engine(cfg)
-    for u in updates:
-        u.to_device(eng)
-    P.to_device(eng, _LL[backend.ll_mode], data["obs"])
+    try:
+        for u in updates:
+            u.to_device(eng)
+        P.to_device(eng, _LL[backend.ll_mode], data["obs"])
+    except L.EMCMCError as e:  # the engine's own "no device plugin" verdicts
+        if e.status == L.UNSUPPORTED_PLUGIN:
+            raise UnsupportedPlugin(str(e)) from e
+        raise
     eng.set_state(np.ascontiguousarray(th0))
     return MI355XGlobalWorkspace(eng, backend, num_mcmc_steps, updates, data)
 

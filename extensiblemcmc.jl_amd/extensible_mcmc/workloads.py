@@ -5,6 +5,11 @@ cfg1  single-chain 2-D Gaussian (the reference's CPU-runnable case; isotropic
       test/runtests.jl:88-111 as ``ref_test``)
 cfg2  65,536 independent RWM chains, D = 32, GsnTargetLaw(μ*, I₃₂), n = 10,
       GaussianRandomWalk(σ²I₃₂), σ = 2.38/√(D·n), θinit = 0, seed 0xC0FFEE
+cfg4  131,072 chains of cfg2's target with GaussianRandomWalkMix(σ²I, σ²I, λ=0.5)
+      + HaarioTypeAdaptation(adapt_every_k_steps=200) and the GenericChainStats
+      mean/cov on device (k = 200 rather than the constructor default 100: with
+      fewer than ~D accepted moves per window the empirical covariance is
+      rank-deficient and cholesky throws PosDefException in the reference)
 cfg5  cfg2 with 1,048,576 chains sharded over GPUs, overdispersed θinit
 There is no network: observations are drawn from fixed numpy seeds.
 """
@@ -29,6 +34,9 @@ class GsnWorkload:
     obs: np.ndarray
     theta_init: np.ndarray  # [D] or [C][D]
     seed: int = SEED
+    sigma_b: np.ndarray = None  # GaussianRandomWalkMix Σ_B (cfg 4)
+    lam: float = None
+    haario_k: int = None
 
     @property
     def nobs(self):
@@ -44,6 +52,15 @@ def cfg2(num_chains: int = 65536, D: int = 32, nobs: int = 10) -> GsnWorkload:
         name=f"rwm_gsn_d{D}_c{num_chains}", D=D, num_chains=num_chains, mu_true=mu, t_sigma=np.eye(D),
         rw_sigma=(sigma * sigma) * np.eye(D), obs=obs, theta_init=np.zeros(D),
     )
+
+
+def cfg4(num_chains: int = 1 << 17, D: int = 32, nobs: int = 10, lam: float = 0.5, k: int = 200) -> GsnWorkload:
+    w = cfg2(num_chains, D, nobs)
+    w.name = f"haario_mix_gsn_d{D}_c{num_chains}"
+    w.sigma_b = w.rw_sigma.copy()
+    w.lam = lam
+    w.haario_k = k
+    return w
 
 
 def cfg5(num_chains: int = 1 << 20, D: int = 32, nobs: int = 10) -> GsnWorkload:

@@ -57,7 +57,7 @@ typedef enum emcmc_status {
 /* Transition kernels — src/transition_kernels/random_walk.jl */
 #define EMCMC_RW_UNIFORM 1u       /* UniformRandomWalk        random_walk.jl:45-94  */
 #define EMCMC_RW_GAUSSIAN 2u      /* GaussianRandomWalk       random_walk.jl:123-171 */
-#define EMCMC_RW_GAUSSIAN_MIX 3u  /* GaussianRandomWalkMix    random_walk.jl:193-232 (reserved) */
+#define EMCMC_RW_GAUSSIAN_MIX 3u  /* GaussianRandomWalkMix    random_walk.jl:193-232 */
 
 /* Priors — src/priors.jl */
 #define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior    priors.jl:18-19 */
@@ -66,7 +66,7 @@ typedef enum emcmc_status {
 /* Adaptation — src/transition_kernels/adaptation.jl */
 #define EMCMC_ADPT_NONE 0u      /* NoAdaptation          adaptation.jl:26 */
 #define EMCMC_ADPT_UNIF_RW 1u   /* AdaptationUnifRW      adaptation.jl:51-329 */
-#define EMCMC_ADPT_HAARIO 2u    /* HaarioTypeAdaptation  adaptation.jl:372-426 (reserved) */
+#define EMCMC_ADPT_HAARIO 2u    /* HaarioTypeAdaptation  adaptation.jl:372-426 (GaussianRandomWalkMix only) */
 
 /* Targets — src/example/gsn_target.jl */
 #define EMCMC_TARGET_GSN 1u     /* GsnTargetLaw(μ, Σ) with coords ⊆ μ */
@@ -92,6 +92,9 @@ typedef enum emcmc_status {
 /* Per-chain fault bits (emcmc_get_faults) */
 #define EMCMC_FAULT_NONFINITE_LL 1u  /* proposal log-likelihood NaN/±Inf */
 #define EMCMC_FAULT_RNG_RETRIES 2u   /* a ziggurat draw exhausted its 65,535 attempt counters */
+#define EMCMC_FAULT_POSDEF 4u        /* Haario readjust: 2.38²/D·cov not positive definite.  The reference
+                                        throws PosDefException at the next MvNormal(θ, Σ_B)
+                                        (random_walk.jl:147,167); the chain keeps its previous Σ_B factor */
 
 typedef struct emcmc_handle emcmc_handle;
 
@@ -110,7 +113,10 @@ typedef struct emcmc_config {
     uint32_t lanes_per_chain;  /* 0 = auto; else 1, 2 or 4 (must divide the work layout) */
     uint32_t steps_per_launch; /* 0 = auto (64) */
     uint32_t kernel_variant;   /* 0 = auto; EMCMC_VARIANT_* tuning flags (results are identical) */
-    uint32_t reserved[6];
+    uint32_t chain_moments;    /* 1 = keep GenericChainStats mean/cov (chain_statistics.jl:46-49) on
+                                  device for a single joint GaussianRandomWalk update (always on with
+                                  GaussianRandomWalkMix); read with emcmc_get_chain_moments */
+    uint32_t reserved[5];
 } emcmc_config;
 
 /* kernel_variant flags: performance-only choices, bit-identical results */
@@ -120,7 +126,7 @@ typedef struct emcmc_config {
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,
  * defaults 100, 0.234, 1.0, 1e-12, 1e7, 1e2).  Passed as
- * emcmc_update_desc.reserved_ptr[0] when adaptation == EMCMC_ADPT_UNIF_RW. */
+ * emcmc_update_desc.adaptation_params when adaptation == EMCMC_ADPT_UNIF_RW. */
 typedef struct emcmc_unifrw_adaptation {
     uint32_t adapt_every_k_steps;
     uint32_t reserved;
@@ -131,22 +137,41 @@ typedef struct emcmc_unifrw_adaptation {
     double offset;
 } emcmc_unifrw_adaptation;
 
+/* `HaarioTypeAdaptation(θ; adapt_every_k_steps, scale, f)` (adaptation.jl:372-397,
+ * defaults 100, 2.38², identity).  Passed as emcmc_update_desc.adaptation_params
+ * when adaptation == EMCMC_ADPT_HAARIO.  `scale` is carried but, as in the
+ * reference, readjust! uses the literal 2.38² (adaptation.jl:423); fλ is the
+ * identity (λ stays at its initial value). */
+typedef struct emcmc_haario_adaptation {
+    uint32_t adapt_every_k_steps;
+    uint32_t reserved;
+    double scale;
+} emcmc_haario_adaptation;
+
 /* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183).
  * Any number of updates, each on any coordinate subset (Metropolis-within-Gibbs,
  * BASELINE cfg 1 and the reference's own test, test/runtests.jl:87-114).  A single
  * GaussianRandomWalk update on coords 1:D without adaptation runs on the fused
- * kernels; every other schedule runs on the general schedule kernel (D ≤ 16). */
+ * kernels; a single GaussianRandomWalkMix update on coords 1:D (optionally with
+ * HaarioTypeAdaptation, BASELINE cfg 4) runs on the mix kernels, which also keep
+ * the chain moments; every other schedule runs on the general schedule kernel
+ * (D ≤ 16). */
 typedef struct emcmc_update_desc {
-    uint32_t kernel;          /* EMCMC_RW_UNIFORM or EMCMC_RW_GAUSSIAN */
+    uint32_t kernel;          /* EMCMC_RW_UNIFORM, EMCMC_RW_GAUSSIAN or EMCMC_RW_GAUSSIAN_MIX */
     uint32_t prior;           /* EMCMC_PRIOR_IMPROPER */
-    uint32_t adaptation;      /* EMCMC_ADPT_NONE, or EMCMC_ADPT_UNIF_RW (UniformRandomWalk only) */
+    uint32_t adaptation;      /* EMCMC_ADPT_NONE, EMCMC_ADPT_UNIF_RW (UniformRandomWalk) or
+                                 EMCMC_ADPT_HAARIO (GaussianRandomWalkMix) */
     uint32_t num_coords;      /* length(coords) */
     const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based), any order */
-    const double *sigma;      /* GaussianRandomWalk Σ: num_coords² column-major */
+    const double *sigma;      /* GaussianRandomWalk Σ, GaussianRandomWalkMix Σ_A: num_coords² column-major */
     const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
     const uint8_t *pos;       /* positivity flags or NULL (all false; true is not on device yet) */
-    const void *reserved_ptr[4]; /* [0]: const emcmc_unifrw_adaptation* for EMCMC_ADPT_UNIF_RW */
-    double reserved_f64[4];
+    const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW) or
+                                      const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
+    const double *sigma_b;    /* GaussianRandomWalkMix Σ_B: num_coords² column-major */
+    const void *reserved_ptr[2];
+    double mix_lambda;        /* GaussianRandomWalkMix λ ∈ [0, 1] (B is picked iff rand() ≤ λ) */
+    double reserved_f64[3];
 } emcmc_update_desc;
 
 /* `data = (P = GsnTargetLaw(μ, Σ), obs = [x_1, …, x_n])` (src/example/gsn_target.jl:1-29,
@@ -229,6 +254,20 @@ emcmc_status emcmc_get_chain_stats(emcmc_handle *h, double *rolling_ar, uint64_t
  * `accepted` counters ([C] each) (adaptation.jl:51-70).  Any pointer may be NULL. */
 emcmc_status emcmc_get_update_state(emcmc_handle *h, uint32_t pidx, double *epsilon, uint32_t *proposed,
                                     uint32_t *accepted);
+
+/* GenericChainStats running mean and covariance of θ (chain_statistics.jl:46-49,
+ * phantom zero sample included), per chain: mean [C][D], cov [C][D][D]
+ * (symmetric).  Kept on device by the mix kernels (and with
+ * emcmc_config.chain_moments); EMCMC_STATE_ERROR otherwise.  Either may be NULL.
+ * With HaarioTypeAdaptation and P = 1 these equal the adaptation's mean/cov
+ * (same recurrence on the same θ, adaptation.jl:406-414). */
+emcmc_status emcmc_get_chain_moments(emcmc_handle *h, double *mean, double *cov);
+
+/* GaussianRandomWalkMix state of update `pidx`: the lower Cholesky factor of
+ * each chain's current Σ_B ([C][D][D], row-major, zeros above the diagonal),
+ * and HaarioTypeAdaptation's M (own-turn steps since the last readjust).
+ * Either may be NULL. */
+emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_sigma_b, uint32_t *steps_since_adapt);
 
 /* Per-chain fault bits (EMCMC_FAULT_*), [C] uint32. */
 emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults);

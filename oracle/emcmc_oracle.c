@@ -383,6 +383,14 @@ ORC_EXPORT void orc_exp_nonpos_vec(const double *x, double *y, uint64_t n) {
 }
 
 /* Ziggurat tables: kn, wn, fn, ke, we, fe (256 each). */
+ORC_EXPORT void orc_exp_any_vec(const double *x, double *y, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) y[i] = orc_exp_any(x[i]);
+}
+
+ORC_EXPORT void orc_log_any_vec(const double *x, double *y, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) y[i] = orc_log_any(x[i]);
+}
+
 ORC_EXPORT void orc_zig_tables_copy(uint64_t *kn, double *wn, double *fn, uint64_t *ke, double *we, double *fe) {
     const orc_zig_tables *t = zig();
     memcpy(kn, t->kn, sizeof t->kn);
@@ -652,5 +660,198 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
     for (uint32_t s = 0; s < nsteps; ++s) last_iter_io[step_pidx[s] - 1] = step_iter[s];
     free(g);
     free(U);
+    return 0;
+}
+
+/* ---- GaussianRandomWalkMix + HaarioTypeAdaptation + GenericChainStats mean/cov
+ *
+ * One joint update (P = 1) on coords 1:D, BASELINE cfg 4.  Restated from
+ * (src/ under /root/reference):
+ *   pick_kernel: B iff rand() ≤ λ (Bernoulli(λ)) ........ random_walk.jl:225-227
+ *   rand(gsn_X, θ): θ° = θ + L_X z ........................ random_walk.jl:145-151
+ *   logpdf(mix) = log((1−λ)·exp(lp_A) + λ·exp(lp_B)),
+ *   lp_X = logpdf(MvNormal(θ, Σ_X), θ°) + logJ (logJ = −0.0 without
+ *   positivity constraints, so the addition is the identity) .. random_walk.jl:161-171,
+ *                                                              229-232
+ *   update_stats!: running mean/cov, phantom zero sample
+ *   (N = 1, mean = 0, cov = 0 at construction) ............ chain_statistics.jl:23-49
+ *   HaarioTypeAdaptation: M += 1 on its own turn, register! θ with the same
+ *   rank-one recurrence (so for P = 1 its mean/cov equal the chain-stats
+ *   mean/cov and are kept once), readjust at M ≥ k:
+ *   Σ_B = 2.38²/D·cov, λ = fλ(λ, N, iter) (identity) ...... adaptation.jl:399-426
+ * cholesky(Symmetric(Σ_B)) of the next MvNormal throws PosDefException in the
+ * reference; here the chain's EMCMC fault bit 4 is set and L_B stays as it was.
+ *
+ * mix = 0: plain GaussianRandomWalk(Σ_A) with on-device chain moments (bitwise
+ * the orc_run_gsn chain plus mean/cov).  haario requires mix.
+ * State: mean [C][D], cov [C][D][D] (symmetric, row-major), LB [C][D][D]
+ * (lower, row-major) in/out; *N_io = GenericChainStats.N (= Haario N),
+ * *M_io = Haario M (uniform over chains).
+ */
+#define ORC_FAULT_POSDEF 4u
+
+static void mix_factor_consts(const double *L, int D, double *iL, double *c0) {
+    for (int i = 0; i < D; ++i) iL[i] = 1.0 / L[(size_t)i * D + i];
+    *c0 = mvnormal_c0(D, logdet_chol(L, D));
+}
+
+ORC_EXPORT int orc_run_mix(int D, uint64_t C, uint32_t chain0, uint64_t seed, const double *sigma_a, int mix,
+                           double lam, int haario, uint32_t k, const double *t_sigma, uint64_t nobs,
+                           const double *obs, int ll_mode, uint32_t W, uint32_t iter0, uint32_t nsteps,
+                           uint64_t *N_io, uint32_t *M_io, double *theta, double *ll, double *ra, uint64_t *ring,
+                           uint32_t *nacc, uint32_t *faults, double *mean, double *cov, double *LB,
+                           double *hist_theta, double *hist_prop, double *hist_ll, uint8_t *hist_acc,
+                           int nthreads) {
+    if (D < 1 || D > 64 || (haario && (!mix || k < 1))) return -2;
+    orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
+    if (!g) return -3;
+    (void)zig();
+    int rc = gsn_prepare(g, D, sigma_a, t_sigma, nobs, obs, ll_mode);
+    if (rc) {
+        free(g);
+        return rc;
+    }
+    const int adiag = is_diag_upper(sigma_a, D);
+    const int tdiag = is_diag_upper(t_sigma, D);
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const orc_zig_tables *zt = zig();
+    const uint64_t N0 = *N_io;
+    const uint32_t M0 = *M_io;
+    const double sB = (2.38 * 2.38) / (double)D; /* 2.38^2/length(rw) */
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t ci = 0; ci < (int64_t)C; ++ci) {
+        const uint64_t c = (uint64_t)ci;
+        const uint32_t gid = chain0 + (uint32_t)c;
+        double th[64], thp[64], z[64], r[64], m[64], iLB[64], c0B = 0.0;
+        double *cv = cov + c * D * D, *Lb = LB + c * D * D;
+        memcpy(th, theta + c * D, sizeof(double) * D);
+        memcpy(m, mean + c * D, sizeof(double) * D);
+        double cll = ll[c], cra = ra[c];
+        uint64_t ring0 = ring[2 * c], ring1 = ring[2 * c + 1];
+        uint32_t na = nacc[c], f = faults[c], M = M0;
+        if (mix) mix_factor_consts(Lb, D, iLB, &c0B);
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            const uint32_t iter = iter0 + s;
+            const uint64_t N = N0 + s;
+            /* proposal!: pick, then θ° = θ + L z */
+            int useB = 0;
+            if (mix) {
+                const orc_u32x4 pr = orc_draw(k0, k1, gid, iter, 0xFFFFFFFEu, 0, 0);
+                useB = orc_u01_closed0(pr.v[0], pr.v[1]) <= lam;
+            }
+            for (int j = 0; j < D; ++j) z[j] = orc_normal(zt, k0, k1, gid, iter, 0, (uint32_t)j, &f);
+            for (int i = 0; i < D; ++i) {
+                double lz;
+                if (useB) {
+                    lz = Lb[(size_t)i * D] * z[0];
+                    for (int j = 1; j <= i; ++j) lz = fma(Lb[(size_t)i * D + j], z[j], lz);
+                } else if (adiag) {
+                    lz = g->Lrw[(size_t)i * D + i] * z[i];
+                } else {
+                    lz = g->Lrw[(size_t)i * D] * z[0];
+                    for (int j = 1; j <= i; ++j) lz = fma(g->Lrw[(size_t)i * D + j], z[j], lz);
+                }
+                thp[i] = th[i] + lz;
+            }
+            /* log_transition_density both ways */
+            double t_fwd = 0.0, t_rev = 0.0;
+            for (int dir = 0; dir < 2; ++dir) {
+                for (int i = 0; i < D; ++i) r[i] = dir ? th[i] - thp[i] : thp[i] - th[i];
+                const double lpA = g->rw_c0 - sqmahal(g->Lrw, g->iLrw, r, D, adiag) / 2.0;
+                double t = lpA;
+                if (mix) {
+                    const double lpB = c0B - sqmahal(Lb, iLB, r, D, 0) / 2.0;
+                    t = orc_log_any((1.0 - lam) * orc_exp_any(lpA) + lam * orc_exp_any(lpB));
+                }
+                if (dir) t_rev = t;
+                else t_fwd = t;
+            }
+            /* compute_ll! */
+            double llp;
+            if (g->ll_mode == 0) {
+                llp = 0.0;
+                for (uint64_t kk = 0; kk < nobs; ++kk) {
+                    for (int i = 0; i < D; ++i) r[i] = obs[kk * D + i] - thp[i];
+                    llp = llp + (g->t_c0 - sqmahal(g->Lt, g->iLt, r, D, tdiag) / 2.0);
+                }
+            } else {
+                for (int i = 0; i < D; ++i) r[i] = g->xbar[i] - thp[i];
+                const double qv = sqmahal(g->Lt, g->iLt, r, D, tdiag);
+                llp = (double)nobs * g->t_c0 - (g->S_c + (double)nobs * qv) * 0.5;
+            }
+            if (!isfinite(llp)) f |= 1u;
+            const double llr = ((((llp - cll) + t_rev) - t_fwd) + 0.0) - 0.0;
+            const double E = orc_exponential(zt, k0, k1, gid, iter, 0, &f);
+            const int acc = E > -llr;
+            if (hist_prop) memcpy(hist_prop + ((uint64_t)s * C + c) * D, thp, sizeof(double) * D);
+            if (acc) {
+                memcpy(th, thp, sizeof(double) * D);
+                cll = llp;
+                na += 1;
+            }
+            if (hist_theta) memcpy(hist_theta + ((uint64_t)s * C + c) * D, th, sizeof(double) * D);
+            if (hist_ll) hist_ll[(uint64_t)s * C + c] = cll;
+            if (hist_acc) hist_acc[(uint64_t)s * C + c] = (uint8_t)acc;
+            /* update_stats!: running mean/cov of θ (chain_statistics.jl:46-49) */
+            {
+                const double a = (double)(N - 1) / (double)N;
+                const double b = (double)N / (double)(N + 1);
+                const double cN = (double)(N + 1) / (double)N;
+                double mo[64];
+                memcpy(mo, m, sizeof(double) * D);
+                for (int i = 0; i < D; ++i) m[i] = m[i] * b + th[i] / (double)(N + 1);
+                for (int i = 0; i < D; ++i)
+                    for (int j = 0; j < D; ++j) {
+                        const double old_sq = a * cv[(size_t)i * D + j] + mo[i] * mo[j];
+                        const double new_sq = old_sq + (th[i] * th[j]) / (double)N;
+                        cv[(size_t)i * D + j] = new_sq - cN * (m[i] * m[j]);
+                    }
+            }
+            /* rolling acceptance (chain_statistics.jl:51-64) */
+            {
+                int outside = 0;
+                if (iter > W) {
+                    uint32_t j = (iter - W) & 127u;
+                    outside = (int)((((j & 64u) ? ring1 : ring0) >> (j & 63u)) & 1u);
+                }
+                const uint64_t mn = N < (uint64_t)W ? N : (uint64_t)W;
+                cra = (cra * (double)W + (double)(acc - outside)) / (double)mn;
+                uint32_t j = iter & 127u;
+                uint64_t bit = 1ull << (j & 63u);
+                if (j & 64u) ring1 = acc ? (ring1 | bit) : (ring1 & ~bit);
+                else ring0 = acc ? (ring0 | bit) : (ring0 & ~bit);
+            }
+            /* update_adaptation!: Haario M, readjust at M ≥ k */
+            if (haario) {
+                M += 1;
+                if (M >= k) {
+                    M = 0;
+                    double S[64 * 64], Ln[64 * 64];
+                    for (int i = 0; i < D; ++i)
+                        for (int j = 0; j < D; ++j) S[(size_t)j * D + i] = sB * cv[(size_t)i * D + j];
+                    if (orc_cholesky(S, D, Ln)) {
+                        f |= ORC_FAULT_POSDEF;
+                    } else {
+                        memcpy(Lb, Ln, sizeof(double) * (size_t)D * D);
+                        mix_factor_consts(Lb, D, iLB, &c0B);
+                    }
+                }
+            }
+        }
+        memcpy(theta + c * D, th, sizeof(double) * D);
+        memcpy(mean + c * D, m, sizeof(double) * D);
+        ll[c] = cll;
+        ra[c] = cra;
+        ring[2 * c] = ring0;
+        ring[2 * c + 1] = ring1;
+        nacc[c] = na;
+        faults[c] = f;
+    }
+    *N_io = N0 + nsteps;
+    if (haario) *M_io = (uint32_t)((M0 + nsteps) % k);
+    (void)nthreads;
+    free(g);
     return 0;
 }

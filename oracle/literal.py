@@ -143,3 +143,67 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
         out["ra"].append(ra[(it, p)])
         out["eps"].append([list(e) if e is not None else None for e in eps])
     return out
+
+
+def run_mix_chain(seed, chain, theta0, sigma_a, sigma_b, lam, t_sigma, obs, nsteps, haario_k=0, mix=True, W=100):
+    """Literal single-chain GaussianRandomWalkMix (+ HaarioTypeAdaptation) and
+    GenericChainStats mean/cov (random_walk.jl:193-232, adaptation.jl:372-426,
+    chain_statistics.jl:41-66), matrix formulas as written: Cholesky of Σ_A and
+    Σ_B at every call (LAPACK), the rank-one recurrence with numpy outer
+    products, Σ_B = 2.38²/D·cov at each readjust."""
+    SA = np.asarray(sigma_a, dtype=float)
+    SB = np.asarray(sigma_b, dtype=float)
+    Lt = np.linalg.cholesky(np.asarray(t_sigma, dtype=float))
+    obs = np.asarray(obs, dtype=float)
+    D = SA.shape[0]
+    th = np.array(theta0, dtype=float)
+    ll = -np.inf
+    ra = 0.0
+    acc_hist = {}
+    mean = np.zeros(D)
+    cov = np.zeros((D, D))
+    N, M = 1, 0
+    out = {"theta": [], "prop": [], "ll": [], "acc": [], "ra": [], "cov": [], "mean": []}
+    for s in range(nsteps):
+        it = 1 + s
+        LA = np.linalg.cholesky(SA)
+        LB = np.linalg.cholesky(SB)            # raises LinAlgError ≙ PosDefException
+        useB = mix and _oracle.pick_uniform(seed, chain, it) <= lam
+        z, E, _ = _oracle.step_variates(seed, chain, it, D)
+        thp = th + (LB if useB else LA) @ z
+        if mix:
+            def lmix(x, m):
+                return np.log((1 - lam) * np.exp(mvnormal_logpdf(x, m, LA) + (-0.0))
+                              + lam * np.exp(mvnormal_logpdf(x, m, LB) + (-0.0)))
+            ltd_fwd, ltd_rev = lmix(thp, th), lmix(th, thp)
+        else:
+            ltd_fwd, ltd_rev = mvnormal_logpdf(thp, th, LA), mvnormal_logpdf(th, thp, LA)
+        llp = 0.0
+        for x in obs:
+            llp += mvnormal_logpdf(x, thp, Lt)
+        llr = llp - ll + ltd_rev - ltd_fwd + 0.0 - 0.0
+        acc = bool(E > -llr)
+        if acc:
+            th = thp
+            ll = llp
+        # update_stats!
+        old_sum_sq = (N - 1) / N * cov + np.outer(mean, mean)
+        mean = mean * (N / (N + 1)) + th / (N + 1)
+        new_sum_sq = old_sum_sq + np.outer(th, th) / N
+        cov = new_sum_sq - (N + 1) / N * np.outer(mean, mean)
+        acc_hist[it] = acc
+        outside = acc_hist.get(it - W, False) if it > W else False
+        ra = (ra * W + (int(acc) - int(outside))) / min(W, N)
+        N += 1
+        if haario_k:                           # M += 1 on own turn; readjust at M ≥ k
+            M += 1
+            if M >= haario_k:
+                M = 0
+                SB = 2.38 ** 2 / D * cov
+        out["theta"].append(th.copy())
+        out["prop"].append(thp.copy())
+        out["ll"].append(ll)
+        out["acc"].append(acc)
+        out["ra"].append(ra)
+    out["cov"], out["mean"], out["sigma_b"] = cov, mean, SB
+    return {k: (np.array(v) if isinstance(v, list) else v) for k, v in out.items()}

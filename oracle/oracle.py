@@ -58,6 +58,9 @@ def lib():
         L.orc_normal_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
         L.orc_exp_vec.restype = None
         L.orc_exp_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
+        for nm in ("orc_exp_any_vec", "orc_log_any_vec"):
+            getattr(L, nm).restype = None
+            getattr(L, nm).argtypes = [dp, dp, C.c_uint64]
         L.orc_markstein_mismatches.restype = C.c_uint64
         L.orc_markstein_mismatches.argtypes = [C.c_double, dp, C.c_uint64]
         L.orc_zig_tables_copy.restype = None
@@ -185,6 +188,20 @@ def exp_nonpos_vec(x):
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.empty_like(x)
     lib().orc_exp_nonpos_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def exp_any_vec(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_exp_any_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def log_any_vec(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_log_any_vec(_d(x), _d(y), x.size)
     return y
 
 
@@ -317,3 +334,62 @@ def uniform01(seed, chain, it, pidx0, j):
     r = philox([chain, it, j >> 1, (pidx0 << 16)], [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
     hi, lo = (int(r[2]), int(r[3])) if j & 1 else (int(r[0]), int(r[1]))
     return float((hi << 21) | (lo >> 11)) * 2.0 ** -53
+
+
+# ---- GaussianRandomWalkMix + HaarioTypeAdaptation + chain moments (cfg 4) ---
+class MixState(OracleState):
+    """OracleState plus GenericChainStats mean/cov (phantom zero sample: N = 1,
+    mean = 0, cov = 0), the per-chain Cholesky factor L_B of Σ_B and Haario's M."""
+
+    def __init__(self, theta, sigma_b=None, ll=None):
+        super().__init__(theta, ll)
+        D = self.D
+        self.mean = np.zeros((self.C, D))
+        self.cov = np.zeros((self.C, D, D))
+        LB = cholesky(sigma_b) if sigma_b is not None else np.eye(D)
+        self.LB = np.ascontiguousarray(np.broadcast_to(LB, (self.C, D, D))).copy()
+        self.M = 0
+
+
+def run_mix(state: MixState, *, seed, sigma_a, t_sigma, obs, iter0, nsteps, mix=True, lam=0.5, haario_k=0,
+            chain0=0, ll_mode=0, W=100, history=True, nthreads=1):
+    """Advance `state` by `nsteps` consecutive iterations of the single joint
+    GaussianRandomWalkMix (mix=True) or GaussianRandomWalk (mix=False) update
+    with on-device chain moments; haario_k > 0 adds HaarioTypeAdaptation(k)."""
+    L = lib()
+    if not hasattr(L, "_mix_ready"):
+        dp, u32p, u64p, u8p = (C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_uint8))
+        L.orc_run_mix.restype = C.c_int
+        L.orc_run_mix.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, dp, C.c_int, C.c_double, C.c_int,
+                                  C.c_uint32, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, u64p,
+                                  u32p, dp, dp, dp, u64p, u32p, u32p, dp, dp, dp, dp, dp, dp, u8p, C.c_int]
+        L._mix_ready = True
+    Cn, D = state.C, state.D
+    X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
+    hist = alloc_history(Cn, D, nsteps) if history else {}
+    if iter0 > 1 and state.last_iter != iter0 - 1:
+        state.ra[:] = 0.0
+    N = np.array([state.N], dtype=np.uint64)
+    M = np.array([state.M], dtype=np.uint32)
+    rc = L.orc_run_mix(
+        D, Cn, chain0, seed & 0xFFFFFFFFFFFFFFFF, _d(_colmajor(sigma_a, D)), int(mix), float(lam),
+        int(haario_k > 0), max(int(haario_k), 1), _d(_colmajor(t_sigma, D)), X.shape[0], _d(X), ll_mode, W, iter0,
+        nsteps, N.ctypes.data_as(C.POINTER(C.c_uint64)), M.ctypes.data_as(C.POINTER(C.c_uint32)), _d(state.theta),
+        _d(state.ll), _d(state.ra), state.ring.ctypes.data_as(C.POINTER(C.c_uint64)),
+        state.nacc.ctypes.data_as(C.POINTER(C.c_uint32)), state.faults.ctypes.data_as(C.POINTER(C.c_uint32)),
+        _d(state.mean), _d(state.cov), _d(state.LB), _d(hist.get("theta")), _d(hist.get("prop")),
+        _d(hist.get("ll")), None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads)
+    if rc != 0:
+        raise ValueError(f"orc_run_mix failed: {rc}")
+    state.N, state.M = int(N[0]), int(M[0])
+    state.last_iter = iter0 + nsteps - 1
+    if history:
+        hist["acc"] = hist["acc"].astype(bool)
+    return hist
+
+
+def pick_uniform(seed, chain, it):
+    """The [0,1) uniform that picks GaussianRandomWalkMix's kernel (B iff u ≤ λ)."""
+    r = philox([chain, it, 0xFFFFFFFE, 0], [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
+    return float((int(r[0]) << 21) | (int(r[1]) >> 11)) * 2.0 ** -53

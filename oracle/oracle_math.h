@@ -130,6 +130,41 @@ static inline double orc_exp_nonpos(double x) {
     return p * orc_u2d((uint64_t)(1023 + k) << 52);
 }
 
+/* exp(x) over the whole double range (the mixture density of
+ * GaussianRandomWalkMix, random_walk.jl:229-232, exponentiates log-densities of
+ * either sign): the orc_exp_nonpos reduction and polynomial, 2^k applied in two
+ * exact steps when the result is subnormal (one rounding) or near overflow. */
+static inline double orc_exp_any(double x) {
+    if (x != x) return x;
+    if (x > 709.782712893384) return INFINITY;
+    if (x < -745.1332191019412) return 0.0;
+    const double invln2 = 1.44269504088896338700e+00;
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    double kd = rint(x * invln2);
+    double r = fma(-kd, ln2_hi, x);
+    r = fma(-kd, ln2_lo, r);
+    static const double inv_fact[14] = {1.0, 1.0, 0.5, 1.0 / 6.0, 1.0 / 24.0, 1.0 / 120.0, 1.0 / 720.0,
+                                        1.0 / 5040.0, 1.0 / 40320.0, 1.0 / 362880.0, 1.0 / 3628800.0,
+                                        1.0 / 39916800.0, 1.0 / 479001600.0, 1.0 / 6227020800.0};
+    double p = inv_fact[13];
+    for (int n = 12; n >= 0; --n) p = fma(p, r, inv_fact[n]);
+    int k = (int)kd;
+    if (k > 1023) return (p * orc_u2d((uint64_t)(1023 + k - 1) << 52)) * 2.0;
+    if (k < -1022) return (p * orc_u2d((uint64_t)(1023 + k + 64) << 52)) * 0x1p-64;
+    return p * orc_u2d((uint64_t)(1023 + k) << 52);
+}
+
+/* log(x) for any x ≥ 0 or NaN: 0 → −Inf, +Inf → +Inf, subnormals scaled by
+ * 2^54 first (one extra rounding in the final subtraction). */
+#define ORC_LN2_54 37.42994775023705 /* 54·ln 2 */
+static inline double orc_log_any(double x) {
+    if (x != x) return x;
+    if (x == 0.0) return -INFINITY;
+    if (x == INFINITY) return INFINITY;
+    if (x < 0x1p-1022) return orc_log(x * 0x1p54) - ORC_LN2_54;
+    return orc_log(x);
+}
+
 /* ---- 256-layer Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---- */
 #define ORC_ZN_R 3.6541528853610088
 #define ORC_ZN_V 4.92867323399e-3

@@ -48,6 +48,9 @@ def test_struct_layout_matches_header(tmp_path):
           printf("%zu %zu %zu %zu %zu\\n", offsetof(emcmc_config, device), offsetof(emcmc_update_desc, pos),
                  offsetof(emcmc_target_desc, ll_mode), sizeof(emcmc_unifrw_adaptation),
                  offsetof(emcmc_unifrw_adaptation, offset));
+          printf("%zu %zu %zu %zu %zu\\n", offsetof(emcmc_config, chain_moments),
+                 offsetof(emcmc_update_desc, adaptation_params), offsetof(emcmc_update_desc, sigma_b),
+                 offsetof(emcmc_update_desc, mix_lambda), sizeof(emcmc_haario_adaptation));
           return 0;
         }
         """
@@ -56,13 +59,17 @@ def test_struct_layout_matches_header(tmp_path):
     c.write_text(src)
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-std=c11", "-I", str(HEADER.parent), str(c), "-o", str(exe)], check=True)
-    sizes, offs = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")[:2]
+    sizes, offs, offs2 = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")[:3]
     assert [int(x) for x in sizes.split()] == [C.sizeof(L.EmcmcConfig), C.sizeof(L.EmcmcUpdateDesc),
                                                C.sizeof(L.EmcmcTargetDesc), C.sizeof(L.EmcmcStep),
                                                C.sizeof(L.EmcmcMoments)]
     assert [int(x) for x in offs.split()] == [L.EmcmcConfig.device.offset, L.EmcmcUpdateDesc.pos.offset,
                                               L.EmcmcTargetDesc.ll_mode.offset, C.sizeof(L.EmcmcUnifRWAdaptation),
                                               L.EmcmcUnifRWAdaptation.offset.offset]
+    assert [int(x) for x in offs2.split()] == [L.EmcmcConfig.chain_moments.offset,
+                                               L.EmcmcUpdateDesc.adaptation_params.offset,
+                                               L.EmcmcUpdateDesc.sigma_b.offset, L.EmcmcUpdateDesc.mix_lambda.offset,
+                                               C.sizeof(L.EmcmcHaarioAdaptation)]
 
 
 def test_no_device_means_no_run():

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from extensible_mcmc import (MCMC, AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMix, GsnTargetLaw,
-                             ImproperPrior, MI355XBackend, RandomWalkUpdate, REPLCallback, SavingCallback,
+                             HaarioTypeAdaptation, ImproperPrior, MI355XBackend, RandomWalkUpdate, REPLCallback, SavingCallback,
                              UniformRandomWalk, UnsupportedPlugin, run)
 from extensible_mcmc import workloads as W
 
@@ -42,14 +42,38 @@ def test_run_bivariate_joint_gaussian_rw(oracle, tmp_path):
 
 def test_unsupported_plugins_raise_not_fallback():
     w = W.ref_test()
-    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(np.eye(2), 2 * np.eye(2)), [1, 2])],
-                backend=MI355XBackend(num_chains=8))
+    # GaussianRandomWalkMix runs on device only as the single joint update on 1:D
+    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(np.eye(1), 2 * np.eye(1)), [1]),
+                 RandomWalkUpdate(GaussianRandomWalk(np.eye(1)), [2])], backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
     mcmc = MCMC([RandomWalkUpdate(UniformRandomWalk([1.0], [True]), [1]),
                  RandomWalkUpdate(UniformRandomWalk([1.0]), [2])], backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):  # positivity-restricted coordinates
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
+
+
+def test_haario_mix_through_the_api(oracle):
+    """GaussianRandomWalkMix + HaarioTypeAdaptation (BASELINE cfg 4 shape at D = 2)
+    through MCMC/run: final state, accept history, per-chain Σ_B factor and the
+    adaptation's mean/cov equal the oracle's."""
+    w = W.ref_test()
+    S = 0.5 * np.eye(2)
+    upd = RandomWalkUpdate(GaussianRandomWalkMix(S, 0.25 * S, 0.4), [1, 2],
+                           adpt=HaarioTypeAdaptation([0.0, 0.0], adapt_every_k_steps=50))
+    mcmc = MCMC([upd], backend=MI355XBackend(num_chains=300, seed=w.seed))
+    ws, lwss = run(mcmc, 400, dict(P=GsnTargetLaw([1.0, 2.0], [[1.0, 0.5], [0.5, 1.0]]), obs=w.obs), [0.0, 0.0])
+    st = oracle.MixState(np.zeros((300, 2)), sigma_b=0.25 * S)
+    h = oracle.run_mix(st, seed=w.seed, sigma_a=S, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=400, lam=0.4,
+                       haario_k=50, nthreads=8)
+    assert "mix_gsn_kernel" in ws.engine.kernel_name()
+    assert np.array_equal(ws.state, st.theta)
+    assert np.array_equal(lwss[0].acceptance_history(1, 400), h["acc"])
+    assert np.array_equal(upd.rw.gsn_B.chol_chains, st.LB)
+    assert np.array_equal(upd.adpt.cov_chains, st.cov) and np.array_equal(upd.adpt.mean_chains, st.mean)
+    assert upd.adpt.M == 0
+    stats = ws.chain_stats()
+    assert np.array_equal(stats["cov"], st.cov)
 
 
 def test_reference_mcmc_testset_through_the_api(oracle):

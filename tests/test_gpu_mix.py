@@ -1,0 +1,164 @@
+"""Row f1 on the GPU (BASELINE cfg 4): mix_gsn_kernel + mix_readjust_kernel
+against the oracle (orc_run_mix), bit for bit — accept stream, state, ll,
+rolling acceptance, GenericChainStats mean/cov, each chain's Σ_B factor after
+Haario readjusts, fault bits — through the C ABI."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc import workloads as W
+from extensible_mcmc.engine import Engine, EngineConfig
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True)
+def _gpu(require_gpu):
+    pass
+
+
+def _problem(D, dense=False):
+    w = W.cfg2(8, D=D)
+    obs = np.asarray(w.obs)[:, :D]
+    ts = np.asarray(w.t_sigma)[:D, :D]
+    mu = np.asarray(w.mu_true)[:D]
+    sa = np.asarray(w.rw_sigma)[:D, :D]
+    if dense:
+        rng = np.random.default_rng(7)
+        A = rng.standard_normal((D, D))
+        ts = A @ A.T / D + np.eye(D)
+        sa = 0.02 * (np.eye(D) + 0.3 * np.ones((D, D)))
+    return w.seed, mu, ts, obs, sa
+
+
+def _engine(D, C, M, seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist, spl=0, moments_only=False):
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
+                              steps_per_launch=spl, chain_moments=moments_only))
+    if moments_only:
+        eng.add_gaussian_rw_update(range(D), sa)
+    else:
+        eng.add_gaussian_rw_mix_update(range(D), sa, sb, lam=lam, haario_k=k or None)
+    eng.set_gsn_target(mu, ts, obs, ll_mode=ll_mode)
+    eng.set_state(np.zeros((C, D)))
+    return eng
+
+
+def _check(eng, st, hists, iters, full, mix=True):
+    eng.synchronize(allow_faults=True)
+    th, ll = eng.get_state()
+    assert np.array_equal(th, st.theta)
+    assert np.array_equal(ll, st.ll)
+    ra, nacc = eng.get_chain_stats()
+    assert np.array_equal(ra[0], st.ra)
+    assert np.array_equal(nacc[0], st.nacc)
+    assert np.array_equal(eng.get_faults(), st.faults)
+    mean, cov = eng.get_chain_moments()
+    assert np.array_equal(mean, st.mean)
+    assert np.array_equal(cov, st.cov)
+    if mix:
+        Lb, M = eng.get_mix_state(1)
+        assert np.array_equal(Lb, st.LB)
+        assert M == st.M
+    acc = np.concatenate([h["acc"] for h in hists])
+    i0, n = iters[0], iters[-1] - iters[0] + 1
+    rows = np.asarray(iters) - i0
+    assert np.array_equal(eng.get_history(L.H_ACCEPT, i0, n)[rows, 0], acc)
+    if full:
+        for which, key in ((L.H_STATE, "theta"), (L.H_PROPOSAL, "prop"), (L.H_LL, "ll")):
+            got = eng.get_history(which, i0, n)[rows, 0]
+            assert np.array_equal(got, np.concatenate([h[key] for h in hists])), key
+
+
+CASES = [  # D, lam, k, ll_mode, hist, dense
+    (2, 0.5, 0, L.LL_PER_OBS, L.HIST_FULL, False),
+    (4, 0.3, 25, L.LL_SUFFSTAT, L.HIST_FULL, True),
+    (8, 0.5, 50, L.LL_PER_OBS, L.HIST_ACCEPT_ONLY, False),
+    (8, 1.0, 40, L.LL_SUFFSTAT, L.HIST_FULL, True),
+    (16, 0.5, 40, L.LL_SUFFSTAT, L.HIST_FULL, False),
+    (32, 0.5, 100, L.LL_PER_OBS, L.HIST_FULL, False),
+    (32, 0.25, 60, L.LL_SUFFSTAT, L.HIST_ACCEPT_ONLY, False),
+]
+
+
+@pytest.mark.parametrize("D,lam,k,ll_mode,hist,dense", CASES)
+def test_mix_haario_matches_oracle(oracle, D, lam, k, ll_mode, hist, dense):
+    """random_walk.jl:193-232, adaptation.jl:372-426, chain_statistics.jl:41-66."""
+    seed, mu, ts, obs, sa = _problem(D, dense)
+    sb = 0.5 * sa
+    C, M = (1024 if D >= 16 else 777), 300
+    eng = _engine(D, C, M, seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist)
+    eng.run_iters(1, M)
+    assert "mix_gsn_kernel<D=%d" % D in eng.kernel_name()
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=sb)
+    h = oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=M, lam=lam, haario_k=k,
+                       ll_mode=ll_mode, nthreads=8)
+    _check(eng, st, [h], list(range(1, M + 1)), hist == L.HIST_FULL)
+
+
+def test_split_calls_launch_cuts_and_gap(oracle):
+    """Three emcmc_run calls, 7-step launches cut again at every readjust (k = 30),
+    and a schedule gap (update excluded on iterations 51:60): rolling_ar restarts
+    from 0.0 after the gap, N and M count steps that ran."""
+    D, C, M, k = 8, 500, 130, 30
+    seed, mu, ts, obs, sa = _problem(D)
+    sb = sa.copy()
+    eng = _engine(D, C, M, seed, mu, ts, obs, sa, sb, 0.5, k, L.LL_PER_OBS, L.HIST_FULL, spl=7)
+    iters = list(range(1, 51)) + list(range(61, 131))
+    for a, b in ((0, 33), (33, 80), (80, len(iters))):
+        eng.run([(i, 1) for i in iters[a:b]])
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=sb)
+    kw = dict(seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, lam=0.5, haario_k=k, nthreads=8)
+    hs = [oracle.run_mix(st, iter0=1, nsteps=50, **kw), oracle.run_mix(st, iter0=61, nsteps=70, **kw)]
+    _check(eng, st, hs, iters, True)
+
+
+def test_posdef_failure_sets_fault_and_keeps_factor(oracle):
+    """Readjust after 3 steps at D = 8: 2.38²/D·cov has rank ≤ 4; the chains whose
+    Cholesky fails raise EMCMC_FAULT_POSDEF (the reference: PosDefException) and
+    keep their Σ_B factor; emcmc_synchronize reports EMCMC_CHAIN_FAULT."""
+    D, C = 8, 256
+    seed, mu, ts, obs, sa = _problem(D)
+    eng = _engine(D, C, 20, seed, mu, ts, obs, sa, sa, 0.5, 3, L.LL_PER_OBS, L.HIST_FULL)
+    eng.run_iters(1, 3)
+    with pytest.raises(L.EMCMCError) as e:
+        eng.synchronize()
+    assert e.value.status == L.CHAIN_FAULT
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=sa)
+    h = oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=3, haario_k=3)
+    assert ((st.faults & L.FAULT_POSDEF) != 0).sum() >= C // 2
+    _check(eng, st, [h], [1, 2, 3], True)
+
+
+@pytest.mark.parametrize("D", [8, 32])
+def test_chain_moments_flag_on_plain_gaussian_rw(oracle, D):
+    """emcmc_config.chain_moments with GaussianRandomWalk: the fused path's bits
+    (orc_run_gsn) plus GenericChainStats mean/cov (orc_run_mix, mix off)."""
+    seed, mu, ts, obs, sa = _problem(D)
+    C, M = 1024, 200
+    eng = _engine(D, C, M, seed, mu, ts, obs, sa, None, 0.0, 0, L.LL_SUFFSTAT, L.HIST_FULL, moments_only=True)
+    eng.run_iters(1, M)
+    assert "GSN_MOMENTS" in eng.kernel_name()
+    st = oracle.MixState(np.zeros((C, D)))
+    h = oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=M, mix=False, ll_mode=1,
+                       nthreads=8)
+    so = oracle.OracleState(np.zeros((C, D)))
+    ho = oracle.run_gsn(so, seed=seed, rw_sigma=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=M, ll_mode=1, nthreads=8)
+    assert np.array_equal(h["acc"], ho["acc"])
+    _check(eng, st, [h], list(range(1, M + 1)), True, mix=False)
+
+
+def test_mix_rejects_unsupported_shapes():
+    """GaussianRandomWalkMix only as the single joint update on 1:D; dense Σ at D = 32."""
+    seed, mu, ts, obs, sa = _problem(4)
+    eng = Engine(EngineConfig(dim=4, num_chains=64, num_mcmc_steps=10, seed=seed))
+    eng.add_gaussian_rw_mix_update([0, 1], sa[:2, :2], sa[:2, :2])
+    with pytest.raises(L.EMCMCError) as e:
+        eng.add_gaussian_rw_update([2, 3], sa[:2, :2])
+        eng.set_gsn_target(mu, ts, obs)
+    assert e.value.status == L.UNSUPPORTED_PLUGIN
+    seed, mu, ts, obs, sa = _problem(32, dense=True)
+    eng = Engine(EngineConfig(dim=32, num_chains=64, num_mcmc_steps=10, seed=seed))
+    eng.add_gaussian_rw_mix_update(range(32), sa, sa)
+    with pytest.raises(L.EMCMCError) as e:
+        eng.set_gsn_target(mu, ts, obs)
+    assert e.value.status == L.UNSUPPORTED_PLUGIN

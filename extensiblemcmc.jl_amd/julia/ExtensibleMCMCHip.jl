@@ -34,7 +34,8 @@ struct EmcmcConfig
     lanes_per_chain::UInt32
     steps_per_launch::UInt32
     kernel_variant::UInt32
-    reserved::NTuple{6,UInt32}
+    chain_moments::UInt32
+    reserved::NTuple{5,UInt32}
 end
 
 struct EmcmcUpdateDesc
@@ -46,8 +47,17 @@ struct EmcmcUpdateDesc
     sigma::Ptr{Float64}
     epsilon::Ptr{Float64}
     pos::Ptr{UInt8}
-    reserved_ptr::NTuple{4,Ptr{Cvoid}}
-    reserved_f64::NTuple{4,Float64}
+    adaptation_params::Ptr{Cvoid}
+    sigma_b::Ptr{Float64}
+    reserved_ptr::NTuple{2,Ptr{Cvoid}}
+    mix_lambda::Float64
+    reserved_f64::NTuple{3,Float64}
+end
+
+struct EmcmcHaarioAdaptation
+    adapt_every_k_steps::UInt32
+    reserved::UInt32
+    scale::Float64
 end
 
 struct EmcmcTargetDesc
@@ -67,6 +77,8 @@ struct EmcmcStep
 end
 
 const RW_GAUSSIAN = UInt32(2)
+const RW_GAUSSIAN_MIX = UInt32(3)
+const ADPT_HAARIO = UInt32(2)
 const PRIOR_IMPROPER = UInt32(0)
 const ADPT_NONE = UInt32(0)
 const TARGET_GSN = UInt32(1)
@@ -93,6 +105,7 @@ Base.@kwdef struct MI355XBackend <: eMCMC.MCMCBackend
     device::Int = 0
     history::Symbol = :full
     ll_mode::Symbol = :per_obs
+    chain_moments::Bool = false   # GenericChainStats mean/cov on device (chain_statistics.jl:46-49)
 end
 
 mutable struct MI355XGlobalWorkspace{T} <: eMCMC.GlobalWorkspace{T}
@@ -133,7 +146,23 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
         Σ = Matrix{Float64}(updt.rw.Σ)                         # column-major already
         push!(keep, Σ)
         return EmcmcUpdateDesc(RW_GAUSSIAN, PRIOR_IMPROPER, ADPT_NONE, UInt32(length(coords)), pointer(coords),
-                               pointer(Σ), C_NULL, C_NULL, (C_NULL, C_NULL, C_NULL, C_NULL), (0.0, 0.0, 0.0, 0.0))
+                               pointer(Σ), C_NULL, C_NULL, C_NULL, C_NULL, (C_NULL, C_NULL), 0.0, (0.0, 0.0, 0.0))
+    elseif updt.rw isa eMCMC.GaussianRandomWalkMix                # random_walk.jl:193-232
+        (any(updt.rw.gsn_A.pos) || any(updt.rw.gsn_B.pos)) &&
+            error("positivity-restricted coordinates are not on device yet")
+        ΣA = Matrix{Float64}(updt.rw.gsn_A.Σ)
+        ΣB = Matrix{Float64}(updt.rw.gsn_B.Σ)
+        push!(keep, ΣA, ΣB)
+        if updt.adpt isa eMCMC.HaarioTypeAdaptation              # adaptation.jl:372-426 (fλ must be identity)
+            p = Ref(EmcmcHaarioAdaptation(UInt32(updt.adpt.adapt_every_k_steps), UInt32(0), updt.adpt.scale))
+            push!(keep, p)
+            adpt, adptp = ADPT_HAARIO, Base.unsafe_convert(Ptr{Cvoid}, p)
+        elseif !(updt.adpt isa eMCMC.NoAdaptation)
+            error("no device plugin for $(typeof(updt.adpt)) with GaussianRandomWalkMix")
+        end
+        return EmcmcUpdateDesc(RW_GAUSSIAN_MIX, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords),
+                               pointer(ΣA), C_NULL, C_NULL, adptp, pointer(ΣB), (C_NULL, C_NULL), updt.rw.λ,
+                               (0.0, 0.0, 0.0))
     elseif updt.rw isa eMCMC.UniformRandomWalk
         any(updt.rw.pos) && error("positivity-restricted coordinates are not on device yet")
         ϵ = Float64.(collect(updt.rw.ϵ))
@@ -148,7 +177,7 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
             error("no device plugin for $(typeof(updt.adpt))")
         end
         return EmcmcUpdateDesc(RW_UNIFORM, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords), C_NULL,
-                               pointer(ϵ), C_NULL, (adptp, C_NULL, C_NULL, C_NULL), (0.0, 0.0, 0.0, 0.0))
+                               pointer(ϵ), C_NULL, adptp, C_NULL, (C_NULL, C_NULL), 0.0, (0.0, 0.0, 0.0))
     end
     error("no device plugin for $(typeof(updt.rw))")
 end
@@ -161,7 +190,7 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
     cfg = Ref(EmcmcConfig(ABI_VERSION, UInt32(D), UInt64(be.num_chains), UInt64(be.first_chain_id),
                           UInt64(num_mcmc_steps), be.seed, Int32(be.device),
                           be.history === :full ? UInt32(0) : UInt32(1), UInt32(100), UInt32(0),
-                          UInt32(0), UInt32(0), ntuple(_ -> UInt32(0), 6)))
+                          UInt32(0), UInt32(0), UInt32(be.chain_moments), ntuple(_ -> UInt32(0), 5)))
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:emcmc_create, LIB), Cint, (Ref{Ptr{Cvoid}}, Ref{EmcmcConfig}), h, cfg), C_NULL, "emcmc_create")
     keep = Any[]

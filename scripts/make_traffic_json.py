@@ -4,7 +4,11 @@ launch of the step kernel (WRITE_SIZE; FETCH_SIZE ×2 on gfx950, per
 MI355X_MICROARCH.md's HBM section) and per chain-step, keyed by the kernel
 name bench.py reports.  Usage: make_traffic_json.py SUMMARY KERNEL_NAME CHAINS STEPS_PER_LAUNCH [TAG]"""
 import json
+import re
 import sys
+
+# step kernels: fused RWM (rwm_gsn_*) and mix / chain-moments (mix_gsn_kernel)
+STEP = re.compile(r"rwm_gsn|mix_gsn_kernel")
 
 summ, name, chains, spl = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 tag = sys.argv[5] if len(sys.argv) > 5 else "r1"
@@ -14,7 +18,7 @@ pm = d["pmc"]
 f = pm["fetch_bytes_corrected_per_launch"][1:] or pm["fetch_bytes_corrected_per_launch"]
 w = pm["write_bytes_per_launch"][1:] or pm["write_bytes_per_launch"]
 fb, wb = sum(f) / len(f), sum(w) / len(w)
-step = [v for k, v in d["kernel_stats"].items() if "rwm_gsn" in k][0]
+step = [v for k, v in d["kernel_stats"].items() if STEP.search(k)][0]
 out = {name: {"bytes_per_chain_step": (fb + wb) / (chains * spl), "fetch_bytes_per_launch": fb,
               "write_bytes_per_launch": wb, "chains": chains, "steps_per_launch": spl,
               "source": f"profiles/{tag}_pmc_fetch_size.csv, profiles/{tag}_pmc_write_size.csv "

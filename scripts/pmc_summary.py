@@ -5,7 +5,11 @@ WRITE_SIZE (KiB units; FETCH_SIZE ×2 on gfx950 per MI355X_MICROARCH.md §HBM)."
 import csv
 import glob
 import json
+import re
 import sys
+
+# step kernels: fused RWM (rwm_gsn_*) and mix / chain-moments (mix_gsn_kernel)
+STEP = re.compile(r"rwm_gsn|mix_gsn_kernel")
 from collections import defaultdict
 
 d = sys.argv[1]
@@ -20,13 +24,13 @@ def rows(pattern):
 
 stats = {r["Name"]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "total_ns": float(r["TotalDurationNs"]),
                      "pct": float(r["Percentage"])} for r in rows("trace/**/*kernel_stats.csv")}
-step = [k for k in stats if "rwm_gsn" in k]
+step = [k for k in stats if STEP.search(k)]
 res = {"kernel_stats": stats}
 pmc = defaultdict(list)
 for name in ("FETCH_SIZE", "WRITE_SIZE"):
     sub = "fetch" if name == "FETCH_SIZE" else "write"
     for r in rows(f"{sub}/**/*counter_collection.csv"):
-        if "rwm_gsn" in r["Kernel_Name"] and r["Counter_Name"] == name:
+        if STEP.search(r["Kernel_Name"]) and r["Counter_Name"] == name:
             pmc[name].append(float(r["Counter_Value"]))
 if pmc:
     f = pmc["FETCH_SIZE"]

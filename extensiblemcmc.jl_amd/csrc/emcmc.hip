@@ -20,6 +20,7 @@
 
 #include "../../include/emcmc.h"
 #include "emcmc_kernels.h"
+#include "emcmc_mala.h"
 #include "emcmc_mix.h"
 #include "emcmc_mwg.h"
 
@@ -103,6 +104,8 @@ struct UpdateHost {
 };
 
 struct TargetHost {
+    uint32_t kind = EMCMC_TARGET_GSN;
+    std::vector<double> labels;  // EMCMC_TARGET_LOGISTIC: y
     uint32_t dim = 0, ll_mode = 0;
     uint64_t nobs = 0;
     std::vector<double> mu, sigma, L, invdiag, obs, xbar;
@@ -114,12 +117,14 @@ using KernelFn = void (*)(StepParams);
 using MwgFn = void (*)(MwgParams);
 using MixFn = void (*)(MixParams);
 using ReadjustFn = void (*)(MixReadjustParams);
+using MalaFn = void (*)(MalaParams);
 
 struct Variant {
     KernelFn fn = nullptr;
     MwgFn mfn = nullptr;  // general schedule kernel (mwg_gsn_kernel) when set
     MixFn xfn = nullptr;  // mix / chain-moments kernel (mix_gsn_kernel) when set
     ReadjustFn rfn = nullptr;  // Haario readjust kernel
+    MalaFn afn = nullptr, ainit = nullptr;  // MALA step / ∇ℓ initialisation kernels
     bool mix = false;
     int lpc = 1;
     bool dense = false;
@@ -163,6 +168,10 @@ struct emcmc_handle {
     double *d_mean = nullptr, *d_cov = nullptr, *d_LB = nullptr, *d_iLB = nullptr, *d_c0B = nullptr;
     double *d_Lnew = nullptr;
     uint32_t mix_M = 0;
+    // MALA path: carried ∇ℓ(θ) (state_pos layout), padded X and y
+    double *d_grad = nullptr, *d_X = nullptr, *d_y = nullptr;
+    uint32_t mala_tiles = 0;
+    bool grad_valid = false;
     // dispatch
     Variant var;
     size_t lds_bytes = 0;
@@ -286,6 +295,7 @@ bool mix_path(const emcmc_handle *h) {
 
 // P°.θ[1:d] ← μ for every chain (workspaces.jl:225-233: P° = deepcopy(data.P))
 emcmc_status reset_mu_p(emcmc_handle *h) {
+    if (h->target.kind != EMCMC_TARGET_GSN) return EMCMC_OK;
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
     std::vector<double> m(C * D);
     for (uint64_t c = 0; c < C; ++c)
@@ -318,6 +328,7 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
         HIPCHK(h, hipMalloc(&h->d_zig, sizeof(Ziggurat)));
         HIPCHK(h, hipMemcpy(h->d_zig, &zt, sizeof(Ziggurat), hipMemcpyHostToDevice));
     }
+    if (h->updates[0].kernel == EMCMC_MALA) HIPCHK(h, hipMalloc(&h->d_grad, C * D * sizeof(double)));
     if (mix_path(h)) {  // GenericChainStats mean/cov; Σ_B factors
         const uint64_t DP = (uint64_t)packed_n((int)D);
         const UpdateHost &u = h->updates[0];
@@ -519,8 +530,56 @@ emcmc_status select_mix(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
+// ---- MALA kernel table ---------------------------------------------------------
+template <int DB, bool FULL, int MODE>
+MalaFn mala_fn() {
+    return &mala_logistic_kernel<DB, FULL, MODE>;
+}
+emcmc_status select_mala(emcmc_handle *h) {
+    const int D = (int)h->cfg.dim;
+    if (!joint_all_coords(h))
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA runs on device as the single joint update on coords 1:D");
+    if (h->target.kind != EMCMC_TARGET_LOGISTIC)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA on device needs the logistic-regression target");
+    const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
+    Variant v;
+    switch (D) {
+    case 16: v.afn = full ? mala_fn<1, true, 0>() : mala_fn<1, false, 0>(); v.ainit = mala_fn<1, true, 1>(); break;
+    case 32: v.afn = full ? mala_fn<2, true, 0>() : mala_fn<2, false, 0>(); v.ainit = mala_fn<2, true, 1>(); break;
+    case 48: v.afn = full ? mala_fn<3, true, 0>() : mala_fn<3, false, 0>(); v.ainit = mala_fn<3, true, 1>(); break;
+    case 64: v.afn = full ? mala_fn<4, true, 0>() : mala_fn<4, false, 0>(); v.ainit = mala_fn<4, true, 1>(); break;
+    default:
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no MALA kernel for D=%d (instantiated: D ∈ {16,32,48,64})", D);
+    }
+    char nm[160];
+    snprintf(nm, sizeof nm, "mala_logistic_kernel<D=%d,%s>", D, full ? "FULL" : "ACCEPT_ONLY");
+    v.name = nm;
+    // X padded to whole 64-row tiles with zero rows (their ℓ terms are masked)
+    const TargetHost &t = h->target;
+    const uint64_t tiles = (t.nobs + kMalaTileRows - 1) / kMalaTileRows;
+    std::vector<double> X(tiles * kMalaTileRows * (size_t)D, 0.0), y(tiles * kMalaTileRows, 0.0);
+    std::copy(t.obs.begin(), t.obs.end(), X.begin());
+    std::copy(t.labels.begin(), t.labels.end(), y.begin());
+    if (h->d_X) (void)hipFree(h->d_X);
+    if (h->d_y) (void)hipFree(h->d_y);
+    h->d_X = h->d_y = nullptr;
+    HIPCHK(h, hipMalloc(&h->d_X, X.size() * sizeof(double)));
+    HIPCHK(h, hipMalloc(&h->d_y, y.size() * sizeof(double)));
+    HIPCHK(h, hipMemcpy(h->d_X, X.data(), X.size() * sizeof(double), hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemcpy(h->d_y, y.data(), y.size() * sizeof(double), hipMemcpyHostToDevice));
+    h->mala_tiles = (uint32_t)tiles;
+    h->grad_valid = false;
+    h->lds_bytes = 0;
+    h->var = v;
+    return EMCMC_OK;
+}
+
 emcmc_status select_variant(emcmc_handle *h) {
     if (!h->target_set || h->updates.empty()) return EMCMC_OK;
+    for (const auto &u : h->updates)
+        if (u.kernel == EMCMC_MALA) return select_mala(h);
+    if (h->target.kind == EMCMC_TARGET_LOGISTIC)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "the logistic-regression target runs on device with MALA only");
     if (mix_path(h)) return select_mix(h);
     for (const auto &u : h->updates)
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX)
@@ -751,6 +810,75 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     return EMCMC_OK;
 }
 
+// MALA: one launch per MCMC step (the X stream dominates; launch cost is
+// negligible); ∇ℓ(θinit) is evaluated by the MODE-1 kernel before the first step.
+emcmc_status run_mala(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps) {
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    const UpdateHost &u = h->updates[0];
+    const TargetHost &t = h->target;
+    MalaParams p{};
+    p.theta = h->d_theta;
+    p.grad = h->d_grad;
+    p.ll = h->d_ll;
+    p.ra = h->d_ra;
+    p.ring = h->d_ring;
+    p.nacc = h->d_nacc;
+    p.faults = h->d_faults;
+    p.hist_theta = h->d_hist_theta;
+    p.hist_prop = h->d_hist_prop;
+    p.hist_ll = h->d_hist_ll;
+    p.hist_acc = h->d_hist_acc;
+    p.zig = h->d_zig;
+    p.X = h->d_X;
+    p.y = h->d_y;
+    p.C = C;
+    p.row_bytes = h->row_bytes;
+    p.nrows = t.nobs;
+    p.ntiles = h->mala_tiles;
+    p.chain0 = (uint32_t)h->cfg.first_chain_id;
+    p.key0 = (uint32_t)h->cfg.seed;
+    p.key1 = (uint32_t)(h->cfg.seed >> 32);
+    p.W = h->cfg.roll_window;
+    const double eps = u.eps[0];
+    p.eps = eps;
+    p.h = (eps * eps) / 2.0;
+    p.ieps = 1.0 / eps;
+    {  // MvNormal(m, ϵ²I): logdet = dd + dd, dd = Σ_d log ϵ
+        double dd = 0.0;
+        for (uint64_t d = 0; d < D; ++d) dd = dd + log_pos(eps);
+        p.c0 = mvnormal_c0((int)D, dd + dd);
+    }
+    p.rcp_W = 1.0 / (double)h->cfg.roll_window;
+    const dim3 block(256), grid((unsigned)((C + kMalaChainsPerWG - 1) / kMalaChainsPerWG));
+    if (!h->grad_valid) {
+        void *args[] = {&p};
+        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.ainit), grid, block, args, 0, h->stream));
+        h->grad_valid = true;
+    }
+    for (uint64_t i = 0; i < num_steps; ++i) {
+        p.iter = steps[i].mcmciter;
+        p.N0 = h->stats_N;
+        if (p.iter > 1 && h->last_iter[0] != p.iter - 1)  // rolling_ar[iter−1] never written → 0.0
+            HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
+        h->last_iter[0] = p.iter;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->timing) {
+            e0 = get_event(h);
+            e1 = get_event(h);
+            HIPCHK(h, hipEventRecord(e0, h->stream));
+        }
+        void *args[] = {&p};
+        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.afn), grid, block, args, 0, h->stream));
+        if (h->timing) {
+            HIPCHK(h, hipEventRecord(e1, h->stream));
+            h->ev.emplace_back(e0, e1);
+            h->pending_bytes += bytes_per_launch(h, 1);
+        }
+        h->stats_N += 1;
+    }
+    return EMCMC_OK;
+}
+
 // General schedule: the step list goes to HBM (4 u32 per step, read by the
 // kernel with scalar loads) and runs in launches of ≤ K steps in schedule order.
 emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps) {
@@ -888,7 +1016,8 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
         for (uint32_t j = 0; j < i; ++j)
             if (u->coords[j] == u->coords[i]) return fail(h, EMCMC_INVALID_ARG, "repeated coord %u", u->coords[i]);
     }
-    if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN_MIX)
+    if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN_MIX &&
+        u->kernel != EMCMC_MALA)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "transition kernel %u has no device plugin yet", u->kernel);
     if (u->prior != EMCMC_PRIOR_IMPROPER)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin yet", u->prior);
@@ -934,6 +1063,10 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
                 uh.haario = *ad;
             }
         }
+    } else if (u->kernel == EMCMC_MALA) {
+        if (!u->epsilon || !(u->epsilon[0] > 0.0)) return fail(h, EMCMC_INVALID_ARG, "MALA needs a step size ϵ > 0");
+        if (u->adaptation != EMCMC_ADPT_NONE) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA adaptation");
+        uh.eps.assign(1, u->epsilon[0]);
     } else {
         if (!u->epsilon) return fail(h, EMCMC_INVALID_ARG, "UniformRandomWalk needs ϵ");
         uh.eps.assign(u->epsilon, u->epsilon + n);
@@ -952,8 +1085,23 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
 
 emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t) {
     if (!h || !t) return EMCMC_INVALID_ARG;
-    if (t->kind != EMCMC_TARGET_GSN) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "target kind %u", t->kind);
+    if (t->kind != EMCMC_TARGET_GSN && t->kind != EMCMC_TARGET_LOGISTIC)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "target kind %u", t->kind);
     const uint32_t d = t->dim;
+    if (t->kind == EMCMC_TARGET_LOGISTIC) {
+        if (d != h->cfg.dim) return fail(h, EMCMC_INVALID_ARG, "logistic target: dim must equal D");
+        if (!t->obs || !t->labels || t->num_obs == 0) return fail(h, EMCMC_INVALID_ARG, "logistic target needs X and y");
+        TargetHost th;
+        th.kind = EMCMC_TARGET_LOGISTIC;
+        th.dim = d;
+        th.nobs = t->num_obs;
+        th.obs.assign(t->obs, t->obs + t->num_obs * d);
+        th.labels.assign(t->labels, t->labels + t->num_obs);
+        h->target = std::move(th);
+        h->target_set = true;
+        h->grad_valid = false;
+        return select_variant(h);
+    }
     if (d != h->cfg.dim)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device GsnTargetLaw needs state = μ (d=%u, D=%u)", d, h->cfg.dim);
     if (!t->mu || !t->sigma || (t->num_obs && !t->obs)) return fail(h, EMCMC_INVALID_ARG, "null target arrays");
@@ -1051,6 +1199,7 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     h->mix_M = 0;
+    h->grad_valid = false;
     h->stats_N = 1;
     h->last_iter.assign(P, 0u);
     return EMCMC_OK;
@@ -1060,7 +1209,8 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     if (!h || (!steps && num_steps)) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
     if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
-    if (!h->var.fn && !h->var.mfn && !h->var.xfn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
+    if (!h->var.fn && !h->var.mfn && !h->var.xfn && !h->var.afn)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
     if (!h->d_zig) return fail(h, EMCMC_STATE_ERROR, "state not allocated");
     const uint32_t P = (uint32_t)h->updates.size();
     for (uint64_t i = 0; i < num_steps; ++i) {
@@ -1071,6 +1221,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     }
     if (h->var.mfn) return run_mwg(h, steps, num_steps);
     if (h->var.xfn) return run_mix(h, steps, num_steps);
+    if (h->var.afn) return run_mala(h, steps, num_steps);
     const uint64_t C = h->cfg.num_chains;
     const int lpc = h->var.lpc;
     const uint64_t threads = C * (uint64_t)lpc;
@@ -1167,7 +1318,8 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_hist_theta, h->d_hist_prop, h->d_hist_ll, h->d_hist_acc, h->d_consts, h->d_obs,
                     h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
-                    h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew};
+                    h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
+                    h->d_grad,      h->d_X,         h->d_y};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);

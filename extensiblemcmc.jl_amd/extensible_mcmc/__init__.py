@@ -15,7 +15,7 @@ from .kernels import (AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMi
 from .mcmc import (MCMC, GenericMCMCBackend, MI355XBackend, MI355XGlobalWorkspace, MI355XLocalWorkspace,
                    create_workspaces, get_decorators, init, run, run_)
 from .schedule import JRange, MCMCSchedule, Step, reschedule, reschedule_
-from .targets import GsnTargetLaw, make_data
+from .targets import GsnTargetLaw, LogisticRegressionLaw, make_data
 from ._lib import EMCMCError, device_count
 
 __all__ = [
@@ -23,5 +23,5 @@ __all__ = [
     "HaarioTypeAdaptation", "NoAdaptation", "RandomWalkUpdate", "GenericMCMCBackend", "MI355XBackend",
     "GsnTargetLaw", "run", "run_", "get_decorators", "isdecorator", "ImproperPosPrior", "ImproperPrior",
     "SavingCallback", "REPLCallback", "MCMCSchedule", "JRange", "reschedule", "Engine", "EngineConfig",
-    "EMCMCError", "device_count", "rhat_from_sums", "allreduce_sums",
+    "EMCMCError", "device_count", "rhat_from_sums", "allreduce_sums", "MALAUpdate", "LogisticRegressionLaw",
 ]

@@ -37,10 +37,10 @@ STATUS_NAMES = {
     8: "EMCMC_STATE_ERROR",
 }
 
-RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX = 1, 2, 3
+RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA = 1, 2, 3, 4
 PRIOR_IMPROPER, PRIOR_IMPROPER_POS = 0, 1
 ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO = 0, 1, 2
-TARGET_GSN = 1
+TARGET_GSN, TARGET_LOGISTIC = 1, 2
 LL_PER_OBS, LL_SUFFSTAT = 0, 1
 HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
 H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
@@ -120,6 +120,7 @@ class EmcmcTargetDesc(C.Structure):
         ("obs", C.POINTER(C.c_double)),
         ("ll_mode", C.c_uint32),
         ("reserved", C.c_uint32),
+        ("labels", C.POINTER(C.c_double)),
     ]
 
 

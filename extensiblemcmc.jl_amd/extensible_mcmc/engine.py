@@ -139,6 +139,32 @@ class Engine:
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
 
+    def add_mala_update(self, coords0, eps, prior=L.PRIOR_IMPROPER):
+        """MALA with step size ϵ on coords0 (0-based; the engine's definition of
+        the reference's stub MALAUpdate, updates.jl:216-218)."""
+        coords = np.ascontiguousarray(coords0, dtype=np.uint32)
+        e = np.array([float(eps)])
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.MALA
+        u.prior = prior
+        u.num_coords = len(coords)
+        u.coords = L.u32ptr(coords)
+        u.epsilon = L.dptr(e)
+        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
+        self.num_updates += 1
+
+    def set_logistic_target(self, X, y):
+        """Logistic regression: ℓ(θ) = Σ_n y_n x_nᵀθ − log(1 + exp(x_nᵀθ))."""
+        X = np.ascontiguousarray(X, dtype=np.float64)
+        yv = np.ascontiguousarray(y, dtype=np.float64).reshape(X.shape[0])
+        t = L.EmcmcTargetDesc()
+        t.kind = L.TARGET_LOGISTIC
+        t.dim = X.shape[1]
+        t.num_obs = X.shape[0]
+        t.obs = L.dptr(X)
+        t.labels = L.dptr(yv)
+        self._check(self._lib.emcmc_set_target(self._h, C.byref(t)), "emcmc_set_target")
+
     def add_update_desc(self, u: L.EmcmcUpdateDesc, keepalive=()):
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1

@@ -383,8 +383,29 @@ class RandomWalkUpdate(MCMCParamUpdate):
                 self.adpt.proposed_chains, self.adpt.accepted_chains = pr, ac
 
 
+@dataclass
 class MALAUpdate(MCMCGradientBasedUpdate):
-    """Stub in the reference (updates.jl:216-218)."""
+    """``MALAUpdate`` — a stub in the reference (updates.jl:216-218, "✗" at
+    updates.jl:7) whose hook is ``compute_gradients_and_momenta!`` (run.jl:110,
+    259).  The engine's definition: θ° = θ + (ϵ²/2)∇ℓ(θ) + ϵz with the MvNormal
+    transition density both ways and the reference's accept_reject!
+    (DESIGN.md §2).  Device plugin: the logistic-regression target."""
+
+    eps: float
+    coords: Sequence[int]
+    prior: Prior = field(default_factory=ImproperPrior)
+    adpt: Adaptation = field(default_factory=NoAdaptation)
+
+    def __post_init__(self):
+        self.coords = [int(c) for c in np.atleast_1d(self.coords)]
+        assert self.eps > 0.0
+
+    def to_device(self, engine):
+        if not isinstance(self.prior, ImproperPrior):
+            raise UnsupportedPlugin(f"prior {type(self.prior).__name__} has no device plugin yet")
+        if not isinstance(self.adpt, NoAdaptation):
+            raise UnsupportedPlugin("MALA step-size adaptation has no device plugin yet")
+        engine.add_mala_update(np.asarray(self.coords, dtype=np.int64) - 1, self.eps, prior=L.PRIOR_IMPROPER)
 
 
 class HamiltonianMCUpdate(MCMCGradientBasedUpdate):

@@ -39,6 +39,25 @@ class GsnTargetLaw:
         engine.set_gsn_target(self.mu, self.Sigma, obs, ll_mode=ll_mode)
 
 
+class LogisticRegressionLaw:
+    """Logistic regression ``ℓ(θ) = Σ_n y_n x_nᵀθ − log(1 + exp(x_nᵀθ))`` with
+    ``obs = (X, y)``: the target of BASELINE cfg 3 (MALA, N = 1e5, D = 64).  It
+    has no counterpart in the reference beyond its target-law interface
+    (``set_parameters!`` + ``loglikelihood(P, obs)``, gsn_target.jl:15-29)."""
+
+    def __init__(self, d):
+        self.d = int(d)
+        self.theta = np.zeros(self.d)
+
+    def set_parameters(self, loc2glob_idx, theta):
+        idx = np.asarray(loc2glob_idx, dtype=int) - 1
+        self.theta[idx] = theta
+
+    def to_device(self, engine, ll_mode, obs):
+        X, y = obs
+        engine.set_logistic_target(X, y)
+
+
 def make_data(P, obs):
     """The ``data = (P = …, obs = …)`` NamedTuple of the reference (basic_use.md:112)."""
     return {"P": P, "obs": np.asarray(obs, dtype=float)}

@@ -10,6 +10,7 @@ cfg4  131,072 chains of cfg2's target with GaussianRandomWalkMix(œÉ¬≤I, œÉ¬≤I, Œ
       mean/cov on device (k = 200 rather than the constructor default 100: with
       fewer than ~D accepted moves per window the empirical covariance is
       rank-deficient and cholesky throws PosDefException in the reference)
+cfg3  32,768 MALA chains on a logistic-regression target, N = 100,000 observations, D = 64
 cfg5  cfg2 with 1,048,576 chains sharded over GPUs, overdispersed Œ∏init
 There is no network: observations are drawn from fixed numpy seeds.
 """
@@ -61,6 +62,38 @@ def cfg4(num_chains: int = 1 << 17, D: int = 32, nobs: int = 10, lam: float = 0.
     w.lam = lam
     w.haario_k = k
     return w
+
+
+@dataclass
+class LogisticWorkload:
+    name: str
+    D: int
+    num_chains: int
+    X: np.ndarray       # [N][D]
+    y: np.ndarray       # [N] in {0, 1}
+    theta_true: np.ndarray
+    eps: float
+    seed: int = SEED
+
+    @property
+    def nobs(self):
+        return self.X.shape[0]
+
+
+def cfg3(num_chains: int = 1 << 15, D: int = 64, nobs: int = 100_000, eps: float = None) -> LogisticWorkload:
+    """BASELINE cfg 3: MALA on a logistic-regression log-likelihood, N = 1e5, D = 64.
+    X ~ N(0, 1/D) entries, Œ∏* ~ N(0, 1), y ~ Bernoulli(œÉ(XŒ∏*)).  œµ defaults to
+    0.045 at the cfg 3 shape (‚âà 61 % acceptance, measured with the oracle; the
+    MALA optimum is ‚âà 57 %), scaled as œµ ‚àù ‚àö(D/N)¬∑D^{-1/6} for other shapes."""
+    rng = np.random.default_rng(OBS_SEED + 3)
+    X = rng.standard_normal((nobs, D)) / np.sqrt(D)
+    theta = rng.standard_normal(D)
+    p = 1.0 / (1.0 + np.exp(-(X @ theta)))
+    y = (rng.random(nobs) < p).astype(np.float64)
+    if eps is None:
+        eps = 0.045 * np.sqrt((D / 64.0) * (100_000.0 / nobs)) * (D / 64.0) ** (-1.0 / 6.0)
+    return LogisticWorkload(name=f"mala_logistic_d{D}_n{nobs}_c{num_chains}", D=D, num_chains=num_chains, X=X, y=y,
+                            theta_true=theta, eps=float(eps))
 
 
 def cfg5(num_chains: int = 1 << 20, D: int = 32, nobs: int = 10) -> GsnWorkload:

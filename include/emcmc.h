@@ -58,6 +58,8 @@ typedef enum emcmc_status {
 #define EMCMC_RW_UNIFORM 1u       /* UniformRandomWalk        random_walk.jl:45-94  */
 #define EMCMC_RW_GAUSSIAN 2u      /* GaussianRandomWalk       random_walk.jl:123-171 */
 #define EMCMC_RW_GAUSSIAN_MIX 3u  /* GaussianRandomWalkMix    random_walk.jl:193-232 */
+#define EMCMC_MALA 4u             /* MALAUpdate: a stub in the reference (updates.jl:216-218); the engine's
+                                     definition is in DESIGN.md §2.  epsilon[0] = step size ϵ. */
 
 /* Priors — src/priors.jl */
 #define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior    priors.jl:18-19 */
@@ -70,6 +72,7 @@ typedef enum emcmc_status {
 
 /* Targets — src/example/gsn_target.jl */
 #define EMCMC_TARGET_GSN 1u     /* GsnTargetLaw(μ, Σ) with coords ⊆ μ */
+#define EMCMC_TARGET_LOGISTIC 2u /* logistic regression: obs = X (n×d), labels = y (n), ℓ = Σ y·η − log(1+e^η) */
 
 /* How the Gaussian log-likelihood Σ_k logpdf(N(μ,Σ), x_k) is evaluated. */
 #define EMCMC_LL_PER_OBS 0u   /* literal gsn_target.jl:23-29: one sqmahal per observation */
@@ -177,14 +180,15 @@ typedef struct emcmc_update_desc {
 /* `data = (P = GsnTargetLaw(μ, Σ), obs = [x_1, …, x_n])` (src/example/gsn_target.jl:1-29,
  * docs/src/get_started/basic_use.md:112). */
 typedef struct emcmc_target_desc {
-    uint32_t kind;        /* EMCMC_TARGET_GSN */
+    uint32_t kind;        /* EMCMC_TARGET_GSN or EMCMC_TARGET_LOGISTIC (the MALA update's target) */
     uint32_t dim;         /* d = length(μ) */
     const double *mu;     /* μ at construction: P.θ[1:d] */
     const double *sigma;  /* Σ: d×d column-major (upper triangle read) */
     uint64_t num_obs;     /* n */
     const double *obs;    /* n×d row-major: obs[k*d + i] = x_k[i] */
-    uint32_t ll_mode;     /* EMCMC_LL_* */
+    uint32_t ll_mode;     /* EMCMC_LL_* (GSN) */
     uint32_t reserved;
+    const double *labels; /* EMCMC_TARGET_LOGISTIC: y, n doubles (0/1 or any real) */
 } emcmc_target_desc;
 
 /* One element of the `MCMCSchedule` iteration (src/schedule.jl:56-66). */

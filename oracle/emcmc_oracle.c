@@ -855,3 +855,160 @@ ORC_EXPORT int orc_run_mix(int D, uint64_t C, uint32_t chain0, uint64_t seed, co
     free(g);
     return 0;
 }
+
+/* ---- MALA on a logistic-regression target (row f2, BASELINE cfg 3) ----------
+ *
+ * The reference stubs MALAUpdate (updates.jl:216-218, "✗" at updates.jl:7) and
+ * provides the hook a gradient-based update uses: compute_gradients_and_momenta!
+ * on the current state (run.jl:110, __PREVIOUS) and on the proposal (run.jl:259,
+ * __PROPOSAL).  No reference numbers exist ("parity unpinned" against the
+ * reference): this is the engine's definition, checked against the literal numpy
+ * restatement (oracle/literal.py run_mala_chain).
+ *   target     ℓ(θ) = Σ_n [y_n η_n − log(1 + e^{η_n})], η = Xθ; ∇ℓ = Xᵀ(y − σ(η))
+ *   proposal   m = θ + h∇ℓ(θ), θ° = m + ϵz, h = ϵ²/2, z ~ N(0, I)
+ *   transition logpdf(MvNormal(m, ϵ²I), θ°) and back with m° = θ° + h∇ℓ(θ°)
+ *   accept     the reference's left-associative llr, E ~ Exp(1) > −llr (run.jl:268-281)
+ * ∇ℓ is carried with the state like ll (the __PREVIOUS hook's value is the
+ * gradient of the current state); it is evaluated once at θinit.
+ * Evaluation orders (the device's, see emcmc_mala.h):
+ *   η_n   = fma chain over d = 0..D−1 from 0.0 (v_mfma_f64_16x16x4f64 is an fma
+ *           chain over its k, scripts/ubench/mfma_f64_probe.hip)
+ *   ∇ℓ_d  = fma chain over n = 0..N−1 from 0.0
+ *   ℓ     = (S_0 + S_1) + (S_2 + S_3), S_g = Σ_{n ≡ g mod 4} ℓ_n in increasing n
+ *   ‖v‖²  = (s_0 + s_1) + (s_2 + s_3), s_g = v_g² then fma over d ≡ g mod 4 ascending
+ *   softplus(η) = max(η, 0) + log1p(e^{−|η|}), σ(η) = 1/(1+t) (η ≥ 0) or t/(1+t), t = e^{−|η|},
+ *   log1p(t) = t if 1 + t == 1 else log(1+t)·(t/((1+t)−1)).
+ */
+static inline double orc_log1p01(double t) {
+    const double u = 1.0 + t;
+    if (u == 1.0) return t;
+    return orc_log(u) * (t / (u - 1.0));
+}
+
+static inline void orc_logistic_terms(double eta, double y, double *ell, double *r) {
+    const double t = orc_exp_any(-fabs(eta));
+    const double sp = (eta > 0.0 ? eta : 0.0) + orc_log1p01(t);
+    const double d = 1.0 + t;
+    const double sig = (eta >= 0.0) ? 1.0 / d : t / d;
+    *ell = y * eta - sp;
+    *r = y - sig;
+}
+
+static double orc_sq4(const double *v, int D) {
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int g = 0; g < 4 && g < D; ++g) {
+        s[g] = v[g] * v[g];
+        for (int d = g + 4; d < D; d += 4) s[g] = fma(v[d], v[d], s[g]);
+    }
+    return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+static void orc_logistic_eval(const double *X, const double *y, uint64_t N, int D, const double *th, double *ll,
+                              double *G) {
+    double S[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int d = 0; d < D; ++d) G[d] = 0.0;
+    for (uint64_t n = 0; n < N; ++n) {
+        const double *x = X + n * (uint64_t)D;
+        double eta = 0.0;
+        for (int d = 0; d < D; ++d) eta = fma(x[d], th[d], eta);
+        double ell, r;
+        orc_logistic_terms(eta, y[n], &ell, &r);
+        S[n & 3] = S[n & 3] + ell;
+        for (int d = 0; d < D; ++d) G[d] = fma(x[d], r, G[d]);
+    }
+    *ll = (S[0] + S[1]) + (S[2] + S[3]);
+}
+
+/* ℓ and ∇ℓ at theta [C][D] → ll [C] (may be NULL), grad [C][D]. */
+ORC_EXPORT void orc_logistic_eval_batch(int D, uint64_t C, const double *X, const double *y, uint64_t N,
+                                        const double *theta, double *ll, double *grad, int nthreads) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(static) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t c = 0; c < (int64_t)C; ++c) {
+        double l;
+        orc_logistic_eval(X, y, N, D, theta + (uint64_t)c * D, &l, grad + (uint64_t)c * D);
+        if (ll) ll[c] = l;
+    }
+    (void)nthreads;
+}
+
+ORC_EXPORT int orc_run_mala(int D, uint64_t C, uint32_t chain0, uint64_t seed, double eps, const double *X,
+                            const double *y, uint64_t N, uint32_t W, uint32_t iter0, uint32_t nsteps, uint64_t N0,
+                            double *theta, double *grad, double *ll, double *ra, uint64_t *ring, uint32_t *nacc,
+                            uint32_t *faults, double *hist_theta, double *hist_prop, double *hist_ll,
+                            uint8_t *hist_acc, int nthreads) {
+    if (D < 1 || D > 64 || !(eps > 0.0)) return -2;
+    (void)zig();
+    const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+    const orc_zig_tables *zt = zig();
+    const double h = (eps * eps) / 2.0, ie = 1.0 / eps;
+    double dd = 0.0;
+    for (int d = 0; d < D; ++d) dd = dd + orc_log(eps);
+    const double c0 = mvnormal_c0(D, dd + dd);
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads > 0 ? nthreads : 1)
+#endif
+    for (int64_t ci = 0; ci < (int64_t)C; ++ci) {
+        const uint64_t c = (uint64_t)ci;
+        const uint32_t gid = chain0 + (uint32_t)c;
+        double th[64], g[64], tp[64], gp[64], m[64], v[64];
+        memcpy(th, theta + c * D, sizeof(double) * D);
+        memcpy(g, grad + c * D, sizeof(double) * D);
+        double cll = ll[c], cra = ra[c];
+        uint64_t ring0 = ring[2 * c], ring1 = ring[2 * c + 1];
+        uint32_t na = nacc[c], f = faults[c];
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            const uint32_t iter = iter0 + s;
+            for (int d = 0; d < D; ++d) {
+                const double z = orc_normal(zt, k0, k1, gid, iter, 0, (uint32_t)d, &f);
+                m[d] = th[d] + h * g[d];
+                tp[d] = m[d] + eps * z;
+                v[d] = (tp[d] - m[d]) * ie;
+            }
+            const double ltd_fwd = c0 - orc_sq4(v, D) / 2.0;
+            double llp;
+            orc_logistic_eval(X, y, N, D, tp, &llp, gp);
+            for (int d = 0; d < D; ++d) v[d] = (th[d] - (tp[d] + h * gp[d])) * ie;
+            const double ltd_rev = c0 - orc_sq4(v, D) / 2.0;
+            if (!isfinite(llp)) f |= 1u;
+            const double llr = ((((llp - cll) + ltd_rev) - ltd_fwd) + 0.0) - 0.0;
+            const double E = orc_exponential(zt, k0, k1, gid, iter, 0, &f);
+            const int acc = E > -llr;
+            if (hist_prop) memcpy(hist_prop + ((uint64_t)s * C + c) * D, tp, sizeof(double) * D);
+            if (acc) {
+                memcpy(th, tp, sizeof(double) * D);
+                memcpy(g, gp, sizeof(double) * D);
+                cll = llp;
+                na += 1;
+            }
+            if (hist_theta) memcpy(hist_theta + ((uint64_t)s * C + c) * D, th, sizeof(double) * D);
+            if (hist_ll) hist_ll[(uint64_t)s * C + c] = cll;
+            if (hist_acc) hist_acc[(uint64_t)s * C + c] = (uint8_t)acc;
+            {
+                const uint64_t Nn = N0 + s;
+                int outside = 0;
+                if (iter > W) {
+                    uint32_t j = (iter - W) & 127u;
+                    outside = (int)((((j & 64u) ? ring1 : ring0) >> (j & 63u)) & 1u);
+                }
+                const uint64_t mn = Nn < (uint64_t)W ? Nn : (uint64_t)W;
+                cra = (cra * (double)W + (double)(acc - outside)) / (double)mn;
+                uint32_t j = iter & 127u;
+                uint64_t bit = 1ull << (j & 63u);
+                if (j & 64u) ring1 = acc ? (ring1 | bit) : (ring1 & ~bit);
+                else ring0 = acc ? (ring0 | bit) : (ring0 & ~bit);
+            }
+        }
+        memcpy(theta + c * D, th, sizeof(double) * D);
+        memcpy(grad + c * D, g, sizeof(double) * D);
+        ll[c] = cll;
+        ra[c] = cra;
+        ring[2 * c] = ring0;
+        ring[2 * c + 1] = ring1;
+        nacc[c] = na;
+        faults[c] = f;
+    }
+    (void)nthreads;
+    return 0;
+}

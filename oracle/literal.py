@@ -207,3 +207,48 @@ def run_mix_chain(seed, chain, theta0, sigma_a, sigma_b, lam, t_sigma, obs, nste
         out["ra"].append(ra)
     out["cov"], out["mean"], out["sigma_b"] = cov, mean, SB
     return {k: (np.array(v) if isinstance(v, list) else v) for k, v in out.items()}
+
+
+def run_mala_chain(seed, chain, theta0, eps, X, y, nsteps, W=100):
+    """Literal MALA on the logistic target: numpy matrix-vector products,
+    np.logaddexp softplus, MvNormal(m, ϵ²I) logpdf via mvnormal_logpdf."""
+    X = np.asarray(X, dtype=float)
+    y = np.asarray(y, dtype=float)
+    D = X.shape[1]
+    h = eps * eps / 2.0
+    L = eps * np.eye(D)
+
+    def ell_grad(th):
+        eta = X @ th
+        ll = float(np.sum(y * eta - np.logaddexp(0.0, eta)))
+        sig = 0.5 * (1.0 + np.tanh(0.5 * eta))
+        return ll, X.T @ (y - sig)
+
+    th = np.array(theta0, dtype=float)
+    _, g = ell_grad(th)
+    ll = -np.inf
+    ra, N = 0.0, 1
+    acc_hist = {}
+    out = {"theta": [], "prop": [], "ll": [], "acc": [], "ra": []}
+    for s in range(nsteps):
+        it = 1 + s
+        z, E, _ = _oracle.step_variates(seed, chain, it, D)
+        m = th + h * g
+        tp = m + eps * z
+        llp, gp = ell_grad(tp)
+        ltd_fwd = mvnormal_logpdf(tp, m, L)
+        ltd_rev = mvnormal_logpdf(th, tp + h * gp, L)
+        llr = llp - ll + ltd_rev - ltd_fwd + 0.0 - 0.0
+        acc = bool(E > -llr)
+        if acc:
+            th, ll, g = tp, llp, gp
+        acc_hist[it] = acc
+        outside = acc_hist.get(it - W, False) if it > W else False
+        ra = (ra * W + (int(acc) - int(outside))) / min(W, N)
+        N += 1
+        out["theta"].append(th.copy())
+        out["prop"].append(tp.copy())
+        out["ll"].append(ll)
+        out["acc"].append(acc)
+        out["ra"].append(ra)
+    return {k: np.array(v) for k, v in out.items()}

@@ -393,3 +393,64 @@ def pick_uniform(seed, chain, it):
     """The [0,1) uniform that picks GaussianRandomWalkMix's kernel (B iff u ≤ λ)."""
     r = philox([chain, it, 0xFFFFFFFE, 0], [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
     return float((int(r[0]) << 21) | (int(r[1]) >> 11)) * 2.0 ** -53
+
+
+# ---- MALA on a logistic-regression target (row f2, cfg 3) -------------------
+def _mala_sigs(L):
+    if not hasattr(L, "_mala_ready"):
+        dp, u32p, u64p, u8p = (C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
+                               C.POINTER(C.c_uint8))
+        L.orc_logistic_eval_batch.restype = None
+        L.orc_logistic_eval_batch.argtypes = [C.c_int, C.c_uint64, dp, dp, C.c_uint64, dp, dp, dp, C.c_int]
+        L.orc_run_mala.restype = C.c_int
+        L.orc_run_mala.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_double, dp, dp, C.c_uint64,
+                                   C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64, dp, dp, dp, dp, u64p, u32p, u32p,
+                                   dp, dp, dp, u8p, C.c_int]
+        L._mala_ready = True
+
+
+def logistic_eval(X, y, theta, nthreads=1):
+    """ℓ [C] and ∇ℓ [C][D] at theta [C][D] (the engine's evaluation order)."""
+    L = lib()
+    _mala_sigs(L)
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    th = np.ascontiguousarray(np.atleast_2d(theta), dtype=np.float64)
+    Cn, D = th.shape
+    ll = np.empty(Cn)
+    g = np.empty((Cn, D))
+    L.orc_logistic_eval_batch(D, Cn, _d(X), _d(y), X.shape[0], _d(th), _d(ll), _d(g), nthreads)
+    return ll, g
+
+
+class MALAState(OracleState):
+    """OracleState plus the carried gradient ∇ℓ(θ), evaluated at θinit."""
+
+    def __init__(self, theta, X, y, ll=None, nthreads=1):
+        super().__init__(theta, ll)
+        _, self.grad = logistic_eval(X, y, self.theta, nthreads)
+
+
+def run_mala(state: MALAState, *, seed, eps, X, y, iter0, nsteps, chain0=0, W=100, history=True, nthreads=1):
+    L = lib()
+    _mala_sigs(L)
+    Cn, D = state.C, state.D
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    hist = alloc_history(Cn, D, nsteps) if history else {}
+    if iter0 > 1 and state.last_iter != iter0 - 1:
+        state.ra[:] = 0.0
+    rc = L.orc_run_mala(D, Cn, chain0, seed & 0xFFFFFFFFFFFFFFFF, float(eps), _d(X), _d(y), X.shape[0], W, iter0,
+                        nsteps, state.N, _d(state.theta), _d(state.grad), _d(state.ll), _d(state.ra),
+                        state.ring.ctypes.data_as(C.POINTER(C.c_uint64)),
+                        state.nacc.ctypes.data_as(C.POINTER(C.c_uint32)),
+                        state.faults.ctypes.data_as(C.POINTER(C.c_uint32)), _d(hist.get("theta")),
+                        _d(hist.get("prop")), _d(hist.get("ll")),
+                        None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads)
+    if rc != 0:
+        raise ValueError(f"orc_run_mala failed: {rc}")
+    state.N += nsteps
+    state.last_iter = iter0 + nsteps - 1
+    if history:
+        hist["acc"] = hist["acc"].astype(bool)
+    return hist

@@ -4,6 +4,8 @@
 --workload cfg4 measures BASELINE cfg 4 instead: GaussianRandomWalkMix +
 HaarioTypeAdaptation with the per-chain running mean/cov kept on device
 (131,072 chains by default); same metric and JSON contract.
+--workload cfg3 measures BASELINE cfg 3: MALA on a logistic-regression
+log-likelihood (N = 100,000, D = 64, 32,768 chains), fp64 MFMA-bound.
 
 One "step" = one MCMC iteration of every chain on every GPU: proposal,
 log-prior, log-likelihood, MH accept/reject, rolling acceptance and the full
@@ -32,6 +34,7 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "extensiblemcmc.jl_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (AMD spec; equal to the FP64 vector peak)
 
 
 def parse():
@@ -39,8 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--workload", choices=["cfg2", "cfg4"], default="cfg2")
-    ap.add_argument("--chains-per-gpu", type=int, default=0, help="0: 65,536 (cfg2) / 131,072 (cfg4)")
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2")
+    ap.add_argument("--chains-per-gpu", type=int, default=0,
+                    help="0: 65,536 (cfg2) / 32,768 (cfg3) / 131,072 (cfg4)")
     ap.add_argument("--haario-k", type=int, default=200)
     ap.add_argument("--history", choices=["full", "accept_only"], default="full")
     ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
@@ -61,8 +65,15 @@ def cpu_baseline(w, seconds, ll_mode):
     threads = max(1, min(threads, 16))
     C = 256 * threads
     chunk = 50
-    mix = w.haario_k is not None
-    if mix:
+    mix = getattr(w, "haario_k", None) is not None
+    if hasattr(w, "X"):  # cfg 3: MALA on the logistic target
+        C = threads
+        chunk = 2
+        st = O.MALAState(np.zeros((C, w.D)), w.X, w.y, nthreads=threads)
+
+        def step(it):
+            O.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=it, nsteps=chunk, nthreads=threads)
+    elif mix:
         st = O.MixState(np.zeros((C, w.D)), sigma_b=w.sigma_b)
 
         def step(it):
@@ -85,6 +96,10 @@ def cpu_baseline(w, seconds, ll_mode):
         it += chunk
         steps += chunk
     dt = time.perf_counter() - t0
+    if hasattr(w, "X"):
+        return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
+                "sample": f"{C} chains x {steps} iterations of the same MALA logistic workload (N={w.nobs}, "
+                          f"D={w.D}), oracle/liboracle.so, {dt:.1f} s"}
     what = ("GaussianRandomWalkMix + HaarioTypeAdaptation(k=%d) + chain mean/cov" % w.haario_k) if mix else "RWM"
     return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
             "sample": f"{C} chains x {steps} iterations of the same D=32 {what} workload ({w.nobs} obs, "
@@ -111,19 +126,24 @@ def main():
     from extensible_mcmc.engine import Engine, EngineConfig
 
     cfg4 = a.workload == "cfg4"
-    Cg = a.chains_per_gpu or (131072 if cfg4 else 65536)
-    w = W.cfg4(Cg, k=a.haario_k) if cfg4 else W.cfg2(Cg)
+    cfg3 = a.workload == "cfg3"
+    Cg = a.chains_per_gpu or (131072 if cfg4 else 32768 if cfg3 else 65536)
+    w = W.cfg4(Cg, k=a.haario_k) if cfg4 else W.cfg3(Cg) if cfg3 else W.cfg2(Cg)
     ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
     hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
     M = a.warmup + a.steps * a.reps
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=rank * Cg,
                               device=local, history_mode=hist, lanes_per_chain=a.lpc,
                               steps_per_launch=a.steps_per_launch))
-    if cfg4:
+    if cfg3:
+        eng.add_mala_update(np.arange(w.D), w.eps)
+        eng.set_logistic_target(w.X, w.y)
+    elif cfg4:
         eng.add_gaussian_rw_mix_update(np.arange(w.D), w.rw_sigma, w.sigma_b, lam=w.lam, haario_k=w.haario_k)
     else:
         eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
-    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
+    if not cfg3:
+        eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
     eng.set_state(np.zeros((Cg, w.D)))
     if a.warmup:
         eng.run_iters(1, a.warmup)
@@ -202,9 +222,13 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (GsnTargetLaw(μ*, I32), 10 obs from numpy default_rng(20261015)), θinit = 0",
+        "data": ("synthetic (X ~ N(0, 1/D), θ* ~ N(0, I), y ~ Bernoulli(σ(Xθ*)), numpy default_rng(20261018)), "
+                 "θinit = 0" if cfg3 else
+                 "synthetic (GsnTargetLaw(μ*, I32), 10 obs from numpy default_rng(20261015)), θinit = 0"),
         "config": {
-            "workload": (f"BASELINE cfg 4: {Cg} adaptive RWM chains per GPU (GaussianRandomWalkMix + "
+            "workload": (f"BASELINE cfg 3: {Cg} MALA chains per GPU on a logistic-regression log-likelihood, "
+                         f"N={w.nobs}, D={w.D}, fp64" if cfg3 else
+                         f"BASELINE cfg 4: {Cg} adaptive RWM chains per GPU (GaussianRandomWalkMix + "
                          f"HaarioTypeAdaptation, per-chain running mean/cov on device), D=32 Gaussian target, fp64"
                          if cfg4 else
                          f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64"),
@@ -212,12 +236,14 @@ def main():
             "total_chains": total_chains,
             "dim": w.D,
             "num_obs": w.nobs,
-            "proposal": (f"GaussianRandomWalkMix(σ²I32, σ²I32, λ={w.lam}) + HaarioTypeAdaptation(k={w.haario_k})"
+            "proposal": (f"MALA(ϵ={w.eps:.4g})" if cfg3 else
+                         f"GaussianRandomWalkMix(σ²I32, σ²I32, λ={w.lam}) + HaarioTypeAdaptation(k={w.haario_k})"
                          if cfg4 else "GaussianRandomWalk(σ²I32), σ=2.38/√(D·n)"),
             "prior": "ImproperPrior",
             "history": a.history,
             "ll_mode": a.ll_mode,
-            "chain_stats": ("rolling acceptance + running mean/cov (chain_statistics.jl:41-66)" if cfg4
+            "chain_stats": ("rolling acceptance (chain_statistics.jl:51-65)" if cfg3 else
+                            "rolling acceptance + running mean/cov (chain_statistics.jl:41-66)" if cfg4
                             else "rolling acceptance (chain_statistics.jl:51-65)"),
             "steps_per_launch": a.steps_per_launch,
             "kernel": kname,
@@ -238,11 +264,19 @@ def main():
         },
         "kernel_chain_steps_per_s": Cg * a.steps / (ms / 1e3),
     }
+    if cfg3:  # MFMA-bound: the two contractions, 4·N·D flop per chain-step
+        flops = 4.0 * w.nobs * w.D * Cg * (a.steps / launches)
+        tfs = flops / avg_launch_s / 1e12
+        out["roofline"] = {"bound": "mfma", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
+                           "frac": tfs / FP64_MFMA_PEAK_TFS, "traffic": traffic, "kernel": kname,
+                           "algorithmic_flops_per_launch": flops, "avg_launch_ms": avg_launch_s * 1e3,
+                           "launches": launches, "flops_per_chain_step": 4.0 * w.nobs * w.D}
     if cfg4:
         out["posdef_faulted_chains"] = int(np.count_nonzero(eng.get_faults() & L.FAULT_POSDEF))
     if diag is not None:
-        out["diagnostics"] = {"accept_rate": diag["accept_rate"], "max_split_rhat": float(np.max(diag["rhat"])),
-                              "max_abs_mean_minus_xbar": float(np.max(np.abs(diag["mean"] - w.obs.mean(0))))}
+        out["diagnostics"] = {"accept_rate": diag["accept_rate"], "max_split_rhat": float(np.max(diag["rhat"]))}
+        if not cfg3:
+            out["diagnostics"]["max_abs_mean_minus_xbar"] = float(np.max(np.abs(diag["mean"] - w.obs.mean(0))))
     if world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds, ll_mode)
@@ -270,6 +304,18 @@ def parity_sample(eng, w, a, ll_mode, n=8):
     acc = eng.get_history(L.H_ACCEPT, 1, S)[:, 0]
     theta, ll = eng.get_state()
     ok_acc = ok_th = True
+    if hasattr(w, "X"):  # MALA: replay the first steps of 2 chains (an oracle step costs 4·N·D flop)
+        S = min(S, 20)
+        acc = acc[:S]
+        ok_acc = ok_th = True
+        hist_theta = eng.get_history(L.H_STATE, S, 1)[0, 0]
+        for c in picks[:2]:
+            st = O.MALAState(np.zeros((1, w.D)), w.X, w.y, nthreads=16)
+            h = O.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=1, nsteps=S, chain0=int(c), nthreads=16)
+            ok_acc &= bool(np.array_equal(acc[:, c], h["acc"][:, 0]))
+            ok_th &= bool(np.array_equal(hist_theta[c], st.theta[0]))
+        return {"chains_replayed": 2, "iterations": int(S), "accept_stream_bitwise": ok_acc,
+                "theta_at_last_replayed_iteration_bitwise": ok_th}
     for c in picks:
         if w.haario_k is not None:
             st = O.MixState(np.zeros((1, w.D)), sigma_b=w.sigma_b)

@@ -53,18 +53,16 @@ struct MalaParams {
     double rcp_W;
 };
 
-// log1p(t), t ∈ [0, 1]: t if 1 + t == 1, else log(1+t)·(t/((1+t)−1))
-__device__ __forceinline__ double log1p01(double t) {
-    const double u = 1.0 + t;
-    return (u == 1.0) ? t : log_pos(u) * (t / (u - 1.0));
-}
-
-// ℓ_n = y·η − softplus(η), r_n = y − σ(η)
+// ℓ_n = y·η − softplus(η), r_n = y − σ(η), one division: t = e^{−|η|},
+// u = 1 + t, v = 1/u, log1p(t) = log(u) − ((u − 1) − t)·v (t if u == 1),
+// σ = (η ≥ 0 ? 1 : t)·v
 __device__ __forceinline__ void logistic_terms(double eta, double y, double &ell, double &r) {
     const double t = exp_any(-fabs(eta));
-    const double sp = (eta > 0.0 ? eta : 0.0) + log1p01(t);
-    const double d = 1.0 + t;
-    const double sig = (eta >= 0.0) ? 1.0 / d : t / d;
+    const double u = 1.0 + t;
+    const double v = 1.0 / u;
+    const double lp1 = (u == 1.0) ? t : log_pos(u) - ((u - 1.0) - t) * v;
+    const double sp = (eta > 0.0 ? eta : 0.0) + lp1;
+    const double sig = (eta >= 0.0 ? 1.0 : t) * v;
     ell = y * eta - sp;
     r = y - sig;
 }
@@ -92,31 +90,33 @@ __global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) 
     const uint64_t chain = (uint64_t)blockIdx.x * kMalaChainsPerWG + wave * 16 + cl;
     const bool valid = chain < C;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
-    auto pos = [&](int d) { return state_pos((uint64_t)d, chain, C, (uint32_t)D); };
+    // element (d, chain) of a state_pos array; `ch` is made opaque per phase so
+    // the J addresses are not kept live across the row loop
+    auto pos = [&](int d, uint64_t ch) { return state_pos((uint64_t)d, ch, C, (uint32_t)D); };
 
     // ---- prologue: θ, ∇ℓ(θ) and the proposal (B operand fragments)
-    double th[J], gr[J], tp[J];
+    double tp[J];
     uint32_t faults = valid ? a.faults[chain] : 0u;
-#pragma unroll
-    for (int j = 0; j < J; ++j) {
-        th[j] = valid ? a.theta[pos(4 * j + g)] : 0.0;
-        gr[j] = (valid && MODE == 0) ? a.grad[pos(4 * j + g)] : 0.0;
-    }
     double ltd_fwd = 0.0;
-    if constexpr (MODE == 0) {
+    {
+        uint64_t ch = chain;
+        asm volatile("" : "+v"(ch));
         double s = 0.0;
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const double z = normal_draw(*a.zig, a.key0, a.key1, gid, a.iter, 0, (uint32_t)(4 * j + g), faults);
-            const double m = th[j] + a.h * gr[j];
-            tp[j] = m + a.eps * z;
-            const double v = (tp[j] - m) * a.ieps;
-            s = (j == 0) ? v * v : fma(v, v, s);
+            const double th = valid ? a.theta[pos(4 * j + g, ch)] : 0.0;
+            if constexpr (MODE == 0) {
+                const double gr = valid ? a.grad[pos(4 * j + g, ch)] : 0.0;
+                const double z = normal_draw(*a.zig, a.key0, a.key1, gid, a.iter, 0, (uint32_t)(4 * j + g), faults);
+                const double m = th + a.h * gr;
+                tp[j] = m + a.eps * z;
+                const double v = (tp[j] - m) * a.ieps;
+                s = (j == 0) ? v * v : fma(v, v, s);
+            } else {
+                tp[j] = th;
+            }
         }
-        ltd_fwd = fma(-0.5, quad_sum(s), a.c0);
-    } else {
-#pragma unroll
-        for (int j = 0; j < J; ++j) tp[j] = th[j];
+        if constexpr (MODE == 0) ltd_fwd = fma(-0.5, quad_sum(s), a.c0);
     }
 
     // ---- η = X θ°, ℓ, r, ∇ℓ over all rows
@@ -140,29 +140,38 @@ __global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) 
             if (threadIdx.x < kMalaTileRows) ys[threadIdx.x] = a.y[n0 + threadIdx.x];
         }
         __syncthreads();
+        // two 16-row blocks at a time: two independent η accumulation chains
 #pragma unroll 1
-        for (int b = 0; b < kMalaTileRows / 16; ++b) {
-            const double *xb = xs + (16 * b) * LD;
-            mala_d4 eta = {0.0, 0.0, 0.0, 0.0};
+        for (int b = 0; b < kMalaTileRows / 16; b += 2) {
+            const double *xb0 = xs + (16 * b) * LD, *xb1 = xb0 + 16 * LD;
+            mala_d4 eta0 = {0.0, 0.0, 0.0, 0.0}, eta1 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < J; ++j)
-                eta = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[cl * LD + 4 * j + g], tp[j], eta, 0, 0, 0);
-            double r[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int row = 4 * q + g;
-                double ell, rr;
-                logistic_terms(eta[q], ys[16 * b + row], ell, rr);
-                const bool in = n0 + 16 * b + row < a.nrows;
-                if (in) S = S + ell;
-                r[q] = in ? rr : 0.0;
+            for (int j = 0; j < J; ++j) {
+                eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb0[cl * LD + 4 * j + g], tp[j], eta0, 0, 0, 0);
+                eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb1[cl * LD + 4 * j + g], tp[j], eta1, 0, 0, 0);
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+            for (int h = 0; h < 2; ++h) {
+                const mala_d4 &eta = h ? eta1 : eta0;
+                const double *xb = h ? xb1 : xb0;
+                const int rb = 16 * (b + h);
+                double r[4];
 #pragma unroll
-                for (int e = 0; e < DB; ++e)
-                    G[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[(4 * q + g) * LD + 16 * e + cl], r[q], G[e], 0, 0,
-                                                               0);
+                for (int q = 0; q < 4; ++q) {
+                    const int row = 4 * q + g;
+                    double ell, rr;
+                    logistic_terms(eta[q], ys[rb + row], ell, rr);
+                    const bool in = n0 + rb + row < a.nrows;
+                    if (in) S = S + ell;
+                    r[q] = in ? rr : 0.0;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int e = 0; e < DB; ++e)
+                        G[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[(4 * q + g) * LD + 16 * e + cl], r[q], G[e], 0,
+                                                                   0, 0);
+            }
         }
     }
     // lane's ∇ℓ coordinates: G[e][i] ↔ d = 16e + g + 4i ↔ j = 4e + i
@@ -172,18 +181,22 @@ __global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) 
 #pragma unroll
         for (int i = 0; i < 4; ++i) gp[4 * e + i] = G[e][i];
 
+    uint64_t ch = chain;
+    asm volatile("" : "+v"(ch));
     if constexpr (MODE == 1) {
         if (valid)
 #pragma unroll
-            for (int j = 0; j < J; ++j) a.grad[pos(4 * j + g)] = gp[j];
+            for (int j = 0; j < J; ++j) a.grad[pos(4 * j + g, ch)] = gp[j];
         return;
     }
 
     // ---- epilogue: reverse density, accept/reject, state, statistics, histories
     const double llp = quad_sum(S);
+    double th[J];
     double s = 0.0;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
+        th[j] = valid ? a.theta[pos(4 * j + g, ch)] : 0.0;
         const double v = (th[j] - (tp[j] + a.h * gp[j])) * a.ieps;
         s = (j == 0) ? v * v : fma(v, v, s);
     }
@@ -200,7 +213,7 @@ __global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) 
     if (valid) {
 #pragma unroll
         for (int j = 0; j < J; ++j) {
-            const uint64_t p = pos(4 * j + g);
+            const uint64_t p = pos(4 * j + g, ch);
             if constexpr (FULL) {
                 __builtin_nontemporal_store(tp[j], a.hist_prop + slot * D * C + p);
                 __builtin_nontemporal_store(acc ? tp[j] : th[j], a.hist_theta + slot * D * C + p);

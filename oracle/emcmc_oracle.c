@@ -876,20 +876,17 @@ ORC_EXPORT int orc_run_mix(int D, uint64_t C, uint32_t chain0, uint64_t seed, co
  *   ∇ℓ_d  = fma chain over n = 0..N−1 from 0.0
  *   ℓ     = (S_0 + S_1) + (S_2 + S_3), S_g = Σ_{n ≡ g mod 4} ℓ_n in increasing n
  *   ‖v‖²  = (s_0 + s_1) + (s_2 + s_3), s_g = v_g² then fma over d ≡ g mod 4 ascending
- *   softplus(η) = max(η, 0) + log1p(e^{−|η|}), σ(η) = 1/(1+t) (η ≥ 0) or t/(1+t), t = e^{−|η|},
- *   log1p(t) = t if 1 + t == 1 else log(1+t)·(t/((1+t)−1)).
+ *   t = e^{−|η|}, u = 1 + t, v = 1/u (the one division per element),
+ *   log1p(t) = t if u == 1 else log(u) − ((u − 1) − t)·v,
+ *   softplus(η) = max(η, 0) + log1p(t), σ(η) = (η ≥ 0 ? 1 : t)·v.
  */
-static inline double orc_log1p01(double t) {
-    const double u = 1.0 + t;
-    if (u == 1.0) return t;
-    return orc_log(u) * (t / (u - 1.0));
-}
-
 static inline void orc_logistic_terms(double eta, double y, double *ell, double *r) {
     const double t = orc_exp_any(-fabs(eta));
-    const double sp = (eta > 0.0 ? eta : 0.0) + orc_log1p01(t);
-    const double d = 1.0 + t;
-    const double sig = (eta >= 0.0) ? 1.0 / d : t / d;
+    const double u = 1.0 + t;
+    const double v = 1.0 / u;
+    const double lp1 = (u == 1.0) ? t : orc_log(u) - ((u - 1.0) - t) * v;
+    const double sp = (eta > 0.0 ? eta : 0.0) + lp1;
+    const double sig = (eta >= 0.0 ? 1.0 : t) * v;
     *ell = y * eta - sp;
     *r = y - sig;
 }

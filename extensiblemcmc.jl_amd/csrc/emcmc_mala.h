@@ -27,7 +27,10 @@ namespace emcmc {
 
 typedef double mala_d4 __attribute__((ext_vector_type(4)));
 
-constexpr int kMalaTileRows = 64;     // rows of X per LDS tile
+#ifndef EMCMC_MALA_ABLATE
+#define EMCMC_MALA_ABLATE 0
+#endif
+constexpr int kMalaTileRows = 64;     // rows of X per LDS tile (33.8 KB at D = 64)
 constexpr int kMalaChainsPerWG = 64;  // 4 waves × 16 chains
 
 struct MalaParams {
@@ -77,7 +80,7 @@ __device__ __forceinline__ double quad_sum(double s) {
 
 // MODE 0: one MCMC step; MODE 1: ∇ℓ at the current θ only (initialisation)
 template <int DB, bool FULL, int MODE>
-__global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) {
+__global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams a) {
     constexpr int D = 16 * DB;
     constexpr int J = 4 * DB;        // coordinates per lane
     constexpr int LD = D + 1;        // padded LDS row stride (doubles)
@@ -127,7 +130,7 @@ __global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) 
     for (uint32_t t = 0; t < a.ntiles; ++t) {
         const uint64_t n0 = (uint64_t)t * kMalaTileRows;
         __syncthreads();  // previous tile consumed
-        {
+        if (!(EMCMC_MALA_ABLATE & 2) || t == 0) {  // timing-only ablation 2: reuse the first tile
             const double2 *src = reinterpret_cast<const double2 *>(a.X + n0 * D);
             constexpr int PAIRS = kMalaTileRows * D / 2;
 #pragma unroll
@@ -140,38 +143,49 @@ __global__ void __launch_bounds__(256) mala_logistic_kernel(const MalaParams a) 
             if (threadIdx.x < kMalaTileRows) ys[threadIdx.x] = a.y[n0 + threadIdx.x];
         }
         __syncthreads();
-        // two 16-row blocks at a time: two independent η accumulation chains
-#pragma unroll 1
-        for (int b = 0; b < kMalaTileRows / 16; b += 2) {
-            const double *xb0 = xs + (16 * b) * LD, *xb1 = xb0 + 16 * LD;
-            mala_d4 eta0 = {0.0, 0.0, 0.0, 0.0}, eta1 = {0.0, 0.0, 0.0, 0.0};
+        // 16-row blocks, software-pipelined: the η MFMAs of block b+1 are issued
+        // in the same scheduling region as the elementwise terms of block b, so
+        // the matrix pipe works while the VALU evaluates exp/log/σ (they are
+        // independent); a region holds one block's temporaries.
+        constexpr int NB = kMalaTileRows / 16;
+        mala_d4 en = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int j = 0; j < J; ++j) {
-                eta0 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb0[cl * LD + 4 * j + g], tp[j], eta0, 0, 0, 0);
-                eta1 = __builtin_amdgcn_mfma_f64_16x16x4f64(xb1[cl * LD + 4 * j + g], tp[j], eta1, 0, 0, 0);
+        for (int j = 0; j < J; ++j)
+            en = __builtin_amdgcn_mfma_f64_16x16x4f64(xs[cl * LD + 4 * j + g], tp[j], en, 0, 0, 0);
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            __builtin_amdgcn_sched_barrier(0);
+            const mala_d4 eta = en;
+            if (b + 1 < NB) {
+                const double *xn = xs + (16 * (b + 1)) * LD;
+                en = mala_d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int j = 0; j < J; ++j)
+                    en = __builtin_amdgcn_mfma_f64_16x16x4f64(xn[cl * LD + 4 * j + g], tp[j], en, 0, 0, 0);
+            }
+            const int rb = 16 * b;
+            const double *xb = xs + rb * LD;
+            double r[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int row = 4 * q + g;
+                double ell, rr;
+#if EMCMC_MALA_ABLATE & 1  // timing-only: no elementwise terms
+                ell = eta[q];
+                rr = eta[q] * ys[rb + row];
+#else
+                logistic_terms(eta[q], ys[rb + row], ell, rr);
+#endif
+                const bool in = n0 + rb + row < a.nrows;
+                if (in) S = S + ell;
+                r[q] = in ? rr : 0.0;
             }
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const mala_d4 &eta = h ? eta1 : eta0;
-                const double *xb = h ? xb1 : xb0;
-                const int rb = 16 * (b + h);
-                double r[4];
+            for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int row = 4 * q + g;
-                    double ell, rr;
-                    logistic_terms(eta[q], ys[rb + row], ell, rr);
-                    const bool in = n0 + rb + row < a.nrows;
-                    if (in) S = S + ell;
-                    r[q] = in ? rr : 0.0;
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int e = 0; e < DB; ++e)
-                        G[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[(4 * q + g) * LD + 16 * e + cl], r[q], G[e], 0,
-                                                                   0, 0);
-            }
+                for (int e = 0; e < DB; ++e)
+                    G[e] = __builtin_amdgcn_mfma_f64_16x16x4f64(xb[(4 * q + g) * LD + 16 * e + cl], r[q], G[e], 0, 0,
+                                                               0);
         }
     }
     // lane's ∇ℓ coordinates: G[e][i] ↔ d = 16e + g + 4i ↔ j = 4e + i

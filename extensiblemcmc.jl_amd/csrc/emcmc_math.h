@@ -198,13 +198,14 @@ EMCMC_HD double exp_nonpos(double x) {
 // k = 1024; 0 below −745.13, +Inf above 709.78.  log_any: 0 → −Inf, +Inf →
 // +Inf, NaN → NaN, subnormals scaled by 2^54 first.
 EMCMC_HD double exp_any(double x) {
-    if (x != x) return x;
-    if (x > 709.782712893384) return __builtin_inf();
-    if (x < -745.1332191019412) return 0.0;
+    // branch-free: the range cases are selects at the end; the scaling is the
+    // two-step form of oracle_math.h orc_exp_any (one rounding for subnormal
+    // results, exact otherwise)
     const double invln2 = 1.44269504088896338700e+00;
     const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
-    const double kd = rint(x * invln2);
-    double r = fma(-kd, ln2_hi, x);
+    const double xc = fmin(fmax(x, -746.0), 710.0);  // keeps k in int range (NaN → −746, selected away)
+    const double kd = rint(xc * invln2);
+    double r = fma(-kd, ln2_hi, xc);
     r = fma(-kd, ln2_lo, r);
     double p = 1.0 / 6227020800.0;
     p = fma(p, r, 1.0 / 479001600.0);
@@ -221,9 +222,12 @@ EMCMC_HD double exp_any(double x) {
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
     const int k = (int)kd;
-    if (k > 1023) return (p * u2d((uint64_t)(1023 + k - 1) << 52)) * 2.0;
-    if (k < -1022) return (p * u2d((uint64_t)(1023 + k + 64) << 52)) * 0x1p-64;
-    return p * u2d((uint64_t)(1023 + k) << 52);
+    const bool lo = k < -1022, hi = k > 1023;
+    double e = p * u2d((uint64_t)(1023 + (lo ? k + 64 : hi ? k - 1 : k)) << 52);
+    e = lo ? e * 0x1p-64 : hi ? e * 2.0 : e;
+    e = (x < -745.1332191019412) ? 0.0 : e;
+    e = (x > 709.782712893384) ? __builtin_inf() : e;
+    return (x != x) ? x : e;
 }
 
 EMCMC_HD double log_any(double x) {

@@ -175,6 +175,17 @@ struct emcmc_handle {
     // dispatch
     Variant var;
     size_t lds_bytes = 0;
+    // history ring (emcmc_config.history_ring) and streaming copies
+    uint64_t ring = 0;     // iterations held per history buffer
+    uint64_t hi_iter = 0;  // highest iteration launched
+    hipStream_t cstream = nullptr;
+    struct Copy {
+        uint64_t lo, hi;  // iterations read
+        hipEvent_t ev;
+    };
+    std::vector<Copy> copies;
+    double *d_stage = nullptr;
+    size_t stage_bytes = 0;
     // timing
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
@@ -342,12 +353,13 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
         if (u.adaptation == EMCMC_ADPT_HAARIO) HIPCHK(h, hipMalloc(&h->d_Lnew, C * DP * sizeof(double)));
     }
     h->row_bytes = ((C + 63) / 64) * 8;
-    HIPCHK(h, hipMalloc(&h->d_hist_acc, M * P * h->row_bytes));
-    HIPCHK(h, hipMemsetAsync(h->d_hist_acc, 0, M * P * h->row_bytes, h->stream));
+    const uint64_t R = h->ring;  // history slots: a ring of R iterations (R = M unless history_ring)
+    HIPCHK(h, hipMalloc(&h->d_hist_acc, R * P * h->row_bytes));
+    HIPCHK(h, hipMemsetAsync(h->d_hist_acc, 0, R * P * h->row_bytes, h->stream));
     if (h->cfg.history_mode == EMCMC_HIST_FULL) {
-        HIPCHK(h, hipMalloc(&h->d_hist_theta, M * P * C * D * sizeof(double)));
-        HIPCHK(h, hipMalloc(&h->d_hist_prop, M * P * C * D * sizeof(double)));
-        HIPCHK(h, hipMalloc(&h->d_hist_ll, M * P * C * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_hist_theta, R * P * C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_hist_prop, R * P * C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_hist_ll, R * P * C * sizeof(double)));
     }
     h->allocated = true;
     return EMCMC_OK;
@@ -713,6 +725,45 @@ emcmc_status drain_timing(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
+// ---- history ring -------------------------------------------------------------
+// Kernels address history slot (iter−1)·P + pidx0; a launch whose iterations all
+// lie in one ring epoch [e·R+1, (e+1)·R] gets history pointers shifted back by
+// e·R iterations, so the same arithmetic lands in ring slot (iter−1) mod R.
+struct HistPtrs {
+    double *theta, *prop, *ll;
+    uint8_t *acc;
+};
+uint64_t ring_epoch(const emcmc_handle *h, uint64_t iter) { return (iter - 1) / h->ring; }
+
+HistPtrs shifted_hist(const emcmc_handle *h, uint64_t iter) {
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, P = h->updates.size();
+    const int64_t sh = -(int64_t)(ring_epoch(h, iter) * h->ring * P);  // slots
+    HistPtrs o;
+    o.theta = h->d_hist_theta ? h->d_hist_theta + sh * (int64_t)(C * D) : nullptr;
+    o.prop = h->d_hist_prop ? h->d_hist_prop + sh * (int64_t)(C * D) : nullptr;
+    o.ll = h->d_hist_ll ? h->d_hist_ll + sh * (int64_t)C : nullptr;
+    o.acc = h->d_hist_acc + sh * (int64_t)h->row_bytes;
+    return o;
+}
+
+// Before a launch writing iterations [a, b] (one epoch): the ring slots it
+// overwrites held iterations [a−R, b−R]; wait for any streaming copy reading them.
+emcmc_status guard_ring(emcmc_handle *h, uint64_t a, uint64_t b) {
+    h->hi_iter = std::max(h->hi_iter, b);
+    if (h->copies.empty() || h->ring >= h->cfg.num_mcmc_steps) return EMCMC_OK;
+    const int64_t lo = (int64_t)a - (int64_t)h->ring, hi = (int64_t)b - (int64_t)h->ring;
+    for (auto it = h->copies.begin(); it != h->copies.end();) {
+        if (hipEventQuery(it->ev) == hipSuccess) {  // finished: forget it
+            (void)hipEventDestroy(it->ev);
+            it = h->copies.erase(it);
+            continue;
+        }
+        if ((int64_t)it->hi >= lo && (int64_t)it->lo <= hi) HIPCHK(h, hipStreamWaitEvent(h->stream, it->ev, 0));
+        ++it;
+    }
+    return EMCMC_OK;
+}
+
 // Mix / chain-moments path: maximal runs of consecutive iterations, cut at
 // K steps and at Haario readjust steps (M reaches k after the run), each
 // followed by the readjust kernel when due.
@@ -773,11 +824,22 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
         uint64_t cap = K;
         if (haario) cap = std::min<uint64_t>(cap, k - h->mix_M);
         uint64_t j = i + 1;
-        while (j < num_steps && j - i < cap && steps[j].mcmciter == steps[j - 1].mcmciter + 1) ++j;
+        while (j < num_steps && j - i < cap && steps[j].mcmciter == steps[j - 1].mcmciter + 1 &&
+               ring_epoch(h, steps[j].mcmciter) == ring_epoch(h, steps[i].mcmciter))
+            ++j;
         const uint64_t n = j - i;
         p.iter0 = steps[i].mcmciter;
         p.nsteps = (uint32_t)n;
         p.N0 = h->stats_N;
+        {
+            const HistPtrs hp = shifted_hist(h, p.iter0);
+            p.hist_theta = hp.theta;
+            p.hist_prop = hp.prop;
+            p.hist_ll = hp.ll;
+            p.hist_acc = hp.acc;
+            emcmc_status gs = guard_ring(h, p.iter0, steps[j - 1].mcmciter);
+            if (gs) return gs;
+        }
         if (p.iter0 > 1 && h->last_iter[0] != p.iter0 - 1)  // rolling_ar[iter−1] never written → 0.0
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[0] = steps[j - 1].mcmciter;
@@ -858,6 +920,15 @@ emcmc_status run_mala(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
     for (uint64_t i = 0; i < num_steps; ++i) {
         p.iter = steps[i].mcmciter;
         p.N0 = h->stats_N;
+        {
+            const HistPtrs hp = shifted_hist(h, p.iter);
+            p.hist_theta = hp.theta;
+            p.hist_prop = hp.prop;
+            p.hist_ll = hp.ll;
+            p.hist_acc = hp.acc;
+            emcmc_status gs = guard_ring(h, p.iter, p.iter);
+            if (gs) return gs;
+        }
         if (p.iter > 1 && h->last_iter[0] != p.iter - 1)  // rolling_ar[iter−1] never written → 0.0
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[0] = p.iter;
@@ -937,11 +1008,27 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.nobs_d = (double)t.nobs;
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
     const uint64_t K = h->cfg.steps_per_launch;
-    for (uint64_t i = 0; i < num_steps; i += K) {
-        const uint64_t n = std::min<uint64_t>(K, num_steps - i);
+    for (uint64_t i = 0, n = 0; i < num_steps; i += n) {
+        n = 1;  // ≤ K steps, all in one ring epoch
+        while (i + n < num_steps && n < K && ring_epoch(h, steps[i + n].mcmciter) == ring_epoch(h, steps[i].mcmciter))
+            ++n;
         a.steps = dst + 4 * i;
         a.nsteps = (uint32_t)n;
         a.N0 = h->stats_N;
+        {
+            uint64_t lo = steps[i].mcmciter, hi = lo;
+            for (uint64_t k = i; k < i + n; ++k) {
+                lo = std::min<uint64_t>(lo, steps[k].mcmciter);
+                hi = std::max<uint64_t>(hi, steps[k].mcmciter);
+            }
+            const HistPtrs hp = shifted_hist(h, lo);
+            a.hist_theta = hp.theta;
+            a.hist_prop = hp.prop;
+            a.hist_ll = hp.ll;
+            a.hist_acc = hp.acc;
+            emcmc_status gs = guard_ring(h, lo, hi);
+            if (gs) return gs;
+        }
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (h->timing) {
             e0 = get_event(h);
@@ -997,6 +1084,12 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
     h->cfg = *cfg;
     if (h->cfg.roll_window == 0) h->cfg.roll_window = kDefaultRollWindow;
     if (h->cfg.steps_per_launch == 0) h->cfg.steps_per_launch = kDefaultStepsPerLaunch;
+    h->ring = (h->cfg.history_ring && h->cfg.history_ring < h->cfg.num_mcmc_steps) ? h->cfg.history_ring
+                                                                                    : h->cfg.num_mcmc_steps;
+    if (hipStreamCreateWithFlags(&h->cstream, hipStreamNonBlocking) != hipSuccess) {
+        delete h;
+        return EMCMC_HIP_ERROR;
+    }
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return EMCMC_HIP_ERROR;
@@ -1200,6 +1293,7 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
     }
     h->mix_M = 0;
     h->grad_valid = false;
+    h->hi_iter = 0;
     h->stats_N = 1;
     h->last_iter.assign(P, 0u);
     return EMCMC_OK;
@@ -1261,9 +1355,19 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
         // maximal run of ≤ K consecutive iterations of the same update
         uint64_t j = i + 1;
         while (j < num_steps && j - i < K && steps[j].pidx == steps[i].pidx &&
-               steps[j].mcmciter == steps[j - 1].mcmciter + 1)
+               steps[j].mcmciter == steps[j - 1].mcmciter + 1 &&
+               ring_epoch(h, steps[j].mcmciter) == ring_epoch(h, steps[i].mcmciter))
             ++j;
         const uint64_t n = j - i;
+        {
+            const HistPtrs hp = shifted_hist(h, steps[i].mcmciter);
+            p.hist_theta = hp.theta;
+            p.hist_prop = hp.prop;
+            p.hist_ll = hp.ll;
+            p.hist_acc = hp.acc;
+            emcmc_status gs = guard_ring(h, steps[i].mcmciter, steps[j - 1].mcmciter);
+            if (gs) return gs;
+        }
         p.pidx0 = steps[i].pidx - 1;
         p.iter0 = steps[i].mcmciter;
         p.nsteps = (uint32_t)n;
@@ -1309,6 +1413,10 @@ void emcmc_destroy(emcmc_handle *h) {
     if (!h) return;
     (void)hipSetDevice(h->cfg.device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+    for (auto &c : h->copies) (void)hipEventDestroy(c.ev);
+    if (h->d_stage) (void)hipFree(h->d_stage);
+    if (h->cstream) (void)hipStreamDestroy(h->cstream);
     for (auto &p : h->ev) {
         (void)hipEventDestroy(p.first);
         (void)hipEventDestroy(p.second);
@@ -1476,26 +1584,56 @@ static emcmc_status copy_state_slots(emcmc_handle *h, const double *base, uint64
     return EMCMC_OK;
 }
 
+// Iterations [i0, i0+n) are on device: inside 1..M and, with a ring, not yet
+// overwritten (the last R iterations launched).
+static emcmc_status check_resident(emcmc_handle *h, uint64_t i0, uint64_t n) {
+    if (i0 < 1 || n == 0 || i0 + n - 1 > h->cfg.num_mcmc_steps)
+        return fail(h, EMCMC_INVALID_ARG, "iteration window outside 1..M");
+    if (h->ring < h->cfg.num_mcmc_steps && h->hi_iter > h->ring && i0 <= h->hi_iter - h->ring)
+        return fail(h, EMCMC_STATE_ERROR,
+                    "iteration %llu was overwritten: the history ring keeps iterations %llu..%llu",
+                    (unsigned long long)i0, (unsigned long long)(h->hi_iter - h->ring + 1),
+                    (unsigned long long)h->hi_iter);
+    return EMCMC_OK;
+}
+
+// Calls fn(ring_iter0, count, done) over the runs of [i0, i0+n) that are
+// contiguous in the ring (split where the ring wraps).
+extern "C++" {
+template <typename F>
+static emcmc_status for_each_ring_run(const emcmc_handle *h, uint64_t i0, uint64_t n, F fn) {
+    for (uint64_t done = 0; done < n;) {
+        const uint64_t r = (i0 + done - 1) % h->ring;
+        const uint64_t len = std::min(n - done, h->ring - r);
+        emcmc_status st = fn(r, len, done);
+        if (st) return st;
+        done += len;
+    }
+    return EMCMC_OK;
+}
+}  // extern "C++"
+
 emcmc_status emcmc_get_history(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
                                void *host_out, size_t host_bytes) {
     if (!h || !host_out) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
-    if (iter_first < 1 || iter_first + num_iters - 1 > h->cfg.num_mcmc_steps)
-        return fail(h, EMCMC_INVALID_ARG, "iteration window outside 1..M");
+    emcmc_status st = check_resident(h, iter_first, num_iters);
+    if (st) return st;
     void *base = nullptr;
     size_t row = 0;
-    emcmc_status st = hist_geometry(h, which, &base, &row);
+    st = hist_geometry(h, which, &base, &row);
     if (st) return st;
     if (host_bytes < row * num_iters) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    if (which == EMCMC_H_STATE || which == EMCMC_H_PROPOSAL) {
-        const uint64_t P = h->updates.size();
-        return copy_state_slots(h, (const double *)base, (iter_first - 1) * P, num_iters * P, 0,
-                                h->cfg.num_chains, (double *)host_out);
-    }
-    HIPCHK(h, hipMemcpy(host_out, (const uint8_t *)base + (iter_first - 1) * row, row * num_iters,
-                        hipMemcpyDeviceToHost));
-    return EMCMC_OK;
+    const uint64_t P = h->updates.size();
+    return for_each_ring_run(h, iter_first, num_iters, [&](uint64_t r, uint64_t len, uint64_t done) {
+        if (which == EMCMC_H_STATE || which == EMCMC_H_PROPOSAL)
+            return copy_state_slots(h, (const double *)base, r * P, len * P, 0, h->cfg.num_chains,
+                                    (double *)((uint8_t *)host_out + done * row));
+        HIPCHK(h, hipMemcpy((uint8_t *)host_out + done * row, (const uint8_t *)base + r * row, row * len,
+                            hipMemcpyDeviceToHost));
+        return EMCMC_OK;
+    });
 }
 
 emcmc_status emcmc_get_history_chains(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
@@ -1503,25 +1641,28 @@ emcmc_status emcmc_get_history_chains(emcmc_handle *h, uint32_t which, uint64_t 
     if (!h || !host_out) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
     if (which == EMCMC_H_ACCEPT) return fail(h, EMCMC_INVALID_ARG, "accept bits: use emcmc_get_history");
-    if (iter_first < 1 || num_iters == 0 || iter_first + num_iters - 1 > h->cfg.num_mcmc_steps)
-        return fail(h, EMCMC_INVALID_ARG, "iteration window outside 1..M");
+    emcmc_status st = check_resident(h, iter_first, num_iters);
+    if (st) return st;
     const uint64_t C = h->cfg.num_chains, P = h->updates.size();
     if (num_chains == 0 || chain_first + num_chains > C) return fail(h, EMCMC_INVALID_ARG, "chain window");
     void *base = nullptr;
     size_t row = 0;
-    emcmc_status st = hist_geometry(h, which, &base, &row);
+    st = hist_geometry(h, which, &base, &row);
     if (st) return st;
     const size_t per_chain = (which == EMCMC_H_LL) ? sizeof(double) : h->cfg.dim * sizeof(double);
     const size_t height = num_iters * P;
     if (host_bytes < num_chains * per_chain * height) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
     HIPCHK(h, hipStreamSynchronize(h->stream));
-    if (which != EMCMC_H_LL)
-        return copy_state_slots(h, (const double *)base, (iter_first - 1) * P, height, chain_first, num_chains,
-                                (double *)host_out);
-    const size_t width = num_chains * per_chain, spitch = C * per_chain;
-    const uint8_t *src = (const uint8_t *)base + (iter_first - 1) * row + chain_first * per_chain;
-    HIPCHK(h, hipMemcpy2D(host_out, width, src, spitch, width, height, hipMemcpyDeviceToHost));
-    return EMCMC_OK;
+    const size_t out_row = P * num_chains * per_chain;  // host bytes per iteration
+    return for_each_ring_run(h, iter_first, num_iters, [&](uint64_t r, uint64_t len, uint64_t done) {
+        uint8_t *dst = (uint8_t *)host_out + done * out_row;
+        if (which != EMCMC_H_LL)
+            return copy_state_slots(h, (const double *)base, r * P, len * P, chain_first, num_chains, (double *)dst);
+        const size_t width = num_chains * per_chain, spitch = C * per_chain;
+        const uint8_t *src = (const uint8_t *)base + r * row + chain_first * per_chain;
+        HIPCHK(h, hipMemcpy2D(dst, width, src, spitch, width, len * P, hipMemcpyDeviceToHost));
+        return EMCMC_OK;
+    });
 }
 
 emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dptr, size_t *bytes) {
@@ -1530,7 +1671,92 @@ emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dp
     size_t row = 0;
     emcmc_status st = hist_geometry(h, which, dptr, &row);
     if (st) return st;
-    *bytes = row * h->cfg.num_mcmc_steps;
+    *bytes = row * h->ring;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_stream_history(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
+                                  uint64_t thin, void *host_out, size_t host_bytes) {
+    if (!h || !host_out || thin == 0) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    const uint64_t last = iter_first + (num_iters - 1) * thin;
+    if (num_iters == 0 || iter_first < 1 || last > h->cfg.num_mcmc_steps)
+        return fail(h, EMCMC_INVALID_ARG, "iteration window outside 1..M");
+    if (last > h->hi_iter) return fail(h, EMCMC_STATE_ERROR, "iteration %llu has not been run", (unsigned long long)last);
+    emcmc_status st = check_resident(h, iter_first, 1);
+    if (st) return st;
+    void *base = nullptr;
+    size_t row = 0;
+    st = hist_geometry(h, which, &base, &row);
+    if (st) return st;
+    if (host_bytes < row * num_iters) return fail(h, EMCMC_INVALID_ARG, "host buffer too small");
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, P = h->updates.size();
+    // ordered after the compute work enqueued so far
+    hipEvent_t ready = nullptr;
+    HIPCHK(h, hipEventCreateWithFlags(&ready, hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(ready, h->stream));
+    HIPCHK(h, hipStreamWaitEvent(h->cstream, ready, 0));
+    (void)hipEventDestroy(ready);
+    uint8_t *out = (uint8_t *)host_out;
+    if (which == EMCMC_H_STATE || which == EMCMC_H_PROPOSAL) {
+        // gather each iteration's P slots (state_pos layout) into host layout on
+        // the copy stream, in chunks through a staging buffer
+        const uint64_t per_it = P * C * D;
+        const uint64_t chunk = std::max<uint64_t>(1, (256ull << 20) / (per_it * sizeof(double)));
+        const size_t need = std::min(num_iters, chunk) * per_it * sizeof(double);
+        if (h->stage_bytes < need) {
+            HIPCHK(h, hipStreamSynchronize(h->cstream));
+            if (h->d_stage) (void)hipFree(h->d_stage);
+            h->d_stage = nullptr;
+            HIPCHK(h, hipMalloc(&h->d_stage, need));
+            h->stage_bytes = need;
+        }
+        for (uint64_t k0 = 0; k0 < num_iters; k0 += chunk) {
+            const uint64_t nk = std::min(chunk, num_iters - k0);
+            for (uint64_t k = 0; k < nk; ++k) {
+                const uint64_t it = iter_first + (k0 + k) * thin;
+                const uint64_t n = per_it;
+                hipLaunchKernelGGL(gather_hist_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, h->cstream,
+                                   (const double *)base, C, (uint32_t)D, ((it - 1) % h->ring) * P, P, (uint64_t)0, C,
+                                   h->d_stage + k * per_it);
+                HIPCHK(h, hipGetLastError());
+            }
+            HIPCHK(h, hipMemcpyAsync(out + k0 * row, h->d_stage, nk * row, hipMemcpyDeviceToHost, h->cstream));
+        }
+    } else {
+        for (uint64_t k = 0; k < num_iters;) {  // contiguous runs when thin == 1
+            const uint64_t it = iter_first + k * thin, r = (it - 1) % h->ring;
+            uint64_t len = 1;
+            if (thin == 1) len = std::min(num_iters - k, h->ring - r);
+            HIPCHK(h, hipMemcpyAsync(out + k * row, (const uint8_t *)base + r * row, len * row, hipMemcpyDeviceToHost,
+                                     h->cstream));
+            k += len;
+        }
+    }
+    hipEvent_t done = nullptr;
+    HIPCHK(h, hipEventCreateWithFlags(&done, hipEventDisableTiming));
+    HIPCHK(h, hipEventRecord(done, h->cstream));
+    h->copies.push_back({iter_first, last, done});
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_stream_wait(emcmc_handle *h) {
+    if (!h) return EMCMC_INVALID_ARG;
+    HIPCHK(h, hipStreamSynchronize(h->cstream));
+    for (auto &c : h->copies) (void)hipEventDestroy(c.ev);
+    h->copies.clear();
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_host_alloc(size_t bytes, void **ptr) {
+    if (!ptr) return EMCMC_INVALID_ARG;
+    *ptr = nullptr;
+    if (hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return EMCMC_OUT_OF_MEMORY;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_host_free(void *ptr) {
+    if (ptr && hipHostFree(ptr) != hipSuccess) return EMCMC_HIP_ERROR;
     return EMCMC_OK;
 }
 
@@ -1541,6 +1767,13 @@ emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t
     if (!h->d_hist_theta) return fail(h, EMCMC_STATE_ERROR, "moments need EMCMC_HIST_FULL");
     if (iter_first < 1 || num_iters < 2 || iter_first + num_iters - 1 > h->cfg.num_mcmc_steps)
         return fail(h, EMCMC_INVALID_ARG, "iteration window");
+    {
+        emcmc_status rs = check_resident(h, iter_first, num_iters);
+        if (rs) return rs;
+        if ((iter_first - 1) % h->ring + num_iters > h->ring)
+            return fail(h, EMCMC_STATE_ERROR, "moments window wraps the history ring");
+    }
+    const uint64_t ring0 = (iter_first - 1) % h->ring;  // ring iteration of iter_first
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, P = h->updates.size();
     const uint32_t halves = split ? 2u : 1u;
     const size_t need = 2 * C * D * halves * sizeof(double) + 3 * D * sizeof(double) + 64;
@@ -1553,7 +1786,7 @@ emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t
     double *mean = h->d_scratch, *var = mean + C * D * halves, *o = var + C * D * halves;
     unsigned long long *cnt = reinterpret_cast<unsigned long long *>(o + 3 * D);
     const uint64_t total = C * D * halves;
-    const uint64_t slot0 = (iter_first - 1) * P + (P - 1);  // state after the last update of the iteration
+    const uint64_t slot0 = ring0 * P + (P - 1);  // state after the last update of the iteration
     hipLaunchKernelGGL(chain_moments_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, h->stream,
                        h->d_hist_theta, C, (uint32_t)D, slot0, (uint32_t)P, (uint32_t)num_iters, halves, mean, var);
     HIPCHK(h, hipGetLastError());
@@ -1563,7 +1796,7 @@ emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t
     HIPCHK(h, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), h->stream));
     const uint64_t words = num_iters * P * h->row_bytes / 8;
     hipLaunchKernelGGL(popcount_kernel, dim3(1024), dim3(256), 0, h->stream,
-                       reinterpret_cast<const uint64_t *>(h->d_hist_acc + (iter_first - 1) * P * h->row_bytes),
+                       reinterpret_cast<const uint64_t *>(h->d_hist_acc + ring0 * P * h->row_bytes),
                        words, cnt);
     HIPCHK(h, hipGetLastError());
     unsigned long long acc = 0;

@@ -66,7 +66,8 @@ class EmcmcConfig(C.Structure):
         ("steps_per_launch", C.c_uint32),
         ("kernel_variant", C.c_uint32),
         ("chain_moments", C.c_uint32),
-        ("reserved", C.c_uint32 * 5),
+        ("history_ring", C.c_uint32),
+        ("reserved", C.c_uint32 * 4),
     ]
 
 
@@ -163,6 +164,10 @@ SIGNATURES = {
         _ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
     ),
     "emcmc_history_device_ptr": (_ST, [_H, C.c_uint32, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "emcmc_stream_history": (_ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]),
+    "emcmc_stream_wait": (_ST, [_H]),
+    "emcmc_host_alloc": (_ST, [C.c_size_t, C.POINTER(C.c_void_p)]),
+    "emcmc_host_free": (_ST, [C.c_void_p]),
     "emcmc_moments_window": (
         _ST,
         [_H, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double), C.POINTER(EmcmcMoments)],

@@ -27,6 +27,39 @@ class EngineConfig:
     steps_per_launch: int = 0
     kernel_variant: int = 0
     chain_moments: bool = False
+    history_ring: int = 0  # iterations of history kept on device (0 = all)
+
+
+class PinnedArray(np.ndarray):
+    """A numpy array over page-locked host memory (emcmc_host_alloc); the memory
+    is released when the array (and every view of it) is garbage collected."""
+
+    def __new__(cls, shape, dtype):
+        dt = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dt.itemsize
+        p = C.c_void_p()
+        st = L.lib().emcmc_host_alloc(max(1, nbytes), C.byref(p))
+        if st != L.OK:
+            raise L.EMCMCError(st, "emcmc_host_alloc")
+        buf = (C.c_char * max(1, nbytes)).from_address(p.value)
+        obj = np.ndarray.__new__(cls, shape, dtype=dt, buffer=buf)
+        obj._owner = _PinnedOwner(p.value)
+        return obj
+
+    def __array_finalize__(self, obj):
+        if obj is not None and not hasattr(self, "_owner"):
+            self._owner = getattr(obj, "_owner", None)
+
+
+class _PinnedOwner:
+    def __init__(self, addr):
+        self.addr = addr
+
+    def __del__(self):
+        try:
+            L.lib().emcmc_host_free(C.c_void_p(self.addr))
+        except Exception:
+            pass
 
 
 class Engine:
@@ -47,6 +80,7 @@ class Engine:
         c.steps_per_launch = cfg.steps_per_launch
         c.kernel_variant = cfg.kernel_variant
         c.chain_moments = int(bool(cfg.chain_moments))
+        c.history_ring = int(cfg.history_ring)
         h = C.c_void_p()
         st = self._lib.emcmc_create(C.byref(h), C.byref(c))
         if st != L.OK:
@@ -300,6 +334,30 @@ class Engine:
             "emcmc_get_history_chains",
         )
         return out
+
+    def stream_history(self, which: int, iter_first: int, num_iters: int, thin: int = 1, out=None):
+        """Enqueue an asynchronous copy of iterations iter_first, iter_first+thin, …
+        of a history into pinned host memory (emcmc_stream_history).  Returns the
+        array (STATE/PROPOSAL [n][P][C][D], LL [n][P][C], ACCEPT [n][P][⌈C/64⌉]
+        u64 words); read it after stream_wait()."""
+        P, Cn, D = self.num_updates, self.cfg.num_chains, self.cfg.dim
+        if which in (L.H_STATE, L.H_PROPOSAL):
+            shape, dt = (num_iters, P, Cn, D), np.float64
+        elif which == L.H_LL:
+            shape, dt = (num_iters, P, Cn), np.float64
+        elif which == L.H_ACCEPT:
+            shape, dt = (num_iters, P, (Cn + 63) // 64), np.uint64
+        else:
+            raise ValueError(which)
+        if out is None:
+            out = PinnedArray(shape, dt)
+        assert out.shape == shape and out.dtype == dt and out.flags.c_contiguous
+        self._check(self._lib.emcmc_stream_history(self._h, which, iter_first, num_iters, thin, out.ctypes.data,
+                                                   out.nbytes), "emcmc_stream_history")
+        return out
+
+    def stream_wait(self):
+        self._check(self._lib.emcmc_stream_wait(self._h), "emcmc_stream_wait")
 
     def moments_window(self, iter_first: int, num_iters: int, split: bool = True):
         out = np.empty(3 * self.cfg.dim, dtype=np.float64)

@@ -35,7 +35,8 @@ struct EmcmcConfig
     steps_per_launch::UInt32
     kernel_variant::UInt32
     chain_moments::UInt32
-    reserved::NTuple{5,UInt32}
+    history_ring::UInt32
+    reserved::NTuple{4,UInt32}
 end
 
 struct EmcmcUpdateDesc
@@ -190,7 +191,7 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
     cfg = Ref(EmcmcConfig(ABI_VERSION, UInt32(D), UInt64(be.num_chains), UInt64(be.first_chain_id),
                           UInt64(num_mcmc_steps), be.seed, Int32(be.device),
                           be.history === :full ? UInt32(0) : UInt32(1), UInt32(100), UInt32(0),
-                          UInt32(0), UInt32(0), UInt32(be.chain_moments), ntuple(_ -> UInt32(0), 5)))
+                          UInt32(0), UInt32(0), UInt32(be.chain_moments), UInt32(0), ntuple(_ -> UInt32(0), 4)))
     h = Ref{Ptr{Cvoid}}(C_NULL)
     check(ccall((:emcmc_create, LIB), Cint, (Ref{Ptr{Cvoid}}, Ref{EmcmcConfig}), h, cfg), C_NULL, "emcmc_create")
     keep = Any[]

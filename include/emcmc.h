@@ -119,7 +119,9 @@ typedef struct emcmc_config {
     uint32_t chain_moments;    /* 1 = keep GenericChainStats mean/cov (chain_statistics.jl:46-49) on
                                   device for a single joint GaussianRandomWalk update (always on with
                                   GaussianRandomWalkMix); read with emcmc_get_chain_moments */
-    uint32_t reserved[5];
+    uint32_t history_ring;     /* iterations of history kept on device as a ring (0 = all num_mcmc_steps);
+                                  older iterations are streamed out with emcmc_stream_history */
+    uint32_t reserved[4];
 } emcmc_config;
 
 /* kernel_variant flags: performance-only choices, bit-identical results */
@@ -287,7 +289,29 @@ emcmc_status emcmc_get_history_chains(emcmc_handle *h, uint32_t which, uint64_t 
                                       uint64_t num_iters, uint64_t chain_first, uint64_t num_chains,
                                       void *host_out, size_t host_bytes);
 
-/* Device pointer + byte size of a whole history buffer (zero-copy interop). */
+/* ---- history streaming (ring buffers on device) -------------------------
+ * With emcmc_config.history_ring = R, iteration i of every history lives in
+ * ring slot (i−1) mod R and is overwritten by iteration i + R.  The getters
+ * above accept only resident iterations (the last R run); older ones return
+ * EMCMC_STATE_ERROR.  Histories leave the device while later steps run: */
+
+/* Enqueue an asynchronous copy of iterations iter_first, iter_first+thin, …
+ * (num_iters of them) of history `which` into host_out, in the emcmc_get_history
+ * layout of a num_iters window ([n][P][C][D], [n][P][C] or [n][P][⌈C/64⌉] u64).
+ * The copy runs on the handle's copy stream: after every emcmc_run enqueued so
+ * far, and before any later step that reuses those ring slots; later steps
+ * overlap it otherwise.  host_out must stay valid until emcmc_stream_wait; use
+ * pinned memory (emcmc_host_alloc) for the copy to be asynchronous. */
+emcmc_status emcmc_stream_history(emcmc_handle *h, uint32_t which, uint64_t iter_first, uint64_t num_iters,
+                                  uint64_t thin, void *host_out, size_t host_bytes);
+/* Wait for every enqueued history copy. */
+emcmc_status emcmc_stream_wait(emcmc_handle *h);
+/* Page-locked host memory for streamed histories (hipHostMalloc / hipHostFree). */
+emcmc_status emcmc_host_alloc(size_t bytes, void **ptr);
+emcmc_status emcmc_host_free(void *ptr);
+
+/* Device pointer + byte size of a whole history buffer (zero-copy interop;
+ * history_ring iterations when a ring is configured). */
 emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dptr,
                                       size_t *bytes);
 

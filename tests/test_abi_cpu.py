@@ -48,7 +48,7 @@ def test_struct_layout_matches_header(tmp_path):
           printf("%zu %zu %zu %zu %zu\\n", offsetof(emcmc_config, device), offsetof(emcmc_update_desc, pos),
                  offsetof(emcmc_target_desc, ll_mode), sizeof(emcmc_unifrw_adaptation),
                  offsetof(emcmc_unifrw_adaptation, offset));
-          printf("%zu %zu %zu %zu %zu\\n", offsetof(emcmc_config, chain_moments),
+          printf("%zu %zu %zu %zu %zu %zu\\n", offsetof(emcmc_config, history_ring), offsetof(emcmc_config, chain_moments),
                  offsetof(emcmc_update_desc, adaptation_params), offsetof(emcmc_update_desc, sigma_b),
                  offsetof(emcmc_update_desc, mix_lambda), sizeof(emcmc_haario_adaptation));
           return 0;
@@ -66,7 +66,7 @@ def test_struct_layout_matches_header(tmp_path):
     assert [int(x) for x in offs.split()] == [L.EmcmcConfig.device.offset, L.EmcmcUpdateDesc.pos.offset,
                                               L.EmcmcTargetDesc.ll_mode.offset, C.sizeof(L.EmcmcUnifRWAdaptation),
                                               L.EmcmcUnifRWAdaptation.offset.offset]
-    assert [int(x) for x in offs2.split()] == [L.EmcmcConfig.chain_moments.offset,
+    assert [int(x) for x in offs2.split()] == [L.EmcmcConfig.history_ring.offset, L.EmcmcConfig.chain_moments.offset,
                                                L.EmcmcUpdateDesc.adaptation_params.offset,
                                                L.EmcmcUpdateDesc.sigma_b.offset, L.EmcmcUpdateDesc.mix_lambda.offset,
                                                C.sizeof(L.EmcmcHaarioAdaptation)]

@@ -46,6 +46,11 @@ def parse():
     ap.add_argument("--chains-per-gpu", type=int, default=0,
                     help="0: 65,536 (cfg2) / 32,768 (cfg3) / 131,072 (cfg4)")
     ap.add_argument("--haario-k", type=int, default=200)
+    ap.add_argument("--history-ring", type=int, default=0,
+                    help="keep this many iterations of history on device (0 = all)")
+    ap.add_argument("--stream-thin", type=int, default=0,
+                    help="stream every k-th iteration's θ history to pinned host memory inside the timed "
+                         "region (needs --history-ring; reports the PCIe-inclusive rate)")
     ap.add_argument("--history", choices=["full", "accept_only"], default="full")
     ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
     ap.add_argument("--lpc", type=int, default=0)
@@ -134,7 +139,12 @@ def main():
     M = a.warmup + a.steps * a.reps
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=rank * Cg,
                               device=local, history_mode=hist, lanes_per_chain=a.lpc,
-                              steps_per_launch=a.steps_per_launch))
+                              steps_per_launch=a.steps_per_launch, history_ring=a.history_ring))
+    stream_bufs = None
+    if a.stream_thin:
+        assert a.history_ring > 0 and a.history_ring % a.stream_thin == 0 and a.steps % a.history_ring == 0
+        from extensible_mcmc.engine import PinnedArray
+        stream_bufs = PinnedArray((a.steps // a.stream_thin, 1, Cg, w.D), np.float64)
     if cfg3:
         eng.add_mala_update(np.arange(w.D), w.eps)
         eng.set_logistic_target(w.X, w.y)
@@ -164,7 +174,16 @@ def main():
 
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        eng.run_iters(it, a.steps)
+        if stream_bufs is None:
+            eng.run_iters(it, a.steps)
+        else:  # half a ring per chunk: a chunk's thinned θ history leaves while the next chunk runs
+            ch = a.history_ring // 2 if a.history_ring >= 2 * a.stream_thin else a.history_ring
+            for c0 in range(0, a.steps, ch):
+                eng.run_iters(it + c0, ch)
+                k0 = c0 // a.stream_thin
+                eng.stream_history(L.H_STATE, it + c0 + a.stream_thin - 1, ch // a.stream_thin, thin=a.stream_thin,
+                                   out=stream_bufs[k0:k0 + ch // a.stream_thin])
+            eng.stream_wait()
         eng.synchronize(allow_faults=cfg4)
         if dist is not None:
             torch.cuda.synchronize()
@@ -185,7 +204,8 @@ def main():
     ms, launches, nbytes = kern[mid]
 
     # diagnostics over the timed window: one all-reduce of 3·D+3 doubles
-    mom = eng.moments_window(a.warmup + 1, a.steps, split=True) if hist == L.HIST_FULL else None
+    mom = eng.moments_window(a.warmup + 1, a.steps, split=True) if hist == L.HIST_FULL and not a.history_ring \
+        else None
     if mom is not None and dist is not None:
         mom = DG.allreduce_sums(mom, w.D, device=f"cuda:{local}")
     diag = DG.rhat_from_sums(mom) if mom is not None else None
@@ -271,6 +291,11 @@ def main():
                            "frac": tfs / FP64_MFMA_PEAK_TFS, "traffic": traffic, "kernel": kname,
                            "algorithmic_flops_per_launch": flops, "avg_launch_ms": avg_launch_s * 1e3,
                            "launches": launches, "flops_per_chain_step": 4.0 * w.nobs * w.D}
+    if stream_bufs is not None:
+        sb = stream_bufs.nbytes
+        out["streaming"] = {"history_ring": a.history_ring, "thin": a.stream_thin, "host_bytes": sb,
+                            "d2h_gb_per_s": sb / dt / 1e9,
+                            "note": "value here includes the D2H stream of every thin-th θ history slot (PCIe)"}
     if cfg4:
         out["posdef_faulted_chains"] = int(np.count_nonzero(eng.get_faults() & L.FAULT_POSDEF))
     if diag is not None:
@@ -283,10 +308,11 @@ def main():
             out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         except Exception as e:  # the oracle is a reported baseline, never the measured path
             out["cpu_baseline"] = {"error": repr(e)}
-        try:
-            out["parity"] = parity_sample(eng, w, a, ll_mode)
-        except Exception as e:
-            out["parity"] = {"error": repr(e)}
+        if not a.history_ring:
+            try:
+                out["parity"] = parity_sample(eng, w, a, ll_mode)
+            except Exception as e:
+                out["parity"] = {"error": repr(e)}
     print(json.dumps(out))
     eng.close()
     if dist is not None:

@@ -16,6 +16,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <tuple>
+#include <utility>
 #include <vector>
 
 #include "../../include/emcmc.h"
@@ -118,12 +120,15 @@ using MwgFn = void (*)(MwgParams);
 using MixFn = void (*)(MixParams);
 using ReadjustFn = void (*)(MixReadjustParams);
 using MalaFn = void (*)(MalaParams);
+using MomentsFn = void (*)(MixMomentsParams);
 
 struct Variant {
     KernelFn fn = nullptr;
     MwgFn mfn = nullptr;  // general schedule kernel (mwg_gsn_kernel) when set
     MixFn xfn = nullptr;  // mix / chain-moments kernel (mix_gsn_kernel) when set
     ReadjustFn rfn = nullptr;  // Haario readjust kernel
+    MomentsFn mofn = nullptr;  // batched chain mean/cov (mix_moments_kernel)
+    int mo_tiles = 0;
     MalaFn afn = nullptr, ainit = nullptr;  // MALA step / ∇ℓ initialisation kernels
     bool mix = false;
     int lpc = 1;
@@ -167,6 +172,7 @@ struct emcmc_handle {
     // per-chain Σ_B factor, Haario M (same for every chain)
     double *d_mean = nullptr, *d_cov = nullptr, *d_LB = nullptr, *d_iLB = nullptr, *d_c0B = nullptr;
     double *d_Lnew = nullptr;
+    double *d_mom_scratch = nullptr;  // ACCEPT_ONLY: θ of each step of a launch, for the moments kernel
     uint32_t mix_M = 0;
     // MALA path: carried ∇ℓ(θ) (state_pos layout), padded X and y
     double *d_grad = nullptr, *d_X = nullptr, *d_y = nullptr;
@@ -351,6 +357,8 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
             HIPCHK(h, hipMalloc(&h->d_c0B, C * sizeof(double)));
         }
         if (u.adaptation == EMCMC_ADPT_HAARIO) HIPCHK(h, hipMalloc(&h->d_Lnew, C * DP * sizeof(double)));
+        if (h->cfg.history_mode != EMCMC_HIST_FULL)
+            HIPCHK(h, hipMalloc(&h->d_mom_scratch, (uint64_t)h->cfg.steps_per_launch * C * D * sizeof(double)));
     }
     h->row_bytes = ((C + 63) / 64) * 8;
     const uint64_t R = h->ring;  // history slots: a ring of R iterations (R = M unless history_ring)
@@ -478,6 +486,23 @@ template <int D>
 ReadjustFn readjust_fn() {
     return &mix_readjust_kernel<D>;
 }
+template <int D>
+std::pair<MomentsFn, int> moments_fn() {
+    return {&mix_moments_kernel<D>, MomentTiles<D>::NT};
+}
+std::pair<MomentsFn, int> moments_lookup(int D) {
+    switch (D) {
+    case 1: return moments_fn<1>();
+    case 2: return moments_fn<2>();
+    case 3: return moments_fn<3>();
+    case 4: return moments_fn<4>();
+    case 8: return moments_fn<8>();
+    case 16: return moments_fn<16>();
+    case 32: return moments_fn<32>();
+    default: return {nullptr, 0};
+    }
+}
+
 ReadjustFn readjust_lookup(int D) {
     switch (D) {
     case 1: return readjust_fn<1>();
@@ -510,9 +535,11 @@ emcmc_status select_mix(emcmc_handle *h) {
         v.rfn = readjust_lookup(D);
         if (!v.rfn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no Haario readjust kernel for D=%d", D);
     }
+    std::tie(v.mofn, v.mo_tiles) = moments_lookup(D);
+    if (!v.mofn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no chain-moments kernel for D=%d", D);
     v.mix = true;
     char nm[160];
-    snprintf(nm, sizeof nm, "mix_gsn_kernel<D=%d,%s,%s,%s,%s>%s", D, full ? "FULL" : "ACCEPT_ONLY",
+    snprintf(nm, sizeof nm, "mix_gsn_kernel<D=%d,%s,%s,%s,%s>+mix_moments_kernel%s", D, full ? "FULL" : "ACCEPT_ONLY",
              ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", mix ? "MIX" : "GSN_MOMENTS", adiag ? "DIAG" : "DENSE",
              v.rfn ? "+mix_readjust_kernel" : "");
     v.name = nm;
@@ -687,10 +714,10 @@ double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps) {
     const double C = (double)h->cfg.num_chains, D = (double)h->cfg.dim;
     double per_step = (h->cfg.history_mode == EMCMC_HIST_FULL) ? (16.0 * D + 8.0 + 0.125) : 0.125;
     double state = 16.0 * D + 2 * 8 + 2 * 8 + 2 * 16 + 2 * 4 + 2 * 4;  // θ, ll, ra, ring, nacc, faults (R+W)
-    if (h->var.xfn) {
-        const double DP = D * (D + 1) / 2;
-        per_step += 16.0 * DP + 16.0 * D;  // cov and mean, read + write
+    if (h->var.xfn) {  // step kernel only (mix_moments_kernel is accounted separately)
+        if (h->cfg.history_mode != EMCMC_HIST_FULL) per_step += 8.0 * D;  // θ for the moments kernel
         if (h->updates[0].kernel == EMCMC_RW_GAUSSIAN_MIX) {
+            const double DP = D * (D + 1) / 2;
             per_step += 8.0 * DP + 8.0 * D;  // L_B and 1/L_B,ii, read
             state += 8.0;                    // c0_B
         }
@@ -780,8 +807,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     p.ring = h->d_ring;
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
-    p.mean = h->d_mean;
-    p.cov = h->d_cov;
+    p.mom_theta = h->d_mom_scratch;
     p.LB = h->d_LB;
     p.iLB = h->d_iLB;
     p.c0B = h->d_c0B;
@@ -856,6 +882,18 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             HIPCHK(h, hipEventRecord(e1, h->stream));
             h->ev.emplace_back(e0, e1);
             h->pending_bytes += bytes_per_launch(h, n);
+        }
+        {  // the launch's mean/cov recurrence, from its θ history
+            MixMomentsParams mp{};
+            mp.theta = p.hist_theta ? p.hist_theta + (uint64_t)(p.iter0 - 1) * h->cfg.dim * C : h->d_mom_scratch;
+            mp.mean = h->d_mean;
+            mp.cov = h->d_cov;
+            mp.C = C;
+            mp.N0 = p.N0;
+            mp.nsteps = p.nsteps;
+            void *margs[] = {&mp};
+            const dim3 mgrid((unsigned)((C + 255) / 256), (unsigned)h->var.mo_tiles);
+            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mofn), mgrid, block, margs, 0, h->stream));
         }
         h->stats_N += n;
         if (haario) {
@@ -1427,7 +1465,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
-                    h->d_grad,      h->d_X,         h->d_y};
+                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);

@@ -48,8 +48,7 @@ struct MixParams {
     uint64_t *ring;  // [C][2]
     uint32_t *nacc;  // [C]
     uint32_t *faults;
-    double *mean;       // [D] state_pos
-    double *cov;        // [DP] packed upper, state_pos(p, c, C, DP)
+    double *mom_theta;  // ACCEPT_ONLY: θ after each step of the launch, [nsteps] slots (state_pos)
     const double *LB;   // [DP] packed lower, state_pos(q, c, C, DP)
     const double *iLB;  // [D][C]
     const double *c0B;  // [C]
@@ -282,34 +281,9 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
             if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
         }
         ra = rolling_update(ra, r0, r1, iter, a.W, N, a.rcp_W, acc);
-        // ---- update_stats!: running mean/cov of θ (chain_statistics.jl:46-49)
-        {
-            const double Nd = (double)N, N1d = (double)(N + 1);
-            const double ca = (double)(N - 1) / Nd;  // (N−1)/N
-            const double cb = Nd / N1d;              // N/(N+1)
-            const double cc = N1d / Nd;              // (N+1)/N
-            const double rN = 1.0 / Nd, rN1 = 1.0 / N1d;
-            const LaneSoA lm = lane_soa(C, chain, D);
-            double mo[D], mn[D];
-#pragma unroll
-            for (int i = 0; i < D; ++i) mo[i] = *soa_ptr<D>(a.mean, lm, i);
-#pragma unroll
-            for (int i = 0; i < D; ++i) mn[i] = mo[i] * cb + div_markstein(th[i], N1d, rN1);
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                __builtin_amdgcn_sched_barrier(0);  // one packed row in flight at a time
-                const LaneSoA lc = lane_soa(C, chain, DP);
-#pragma unroll
-                for (int j = i; j < D; ++j) {
-                    double *pc = soa_ptr<DP>(a.cov, lc, up_idx(D, i, j));
-                    const double old_sq = ca * *pc + mo[i] * mo[j];
-                    const double new_sq = old_sq + div_markstein(th[i] * th[j], Nd, rN);
-                    *pc = new_sq - cc * (mn[i] * mn[j]);
-                }
-            }
-#pragma unroll
-            for (int i = 0; i < D; ++i) *soa_ptr<D>(a.mean, lm, i) = mn[i];
-        }
+        // update_stats!' mean/cov recurrence runs batched over the launch in
+        // mix_moments_kernel; it reads θ from the θ history (FULL) or here:
+        if constexpr (!FULL) store_slot<D>(a.mom_theta + (uint64_t)s * D * C, soff, th);
     }
     a.ll[chain] = ll;
     a.ra[chain] = ra;
@@ -318,6 +292,106 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
     a.nacc[chain] = nacc;
     a.faults[chain] = faults;
     store_state<D>(a.theta, C, chain, 0, th, false);
+}
+
+// ---- GenericChainStats mean/cov (chain_statistics.jl:46-49), batched ----------
+// Nothing reads the running cov between readjusts (the proposals use L_B), so
+// the recurrence of every step of a launch runs here, after the step kernel,
+// from the θ history of the launch.  Each cov element follows exactly the
+// per-step recurrence (elements are independent):
+//   old = (N−1)/N·c + m_i m_j;  new = old + (θ_i θ_j)/N;  c = new − (N+1)/N·(m'_i m'_j)
+//   m' = m·(N/(N+1)) + θ/(N+1)
+// One thread per (chain, tile): tiles are TB×TB blocks (bi ≤ bj) of the upper
+// triangle; a tile sweeps the launch's steps with its cov block, the means of
+// its coordinates and their θ in registers.  The cov is read and written once
+// per launch instead of once per step.
+struct MixMomentsParams {
+    const double *theta;  // θ after step s of the launch at theta + s·D·C (state_pos layout)
+    double *mean;         // [D] state_pos
+    double *cov;          // [DP] packed upper
+    uint64_t C;
+    uint64_t N0;          // GenericChainStats.N at the launch's first step
+    uint32_t nsteps;
+};
+
+template <int D>
+struct MomentTiles {
+    static constexpr int TB = D <= 8 ? D : 8;  // tile edge
+    static constexpr int NB = D / TB;          // blocks per edge
+    static constexpr int NT = NB * (NB + 1) / 2;
+};
+
+template <int D>
+__global__ void __launch_bounds__(256) mix_moments_kernel(const MixMomentsParams a) {
+    constexpr int DP = packed_n(D);
+    constexpr int TB = MomentTiles<D>::TB, NB = MomentTiles<D>::NB;
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint64_t C = a.C;
+    // tile (bi, bj), bi ≤ bj, from blockIdx.y (uniform)
+    int bi = 0, rem = (int)blockIdx.y;
+    while (rem >= NB - bi) {
+        rem -= NB - bi;
+        ++bi;
+    }
+    const int bj = bi + rem;
+    const bool diag = bi == bj;
+    const int i0 = bi * TB, j0 = bj * TB;
+    const LaneSoA lm = lane_soa(C, chain, D), lc = lane_soa(C, chain, DP);
+    double c[TB][TB], mi[TB], mj[TB];
+#pragma unroll
+    for (int u = 0; u < TB; ++u) {
+        mi[u] = *soa_ptr<D>(a.mean, lm, i0 + u);
+        mj[u] = *soa_ptr<D>(a.mean, lm, j0 + u);
+#pragma unroll
+        for (int v = 0; v < TB; ++v)
+            if (!diag || u <= v) c[u][v] = *soa_ptr<DP>(a.cov, lc, up_idx(D, i0 + u, j0 + v));
+    }
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint64_t N = a.N0 + s;
+        const double Nd = (double)N, N1d = (double)(N + 1);
+        const double ca = (double)(N - 1) / Nd, cb = Nd / N1d, cc = N1d / Nd;
+        const double rN = 1.0 / Nd, rN1 = 1.0 / N1d;
+        const LaneSoA lt = lane_soa(C, chain, D);
+        const double *ths = a.theta + (uint64_t)s * D * C;
+        double ti[TB], tj[TB];
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+            ti[u] = *soa_ptr<D>(ths, lt, i0 + u);
+            tj[u] = diag ? ti[u] : *soa_ptr<D>(ths, lt, j0 + u);
+        }
+        // old_sq + (θ_i θ_j)/N with the means before the step, then the means in
+        // place (m' = m·cb + θ/(N+1)) and the subtraction: two passes keep one
+        // set of mean registers
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+            for (int v = 0; v < TB; ++v)
+                if (!diag || u <= v) {
+                    const double old_sq = ca * c[u][v] + mi[u] * mj[v];
+                    c[u][v] = old_sq + div_markstein(ti[u] * tj[v], Nd, rN);
+                }
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+            mi[u] = mi[u] * cb + div_markstein(ti[u], N1d, rN1);
+            mj[u] = diag ? mi[u] : mj[u] * cb + div_markstein(tj[u], N1d, rN1);
+        }
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+            for (int v = 0; v < TB; ++v)
+                if (!diag || u <= v) c[u][v] = c[u][v] - cc * (mi[u] * mj[v]);
+    }
+    // fresh opaque strides: the load addresses above are not kept live across the sweep
+    const LaneSoA lm2 = lane_soa(C, chain, D), lc2 = lane_soa(C, chain, DP);
+#pragma unroll
+    for (int u = 0; u < TB; ++u)
+#pragma unroll
+        for (int v = 0; v < TB; ++v)
+            if (!diag || u <= v) *soa_ptr<DP>(a.cov, lc2, up_idx(D, i0 + u, j0 + v)) = c[u][v];
+    if (diag)
+#pragma unroll
+        for (int u = 0; u < TB; ++u) *soa_ptr<D>(a.mean, lm2, i0 + u) = mi[u];
 }
 
 // ---- HaarioTypeAdaptation readjust! (adaptation.jl:422-426) -----------------

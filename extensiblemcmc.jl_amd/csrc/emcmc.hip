@@ -172,6 +172,7 @@ struct emcmc_handle {
     // per-chain Σ_B factor, Haario M (same for every chain)
     double *d_mean = nullptr, *d_cov = nullptr, *d_LB = nullptr, *d_iLB = nullptr, *d_c0B = nullptr;
     double *d_Lnew = nullptr;
+    double *d_mean_alt = nullptr;  // the moments kernel's output mean (swapped with d_mean per launch)
     double *d_mom_scratch = nullptr;  // ACCEPT_ONLY: θ of each step of a launch, for the moments kernel
     uint32_t mix_M = 0;
     // MALA path: carried ∇ℓ(θ) (state_pos layout), padded X and y
@@ -350,6 +351,7 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
         const uint64_t DP = (uint64_t)packed_n((int)D);
         const UpdateHost &u = h->updates[0];
         HIPCHK(h, hipMalloc(&h->d_mean, C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_mean_alt, C * D * sizeof(double)));
         HIPCHK(h, hipMalloc(&h->d_cov, C * DP * sizeof(double)));
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) {
             HIPCHK(h, hipMalloc(&h->d_LB, C * DP * sizeof(double)));
@@ -887,6 +889,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             MixMomentsParams mp{};
             mp.theta = p.hist_theta ? p.hist_theta + (uint64_t)(p.iter0 - 1) * h->cfg.dim * C : h->d_mom_scratch;
             mp.mean = h->d_mean;
+            mp.mean_out = h->d_mean_alt;
             mp.cov = h->d_cov;
             mp.C = C;
             mp.N0 = p.N0;
@@ -894,6 +897,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             void *margs[] = {&mp};
             const dim3 mgrid((unsigned)((C + 255) / 256), (unsigned)h->var.mo_tiles);
             HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mofn), mgrid, block, margs, 0, h->stream));
+            std::swap(h->d_mean, h->d_mean_alt);
         }
         h->stats_N += n;
         if (haario) {
@@ -1465,7 +1469,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
-                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch};
+                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);

@@ -304,10 +304,15 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
 // One thread per (chain, tile): tiles are TB×TB blocks (bi ≤ bj) of the upper
 // triangle; a tile sweeps the launch's steps with its cov block, the means of
 // its coordinates and their θ in registers.  The cov is read and written once
-// per launch instead of once per step.
+// per launch instead of once per step.  The means are double-buffered: the
+// off-diagonal tiles of a chain may run after its diagonal tiles have finished
+// (blocks of later blockIdx.y start as earlier ones retire), so an in-place
+// mean update would be read back by them.
 struct MixMomentsParams {
     const double *theta;  // θ after step s of the launch at theta + s·D·C (state_pos layout)
-    double *mean;         // [D] state_pos
+    const double *mean;   // [D] state_pos, before the launch
+    double *mean_out;     // [D] state_pos, after the launch (a different buffer: every tile
+                          // of a chain reads `mean`, only the diagonal tiles write)
     double *cov;          // [DP] packed upper
     uint64_t C;
     uint64_t N0;          // GenericChainStats.N at the launch's first step
@@ -391,7 +396,7 @@ __global__ void __launch_bounds__(256) mix_moments_kernel(const MixMomentsParams
             if (!diag || u <= v) *soa_ptr<DP>(a.cov, lc2, up_idx(D, i0 + u, j0 + v)) = c[u][v];
     if (diag)
 #pragma unroll
-        for (int u = 0; u < TB; ++u) *soa_ptr<D>(a.mean, lm2, i0 + u) = mi[u];
+        for (int u = 0; u < TB; ++u) *soa_ptr<D>(a.mean_out, lm2, i0 + u) = mi[u];
 }
 
 // ---- HaarioTypeAdaptation readjust! (adaptation.jl:422-426) -----------------

@@ -162,3 +162,35 @@ def test_mix_rejects_unsupported_shapes():
     with pytest.raises(L.EMCMCError) as e:
         eng.set_gsn_target(mu, ts, obs)
     assert e.value.status == L.UNSUPPORTED_PLUGIN
+
+
+@pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
+def test_cfg4_shape_moments_match_oracle_on_sampled_chains(oracle, hist):
+    """The cfg 4 shape (131,072 chains, D = 32): the moments kernel's grid is
+    far larger than the chip, so tiles of one chain run at different times —
+    every tile must see the launch's input means (regression: off-diagonal
+    tiles read means already advanced by the diagonal tiles of the same chain).
+    Sampled chains are replayed on the oracle through two readjusts."""
+    D, C, M, k = 32, 131072, 60, 20
+    w = W.cfg4(C, k=k)
+    eng = _engine(D, C, M, w.seed, w.mu_true, w.t_sigma, w.obs, w.rw_sigma, w.sigma_b, w.lam, k, L.LL_PER_OBS, hist,
+                  spl=20)
+    eng.run_iters(1, 10)
+    eng.run_iters(11, M - 10)
+    eng.synchronize(allow_faults=True)
+    th, ll = eng.get_state()
+    mean, cov = eng.get_chain_moments()
+    Lb, _ = eng.get_mix_state(1)
+    acc = eng.get_history(L.H_ACCEPT, 1, M)[:, 0]
+    faults = eng.get_faults()
+    picks = [0, 1, 4095, 70001, C - 1]
+    for c in picks:
+        st = oracle.MixState(np.zeros((1, D)), sigma_b=w.sigma_b)
+        h = oracle.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=M,
+                           lam=w.lam, haario_k=k, chain0=c)
+        assert np.array_equal(acc[:, c], h["acc"][:, 0]), c
+        assert np.array_equal(th[c], st.theta[0]) and ll[c] == st.ll[0], c
+        assert np.array_equal(mean[c], st.mean[0]), c
+        assert np.array_equal(cov[c], st.cov[0]), c
+        assert np.array_equal(Lb[c], st.LB[0]), c
+        assert faults[c] == st.faults[0], c

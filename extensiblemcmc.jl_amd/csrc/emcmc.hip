@@ -32,7 +32,7 @@ namespace {
 
 constexpr uint32_t kDefaultRollWindow = 100;  // chain_statistics.jl:27
 constexpr uint32_t kDefaultStepsPerLaunch = 64;
-constexpr size_t kMaxLds = 64 * 1024;
+constexpr size_t kMaxLds = 160 * 1024;  // gfx950: 160 KiB of LDS per CU, all of it addressable by one workgroup
 
 // ----------------------------------------------------------------------------
 // Canonical Cholesky (lower factor L of the upper-stored symmetric Σ), the
@@ -394,6 +394,14 @@ const std::vector<MwgEntry> &mwg_table() {
 // Every schedule but one joint GaussianRandomWalk update on coords 1:D runs on
 // mwg_gsn_kernel: per-update constants as MwgUpdate records (scalar loads),
 // target factor / x̄ / observations in plain global memory.
+// Dynamic LDS beyond 64 KiB in total (with the static tables) must be allowed
+// per kernel.
+emcmc_status allow_lds(emcmc_handle *h, const void *fn, size_t bytes) {
+    if (fn && kZigLdsBytes + bytes > 64 * 1024)
+        HIPCHK(h, hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    return EMCMC_OK;
+}
+
 emcmc_status select_mwg(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
@@ -452,7 +460,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
     snprintf(nm, sizeof nm, "mwg_gsn_kernel<D=%d,P=%zu,%s,%s>", D, h->updates.size(), full ? "FULL" : "ACCEPT_ONLY",
              ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
     v.name = nm;
-    h->lds_bytes = sizeof(Ziggurat);
+    h->lds_bytes = 0;  // tables only, in static LDS
     h->var = v;
     return EMCMC_OK;
 }
@@ -554,8 +562,8 @@ emcmc_status select_mix(emcmc_handle *h) {
     std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
     std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    const size_t lds = sizeof(Ziggurat) + (c.size() + obs_doubles) * sizeof(double);
-    if (lds > kMaxLds)
+    const size_t lds = (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
+    if (kZigLdsBytes + lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu", lds,
                     kMaxLds, (unsigned long long)t.nobs);
@@ -567,6 +575,7 @@ emcmc_status select_mix(emcmc_handle *h) {
     HIPCHK(h, hipMalloc(&h->d_obs, t.obs.size() * sizeof(double)));
     HIPCHK(h, hipMemcpy(h->d_obs, t.obs.data(), t.obs.size() * sizeof(double), hipMemcpyHostToDevice));
     h->lds_bytes = lds;
+    if (emcmc_status st2 = allow_lds(h, reinterpret_cast<const void *>(v.xfn), lds)) return st2;
     h->var = v;
     return EMCMC_OK;
 }
@@ -692,9 +701,9 @@ emcmc_status select_variant(emcmc_handle *h) {
         std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     }
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    size_t lds = sizeof(Ziggurat) + (c.size() + obs_doubles) * sizeof(double);
+    size_t lds = (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
     if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc);
-    if (lds > kMaxLds)
+    if (kZigLdsBytes + lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu",
                     lds, kMaxLds, (unsigned long long)t.nobs);
@@ -708,6 +717,7 @@ emcmc_status select_variant(emcmc_handle *h) {
         HIPCHK(h, hipMemcpy(h->d_obs, t.obs.data(), t.obs.size() * sizeof(double), hipMemcpyHostToDevice));
     }
     h->lds_bytes = lds;
+    if (emcmc_status st2 = allow_lds(h, reinterpret_cast<const void *>(v.fn), lds)) return st2;
     h->var = v;
     return EMCMC_OK;
 }

@@ -88,21 +88,26 @@ __host__ __device__ __forceinline__ uint64_t state_pos(uint64_t d, uint64_t c, u
 
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-// Stage the ziggurat tables (12 KiB, 16-byte aligned at LDS offset 0) and then
-// `nconst` constants and `nobs_d` observation doubles behind them.
-constexpr int kZigLdsDoubles = (int)(sizeof(Ziggurat) / sizeof(double));
-__device__ __forceinline__ void stage_lds(double *lds, const Ziggurat *zig, const double *consts, int nconst,
-                                          const double *obs, int nobs_d) {
-    const double *zsrc = reinterpret_cast<const double *>(zig);
-    const int total = kZigLdsDoubles + nconst + nobs_d;
-    for (int i = threadIdx.x; i < total; i += blockDim.x) {
-        double v;
-        if (i < kZigLdsDoubles) v = zsrc[i];
-        else if (i < kZigLdsDoubles + nconst) v = consts[i - kZigLdsDoubles];
-        else v = obs[i - kZigLdsDoubles - nconst];
-        lds[i] = v;
-    }
+// Stage the LDS part of the ziggurat tables (N(0,1) 4096 + Exp(1) 256 layers,
+// 70 KiB) into the kernel's STATIC LDS — their addresses are then link-time
+// constants that fold into the ds_read offset field — and `nconst` constants
+// followed by `nobs_d` observation doubles into the dynamic LDS at offset 0
+// (offsets below 64 KiB: a row's reads share one address register).
+struct ZigLds {
+    ZigEntry e[256];
+    double ef[256];
+    ZigEntry n[kZigNL];
+};
+static_assert(sizeof(ZigLds) == kZigLdsBytes, "LDS prefix of Ziggurat");
+__device__ __forceinline__ ZigTabs stage_lds(double *lds, const Ziggurat *zig, const double *consts, int nconst,
+                                             const double *obs, int nobs_d) {
+    __shared__ ZigLds tabs;
+    const d2v *zsrc = reinterpret_cast<const d2v *>(zig);
+    d2v *zdst = reinterpret_cast<d2v *>(&tabs);
+    for (int i = threadIdx.x; i < (int)(kZigLdsBytes / 16); i += blockDim.x) zdst[i] = zsrc[i];
+    for (int i = threadIdx.x; i < nconst + nobs_d; i += blockDim.x) lds[i] = (i < nconst) ? consts[i] : obs[i - nconst];
     __syncthreads();
+    return ZigTabs{tabs.n, zig->nf, tabs.e, tabs.ef};
 }
 
 #ifndef EMCMC_SERIAL_PAIRS
@@ -119,7 +124,7 @@ constexpr bool kSerialPairs = EMCMC_SERIAL_PAIRS != 0;
 // (with 64 lanes × N draws per wave most steps take one trip, so the trip only
 // fixes z[i]; the proposal arithmetic runs once, after it).
 template <int N>
-__device__ __forceinline__ void propose_diag(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+__device__ __forceinline__ void propose_diag(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain,
                                              uint32_t iter, uint32_t pidx0, uint32_t g0, const double (&base)[N],
                                              const double *scale, double (&out)[N], uint32_t &faults) {
     constexpr int NP = (N + 1) / 2;
@@ -128,20 +133,23 @@ __device__ __forceinline__ void propose_diag(const Ziggurat &zt, uint32_t key0, 
     for (int j = 0; j < NP; ++j) {
         if constexpr (kSerialPairs) __builtin_amdgcn_sched_barrier(0);
         const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
-        if (!zig_normal_fast(zig_split(r.x, r.y), zt.n, out[2 * j])) pend |= 1u << (2 * j);
+        if (!zig_normal_fast(zig_split_n(r.x, r.y), zt.n, out[2 * j])) pend |= 1u << (2 * j);
         if (2 * j + 1 < N)
-            if (!zig_normal_fast(zig_split(r.z, r.w), zt.n, out[2 * j + 1])) pend |= 1u << (2 * j + 1);
+            if (!zig_normal_fast(zig_split_n(r.z, r.w), zt.n, out[2 * j + 1])) pend |= 1u << (2 * j + 1);
     }
     if constexpr ((EMCMC_ABLATE & 2) != 0) pend = 0;  // timing-only build: no rare paths
+    // wave-uniform loop, one pending draw per lane per trip (with 4096 normal
+    // layers a wave of 1024 draws has ≈ 1.2 pending, usually on one lane); the
+    // result is written with selects OUTSIDE the divergent region, so the
+    // per-element update stays branch-free v_cndmask code
     while (__ballot(pend != 0) != 0) {
-        if (pend != 0) {
-            const int i = __builtin_ctz(pend);
-            pend &= pend - 1;
-            const double z = normal_draw(zt, key0, key1, chain, iter, pidx0, g0 + (uint32_t)i, faults);
+        const bool act = pend != 0;
+        const uint32_t i = act ? (uint32_t)__builtin_ctz(pend) : 0xFFu;
+        pend &= pend - 1;
+        double z = 0.0;
+        if (act) z = normal_draw(zt, key0, key1, chain, iter, pidx0, g0 + i, faults);
 #pragma unroll
-            for (int q = 0; q < N; ++q)
-                if (q == i) out[q] = z;
-        }
+        for (int q = 0; q < N; ++q) out[q] = (i == (uint32_t)q) ? z : out[q];
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = base[i] + scale[i] * out[i];
@@ -179,7 +187,7 @@ struct WaveScratch {
 // (batched only for ≤ 16 coordinates per lane: 4 waves × 64 lanes × 16 × 8 B
 // = 32 KiB of normals per block keeps the block within 64 KiB of LDS)
 #ifndef EMCMC_BATCHED
-#define EMCMC_BATCHED 1
+#define EMCMC_BATCHED 0  // 1: wave-batched rare paths (the better choice with 256 normal layers)
 #endif
 constexpr bool diag_batched(int D, int LPC) { return EMCMC_BATCHED && (D / LPC) % 2 == 0 && D / LPC <= 16; }
 constexpr size_t diag_scratch_bytes(int D, int LPC) {
@@ -204,7 +212,7 @@ __device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
 // normal g0 + i of chain `chain`); LPC lanes per chain, so lane L of the wave
 // owns chain gid0 + L/LPC and normals (L % LPC)·N + i.
 template <int N, int LPC>
-__device__ __forceinline__ void propose_diag_batched(const Ziggurat &zt, const WaveScratch<N> &ws, uint32_t key0,
+__device__ __forceinline__ void propose_diag_batched(const ZigTabs &zt, const WaveScratch<N> &ws, uint32_t key0,
                                                      uint32_t key1, uint32_t chain, uint32_t wave_gid0,
                                                      uint32_t iter, uint32_t pidx0, uint32_t g0,
                                                      const double (&base)[N], const double *scale,
@@ -224,8 +232,8 @@ __device__ __forceinline__ void propose_diag_batched(const Ziggurat &zt, const W
         if (j < N / 2) {
             __builtin_amdgcn_sched_barrier(0);
             const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
-            na = zig_split(r.x, r.y);
-            nb = zig_split(r.z, r.w);
+            na = zig_split_n(r.x, r.y);
+            nb = zig_split_n(r.z, r.w);
             sa = zig_entry(zt.n, na);
             sb = zig_entry(zt.n, nb);
         }
@@ -310,7 +318,7 @@ __device__ __forceinline__ void propose_diag_batched(const Ziggurat &zt, const W
 
 // The N standard normals themselves (dense-L proposals).
 template <int N>
-__device__ __forceinline__ void normals(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+__device__ __forceinline__ void normals(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain,
                                         uint32_t iter, uint32_t pidx0, double (&z)[N], uint32_t &faults) {
     constexpr int NP = (N + 1) / 2;
     uint64_t pend = 0;
@@ -318,9 +326,9 @@ __device__ __forceinline__ void normals(const Ziggurat &zt, uint32_t key0, uint3
     for (int j = 0; j < NP; ++j) {
         if constexpr (N > 8) __builtin_amdgcn_sched_barrier(0);  // one Philox block at a time
         const u32x4 r = draw(key0, key1, chain, iter, j, pidx0, 0);
-        if (!zig_normal_fast(zig_split(r.x, r.y), zt.n, z[2 * j])) pend |= 1ull << (2 * j);
+        if (!zig_normal_fast(zig_split_n(r.x, r.y), zt.n, z[2 * j])) pend |= 1ull << (2 * j);
         if (2 * j + 1 < N)
-            if (!zig_normal_fast(zig_split(r.z, r.w), zt.n, z[2 * j + 1])) pend |= 1ull << (2 * j + 1);
+            if (!zig_normal_fast(zig_split_n(r.z, r.w), zt.n, z[2 * j + 1])) pend |= 1ull << (2 * j + 1);
     }
     while (__ballot(pend != 0) != 0) {
         if (pend != 0) {
@@ -339,7 +347,7 @@ __device__ __forceinline__ void normals(const Ziggurat &zt, uint32_t key0, uint3
 // half a block per step.  `first` forces the block at the launch's first step.
 struct AcceptStream {
     u32x4 r;
-    __device__ __forceinline__ double next(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain,
+    __device__ __forceinline__ double next(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain,
                                            uint32_t iter, uint32_t pidx0, bool first, uint32_t &faults) {
         if (first || (iter & 1u) == 0) r = draw(key0, key1, chain, iter >> 1, kBlockAccept, pidx0, 0);
         const ZigDraw d = accept_split(r, iter);
@@ -354,8 +362,10 @@ struct AcceptStream {
 template <int CTRL>
 __device__ __forceinline__ double dpp_perm(double v) {
     const uint64_t b = __builtin_bit_cast(uint64_t, v);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, false);
+    // mov_dpp: every lane of a quad permute has a source, so no "old" value is
+    // needed (update_dpp(0, …) materialises one with an extra v_mov per dword)
+    const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
     return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 // quad_perm [1,0,3,2] = 0xB1 (xor 1), [2,3,0,1] = 0x4E (xor 2)
@@ -607,9 +617,8 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 4 * D;
-    stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
-    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
-    const double *cst0 = lds + kZigLdsDoubles;
+    const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
+    const double *cst0 = lds;
 
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t chain = tid / LPC;
@@ -629,7 +638,7 @@ __global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParam
     uint32_t nacc = chain_elem(a.nacc, c32);
     uint32_t faults = chain_elem(a.faults, c32);
     constexpr bool kBatched = diag_batched(D, LPC);
-    const size_t used = lds_align16(sizeof(Ziggurat) + sizeof(double) * (size_t)(nconst + ((LLMODE == LL_PER_OBS) ? (int)nobs * D : 0)));
+    const size_t used = lds_align16(sizeof(double) * (size_t)(nconst + ((LLMODE == LL_PER_OBS) ? (int)nobs * D : 0)));
     const WaveScratch<DPL> ws(reinterpret_cast<char *>(lds) + used +
                               (threadIdx.x >> 6) * (size_t)WaveScratch<DPL>::kBytes);
     const uint32_t wave_gid0 = a.chain0 + (uint32_t)((tid & ~(uint64_t)63) / LPC);
@@ -766,9 +775,8 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 2 * D * D + 3 * D;
-    stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
-    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
-    const double *cst = lds + kZigLdsDoubles;
+    const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
+    const double *cst = lds;
     const double *Lrw = cst;
     const double *iLrw = cst + D * D;
     const double *Lt = cst + D * D + D;
@@ -964,8 +972,8 @@ probe_variates_kernel(const Ziggurat *__restrict__ zig, uint32_t key0, uint32_t 
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     uint32_t faults = 0;
-    for (uint32_t j = 0; j < D; ++j) z[t * D + j] = normal_draw(*zig, key0, key1, chains[t], iters[t], pidx0, j, faults);
-    E[t] = exp_draw(*zig, key0, key1, chains[t], iters[t], pidx0, faults);
+    for (uint32_t j = 0; j < D; ++j) z[t * D + j] = normal_draw(zig_tabs(*zig), key0, key1, chains[t], iters[t], pidx0, j, faults);
+    E[t] = exp_draw(zig_tabs(*zig), key0, key1, chains[t], iters[t], pidx0, faults);
 }
 
 __global__ void __launch_bounds__(256) probe_log_kernel(const double *__restrict__ x, double *__restrict__ y,

@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
             const double th = valid ? a.theta[pos(4 * j + g, ch)] : 0.0;
             if constexpr (MODE == 0) {
                 const double gr = valid ? a.grad[pos(4 * j + g, ch)] : 0.0;
-                const double z = normal_draw(*a.zig, a.key0, a.key1, gid, a.iter, 0, (uint32_t)(4 * j + g), faults);
+                const double z = normal_draw(zig_tabs(*a.zig), a.key0, a.key1, gid, a.iter, 0, (uint32_t)(4 * j + g), faults);
                 const double m = th + a.h * gr;
                 tp[j] = m + a.eps * z;
                 const double v = (tp[j] - m) * a.ieps;
@@ -218,7 +218,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
     const double ll = valid ? a.ll[chain] : 0.0;
     if (!(llp - llp == 0.0)) faults |= 1u;
     const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + 0.0) - 0.0;
-    const double E = exp_draw(*a.zig, a.key0, a.key1, gid, a.iter, 0, faults);
+    const double E = exp_draw(zig_tabs(*a.zig), a.key0, a.key1, gid, a.iter, 0, faults);
     const bool acc = E > -llr;
     // the four lanes of a chain drew different normals: merge their fault bits
     faults |= (uint32_t)__shfl_xor((int)faults, 16);

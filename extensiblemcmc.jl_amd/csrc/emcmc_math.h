@@ -20,6 +20,7 @@
 // "Hard parts" 1), so the stream is defined here and shared with oracle/.
 #pragma once
 
+#include <stddef.h>
 #include <stdint.h>
 #include <math.h>
 
@@ -238,48 +239,67 @@ EMCMC_HD double log_any(double x) {
     return log_pos(x);
 }
 
-// ---- Marsaglia–Tsang ziggurat, 256 layers (J. Stat. Softw. 5(8), 2000) ------
+// ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---------------
 // The same sampler family as Julia's randn/randexp (Random stdlib), fed by the
-// Philox stream.  One 64-bit draw (hi:lo) per variate:
-//   layer = lo[11:4]   sign = lo[0]   magnitude u = (hi:lo)[63:12] / 2^52
-// Bits lo[3:1] are unused.  The layout is chosen for gfx950: the LDS byte
-// address of the 16-byte table entry is lo & 0xFF0, and v = 1 + u is built
-// directly as a double from two v_alignbit_b32, so the fast path is
-//   x = fma(v, W, −W) = u·W (one rounding, the bits of (double)mag · W/2^52),
-//   accepted iff v < 1 + k/2^52 (the integer test mag < k, exactly).
-// ≈ 99% of draws take the fast path; wedge/tail draws use the portable
+// Philox stream: 4096 layers for N(0,1), 256 for Exp(1).  One 64-bit draw
+// (hi:lo) per variate.
+//   N(0,1): layer = lo[11:0], magnitude = (hi:lo)[63:12] (52 bits), sign = lo[12]
+//           (the sign shares the magnitude's last bit, as Julia's randn shares
+//           its 8 layer bits with the magnitude: Random/src/normal.jl)
+//   Exp(1): layer = lo[11:4], magnitude = (hi:lo)[63:12] (52 bits), lo[3:0] unused
+// The LDS byte address of the 16-byte table entry is (layer << 4), and
+// v = 1 + u (u = magnitude / 2^bits) is built directly as a double from two
+// v_alignbit_b32, so the fast path is
+//   x = fma(v, W, −W) = u·W (one rounding, the bits of (double)mag · W/2^bits),
+//   accepted iff v < 1 + k/2^bits (the integer test mag < k, exactly).
+// With 4096 normal layers 99.88 % of draws take the fast path (256 layers:
+// 98.5 %), so a wave drawing 1024 normals needs a rare-path pass on ≈ 70 % of
+// its steps instead of on every step.  Wedge/tail draws use the portable
 // log/exp above with fresh counter blocks.  Tables are built on the host by
 // build_ziggurat() (oracle/ restates the same construction).
-constexpr double kZigNR = 3.6541528853610088;       // normal: rightmost layer edge r
-constexpr double kZigNV = 4.92867323399e-3;         // normal: area per layer v
-constexpr double kZigNInvR = 1.0 / 3.6541528853610088;
-constexpr double kZigER = 7.69711747013104972;      // exponential: r
+constexpr int kZigNL = 4096;                        // normal layers
+constexpr double kZigNR = 4.3859450348713045;       // normal: rightmost layer edge r (4096 layers)
+constexpr double kZigNV = 3.061541032784645e-4;     // normal: area per layer v
+constexpr double kZigNInvR = 1.0 / 4.3859450348713045;
+constexpr double kZigER = 7.69711747013104972;      // exponential: r (256 layers)
 constexpr double kZigEV = 3.949659822581572e-3;     // exponential: v
 
 struct ZigEntry {
-    double kv;  // 1 + k/2^52: fast-accept bound on v = 1 + u
+    double kv;  // 1 + k/2^bits: fast-accept bound on v = 1 + u
     double w;   // layer width x_i (base layer: q = v/f(r))
 };
+// Layout: the prefix [e, ef, n] is what the step kernels stage into LDS
+// (70 KiB); nf is read from global memory on the rare path only.
 struct Ziggurat {
-    ZigEntry n[256];
-    double nf[256];  // exp(−x_i²/2)
     ZigEntry e[256];
     double ef[256];  // exp(−x_i)
+    ZigEntry n[kZigNL];
+    double nf[kZigNL];  // exp(−x_i²/2)
 };
+constexpr size_t kZigLdsBytes = offsetof(Ziggurat, nf);
 
+// Where a kernel finds the tables (LDS prefix + global nf, or all global).
+struct ZigTabs {
+    const ZigEntry *n;
+    const double *nf;
+    const ZigEntry *e;
+    const double *ef;
+};
+EMCMC_HD ZigTabs zig_tabs(const Ziggurat &z) { return ZigTabs{z.n, z.nf, z.e, z.ef}; }
 inline void build_ziggurat(Ziggurat &z) {
-    const double m = 0x1p52;
-    auto kv = [](uint64_t k) { return u2d(0x3FF0000000000000ull | k); };
-    {  // N(0,1), f(x) = exp(−x²/2)
+    {  // N(0,1), f(x) = exp(−x²/2), 52-bit magnitudes
+        const double m = 0x1p52;
+        auto kv = [](uint64_t k) { return u2d(0x3FF0000000000000ull | k); };
+        constexpr int L = kZigNL;
         double dn = kZigNR, tn = dn;
         const double q = kZigNV / exp_nonpos(-0.5 * (dn * dn));
         z.n[0].kv = kv((uint64_t)((dn / q) * m));
         z.n[1].kv = kv(0);
         z.n[0].w = q;
-        z.n[255].w = dn;
+        z.n[L - 1].w = dn;
         z.nf[0] = 1.0;
-        z.nf[255] = exp_nonpos(-0.5 * (dn * dn));
-        for (int i = 254; i >= 1; --i) {
+        z.nf[L - 1] = exp_nonpos(-0.5 * (dn * dn));
+        for (int i = L - 2; i >= 1; --i) {
             dn = sqrt(-2.0 * log_pos(kZigNV / dn + exp_nonpos(-0.5 * (dn * dn))));
             z.n[i + 1].kv = kv((uint64_t)((dn / tn) * m));
             tn = dn;
@@ -287,7 +307,9 @@ inline void build_ziggurat(Ziggurat &z) {
             z.n[i].w = dn;
         }
     }
-    {  // Exp(1), f(x) = exp(−x)
+    {  // Exp(1), f(x) = exp(−x), 52-bit magnitudes
+        const double m = 0x1p52;
+        auto kv = [](uint64_t k) { return u2d(0x3FF0000000000000ull | k); };
         double de = kZigER, te = de;
         const double q = kZigEV / exp_nonpos(-de);
         z.e[0].kv = kv((uint64_t)((de / q) * m));
@@ -308,13 +330,29 @@ inline void build_ziggurat(Ziggurat &z) {
 
 struct ZigDraw {
     uint32_t off;   // byte offset of the layer's ZigEntry (layer · 16)
-    uint32_t sbit;  // sign in bit 31
-    double v;       // 1 + u, u = 52-bit magnitude / 2^52
+    uint32_t sbit;  // sign in bit 31 (normals)
+    double v;       // 1 + u
 };
-EMCMC_HD ZigDraw zig_split(uint32_t hi, uint32_t lo) {
+// N(0,1) draw: layer lo[11:0], magnitude (hi:lo)[63:12], sign lo[12]
+EMCMC_HD ZigDraw zig_split_n(uint32_t hi, uint32_t lo) {
+    ZigDraw d;
+    d.off = (lo << 4) & 0xFFF0u;
+    d.sbit = (lo << 19) & 0x80000000u;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t vlo = __builtin_amdgcn_alignbit(hi, lo, 12);
+    const uint32_t vhi = __builtin_amdgcn_alignbit(0x3FFu, hi, 12);
+#else
+    const uint32_t vlo = (hi << 20) | (lo >> 12);
+    const uint32_t vhi = 0x3FF00000u | (hi >> 12);
+#endif
+    d.v = u2d(((uint64_t)vhi << 32) | vlo);
+    return d;
+}
+// Exp(1) draw: layer lo[11:4], magnitude (hi:lo)[63:12]
+EMCMC_HD ZigDraw zig_split_e(uint32_t hi, uint32_t lo) {
     ZigDraw d;
     d.off = lo & 0xFF0u;
-    d.sbit = lo << 31;
+    d.sbit = 0;
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t vlo = __builtin_amdgcn_alignbit(hi, lo, 12);
     const uint32_t vhi = __builtin_amdgcn_alignbit(0x3FFu, hi, 12);
@@ -366,7 +404,7 @@ EMCMC_HD double zig_normal_slow(ZigDraw d, const ZigEntry *tab, const double *f,
             const double x = zig_scale(d.v, tab[L].w);
             const double u = u01_closed0(b.x, b.y);
             if (fma(u, f[L - 1] - f[L], f[L]) < exp_nonpos(-0.5 * (x * x))) return with_sign(x, d.sbit);
-            d = zig_split(b.z, b.w);
+            d = zig_split_n(b.z, b.w);
             double z;
             if (zig_normal_fast(d, tab, z)) return z;
         }
@@ -394,7 +432,7 @@ EMCMC_HD double zig_exp_slow(ZigDraw d, const ZigEntry *tab, const double *f, ui
         const double x = zig_scale(d.v, tab[L].w);
         const double u = u01_closed0(b.x, b.y);
         if (fma(u, f[L - 1] - f[L], f[L]) < exp_nonpos(-x)) return x;
-        d = zig_split(b.z, b.w);
+        d = zig_split_e(b.z, b.w);
         double e;
         if (zig_exp_fast(d, tab, e)) return e;
     }
@@ -403,20 +441,20 @@ EMCMC_HD double zig_exp_slow(ZigDraw d, const ZigEntry *tab, const double *f, ui
 // The attempt-0 draw of the accept exponential of `iter` (shared block, see
 // kBlockAccept).
 EMCMC_HD ZigDraw accept_split(const u32x4 &r, uint32_t iter) {
-    return (iter & 1u) ? zig_split(r.z, r.w) : zig_split(r.x, r.y);
+    return (iter & 1u) ? zig_split_e(r.z, r.w) : zig_split_e(r.x, r.y);
 }
 
 // Scalar reference forms (probes, host code): the full draw of normal gj and
 // of the accept exponential.
-EMCMC_HD double normal_draw(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
+EMCMC_HD double normal_draw(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
                             uint32_t pidx0, uint32_t gj, uint32_t &faults) {
     const u32x4 r = draw(key0, key1, chain, iter, gj >> 1, pidx0, 0);
-    const ZigDraw d = (gj & 1u) ? zig_split(r.z, r.w) : zig_split(r.x, r.y);
+    const ZigDraw d = (gj & 1u) ? zig_split_n(r.z, r.w) : zig_split_n(r.x, r.y);
     double z;
     if (zig_normal_fast(d, zt.n, z)) return z;
     return zig_normal_slow(d, zt.n, zt.nf, key0, key1, chain, iter, pidx0, gj, faults);
 }
-EMCMC_HD double exp_draw(const Ziggurat &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
+EMCMC_HD double exp_draw(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain, uint32_t iter,
                          uint32_t pidx0, uint32_t &faults) {
     const u32x4 r = draw(key0, key1, chain, iter >> 1, kBlockAccept, pidx0, 0);
     const ZigDraw d = accept_split(r, iter);

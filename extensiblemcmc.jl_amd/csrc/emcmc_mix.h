@@ -153,8 +153,8 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
     constexpr int DP = packed_n(D);
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
-    stage_lds(lds, a.zig, a.consts, 2 * D * D + 3 * D, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
-    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
+    const ZigTabs zt =
+        stage_lds(lds, a.zig, a.consts, 2 * D * D + 3 * D, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
 
     const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
         // loads (up to 2·D² of them) must not be hoisted out of the step loop
         uint32_t o = 0;
         asm volatile("" : "+s"(o));
-        const double *LA = lds + kZigLdsDoubles + o;
+        const double *LA = lds + o;
         const double *iLA = LA + D * D;
         const double *Lt = LA + D * D + D;
         const double *iLt = LA + 2 * D * D + D;

@@ -129,13 +129,8 @@ __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, 
 template <int D, bool FULL, int LLMODE>
 __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
     static_assert(D <= kMwgMaxD, "MWG kernel supports D ≤ 16");
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    {  // ziggurat tables → LDS (the only lane-indexed constants)
-        const double *zsrc = reinterpret_cast<const double *>(a.zig);
-        for (int i = threadIdx.x; i < kZigLdsDoubles; i += blockDim.x) lds[i] = zsrc[i];
-        __syncthreads();
-    }
-    const Ziggurat &zt = *reinterpret_cast<const Ziggurat *>(lds);
+    // ziggurat tables → static LDS (the only lane-indexed constants)
+    const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
     const uint64_t C = a.C;

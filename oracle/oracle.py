@@ -217,10 +217,14 @@ def exponentials(seed, n, chain0=0, it=1):
     return out
 
 
+ZIG_NORMAL_LAYERS = 4096  # oracle_math.h ORC_ZN_L
+
+
 def zig_tables():
-    kn = np.empty(256, dtype=np.uint64)
+    kn = np.empty(ZIG_NORMAL_LAYERS, dtype=np.uint64)
     ke = np.empty(256, dtype=np.uint64)
-    wn, fn, we, fe = (np.empty(256) for _ in range(4))
+    wn, fn = np.empty(ZIG_NORMAL_LAYERS), np.empty(ZIG_NORMAL_LAYERS)
+    we, fe = np.empty(256), np.empty(256)
     u64 = C.POINTER(C.c_uint64)
     lib().orc_zig_tables_copy(kn.ctypes.data_as(u64), _d(wn), _d(fn), ke.ctypes.data_as(u64), _d(we), _d(fe))
     return {"kn": kn, "wn": wn, "fn": fn, "ke": ke, "we": we, "fe": fe}

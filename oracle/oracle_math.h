@@ -165,62 +165,74 @@ static inline double orc_log_any(double x) {
     return orc_log(x);
 }
 
-/* ---- 256-layer Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---- */
-#define ORC_ZN_R 3.6541528853610088
-#define ORC_ZN_V 4.92867323399e-3
+/* ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ----
+ * N(0,1): 4096 strips, Exp(1): 256 strips, 52-bit magnitudes.  r and v of the 4096-strip normal table solve the M&T closure
+ * (top strip area = v) to double precision. */
+#define ORC_ZN_L 4096
+#define ORC_ZN_R 4.3859450348713045
+#define ORC_ZN_V 3.061541032784645e-4
 #define ORC_ZE_R 7.69711747013104972
 #define ORC_ZE_V 3.949659822581572e-3
 
 typedef struct {
-    uint64_t kn[256];
-    double wn[256], fn[256];
+    uint64_t kn[ORC_ZN_L];
+    double wn[ORC_ZN_L], fn[ORC_ZN_L];
     uint64_t ke[256];
     double we[256], fe[256];
 } orc_zig_tables;
 
-/* zigset (M&T Fig. 1) for 256 strips and 52-bit magnitudes */
+/* zigset (M&T Fig. 1): strip i ≥ 1 spans [0, x_i] × [f(x_i), f(x_{i−1})],
+ * x_{L−1} = r; strip 0 is the base rectangle of width q = v/f(r) plus the tail */
 static inline void orc_zig_build(orc_zig_tables *t) {
-    const double m = 4503599627370496.0; /* 2^52 */
+    const double mn = 4503599627370496.0; /* 2^52 */
     double dn = ORC_ZN_R, tn = dn;
     double q = ORC_ZN_V / orc_exp_nonpos(-0.5 * (dn * dn));
-    t->kn[0] = (uint64_t)((dn / q) * m);
+    t->kn[0] = (uint64_t)((dn / q) * mn);
     t->kn[1] = 0;
-    t->wn[0] = q / m;
-    t->wn[255] = dn / m;
+    t->wn[0] = q / mn;
+    t->wn[ORC_ZN_L - 1] = dn / mn;
     t->fn[0] = 1.0;
-    t->fn[255] = orc_exp_nonpos(-0.5 * (dn * dn));
-    for (int i = 254; i >= 1; --i) {
+    t->fn[ORC_ZN_L - 1] = orc_exp_nonpos(-0.5 * (dn * dn));
+    for (int i = ORC_ZN_L - 2; i >= 1; --i) {
         dn = sqrt(-2.0 * orc_log(ORC_ZN_V / dn + orc_exp_nonpos(-0.5 * (dn * dn))));
-        t->kn[i + 1] = (uint64_t)((dn / tn) * m);
+        t->kn[i + 1] = (uint64_t)((dn / tn) * mn);
         tn = dn;
         t->fn[i] = orc_exp_nonpos(-0.5 * (dn * dn));
-        t->wn[i] = dn / m;
+        t->wn[i] = dn / mn;
     }
+    const double me = 4503599627370496.0; /* 2^52 */
     double de = ORC_ZE_R, te = de;
     q = ORC_ZE_V / orc_exp_nonpos(-de);
-    t->ke[0] = (uint64_t)((de / q) * m);
+    t->ke[0] = (uint64_t)((de / q) * me);
     t->ke[1] = 0;
-    t->we[0] = q / m;
-    t->we[255] = de / m;
+    t->we[0] = q / me;
+    t->we[255] = de / me;
     t->fe[0] = 1.0;
     t->fe[255] = orc_exp_nonpos(-de);
     for (int i = 254; i >= 1; --i) {
         de = -orc_log(ORC_ZE_V / de + orc_exp_nonpos(-de));
-        t->ke[i + 1] = (uint64_t)((de / te) * m);
+        t->ke[i + 1] = (uint64_t)((de / te) * me);
         te = de;
         t->fe[i] = orc_exp_nonpos(-de);
-        t->we[i] = de / m;
+        t->we[i] = de / me;
     }
 }
 
-/* one 64-bit draw: layer = lo[11:4], sign = lo[0], magnitude = hi:lo[31:12] (52 bits) */
+/* one 64-bit draw (hi:lo) */
 typedef struct {
     uint32_t layer, negative;
     uint64_t mag;
 } orc_zdraw;
 
-static inline orc_zdraw orc_zsplit(uint32_t hi, uint32_t lo) {
-    orc_zdraw d = {(lo >> 4) & 255u, lo & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
+/* normal: layer = lo[11:0], magnitude = (hi:lo)[63:12] (52 bits), sign = lo[12]
+ * (the magnitude's last bit; Julia's randn likewise reuses its layer bits) */
+static inline orc_zdraw orc_zsplit_n(uint32_t hi, uint32_t lo) {
+    orc_zdraw d = {lo & 4095u, (lo >> 12) & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
+    return d;
+}
+/* exponential: layer = lo[11:4], magnitude = (hi:lo)[63:12] (52 bits) */
+static inline orc_zdraw orc_zsplit_e(uint32_t hi, uint32_t lo) {
+    orc_zdraw d = {(lo >> 4) & 255u, 0u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
     return d;
 }
 
@@ -234,7 +246,7 @@ static inline double orc_signed(double x, uint32_t negative) { return negative ?
 static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k1, uint32_t chain, uint32_t iter,
                                 uint32_t pidx0, uint32_t g, uint32_t *faults) {
     orc_u32x4 r0 = orc_draw(k0, k1, chain, iter, g >> 1, pidx0, 0);
-    orc_zdraw d = (g & 1u) ? orc_zsplit(r0.v[2], r0.v[3]) : orc_zsplit(r0.v[0], r0.v[1]);
+    orc_zdraw d = (g & 1u) ? orc_zsplit_n(r0.v[2], r0.v[3]) : orc_zsplit_n(r0.v[0], r0.v[1]);
     if (d.mag < t->kn[d.layer]) return orc_signed((double)d.mag * t->wn[d.layer], d.negative);
     for (uint32_t step = 0;; ++step) {
         uint32_t attempt = 1u + 2u * step + (g & 1u);
@@ -252,7 +264,7 @@ static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k
             double u = orc_u01_closed0(b.v[0], b.v[1]);
             if (fma(u, t->fn[d.layer - 1] - t->fn[d.layer], t->fn[d.layer]) < orc_exp_nonpos(-0.5 * (x * x)))
                 return orc_signed(x, d.negative);
-            d = orc_zsplit(b.v[2], b.v[3]);
+            d = orc_zsplit_n(b.v[2], b.v[3]);
             if (d.mag < t->kn[d.layer]) return orc_signed((double)d.mag * t->wn[d.layer], d.negative);
         }
     }
@@ -266,7 +278,7 @@ static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k
 static inline double orc_exponential(const orc_zig_tables *t, uint32_t k0, uint32_t k1, uint32_t chain,
                                      uint32_t iter, uint32_t pidx0, uint32_t *faults) {
     orc_u32x4 r0 = orc_draw(k0, k1, chain, iter >> 1, ORC_BLOCK_ACCEPT, pidx0, 0);
-    orc_zdraw d = (iter & 1u) ? orc_zsplit(r0.v[2], r0.v[3]) : orc_zsplit(r0.v[0], r0.v[1]);
+    orc_zdraw d = (iter & 1u) ? orc_zsplit_e(r0.v[2], r0.v[3]) : orc_zsplit_e(r0.v[0], r0.v[1]);
     if (d.mag < t->ke[d.layer]) return (double)d.mag * t->we[d.layer];
     for (uint32_t step = 0;; ++step) {
         uint32_t attempt = 1u + step;
@@ -279,7 +291,7 @@ static inline double orc_exponential(const orc_zig_tables *t, uint32_t k0, uint3
         double x = (double)d.mag * t->we[d.layer];
         double u = orc_u01_closed0(b.v[0], b.v[1]);
         if (fma(u, t->fe[d.layer - 1] - t->fe[d.layer], t->fe[d.layer]) < orc_exp_nonpos(-x)) return x;
-        d = orc_zsplit(b.v[2], b.v[3]);
+        d = orc_zsplit_e(b.v[2], b.v[3]);
         if (d.mag < t->ke[d.layer]) return (double)d.mag * t->we[d.layer];
     }
 }

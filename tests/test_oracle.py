@@ -43,23 +43,40 @@ def test_exp_accuracy(oracle):
 
 
 def test_ziggurat_tables(oracle):
-    """256 strips of equal area v (M&T construction): x_255 = r, top strip
-    reaches x_0 ≈ 0, thresholds below 2^52 and increasing towards the base."""
+    """Strips of equal area v (M&T construction) — 4096 for N(0,1), 256 for
+    Exp(1), 52-bit magnitudes: x_{L-1} = r, top strip
+    reaches x_0 ≈ 0, thresholds below 2^bits and increasing towards the base."""
     t = oracle.zig_tables()
-    m = 2.0 ** 52
-    for k, w, f, r, v, fx in ((t["kn"], t["wn"], t["fn"], 3.6541528853610088, 4.92867323399e-3,
-                               lambda x: np.exp(-0.5 * x * x)),
-                              (t["ke"], t["we"], t["fe"], 7.69711747013104972, 3.949659822581572e-3,
-                               lambda x: np.exp(-x))):
+    for k, w, f, r, v, fx, L, m in ((t["kn"], t["wn"], t["fn"], 4.3859450348713045, 3.061541032784645e-4,
+                                     lambda x: np.exp(-0.5 * x * x), 4096, 2.0 ** 52),
+                                    (t["ke"], t["we"], t["fe"], 7.69711747013104972, 3.949659822581572e-3,
+                                     lambda x: np.exp(-x), 256, 2.0 ** 52)):
+        assert len(k) == L
         x = w * m  # x_i for i ≥ 1; base strip width for i = 0
-        assert x[255] == pytest.approx(r, rel=1e-15)
+        assert x[L - 1] == pytest.approx(r, rel=1e-15)
         assert np.all(np.diff(x[1:]) > 0)
         assert np.allclose(f[1:], fx(x[1:]), rtol=1e-14)
         areas = x[1:] * (f[:-1] - f[1:])  # strip i spans f(x_i)..f(x_{i-1})
         assert np.allclose(areas, v, rtol=1e-9)
         assert x[0] * fx(r) == pytest.approx(v, rel=1e-12)  # base rectangle width q
-        assert k[1] == 0 and np.all(k < 2 ** 52)
-        assert np.allclose(k[2:] / m, x[1:-1] / x[2:], rtol=1e-15, atol=2.0 ** -52)
+        assert k[1] == 0 and np.all(k < m)
+        assert np.allclose(k[2:] / m, x[1:-1] / x[2:], rtol=1e-15, atol=1.0 / m)
+
+
+def test_ziggurat_normal_constants_close_the_table():
+    """r, v of the 4096-strip normal table: v = r·f(r) + ∫_r^∞ f, and the
+    recursion from x = r up through the strips ends with the top strip's area
+    equal to v (checked in 50-digit arithmetic)."""
+    import mpmath as mp
+
+    mp.mp.dps = 50
+    r, v = mp.mpf(4.3859450348713045), mp.mpf(3.061541032784645e-4)
+    f = lambda x: mp.e ** (-x * x / 2)  # noqa: E731
+    assert abs(r * f(r) + mp.sqrt(2 * mp.pi) * mp.ncdf(-r) - v) / v < 1e-14  # r, v rounded to double
+    x = r
+    for _ in range(4096 - 2):
+        x = mp.sqrt(-2 * mp.log(v / x + f(x)))
+    assert abs(x * (1 - f(x)) - v) / v < 1e-9
 
 
 def test_ziggurat_distributions(oracle):
@@ -68,9 +85,10 @@ def test_ziggurat_distributions(oracle):
     z = oracle.normals(W.SEED, 400_000)
     assert abs(z.mean()) < 0.006 and abs(z.std() - 1.0) < 0.006
     assert stats.kstest(z, "norm").pvalue > 1e-3
-    # tail beyond r = 3.654 is reached through the rare path and has the right mass
-    tail = (np.abs(z) > 3.6541528853610088).mean()
-    assert abs(tail - 2 * stats.norm.sf(3.6541528853610088)) < 3e-4
+    # tail beyond r = 4.386 is reached through the rare path and has the right mass
+    tail = (np.abs(z) > 4.3859450348713045).mean()
+    assert abs(tail - 2 * stats.norm.sf(4.3859450348713045)) < 4e-5
+    assert tail > 0
     e = oracle.exponentials(W.SEED, 200_000)
     assert abs(e.mean() - 1.0) < 0.01
     assert stats.kstest(e, "expon").pvalue > 1e-3

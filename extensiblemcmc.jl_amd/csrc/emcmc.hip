@@ -498,7 +498,7 @@ ReadjustFn readjust_fn() {
 }
 template <int D>
 std::pair<MomentsFn, int> moments_fn() {
-    return {&mix_moments_kernel<D>, MomentTiles<D>::NT};
+    return {&mix_moments_kernel<D>, MomentTiles<D>::WPB};
 }
 std::pair<MomentsFn, int> moments_lookup(int D) {
     switch (D) {
@@ -905,8 +905,9 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             mp.N0 = p.N0;
             mp.nsteps = p.nsteps;
             void *margs[] = {&mp};
-            const dim3 mgrid((unsigned)((C + 255) / 256), (unsigned)h->var.mo_tiles);
-            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mofn), mgrid, block, margs, 0, h->stream));
+            // one block per 64 chains, one wave per unit of the packed triangle
+            const dim3 mgrid((unsigned)((C + 63) / 64)), mblock((unsigned)(64 * h->var.mo_tiles));
+            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mofn), mgrid, mblock, margs, 0, h->stream));
             std::swap(h->d_mean, h->d_mean_alt);
         }
         h->stats_N += n;

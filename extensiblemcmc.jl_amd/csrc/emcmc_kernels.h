@@ -190,8 +190,13 @@ struct WaveScratch {
 #define EMCMC_BATCHED 0  // 1: wave-batched rare paths (the better choice with 256 normal layers)
 #endif
 constexpr bool diag_batched(int D, int LPC) { return EMCMC_BATCHED && (D / LPC) % 2 == 0 && D / LPC <= 16; }
-constexpr size_t diag_scratch_bytes(int D, int LPC) {
-    return diag_batched(D, LPC) ? 4 * (size_t)(((EMCMC_BATCH_MODE == 1) ? 64 * (D / LPC) * 8 : 64 * 8) + 64 * 4 + 64 * 4)
+// threads per block of the diag kernel: one block per CU holds 256·MINW
+// threads when MINW ≥ 3, so a single copy of the 70 KiB of tables serves
+// MINW waves per SIMD (two 256-thread blocks, each with its own copy, are
+// all the LDS allows)
+constexpr int diag_block(int MINW) { return MINW >= 3 ? 256 * MINW : 256; }
+constexpr size_t diag_scratch_bytes(int D, int LPC, int waves = 4) {
+    return diag_batched(D, LPC) ? waves * (size_t)(((EMCMC_BATCH_MODE == 1) ? 64 * (D / LPC) * 8 : 64 * 8) + 64 * 4 + 64 * 4)
                                 : 0;
 }
 __host__ __device__ constexpr size_t lds_align16(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -608,7 +613,7 @@ __device__ __forceinline__ T &chain_elem(T *base, uint32_t c) {
 // MINW = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
 template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1>
-__global__ void __launch_bounds__(256, MINW) rwm_gsn_diag_kernel(const StepParams a) {
+__global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(const StepParams a) {
     static_assert(D % LPC == 0, "D must split evenly over the chain's lanes");
     constexpr int DPL = D / LPC;  // coordinates per lane
     static_assert(LPC == 1 || DPL % 8 == 0, "multi-lane chains need whole 8-blocks");

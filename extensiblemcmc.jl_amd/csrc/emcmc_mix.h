@@ -301,18 +301,18 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
 // per-step recurrence (elements are independent):
 //   old = (N−1)/N·c + m_i m_j;  new = old + (θ_i θ_j)/N;  c = new − (N+1)/N·(m'_i m'_j)
 //   m' = m·(N/(N+1)) + θ/(N+1)
-// One thread per (chain, tile): tiles are TB×TB blocks (bi ≤ bj) of the upper
-// triangle; a tile sweeps the launch's steps with its cov block, the means of
-// its coordinates and their θ in registers.  The cov is read and written once
-// per launch instead of once per step.  The means are double-buffered: the
-// off-diagonal tiles of a chain may run after its diagonal tiles have finished
-// (blocks of later blockIdx.y start as earlier ones retire), so an in-place
-// mean update would be read back by them.
+// One block = 64 consecutive chains; one wave = one "unit" of the packed
+// triangle held in registers for the whole launch: a TB×TB diagonal block
+// (upper part) or half (TB×TB/2) of an off-diagonal block.  The chains' θ of a
+// step is staged once per block into LDS (double-buffered, the next step's
+// global load in flight while this step computes) and read by every unit, so
+// HBM sees θ once and the cov once per launch.  The means are double-buffered
+// across launches (`mean` in, `mean_out` out); every unit advances its own
+// copy of the means it needs (the same formula, the same bits).
 struct MixMomentsParams {
     const double *theta;  // θ after step s of the launch at theta + s·D·C (state_pos layout)
     const double *mean;   // [D] state_pos, before the launch
-    double *mean_out;     // [D] state_pos, after the launch (a different buffer: every tile
-                          // of a chain reads `mean`, only the diagonal tiles write)
+    double *mean_out;     // [D] state_pos, after the launch (written by the diagonal units)
     double *cov;          // [DP] packed upper
     uint64_t C;
     uint64_t N0;          // GenericChainStats.N at the launch's first step
@@ -321,82 +321,189 @@ struct MixMomentsParams {
 
 template <int D>
 struct MomentTiles {
-    static constexpr int TB = D <= 8 ? D : 8;  // tile edge
-    static constexpr int NB = D / TB;          // blocks per edge
-    static constexpr int NT = NB * (NB + 1) / 2;
+    static constexpr int TB = D <= 8 ? D : 8;                 // block edge
+    static constexpr int NB = D / TB;                         // blocks per edge
+    static constexpr int HALF = TB == 8 ? 4 : TB;             // columns per off-diagonal unit
+    static constexpr int NOFF = NB * (NB - 1) / 2 * (TB / HALF);
+    static constexpr int NU = NB + NOFF;                      // units of the packed triangle
+    static constexpr int WPB = NU < 8 ? NU : 8;               // waves per block
+    static constexpr int UPW = NU / WPB;                      // units per wave (1 or 2)
+    static constexpr int BLOCK = 64 * WPB;
+    static constexpr int PR = (D % 2 == 0) ? D / 2 : D;       // LDS rows: coordinate pairs (even D) or coordinates
+    static constexpr int EW = (D % 2 == 0) ? 2 : 1;           // doubles per row element
+    static constexpr int NPF = (PR * 64 + BLOCK - 1) / BLOCK; // staged row elements per thread
+    static_assert(NU % WPB == 0, "units per wave");
 };
 
-template <int D>
-__global__ void __launch_bounds__(256) mix_moments_kernel(const MixMomentsParams a) {
-    constexpr int DP = packed_n(D);
-    constexpr int TB = MomentTiles<D>::TB, NB = MomentTiles<D>::NB;
-    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (chain >= a.C) return;
+// unit U → its block of the packed triangle (compile time)
+template <int D, int U>
+struct MomentUnit {
+    using MT = MomentTiles<D>;
+    static constexpr bool DIAG = U < MT::NB;
+    static constexpr int O = DIAG ? 0 : U - MT::NB, PER = MT::TB / MT::HALF;
+    static constexpr int bi_of(int p, int bi) { return p < MT::NB - 1 - bi ? bi : bi_of(p - (MT::NB - 1 - bi), bi + 1); }
+    static constexpr int p_of(int p, int bi) { return p < MT::NB - 1 - bi ? p : p_of(p - (MT::NB - 1 - bi), bi + 1); }
+    static constexpr int BI = DIAG ? U : bi_of(O / PER, 0);
+    static constexpr int I0 = BI * MT::TB;
+    static constexpr int J0 = DIAG ? I0 : (BI + 1 + p_of(O / PER, 0)) * MT::TB + (O % PER) * MT::HALF;
+    static constexpr int NJ = DIAG ? MT::TB : MT::HALF;
+    static constexpr int NC = DIAG ? MT::TB * (MT::TB + 1) / 2 : MT::TB * NJ;
+    // register slot of element (u, v): diagonal units u ≤ v (row-major upper),
+    // off-diagonal units u·NJ + v
+    static constexpr int slot(int u, int v) { return DIAG ? u * MT::TB - u * (u - 1) / 2 + (v - u) : u * NJ + v; }
+};
+
+// One unit's registers for the whole launch: its cov block and the means of
+// its rows / columns (each unit advances its own copy of the means: the same
+// formula, the same bits).
+template <int D, int U>
+struct MomentUnitState {
+    using MT = MomentTiles<D>;
+    using UT = MomentUnit<D, U>;
+    static constexpr int TB = MT::TB, NJ = UT::NJ, I0 = UT::I0, J0 = UT::J0, DP = packed_n(D);
+    static constexpr bool DIAG = UT::DIAG;
+    double c[UT::NC], mi[TB], mj[DIAG ? 1 : NJ];
+
+    __device__ __forceinline__ void load(const MixMomentsParams &a, uint64_t chain) {
+        const LaneSoA lm = lane_soa(a.C, chain, D), lc = lane_soa(a.C, chain, DP);
+#pragma unroll
+        for (int u = 0; u < TB; ++u) mi[u] = *soa_ptr<D>(a.mean, lm, I0 + u);
+        if constexpr (!DIAG) {
+#pragma unroll
+            for (int v = 0; v < NJ; ++v) mj[v] = *soa_ptr<D>(a.mean, lm, J0 + v);
+        }
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+            for (int v = DIAG ? u : 0; v < NJ; ++v) c[UT::slot(u, v)] = *soa_ptr<DP>(a.cov, lc, up_idx(D, I0 + u, J0 + v));
+    }
+    // one step of chain_statistics.jl:46-49 with θ from the staged rows
+    template <typename TH>
+    __device__ __forceinline__ void step(TH theta_at, double Nd, double N1d, double ca, double cb, double cc, double rN,
+                                         double rN1) {
+        double ti[TB], tj[NJ];
+#pragma unroll
+        for (int u = 0; u < TB; ++u) ti[u] = theta_at(I0 + u);
+#pragma unroll
+        for (int v = 0; v < NJ; ++v) tj[v] = DIAG ? ti[v] : theta_at(J0 + v);
+        // old_sq + (θ_i θ_j)/N with the means before the step, then the means
+        // (m' = m·cb + θ/(N+1)) and the subtraction
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+            __builtin_amdgcn_sched_barrier(0);  // one row at a time: bounded live temporaries
+#pragma unroll
+            for (int v = DIAG ? u : 0; v < NJ; ++v) {
+                const double old_sq = ca * c[UT::slot(u, v)] + mi[u] * (DIAG ? mi[v] : mj[v]);
+                c[UT::slot(u, v)] = old_sq + div_markstein(ti[u] * tj[v], Nd, rN);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < TB; ++u) mi[u] = mi[u] * cb + div_markstein(ti[u], N1d, rN1);
+        if constexpr (!DIAG) {
+#pragma unroll
+            for (int v = 0; v < NJ; ++v) mj[v] = mj[v] * cb + div_markstein(tj[v], N1d, rN1);
+        }
+#pragma unroll
+        for (int u = 0; u < TB; ++u) {
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int v = DIAG ? u : 0; v < NJ; ++v)
+                c[UT::slot(u, v)] = c[UT::slot(u, v)] - cc * (mi[u] * (DIAG ? mi[v] : mj[v]));
+        }
+    }
+    __device__ __forceinline__ void store(const MixMomentsParams &a, uint64_t chain) const {
+        // fresh opaque strides: the load addresses are not kept live across the sweep
+        const LaneSoA lm = lane_soa(a.C, chain, D), lc = lane_soa(a.C, chain, DP);
+#pragma unroll
+        for (int u = 0; u < TB; ++u)
+#pragma unroll
+            for (int v = DIAG ? u : 0; v < NJ; ++v) *soa_ptr<DP>(a.cov, lc, up_idx(D, I0 + u, J0 + v)) = c[UT::slot(u, v)];
+        if constexpr (DIAG) {
+#pragma unroll
+            for (int u = 0; u < TB; ++u) *soa_ptr<D>(a.mean_out, lm, I0 + u) = mi[u];
+        }
+    }
+};
+
+// The whole launch sweep of wave W (units W and W + WPB); every wave runs the
+// same number of block barriers.
+template <int D, int W>
+__device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *stage0, double *stage1) {
+    using MT = MomentTiles<D>;
+    constexpr int PR = MT::PR, EW = MT::EW, NPF = MT::NPF, WPB = MT::WPB;
+    constexpr bool TWO = MT::UPW == 2;
+    typedef double rowv __attribute__((ext_vector_type(EW)));
+    const int lane = threadIdx.x & 63;
     const uint64_t C = a.C;
-    // tile (bi, bj), bi ≤ bj, from blockIdx.y (uniform)
-    int bi = 0, rem = (int)blockIdx.y;
-    while (rem >= NB - bi) {
-        rem -= NB - bi;
-        ++bi;
-    }
-    const int bj = bi + rem;
-    const bool diag = bi == bj;
-    const int i0 = bi * TB, j0 = bj * TB;
-    const LaneSoA lm = lane_soa(C, chain, D), lc = lane_soa(C, chain, DP);
-    double c[TB][TB], mi[TB], mj[TB];
+    const uint64_t c0 = (uint64_t)blockIdx.x * 64u;
+    const uint64_t chain = c0 + (uint64_t)lane;
+    const bool live = chain < C;
+    const uint64_t cl = live ? chain : c0;  // chains past C read chain c0's values and store nothing
+    auto fetch = [&](uint32_t s, rowv (&pf)[NPF]) {
+        const rowv *src = reinterpret_cast<const rowv *>(a.theta + (uint64_t)s * D * C);
 #pragma unroll
-    for (int u = 0; u < TB; ++u) {
-        mi[u] = *soa_ptr<D>(a.mean, lm, i0 + u);
-        mj[u] = *soa_ptr<D>(a.mean, lm, j0 + u);
+        for (int q = 0; q < NPF; ++q) {
+            const int e = (int)threadIdx.x + q * MT::BLOCK;
+            const int k = e >> 6, l = e & 63;
+            const uint64_t cc = (c0 + (uint64_t)l < C) ? c0 + (uint64_t)l : c0;
+            pf[q] = (e < PR * 64) ? __builtin_nontemporal_load(src + (uint64_t)k * C + cc) : rowv{};
+        }
+    };
+    auto put = [&](double *st, const rowv (&pf)[NPF]) {
+        rowv *dst = reinterpret_cast<rowv *>(st);
 #pragma unroll
-        for (int v = 0; v < TB; ++v)
-            if (!diag || u <= v) c[u][v] = *soa_ptr<DP>(a.cov, lc, up_idx(D, i0 + u, j0 + v));
+        for (int q = 0; q < NPF; ++q) {
+            const int e = (int)threadIdx.x + q * MT::BLOCK;
+            if (e < PR * 64) dst[e] = pf[q];
+        }
+    };
+    MomentUnitState<D, W> ua;
+    MomentUnitState<D, TWO ? W + WPB : W> ub;
+    ua.load(a, cl);
+    if constexpr (TWO) ub.load(a, cl);
+    {
+        rowv pf[NPF];
+        fetch(0, pf);
+        put(stage0, pf);
     }
+    __syncthreads();
     for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const double *st = (s & 1u) ? stage1 : stage0;
+        rowv pf[NPF];
+        if (s + 1 < a.nsteps) fetch(s + 1, pf);  // in flight during this step
+        auto theta_at = [&](int d) -> double {
+            const rowv v = reinterpret_cast<const rowv *>(st)[(EW == 2 ? d >> 1 : d) * 64 + lane];
+            if constexpr (EW == 2) return (d & 1) ? v[1] : v[0];
+            else return v[0];
+        };
         const uint64_t N = a.N0 + s;
         const double Nd = (double)N, N1d = (double)(N + 1);
         const double ca = (double)(N - 1) / Nd, cb = Nd / N1d, cc = N1d / Nd;
         const double rN = 1.0 / Nd, rN1 = 1.0 / N1d;
-        const LaneSoA lt = lane_soa(C, chain, D);
-        const double *ths = a.theta + (uint64_t)s * D * C;
-        double ti[TB], tj[TB];
-#pragma unroll
-        for (int u = 0; u < TB; ++u) {
-            ti[u] = *soa_ptr<D>(ths, lt, i0 + u);
-            tj[u] = diag ? ti[u] : *soa_ptr<D>(ths, lt, j0 + u);
-        }
-        // old_sq + (θ_i θ_j)/N with the means before the step, then the means in
-        // place (m' = m·cb + θ/(N+1)) and the subtraction: two passes keep one
-        // set of mean registers
-#pragma unroll
-        for (int u = 0; u < TB; ++u)
-#pragma unroll
-            for (int v = 0; v < TB; ++v)
-                if (!diag || u <= v) {
-                    const double old_sq = ca * c[u][v] + mi[u] * mj[v];
-                    c[u][v] = old_sq + div_markstein(ti[u] * tj[v], Nd, rN);
-                }
-#pragma unroll
-        for (int u = 0; u < TB; ++u) {
-            mi[u] = mi[u] * cb + div_markstein(ti[u], N1d, rN1);
-            mj[u] = diag ? mi[u] : mj[u] * cb + div_markstein(tj[u], N1d, rN1);
-        }
-#pragma unroll
-        for (int u = 0; u < TB; ++u)
-#pragma unroll
-            for (int v = 0; v < TB; ++v)
-                if (!diag || u <= v) c[u][v] = c[u][v] - cc * (mi[u] * mj[v]);
+        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
+        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
+        if (s + 1 < a.nsteps) put((s & 1u) ? stage0 : stage1, pf);
+        __syncthreads();
     }
-    // fresh opaque strides: the load addresses above are not kept live across the sweep
-    const LaneSoA lm2 = lane_soa(C, chain, D), lc2 = lane_soa(C, chain, DP);
-#pragma unroll
-    for (int u = 0; u < TB; ++u)
-#pragma unroll
-        for (int v = 0; v < TB; ++v)
-            if (!diag || u <= v) *soa_ptr<DP>(a.cov, lc2, up_idx(D, i0 + u, j0 + v)) = c[u][v];
-    if (diag)
-#pragma unroll
-        for (int u = 0; u < TB; ++u) *soa_ptr<D>(a.mean_out, lm2, i0 + u) = mi[u];
+    if (!live) return;
+    ua.store(a, chain);
+    if constexpr (TWO) ub.store(a, chain);
+}
+
+template <int D, int W>
+__device__ __forceinline__ void moments_dispatch(int wave, const MixMomentsParams &a, double *stage0, double *stage1) {
+    if constexpr (W < MomentTiles<D>::WPB) {
+        if (wave == W) moments_wave<D, W>(a, stage0, stage1);
+        else moments_dispatch<D, W + 1>(wave, a, stage0, stage1);
+    }
+}
+
+template <int D>
+__global__ void __launch_bounds__(MomentTiles<D>::BLOCK) mix_moments_kernel(const MixMomentsParams a) {
+    using MT = MomentTiles<D>;
+    __shared__ __attribute__((aligned(16))) double stage[2][MT::PR * 64 * MT::EW];
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
+    moments_dispatch<D, 0>(wave, a, stage[0], stage[1]);
 }
 
 // ---- HaarioTypeAdaptation readjust! (adaptation.jl:422-426) -----------------

@@ -358,7 +358,6 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
             HIPCHK(h, hipMalloc(&h->d_iLB, C * D * sizeof(double)));
             HIPCHK(h, hipMalloc(&h->d_c0B, C * sizeof(double)));
         }
-        if (u.adaptation == EMCMC_ADPT_HAARIO) HIPCHK(h, hipMalloc(&h->d_Lnew, C * DP * sizeof(double)));
         if (h->cfg.history_mode != EMCMC_HIST_FULL)
             HIPCHK(h, hipMalloc(&h->d_mom_scratch, (uint64_t)h->cfg.steps_per_launch * C * D * sizeof(double)));
     }
@@ -513,6 +512,12 @@ std::pair<MomentsFn, int> moments_lookup(int D) {
     }
 }
 
+// chains per 256-thread block of mix_readjust_kernel<D> (R lanes per chain)
+int readjust_chains_per_block(int D) {
+    int r = 1;
+    while (r < D) r <<= 1;
+    return 4 * (64 / r);
+}
 ReadjustFn readjust_lookup(int D) {
     switch (D) {
     case 1: return readjust_fn<1>();
@@ -851,7 +856,6 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     r.LB = h->d_LB;
     r.iLB = h->d_iLB;
     r.c0B = h->d_c0B;
-    r.Lnew = h->d_Lnew;
     r.faults = h->d_faults;
     r.C = C;
     r.sB = (2.38 * 2.38) / (double)h->cfg.dim;  // 2.38^2/length(rw), adaptation.jl:423
@@ -915,7 +919,9 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             h->mix_M += (uint32_t)n;
             if (h->mix_M >= k) {  // time_to_update: readjust!, M = 0
                 void *rargs[] = {&r};
-                HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.rfn), grid, block, rargs, 0,
+                const int cpb = readjust_chains_per_block((int)h->cfg.dim);
+                const dim3 rgrid((unsigned)((C + cpb - 1) / cpb));
+                HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.rfn), rgrid, block, rargs, 0,
                                           h->stream));
                 h->mix_M = 0;
             }

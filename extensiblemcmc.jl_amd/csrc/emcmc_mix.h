@@ -106,6 +106,17 @@ template <int NP>
 __device__ __forceinline__ const double *soa_ptr(const double *base, const LaneSoA &l, int q) {
     return soa_ptr<NP>(const_cast<double *>(base), l, q);
 }
+// element q (lane-dependent) of a packed per-chain vector in state_pos layout
+template <int NP>
+__device__ __forceinline__ double *soa_ptr_dyn(double *base, const LaneSoA &l, int q) {
+    const uint32_t row = (NP % 2 == 0) ? (uint32_t)q >> 1 : (uint32_t)q;
+    return reinterpret_cast<double *>(reinterpret_cast<char *>(base) + (uint64_t)row * l.stride + l.off) +
+           ((NP % 2 == 0) ? (q & 1) : 0);
+}
+template <int NP>
+__device__ __forceinline__ const double *soa_ptr_dyn(const double *base, const LaneSoA &l, int q) {
+    return soa_ptr_dyn<NP>(const_cast<double *>(base), l, q);
+}
 // plain [n][C] layout (element q of chain c at q·C + c)
 __device__ __forceinline__ LaneSoA lane_plain(uint64_t C, uint64_t chain) {
     uint64_t stride = C * 8u;
@@ -512,65 +523,106 @@ struct MixReadjustParams {
     double *LB;         // [DP] packed lower
     double *iLB;        // [D][C]
     double *c0B;        // [C]
-    double *Lnew;       // [DP] packed lower scratch
     uint32_t *faults;
     uint64_t C;
     double sB;  // 2.38²/D
 };
 
+// R lanes per chain (R = D rounded up to a power of two), 64/R chains per wave,
+// 4 waves per block.
+template <int D>
+struct ReadjustShape {
+    static constexpr int R = D <= 1 ? 1 : D <= 2 ? 2 : D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : 32;
+    static constexpr int CPW = 64 / R;
+    static constexpr int CPB = 4 * CPW;
+};
+
 // Σ_B = sB·cov; L_B = cholesky(Symmetric(Σ_B)).L in the canonical order of
 // oracle/emcmc_oracle.c orc_cholesky (each element's sum over k ascending, the
-// products rounded before subtraction), computed row by row: the row being
-// built stays in registers, earlier rows are re-read from the scratch copy
-// (volatile loads: program order, no store-to-load forwarding into registers).
+// products rounded before the subtraction).  Lane i of a chain's R lanes owns
+// row i; a sweep over the columns j = 0..D−1: lane j takes the square root of
+// its finished diagonal sum and publishes it, then every lane i > j forms
+// L_ij = (Σ_B,ij − Σ_{k<j} L_ik L_jk) / L_jj with row j read from LDS
+// (broadcast), publishes L_ij and subtracts L_ij² from its own diagonal sum.
 template <int D>
 __global__ void __launch_bounds__(256) mix_readjust_kernel(const MixReadjustParams a) {
-    constexpr int DP = packed_n(D);
-    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (chain >= a.C) return;
+    using RS = ReadjustShape<D>;
+    constexpr int R = RS::R, CPW = RS::CPW, DP = packed_n(D);
+    __shared__ double Ls[4 * CPW][DP];  // each chain's factor, packed lower (row-major)
+    __shared__ double dgs[4 * CPW][D];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int g = lane / R, i = lane % R;
+    const int lc = w * CPW + g;
     const uint64_t C = a.C;
-    double dg[D];
+    const uint64_t chain = (uint64_t)blockIdx.x * RS::CPB + (uint64_t)lc;
+    const bool live = chain < C && i < D;
+    const uint64_t cl = chain < C ? chain : 0;  // tail lanes read chain 0 and write nothing
+    const int ic = i < D ? i : D - 1;
+    // column i of the upper triangle: Σ_B[j][i] = sB·cov(j, i), j ≤ i
+    double col[D], row[D];
+    {
+        const LaneSoA lp = lane_soa(C, cl, DP);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            // up_idx(D, j, i) for j ≤ i (lanes with j > i read their own diagonal: unused)
+            const int jj = j <= ic ? j : ic;
+            col[j] = a.sB * *soa_ptr_dyn<DP>(a.cov, lp, up_idx(D, jj, ic));
+        }
+    }
+    double s = col[D - 1];  // replaced below by the diagonal once j reaches i
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        if (j == ic) s = col[j];  // Σ_B[i][i]
     bool ok = true;
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-        __builtin_amdgcn_sched_barrier(0);
-        // fresh opaque stride per row: addresses are not CSE'd across rows
-        const LaneSoA lp = lane_soa(C, chain, DP);
-        double row[D];
-#pragma unroll
-        for (int j = 0; j < i; ++j) {
-            double t = a.sB * *soa_ptr<DP>(a.cov, lp, up_idx(D, j, i));
-#pragma unroll
-            for (int k = 0; k < j; ++k)
-                t = t - row[k] * *reinterpret_cast<const volatile double *>(soa_ptr<DP>(a.Lnew, lp, lo_idx(j, k)));
-            row[j] = t / dg[j];
-            pin(row[j]);
+    for (int j = 0; j < D; ++j) {
+        if (live && i == j) {
+            ok = s > 0.0;
+            const double d = sqrt(s);
+            row[j] = d;
+            dgs[lc][j] = d;
+            Ls[lc][lo_idx(j, j)] = d;
         }
-        double s = a.sB * *soa_ptr<DP>(a.cov, lp, up_idx(D, i, i));
+        wave_lds_sync();
+        if (live && i > j) {
+            double t = col[j];
 #pragma unroll
-        for (int k = 0; k < i; ++k) s = s - row[k] * row[k];
-        ok = ok && (s > 0.0);
-        dg[i] = sqrt(s);
-        pin(dg[i]);
-        row[i] = dg[i];
-#pragma unroll
-        for (int j = 0; j <= i; ++j) *soa_ptr<DP>(a.Lnew, lp, lo_idx(i, j)) = row[j];
+            for (int k = 0; k < j; ++k) t = t - row[k] * Ls[lc][lo_idx(j, k)];
+            row[j] = t / dgs[lc][j];
+            Ls[lc][lo_idx(i, j)] = row[j];
+            s = s - row[j] * row[j];
+        }
+        wave_lds_sync();
     }
-    if (!ok) {
-        a.faults[chain] |= 4u;  // EMCMC_FAULT_POSDEF
+    // every row of the chain must have had a positive diagonal (NaN fails)
+    const uint64_t okm = __ballot(!live || ok);
+    const uint64_t gm = (R == 64 ? ~0ull : ((1ull << R) - 1)) << (g * R);
+    const bool chain_ok = (okm & gm) == gm;
+    if (chain >= C) return;
+    if (!chain_ok) {
+        if (i == 0) a.faults[chain] |= 4u;  // EMCMC_FAULT_POSDEF
         return;
     }
-    const LaneSoA lp = lane_soa(C, chain, DP);
+    if (i >= D) return;
+    {
+        const LaneSoA lp = lane_soa(C, chain, DP);
 #pragma unroll
-    for (int q = 0; q < DP; ++q)
-        *soa_ptr<DP>(a.LB, lp, q) = *reinterpret_cast<const volatile double *>(soa_ptr<DP>(a.Lnew, lp, q));
-    double dd = 0.0;
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-        a.iLB[(uint64_t)i * C + chain] = 1.0 / dg[i];
-        dd = dd + log_pos(dg[i]);
+        for (int j = 0; j < D; ++j)
+            if (j <= i) *soa_ptr_dyn<DP>(a.LB, lp, lo_idx(i, j)) = row[j];
     }
-    a.c0B[chain] = -((double)D * kLog2Pi + (dd + dd)) / 2.0;
+    double dgi = 0.0;
+#pragma unroll
+    for (int j = 0; j < D; ++j)
+        if (j == i) dgi = row[j];
+    a.iLB[(uint64_t)i * C + chain] = 1.0 / dgi;
+    dgs[lc][i] = log_pos(dgi);
+    wave_lds_sync();
+    if (i == 0) {
+        double dd = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) dd = dd + dgs[lc][k];
+        a.c0B[chain] = -((double)D * kLog2Pi + (dd + dd)) / 2.0;
+    }
 }
 
 }  // namespace emcmc

@@ -284,6 +284,9 @@ def main():
         },
         "kernel_chain_steps_per_s": Cg * a.steps / (ms / 1e3),
     }
+    if cfg4:  # HIP events bracket the launch group, and its bytes cover all three kernels
+        out["roofline"]["timed_region"] = ("per launch group: mix_gsn_kernel (steps) + mix_moments_kernel (batched "
+                                           "GenericChainStats mean/cov) + mix_readjust_kernel when Haario is due")
     if cfg3:  # MFMA-bound: the two contractions, 4·N·D flop per chain-step
         flops = 4.0 * w.nobs * w.D * Cg * (a.steps / launches)
         tfs = flops / avg_launch_s / 1e12

@@ -727,17 +727,25 @@ emcmc_status select_variant(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
-double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps) {
+// Algorithmic HBM bytes of one launch group: the step kernel
+// and, on the mix / chain-moments path, the batched mean/cov kernel and the
+// Haario readjust when it follows the group.
+double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps, bool readjust) {
     const double C = (double)h->cfg.num_chains, D = (double)h->cfg.dim;
     double per_step = (h->cfg.history_mode == EMCMC_HIST_FULL) ? (16.0 * D + 8.0 + 0.125) : 0.125;
     double state = 16.0 * D + 2 * 8 + 2 * 8 + 2 * 16 + 2 * 4 + 2 * 4;  // θ, ll, ra, ring, nacc, faults (R+W)
-    if (h->var.xfn) {  // step kernel only (mix_moments_kernel is accounted separately)
-        if (h->cfg.history_mode != EMCMC_HIST_FULL) per_step += 8.0 * D;  // θ for the moments kernel
+    if (h->var.xfn) {
+        const double DP = D * (D + 1) / 2;
+        // mix_moments_kernel: θ of every step once (ACCEPT_ONLY: written by the
+        // step kernel to a scratch and read back), mean and cov read + written
+        per_step += (h->cfg.history_mode == EMCMC_HIST_FULL) ? 8.0 * D : 16.0 * D;
+        state += 16.0 * DP + 16.0 * D;
         if (h->updates[0].kernel == EMCMC_RW_GAUSSIAN_MIX) {
-            const double DP = D * (D + 1) / 2;
-            per_step += 8.0 * DP + 8.0 * D;  // L_B and 1/L_B,ii, read
+            per_step += 8.0 * DP + 8.0 * D;  // L_B and 1/L_B,ii, read by every step
             state += 8.0;                    // c0_B
         }
+        // readjust: cov read, L_B / 1/L_B,ii / c0_B written
+        if (readjust) state += 8.0 * DP + 8.0 * DP + 8.0 * D + 8.0;
     }
     return C * ((double)nsteps * per_step + state);
 }
@@ -894,11 +902,6 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
         void *args[] = {&p};
         HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.xfn), grid, block, args, h->lds_bytes,
                                   h->stream));
-        if (h->timing) {
-            HIPCHK(h, hipEventRecord(e1, h->stream));
-            h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, n);
-        }
         {  // the launch's mean/cov recurrence, from its θ history
             MixMomentsParams mp{};
             mp.theta = p.hist_theta ? p.hist_theta + (uint64_t)(p.iter0 - 1) * h->cfg.dim * C : h->d_mom_scratch;
@@ -915,6 +918,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             std::swap(h->d_mean, h->d_mean_alt);
         }
         h->stats_N += n;
+        bool readjusted = false;
         if (haario) {
             h->mix_M += (uint32_t)n;
             if (h->mix_M >= k) {  // time_to_update: readjust!, M = 0
@@ -924,7 +928,13 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
                 HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.rfn), rgrid, block, rargs, 0,
                                           h->stream));
                 h->mix_M = 0;
+                readjusted = true;
             }
+        }
+        if (h->timing) {  // the whole group: step kernel, mean/cov kernel, readjust
+            HIPCHK(h, hipEventRecord(e1, h->stream));
+            h->ev.emplace_back(e0, e1);
+            h->pending_bytes += bytes_per_launch(h, n, readjusted);
         }
         i = j;
     }
@@ -1002,7 +1012,7 @@ emcmc_status run_mala(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
         if (h->timing) {
             HIPCHK(h, hipEventRecord(e1, h->stream));
             h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, 1);
+            h->pending_bytes += bytes_per_launch(h, 1, false);
         }
         h->stats_N += 1;
     }
@@ -1100,7 +1110,7 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
         if (h->timing) {
             HIPCHK(h, hipEventRecord(e1, h->stream));
             h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, n);
+            h->pending_bytes += bytes_per_launch(h, n, false);
         }
         h->stats_N += n;
     }
@@ -1448,7 +1458,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
         if (h->timing) {
             HIPCHK(h, hipEventRecord(e1, h->stream));
             h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, n);
+            h->pending_bytes += bytes_per_launch(h, n, false);
         }
         h->stats_N += n;
         i = j;

@@ -13,11 +13,14 @@ STEP = re.compile(r"rwm_gsn|mix_gsn_kernel")
 summ, name, chains, spl = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
 tag = sys.argv[5] if len(sys.argv) > 5 else "r1"
 d = json.load(open(summ))
-pm = d["pmc"]
-# the first launch of a bench run is the warm-up launch; use the timed ones
-f = pm["fetch_bytes_corrected_per_launch"][1:] or pm["fetch_bytes_corrected_per_launch"]
-w = pm["write_bytes_per_launch"][1:] or pm["write_bytes_per_launch"]
-fb, wb = sum(f) / len(f), sum(w) / len(w)
+if "group" in d:  # mix path: the whole launch group (step + moments + readjust), averaged per step launch
+    fb, wb = d["group"]["fetch_bytes_corrected_per_group"], d["group"]["write_bytes_per_group"]
+else:
+    pm = d["pmc"]
+    # the first launch of a bench run is the warm-up launch; use the timed ones
+    f = pm["fetch_bytes_corrected_per_launch"][1:] or pm["fetch_bytes_corrected_per_launch"]
+    w = pm["write_bytes_per_launch"][1:] or pm["write_bytes_per_launch"]
+    fb, wb = sum(f) / len(f), sum(w) / len(w)
 step = [v for k, v in d["kernel_stats"].items() if STEP.search(k)][0]
 out = {name: {"bytes_per_chain_step": (fb + wb) / (chains * spl), "fetch_bytes_per_launch": fb,
               "write_bytes_per_launch": wb, "chains": chains, "steps_per_launch": spl,

@@ -27,11 +27,17 @@ stats = {r["Name"]: {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), 
 step = [k for k in stats if STEP.search(k)]
 res = {"kernel_stats": stats}
 pmc = defaultdict(list)
+by_kernel = defaultdict(lambda: defaultdict(list))
+GROUP = re.compile(r"mix_gsn_kernel|mix_moments_kernel|mix_readjust_kernel")
 for name in ("FETCH_SIZE", "WRITE_SIZE"):
     sub = "fetch" if name == "FETCH_SIZE" else "write"
     for r in rows(f"{sub}/**/*counter_collection.csv"):
-        if STEP.search(r["Kernel_Name"]) and r["Counter_Name"] == name:
+        if r["Counter_Name"] != name:
+            continue
+        if STEP.search(r["Kernel_Name"]):
             pmc[name].append(float(r["Counter_Value"]))
+        if GROUP.search(r["Kernel_Name"]):
+            by_kernel[r["Kernel_Name"]][name].append(float(r["Counter_Value"]))
 if pmc:
     f = pmc["FETCH_SIZE"]
     w = pmc["WRITE_SIZE"]
@@ -39,4 +45,15 @@ if pmc:
     res["pmc"] = {"fetch_kib_per_launch": f, "write_kib_per_launch": w,
                   "fetch_bytes_corrected_per_launch": [2 * 1024 * x for x in f],
                   "write_bytes_per_launch": [1024 * x for x in w]}
+if by_kernel:
+    # mix path: HBM bytes of the whole launch group (step + moments + readjust)
+    # per step-kernel launch, FETCH_SIZE x2 as above
+    nstep = max(len(v["FETCH_SIZE"]) for k, v in by_kernel.items() if "mix_gsn_kernel" in k)
+    tot_f = sum(2 * 1024 * sum(v["FETCH_SIZE"]) for v in by_kernel.values())
+    tot_w = sum(1024 * sum(v["WRITE_SIZE"]) for v in by_kernel.values())
+    res["group"] = {"kernels": {k: {"fetch_bytes_corrected": 2 * 1024 * sum(v["FETCH_SIZE"]),
+                                    "write_bytes": 1024 * sum(v["WRITE_SIZE"]), "launches": len(v["FETCH_SIZE"])}
+                                for k, v in by_kernel.items()},
+                    "step_launches": nstep, "fetch_bytes_corrected_per_group": tot_f / nstep,
+                    "write_bytes_per_group": tot_w / nstep}
 print(json.dumps(res, indent=1))

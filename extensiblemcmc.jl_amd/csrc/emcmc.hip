@@ -707,7 +707,7 @@ emcmc_status select_variant(emcmc_handle *h) {
     }
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
     size_t lds = (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
-    if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc);
+    if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc, diag_block(v.occ) / 64);
     if (kZigLdsBytes + lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu",
@@ -1388,7 +1388,8 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     const uint64_t C = h->cfg.num_chains;
     const int lpc = h->var.lpc;
     const uint64_t threads = C * (uint64_t)lpc;
-    const dim3 block(256), grid((unsigned)((threads + 255) / 256));
+    const unsigned bs = h->var.dense ? 256u : (unsigned)diag_block(h->var.occ);
+    const dim3 block(bs), grid((unsigned)((threads + bs - 1) / bs));
     const TargetHost &t = h->target;
     StepParams p{};
     p.theta = h->d_theta;

@@ -58,12 +58,18 @@ struct MalaParams {
 
 // ℓ_n = y·η − softplus(η), r_n = y − σ(η), one division: t = e^{−|η|},
 // u = 1 + t, v = 1/u, log1p(t) = log(u) − ((u − 1) − t)·v (t if u == 1),
-// σ = (η ≥ 0 ? 1 : t)·v
-__device__ __forceinline__ void logistic_terms(double eta, double y, double &ell, double &r) {
-    const double t = exp_any(-fabs(eta));
+// σ = (η ≥ 0 ? 1 : t)·v.  exp and log are the table-driven forms
+// (emcmc_math.h exp_le0 / log_1_2) with their tables in LDS.
+struct MathLds {
+    double exp2_64[64];
+    double invc[128];
+    double logc[128];
+};
+__device__ __forceinline__ void logistic_terms(double eta, double y, double &ell, double &r, const MathLds &mt) {
+    const double t = exp_le0(-fabs(eta), mt.exp2_64);
     const double u = 1.0 + t;
     const double v = 1.0 / u;
-    const double lp1 = (u == 1.0) ? t : log_pos(u) - ((u - 1.0) - t) * v;
+    const double lp1 = (u == 1.0) ? t : log_1_2(u, mt.invc, mt.logc) - ((u - 1.0) - t) * v;
     const double sp = (eta > 0.0 ? eta : 0.0) + lp1;
     const double sig = (eta >= 0.0 ? 1.0 : t) * v;
     ell = y * eta - sp;
@@ -86,6 +92,12 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
     constexpr int LD = D + 1;        // padded LDS row stride (doubles)
     __shared__ double xs[kMalaTileRows * LD];
     __shared__ double ys[kMalaTileRows];
+    __shared__ MathLds mt;
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) mt.exp2_64[i] = EXP2_64[i];
+    for (int i = threadIdx.x; i < 128; i += blockDim.x) {
+        mt.invc[i] = LOG_INVC[i];
+        mt.logc[i] = LOG_LOGC[i];
+    }  // (the first tile's __syncthreads orders these before any use)
 
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int g = lane >> 4, cl = lane & 15;
@@ -174,7 +186,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
                 ell = eta[q];
                 rr = eta[q] * ys[rb + row];
 #else
-                logistic_terms(eta[q], ys[rb + row], ell, rr);
+                logistic_terms(eta[q], ys[rb + row], ell, rr, mt);
 #endif
                 const bool in = n0 + rb + row < a.nrows;
                 if (in) S = S + ell;

@@ -24,6 +24,8 @@
 #include <stdint.h>
 #include <math.h>
 
+#include "emcmc_tables.h"
+
 #if defined(__HIPCC__)
 #define EMCMC_HD __host__ __device__ __forceinline__
 #else
@@ -237,6 +239,57 @@ EMCMC_HD double log_any(double x) {
     if (x == __builtin_inf()) return x;
     if (x < 0x1p-1022) return log_pos(x * 0x1p54) - 37.42994775023705;
     return log_pos(x);
+}
+
+// ---- table-driven exp (x ≤ 0) and log (1 ≤ u ≤ 2): the MALA logistic terms --
+// e^{−|η|} and log(1 + e^{−|η|}) run once per observation and chain (4·10⁹ times
+// per cfg 3 step), so they get shorter forms than exp_any / log_pos; the
+// correctly rounded tables come from scripts/gen_math_tables.py
+// (emcmc_tables.h; the oracle holds its own copy).
+//
+// exp_le0: x = k·ln2/64 + r, |r| ≤ ln2/128 (Cody–Waite, ln2/64 split so k·hi is
+// exact), e^x = 2^⌊k/64⌋ · 2^{(k mod 64)/64} · e^r with e^r − 1 by a degree-6
+// polynomial (truncation < 3e-20); the table entry times (1 + p) in one fma,
+// the power of two by ldexp (IEEE: subnormal results rounded once, 0 below
+// −745.13).  ≤ 1 ulp (tests/test_oracle.py).  NaN → NaN.
+EMCMC_HD double exp_le0(double x, const double *exp2_64) {
+    const double ln2_64_hi = 6.93147180369123816490e-01 / 64.0, ln2_64_lo = 1.90821492927058770002e-10 / 64.0;
+    const double xc = fmax(x, -746.0);  // keeps k in int range (NaN → −746, selected away)
+    const double kd = rint(xc * 92.332482616893656);  // 64/ln2
+    double r = fma(-kd, ln2_64_hi, xc);
+    r = fma(-kd, ln2_64_lo, r);
+    const int k = (int)kd;
+    const int j = k & 63, m = k >> 6;  // floor(k/64) (arithmetic shift)
+    double q = 1.0 / 720.0;
+    q = fma(q, r, 1.0 / 120.0);
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    const double pm1 = fma(q * r, r, r);  // e^r − 1
+    const double tj = exp2_64[j];
+    const double e = ldexp(fma(tj, pm1, tj), m);
+    return (x != x) ? x : e;
+}
+// log_1_2: u ∈ [1, 2]; u = 2^e·w, w ∈ [1, 2), w in interval j of 128 with
+// centre c_j: log u = e·ln2 − log(RN(1/c_j)) + log1p(r), r = w·RN(1/c_j) − 1
+// (|r| < 2^-8, one fma) by a degree-7 series (truncation < 5e-21).  The error
+// is absolute, ≤ 2^-60 for u near 1 (relative ≤ 1.5 ulp away from 1): what
+// the log-likelihood sum needs, where log1p(t) is added to terms of order 1.
+EMCMC_HD double log_1_2(double u, const double *invc, const double *logc) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const uint64_t b = d2u(u);
+    const double e = (double)((int)(b >> 52) - 1023);  // 0, or 1 at u = 2
+    const double w = u2d((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int j = (int)((b >> 45) & 127u);
+    const double r = fma(w, invc[j], -1.0);
+    double q = 1.0 / 7.0;
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double l1 = fma(q * r, r, r);  // log1p(r)
+    return fma(e, ln2_hi, logc[j]) + fma(e, ln2_lo, l1);
 }
 
 // ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---------------

@@ -58,7 +58,7 @@ def lib():
         L.orc_normal_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
         L.orc_exp_vec.restype = None
         L.orc_exp_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
-        for nm in ("orc_exp_any_vec", "orc_log_any_vec"):
+        for nm in ("orc_exp_any_vec", "orc_log_any_vec", "orc_exp_le0_vec", "orc_log_1_2_vec"):
             getattr(L, nm).restype = None
             getattr(L, nm).argtypes = [dp, dp, C.c_uint64]
         L.orc_markstein_mismatches.restype = C.c_uint64
@@ -195,6 +195,20 @@ def exp_any_vec(x):
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.empty_like(x)
     lib().orc_exp_any_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def exp_le0_vec(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_exp_le0_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def log_1_2_vec(x):
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_log_1_2_vec(_d(x), _d(y), x.size)
     return y
 
 

@@ -29,6 +29,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "oracle_tables.h"
+
 typedef struct {
     uint32_t v[4];
 } orc_u32x4;
@@ -163,6 +165,49 @@ static inline double orc_log_any(double x) {
     if (x == INFINITY) return INFINITY;
     if (x < 0x1p-1022) return orc_log(x * 0x1p54) - ORC_LN2_54;
     return orc_log(x);
+}
+
+/* ---- table-driven exp (x <= 0) and log (1 <= u <= 2) of the MALA logistic
+ * terms.  exp: x = k·ln2/64 + r (Cody–Waite), e^x = 2^floor(k/64) ·
+ * 2^((k mod 64)/64) · (1 + (e^r − 1)), e^r − 1 to degree 6, scaled by ldexp.
+ * log: u = 2^e·w, w in interval j of 128 with centre c_j, log u = e·ln2 −
+ * log(RN(1/c_j)) + log1p(w·RN(1/c_j) − 1), log1p to degree 7.  Tables in
+ * oracle_tables.h (scripts/gen_math_tables.py, correctly rounded). */
+static inline double orc_exp_le0(double x) {
+    const double ln2_64_hi = 6.93147180369123816490e-01 / 64.0, ln2_64_lo = 1.90821492927058770002e-10 / 64.0;
+    if (x != x) return x;
+    const double xc = x < -746.0 ? -746.0 : x;
+    const double kd = rint(xc * 92.332482616893656);
+    double r = fma(-kd, ln2_64_hi, xc);
+    r = fma(-kd, ln2_64_lo, r);
+    const int k = (int)kd;
+    const int j = k & 63;
+    const int m = (k - j) / 64; /* floor(k/64) */
+    double q = 1.0 / 720.0;
+    q = fma(q, r, 1.0 / 120.0);
+    q = fma(q, r, 1.0 / 24.0);
+    q = fma(q, r, 1.0 / 6.0);
+    q = fma(q, r, 0.5);
+    const double pm1 = fma(q * r, r, r);
+    const double tj = ORC_EXP2_64[j];
+    return ldexp(fma(tj, pm1, tj), m);
+}
+
+static inline double orc_log_1_2(double u) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const uint64_t b = orc_d2u(u);
+    const double e = (double)((int)(b >> 52) - 1023);
+    const double w = orc_u2d((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int j = (int)((b >> 45) & 127u);
+    const double r = fma(w, ORC_LOG_INVC[j], -1.0);
+    double q = 1.0 / 7.0;
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double l1 = fma(q * r, r, r);
+    return fma(e, ln2_hi, ORC_LOG_LOGC[j]) + fma(e, ln2_lo, l1);
 }
 
 /* ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ----

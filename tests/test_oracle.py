@@ -171,3 +171,45 @@ def test_markstein_quotient_is_ieee_division(oracle):
     xs = np.concatenate([x, ints, halves])
     for b in list(range(1, 129)):
         assert oracle.markstein_mismatches(b, xs if b in (1, 7, 100, 127, 128) else xs[::16]) == 0
+
+
+def _ulps(a, b):
+    a, b = np.asarray(a, dtype=np.float64), np.asarray(b, dtype=np.float64)
+    ia = a.view(np.int64)
+    ib = b.view(np.int64)
+    return np.abs(ia - ib)
+
+
+def test_exp_le0_table_driven(oracle):
+    """The MALA exp: ≤ 1 ulp against 50-digit e^x on random x ≤ 0 (normal
+    results), IEEE-rounded subnormals, 0 below −745.13, NaN kept."""
+    import mpmath as mp
+
+    rng = np.random.default_rng(5)
+    x = np.concatenate([-rng.exponential(3.0, 4000), -rng.uniform(0, 700, 2000), [0.0, -0.0, -1e-300, -np.log(2)]])
+    y = oracle.exp_le0_vec(x)
+    mp.mp.dps = 40
+    ref = np.array([float(mp.e ** mp.mpf(v)) for v in x])
+    assert _ulps(y, ref).max() <= 1
+    sub = np.array([-709.0, -720.0, -740.0, -745.0, -745.2, -800.0, -np.inf])
+    ys = oracle.exp_le0_vec(sub)
+    refs = np.array([float(mp.e ** mp.mpf(v)) if np.isfinite(v) else 0.0 for v in sub])
+    assert np.all(np.abs(ys - refs) <= 2 * 5e-324 + 2.3e-16 * refs)
+    assert np.isnan(oracle.exp_le0_vec(np.array([np.nan]))[0])
+
+
+def test_log_1_2_table_driven(oracle):
+    """The MALA log on [1, 2]: relative error ≤ 1.5 ulp away from 1, absolute
+    error ≤ 2^-60 near 1 (the log-likelihood adds it to O(1) terms)."""
+    import mpmath as mp
+
+    rng = np.random.default_rng(6)
+    u = np.concatenate([1.0 + rng.random(6000), 1.0 + np.exp(-rng.uniform(0, 40, 2000)), [1.0, 2.0, 1.5, np.nextafter(2.0, 0)]])
+    y = oracle.log_1_2_vec(u)
+    mp.mp.dps = 40
+    ref = np.array([float(mp.log(mp.mpf(v))) for v in u])
+    err = np.abs(y - ref)
+    far = u > 1.01
+    assert np.all(err[far] <= 1.5 * np.spacing(ref[far]))
+    assert np.all(err <= 2.0 ** -60 + 1.5 * np.spacing(ref))
+    assert oracle.log_1_2_vec(np.array([1.0]))[0] == 0.0 or abs(oracle.log_1_2_vec(np.array([1.0]))[0]) < 2 ** -60

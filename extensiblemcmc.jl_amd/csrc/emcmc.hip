@@ -173,6 +173,7 @@ struct emcmc_handle {
     double *d_mean = nullptr, *d_cov = nullptr, *d_LB = nullptr, *d_iLB = nullptr, *d_c0B = nullptr;
     double *d_Lnew = nullptr;
     double *d_mean_alt = nullptr;  // the moments kernel's output mean (swapped with d_mean per launch)
+    double *d_mom_consts = nullptr;  // [steps_per_launch][8] per-step scalars of the moments recurrence
     double *d_mom_scratch = nullptr;  // ACCEPT_ONLY: θ of each step of a launch, for the moments kernel
     uint32_t mix_M = 0;
     // MALA path: carried ∇ℓ(θ) (state_pos layout), padded X and y
@@ -352,6 +353,7 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
         const UpdateHost &u = h->updates[0];
         HIPCHK(h, hipMalloc(&h->d_mean, C * D * sizeof(double)));
         HIPCHK(h, hipMalloc(&h->d_mean_alt, C * D * sizeof(double)));
+        HIPCHK(h, hipMalloc(&h->d_mom_consts, (uint64_t)h->cfg.steps_per_launch * 8 * sizeof(double)));
         HIPCHK(h, hipMalloc(&h->d_cov, C * DP * sizeof(double)));
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) {
             HIPCHK(h, hipMalloc(&h->d_LB, C * DP * sizeof(double)));
@@ -911,6 +913,15 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             mp.C = C;
             mp.N0 = p.N0;
             mp.nsteps = p.nsteps;
+            mp.kst = h->d_mom_consts;
+            {
+                uint64_t n0 = p.N0;
+                uint32_t ns = p.nsteps;
+                double *kst = h->d_mom_consts;
+                void *kargs[] = {&n0, &ns, &kst};
+                HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(&moments_consts_kernel),
+                                          dim3((ns + 63) / 64), dim3(64), kargs, 0, h->stream));
+            }
             void *margs[] = {&mp};
             // one block per 64 chains, one wave per unit of the packed triangle
             const dim3 mgrid((unsigned)((C + 63) / 64)), mblock((unsigned)(64 * h->var.mo_tiles));
@@ -1497,7 +1508,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
-                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt};
+                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->stream) (void)hipStreamDestroy(h->stream);

@@ -325,10 +325,31 @@ struct MixMomentsParams {
     const double *mean;   // [D] state_pos, before the launch
     double *mean_out;     // [D] state_pos, after the launch (written by the diagonal units)
     double *cov;          // [DP] packed upper
+    const double *kst;    // [nsteps][8] per-step scalars (moments_consts_kernel)
     uint64_t C;
     uint64_t N0;          // GenericChainStats.N at the launch's first step
     uint32_t nsteps;
 };
+
+// The step-dependent scalars of the recurrence, (N, N+1, (N−1)/N, N/(N+1),
+// (N+1)/N, 1/N, 1/(N+1)) for the launch's steps, computed once per launch
+// (the same IEEE divisions, so the same bits) instead of by every lane of
+// every wave; the moments kernel reads them with scalar loads.
+__global__ void __launch_bounds__(64) moments_consts_kernel(uint64_t N0, uint32_t nsteps, double *kst) {
+    const uint32_t s = blockIdx.x * 64u + threadIdx.x;
+    if (s >= nsteps) return;
+    const uint64_t N = N0 + s;
+    const double Nd = (double)N, N1d = (double)(N + 1);
+    double *k = kst + 8 * (uint64_t)s;
+    k[0] = Nd;
+    k[1] = N1d;
+    k[2] = (double)(N - 1) / Nd;
+    k[3] = Nd / N1d;
+    k[4] = N1d / Nd;
+    k[5] = 1.0 / Nd;
+    k[6] = 1.0 / N1d;
+    k[7] = 0.0;
+}
 
 template <int D>
 struct MomentTiles {
@@ -487,10 +508,8 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
             if constexpr (EW == 2) return (d & 1) ? v[1] : v[0];
             else return v[0];
         };
-        const uint64_t N = a.N0 + s;
-        const double Nd = (double)N, N1d = (double)(N + 1);
-        const double ca = (double)(N - 1) / Nd, cb = Nd / N1d, cc = N1d / Nd;
-        const double rN = 1.0 / Nd, rN1 = 1.0 / N1d;
+        const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
+        const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
         ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
         if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
         if (s + 1 < a.nsteps) put((s & 1u) ? stage0 : stage1, pf);

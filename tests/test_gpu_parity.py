@@ -141,3 +141,29 @@ def test_fused_schedule_gap_restarts_rolling_rate(oracle):
     ra, _ = eng.get_chain_stats()
     assert np.array_equal(th, st.theta) and np.array_equal(ll, st.ll)
     assert np.array_equal(ra[0], st.ra)
+
+
+@pytest.mark.parametrize("C", [1, 63, 65, 257])
+def test_ragged_and_tiny_chain_counts(oracle, C):
+    """One chain, and counts that leave partial waves / blocks at LPC = 2:
+    every chain still matches the oracle bit for bit."""
+    w = W.cfg2(C)
+    e = run_engine(w, C, 40, lpc=2)
+    o = run_oracle(oracle, w, C, 40)
+    assert_bitwise(e, o)
+
+
+def test_empty_schedule_is_a_no_op(oracle):
+    """emcmc_run with zero steps launches nothing and leaves the state as set."""
+    w = W.cfg2(128)
+    eng = Engine(EngineConfig(dim=w.D, num_chains=128, num_mcmc_steps=10, seed=w.seed))
+    eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    th0 = np.random.default_rng(3).standard_normal((128, w.D))
+    eng.set_state(th0)
+    eng.run(np.zeros((0, 2), dtype=np.uint32))
+    eng.synchronize()
+    th, ll = eng.get_state()
+    assert np.array_equal(th, th0)
+    assert np.all(ll == -np.inf)
+    eng.close()

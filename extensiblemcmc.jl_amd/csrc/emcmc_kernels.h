@@ -88,15 +88,15 @@ __host__ __device__ __forceinline__ uint64_t state_pos(uint64_t d, uint64_t c, u
 
 typedef double d2v __attribute__((ext_vector_type(2)));
 
-// Stage the LDS part of the ziggurat tables (N(0,1) 4096 + Exp(1) 256 layers,
+// Stage the LDS part of the ziggurat tables (N(0,1) 8192 + Exp(1) 256 layers,
 // 70 KiB) into the kernel's STATIC LDS — their addresses are then link-time
 // constants that fold into the ds_read offset field — and `nconst` constants
 // followed by `nobs_d` observation doubles into the dynamic LDS at offset 0
 // (offsets below 64 KiB: a row's reads share one address register).
 struct ZigLds {
+    double n[kZigNL + 2];
     ZigEntry e[256];
     double ef[256];
-    ZigEntry n[kZigNL];
 };
 static_assert(sizeof(ZigLds) == kZigLdsBytes, "LDS prefix of Ziggurat");
 __device__ __forceinline__ ZigTabs stage_lds(double *lds, const Ziggurat *zig, const double *consts, int nconst,
@@ -138,8 +138,8 @@ __device__ __forceinline__ void propose_diag(const ZigTabs &zt, uint32_t key0, u
             if (!zig_normal_fast(zig_split_n(r.z, r.w), zt.n, out[2 * j + 1])) pend |= 1u << (2 * j + 1);
     }
     if constexpr ((EMCMC_ABLATE & 2) != 0) pend = 0;  // timing-only build: no rare paths
-    // wave-uniform loop, one pending draw per lane per trip (with 4096 normal
-    // layers a wave of 1024 draws has ≈ 1.2 pending, usually on one lane); the
+    // wave-uniform loop, one pending draw per lane per trip (with 8192 normal
+    // layers a wave of 1024 draws has ≈ 0.6 pending, usually on one lane); the
     // result is written with selects OUTSIDE the divergent region, so the
     // per-element update stays branch-free v_cndmask code
     while (__ballot(pend != 0) != 0) {
@@ -229,26 +229,26 @@ __device__ __forceinline__ void propose_diag_batched(const ZigTabs &zt, const Wa
     // issued before pair j−1 is consumed, so the LDS latency of the lookups
     // hides behind the next block's integer work
     ZigDraw pa, pb;
-    ZigEntry ta, tb;
+    ZigNPair ta, tb;
 #pragma unroll
     for (int j = 0; j <= N / 2; ++j) {
         ZigDraw na, nb;
-        ZigEntry sa, sb;
+        ZigNPair sa, sb;
         if (j < N / 2) {
             __builtin_amdgcn_sched_barrier(0);
             const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
             na = zig_split_n(r.x, r.y);
             nb = zig_split_n(r.z, r.w);
-            sa = zig_entry(zt.n, na);
-            sb = zig_entry(zt.n, nb);
+            sa = zig_npair(zt.n, na);
+            sb = zig_npair(zt.n, nb);
         }
         __builtin_amdgcn_sched_barrier(0);
         if (j > 0) {
             const int k = j - 1;
             out[2 * k] = zig_scale(pa.v, with_sign(ta.w, pa.sbit));
             out[2 * k + 1] = zig_scale(pb.v, with_sign(tb.w, pb.sbit));
-            if (!(pa.v < ta.kv)) pend |= 1u << (2 * k);
-            if (!(pb.v < tb.kv)) pend |= 1u << (2 * k + 1);
+            if (!(fabs(out[2 * k]) < ta.b)) pend |= 1u << (2 * k);
+            if (!(fabs(out[2 * k + 1]) < tb.b)) pend |= 1u << (2 * k + 1);
             if constexpr (EMCMC_BATCH_MODE == 1)
                 reinterpret_cast<d2v *>(ws.zs + lane * N)[k] = d2v{out[2 * k], out[2 * k + 1]};
         }

@@ -294,26 +294,32 @@ EMCMC_HD double log_1_2(double u, const double *invc, const double *logc) {
 
 // ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---------------
 // The same sampler family as Julia's randn/randexp (Random stdlib), fed by the
-// Philox stream: 4096 layers for N(0,1), 256 for Exp(1).  One 64-bit draw
+// Philox stream: 8192 layers for N(0,1), 256 for Exp(1).  One 64-bit draw
 // (hi:lo) per variate.
-//   N(0,1): layer = lo[11:0], magnitude = (hi:lo)[63:12] (52 bits), sign = lo[12]
-//           (the sign shares the magnitude's last bit, as Julia's randn shares
-//           its 8 layer bits with the magnitude: Random/src/normal.jl)
+//   N(0,1): layer ℓ = lo[12:0], magnitude = (hi:lo)[63:12] (52 bits), sign = lo[13]
+//           (layer and sign share the magnitude's last two bits, as Julia's
+//           randn shares its 8 layer bits with the magnitude: Random/src/normal.jl)
 //   Exp(1): layer = lo[11:4], magnitude = (hi:lo)[63:12] (52 bits), lo[3:0] unused
-// The LDS byte address of the 16-byte table entry is (layer << 4), and
-// v = 1 + u (u = magnitude / 2^bits) is built directly as a double from two
-// v_alignbit_b32, so the fast path is
-//   x = fma(v, W, −W) = u·W (one rounding, the bits of (double)mag · W/2^bits),
-//   accepted iff v < 1 + k/2^bits (the integer test mag < k, exactly).
-// With 4096 normal layers 99.88 % of draws take the fast path (256 layers:
-// 98.5 %), so a wave drawing 1024 normals needs a rare-path pass on ≈ 70 % of
-// its steps instead of on every step.  Wedge/tail draws use the portable
-// log/exp above with fresh counter blocks.  Tables are built on the host by
+// v = 1 + u (u = magnitude / 2^52) is built directly as a double from two
+// v_alignbit_b32, and x = fma(v, W, −W) = u·W is one rounding (the bits of
+// (double)mag · W/2^52).
+// N(0,1) table: 8-byte entries n[0..L] — n[0] = 0, n[j] = x_j (strip j's
+// width, x_1 < … < x_{L−1} = r), n[L] = q (the base strip's width).  Layer ℓ
+// reads the pair (n[ℓ], n[ℓ+1]) = (bound, width) of strip j = ℓ + 1 at byte
+// address ℓ·8 (one ds_read2_b64): accepted iff |x| < bound, i.e. the point
+// lies inside the strip's rectangle (layer L − 1 is the base strip, bound r;
+// layer 0 the top strip, bound 0: never).  8192 layers in the LDS footprint
+// 4096 16-byte entries took: 99.94 % of normals take the fast path (4096:
+// 99.88 %), so a wave drawing 1024 normals needs a rare-path pass on ≈ 45 %
+// of its steps instead of ≈ 70 %.
+// Exp(1) table: 16-byte entries (kv, w), accepted iff v < kv = 1 + k/2^52 (the
+// integer test mag < k, exactly).  Wedge/tail draws use the portable log/exp
+// above with fresh counter blocks.  Tables are built on the host by
 // build_ziggurat() (oracle/ restates the same construction).
-constexpr int kZigNL = 4096;                        // normal layers
-constexpr double kZigNR = 4.3859450348713045;       // normal: rightmost layer edge r (4096 layers)
-constexpr double kZigNV = 3.061541032784645e-4;     // normal: area per layer v
-constexpr double kZigNInvR = 1.0 / 4.3859450348713045;
+constexpr int kZigNL = 8192;                        // normal layers
+constexpr double kZigNR = 4.548600609949139;        // normal: rightmost strip edge r (8192 layers)
+constexpr double kZigNV = 1.5303723494629906e-4;    // normal: area per strip v
+constexpr double kZigNInvR = 1.0 / 4.548600609949139;
 constexpr double kZigER = 7.69711747013104972;      // exponential: r (256 layers)
 constexpr double kZigEV = 3.949659822581572e-3;     // exponential: v
 
@@ -321,43 +327,43 @@ struct ZigEntry {
     double kv;  // 1 + k/2^bits: fast-accept bound on v = 1 + u
     double w;   // layer width x_i (base layer: q = v/f(r))
 };
-// Layout: the prefix [e, ef, n] is what the step kernels stage into LDS
-// (70 KiB); nf is read from global memory on the rare path only.
+// Layout: the prefix [n, e, ef] is what the step kernels stage into LDS
+// (70 KiB; n first, at LDS address 0, so both reads of a layer's pair fold
+// into one ds_read2_b64 on the layer's byte offset); nf is read from global
+// memory on the rare path only.
 struct Ziggurat {
+    double n[kZigNL + 2];  // n[0] = 0, n[j] = x_j (1 ≤ j < L), n[L] = q, n[L+1] = 0 (pad)
     ZigEntry e[256];
-    double ef[256];  // exp(−x_i)
-    ZigEntry n[kZigNL];
-    double nf[kZigNL];  // exp(−x_i²/2)
+    double ef[256];          // exp(−x_i)
+    double nf[kZigNL + 2];   // nf[j] = f(x_j) = exp(−x_j²/2), nf[0] = 1 (x_0 = 0)
 };
 constexpr size_t kZigLdsBytes = offsetof(Ziggurat, nf);
 
 // Where a kernel finds the tables (LDS prefix + global nf, or all global).
 struct ZigTabs {
-    const ZigEntry *n;
+    const double *n;
     const double *nf;
     const ZigEntry *e;
     const double *ef;
 };
 EMCMC_HD ZigTabs zig_tabs(const Ziggurat &z) { return ZigTabs{z.n, z.nf, z.e, z.ef}; }
 inline void build_ziggurat(Ziggurat &z) {
-    {  // N(0,1), f(x) = exp(−x²/2), 52-bit magnitudes
-        const double m = 0x1p52;
-        auto kv = [](uint64_t k) { return u2d(0x3FF0000000000000ull | k); };
+    {  // N(0,1), f(x) = exp(−x²/2): strips x_{L−1} = r down to x_1, then x_0 = 0
         constexpr int L = kZigNL;
-        double dn = kZigNR, tn = dn;
+        double dn = kZigNR;
         const double q = kZigNV / exp_nonpos(-0.5 * (dn * dn));
-        z.n[0].kv = kv((uint64_t)((dn / q) * m));
-        z.n[1].kv = kv(0);
-        z.n[0].w = q;
-        z.n[L - 1].w = dn;
+        z.n[0] = 0.0;
+        z.n[L - 1] = dn;
+        z.n[L] = q;
+        z.n[L + 1] = 0.0;
         z.nf[0] = 1.0;
         z.nf[L - 1] = exp_nonpos(-0.5 * (dn * dn));
+        z.nf[L] = z.nf[L - 1];
+        z.nf[L + 1] = 0.0;
         for (int i = L - 2; i >= 1; --i) {
             dn = sqrt(-2.0 * log_pos(kZigNV / dn + exp_nonpos(-0.5 * (dn * dn))));
-            z.n[i + 1].kv = kv((uint64_t)((dn / tn) * m));
-            tn = dn;
             z.nf[i] = exp_nonpos(-0.5 * (dn * dn));
-            z.n[i].w = dn;
+            z.n[i] = dn;
         }
     }
     {  // Exp(1), f(x) = exp(−x), 52-bit magnitudes
@@ -386,11 +392,11 @@ struct ZigDraw {
     uint32_t sbit;  // sign in bit 31 (normals)
     double v;       // 1 + u
 };
-// N(0,1) draw: layer lo[11:0], magnitude (hi:lo)[63:12], sign lo[12]
+// N(0,1) draw: layer lo[12:0] (off = ℓ·8), magnitude (hi:lo)[63:12], sign lo[13]
 EMCMC_HD ZigDraw zig_split_n(uint32_t hi, uint32_t lo) {
     ZigDraw d;
-    d.off = (lo << 4) & 0xFFF0u;
-    d.sbit = (lo << 19) & 0x80000000u;
+    d.off = (lo << 3) & 0xFFF8u;
+    d.sbit = (lo << 18) & 0x80000000u;
 #if defined(__HIP_DEVICE_COMPILE__)
     const uint32_t vlo = __builtin_amdgcn_alignbit(hi, lo, 12);
     const uint32_t vhi = __builtin_amdgcn_alignbit(0x3FFu, hi, 12);
@@ -416,9 +422,18 @@ EMCMC_HD ZigDraw zig_split_e(uint32_t hi, uint32_t lo) {
     d.v = u2d(((uint64_t)vhi << 32) | vlo);
     return d;
 }
-EMCMC_HD uint32_t zig_layer(const ZigDraw &d) { return d.off >> 4; }
+EMCMC_HD uint32_t zig_layer(const ZigDraw &d) { return d.off >> 4; }    // Exp(1) draws
+EMCMC_HD uint32_t zig_layer_n(const ZigDraw &d) { return d.off >> 3; }  // N(0,1) draws: ℓ
 EMCMC_HD const ZigEntry &zig_entry(const ZigEntry *tab, const ZigDraw &d) {
     return *reinterpret_cast<const ZigEntry *>(reinterpret_cast<const char *>(tab) + d.off);
+}
+// (bound, width) of the strip of N(0,1) layer ℓ: (n[ℓ], n[ℓ+1])
+struct ZigNPair {
+    double b, w;
+};
+EMCMC_HD ZigNPair zig_npair(const double *tab, const ZigDraw &d) {
+    const double *p = reinterpret_cast<const double *>(reinterpret_cast<const char *>(tab) + d.off);
+    return ZigNPair{p[0], p[1]};
 }
 EMCMC_HD double with_sign(double x, uint32_t sbit) { return u2d(d2u(x) | ((uint64_t)sbit << 32)); }
 // u·W with one rounding (v = 1 + u exactly)
@@ -427,18 +442,17 @@ EMCMC_HD double zig_scale(double v, double w) { return fma(v, w, -w); }
 constexpr uint32_t kFaultRngRetries = 2u;  // EMCMC_FAULT_RNG_RETRIES
 constexpr uint32_t kMaxAttempt = 0xFFFFu;
 
-EMCMC_HD bool zig_normal_fast(ZigDraw d, const ZigEntry *tab, double &z) {
-    const ZigEntry t = zig_entry(tab, d);
-    const double ws = with_sign(t.w, d.sbit);
-    z = zig_scale(d.v, ws);
-    return d.v < t.kv;
+EMCMC_HD bool zig_normal_fast(ZigDraw d, const double *tab, double &z) {
+    const ZigNPair t = zig_npair(tab, d);
+    z = zig_scale(d.v, with_sign(t.w, d.sbit));
+    return fabs(z) < t.b;
 }
 
 // Rare path of normal number `gj` of (chain, iter, pidx0) whose attempt-0
 // draw `d` failed the fast test.  Slow step k uses the counter block
 // (pair = gj/2, attempt = 1 + 2k + gj%2), so the two normals of a pair never
 // share a block.
-EMCMC_HD double zig_normal_slow(ZigDraw d, const ZigEntry *tab, const double *f, uint32_t key0, uint32_t key1,
+EMCMC_HD double zig_normal_slow(ZigDraw d, const double *tab, const double *f, uint32_t key0, uint32_t key1,
                                 uint32_t chain, uint32_t iter, uint32_t pidx0, uint32_t gj, uint32_t &faults) {
     const uint32_t pair = gj >> 1, h = gj & 1u;
     for (uint32_t k = 0;; ++k) {
@@ -448,15 +462,15 @@ EMCMC_HD double zig_normal_slow(ZigDraw d, const ZigEntry *tab, const double *f,
             return 0.0;
         }
         const u32x4 b = draw(key0, key1, chain, iter, pair, pidx0, attempt);
-        const uint32_t L = zig_layer(d);
-        if (L == 0) {  // base strip beyond the rectangle: tail x > r
+        const uint32_t j = zig_layer_n(d) + 1u;  // strip
+        if (j == (uint32_t)kZigNL) {  // base strip beyond the rectangle: tail x > r
             const double xx = -log_pos(u01_open0(b.x, b.y)) * kZigNInvR;
             const double yy = -log_pos(u01_open0(b.z, b.w));
             if (yy + yy > xx * xx) return with_sign(kZigNR + xx, d.sbit);
         } else {  // wedge test, else a fresh draw
-            const double x = zig_scale(d.v, tab[L].w);
+            const double x = zig_scale(d.v, tab[j]);
             const double u = u01_closed0(b.x, b.y);
-            if (fma(u, f[L - 1] - f[L], f[L]) < exp_nonpos(-0.5 * (x * x))) return with_sign(x, d.sbit);
+            if (fma(u, f[j - 1] - f[j], f[j]) < exp_nonpos(-0.5 * (x * x))) return with_sign(x, d.sbit);
             d = zig_split_n(b.z, b.w);
             double z;
             if (zig_normal_fast(d, tab, z)) return z;

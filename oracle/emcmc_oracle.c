@@ -382,7 +382,7 @@ ORC_EXPORT void orc_exp_nonpos_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_exp_nonpos(x[i]);
 }
 
-/* Ziggurat tables: kn, wn, fn, ke, we, fe (256 each). */
+/* Ziggurat tables: an, fn (ORC_ZN_L + 2 each), ke, we, fe (256 each). */
 ORC_EXPORT void orc_exp_le0_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_exp_le0(x[i]);
 }
@@ -397,10 +397,9 @@ ORC_EXPORT void orc_log_any_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_log_any(x[i]);
 }
 
-ORC_EXPORT void orc_zig_tables_copy(uint64_t *kn, double *wn, double *fn, uint64_t *ke, double *we, double *fe) {
+ORC_EXPORT void orc_zig_tables_copy(double *an, double *fn, uint64_t *ke, double *we, double *fe) {
     const orc_zig_tables *t = zig();
-    memcpy(kn, t->kn, sizeof t->kn);
-    memcpy(wn, t->wn, sizeof t->wn);
+    memcpy(an, t->an, sizeof t->an);
     memcpy(fn, t->fn, sizeof t->fn);
     memcpy(ke, t->ke, sizeof t->ke);
     memcpy(we, t->we, sizeof t->we);

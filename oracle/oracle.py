@@ -64,7 +64,7 @@ def lib():
         L.orc_markstein_mismatches.restype = C.c_uint64
         L.orc_markstein_mismatches.argtypes = [C.c_double, dp, C.c_uint64]
         L.orc_zig_tables_copy.restype = None
-        L.orc_zig_tables_copy.argtypes = [u64p, dp, dp, u64p, dp, dp]
+        L.orc_zig_tables_copy.argtypes = [dp, dp, u64p, dp, dp]
         _lib = L
     return _lib
 
@@ -231,17 +231,18 @@ def exponentials(seed, n, chain0=0, it=1):
     return out
 
 
-ZIG_NORMAL_LAYERS = 4096  # oracle_math.h ORC_ZN_L
+ZIG_NORMAL_LAYERS = 8192  # oracle_math.h ORC_ZN_L
 
 
 def zig_tables():
-    kn = np.empty(ZIG_NORMAL_LAYERS, dtype=np.uint64)
+    """an[0..L+1] / fn[0..L+1]: normal strip edges x_j (an[L] = base width q)
+    and f(x_j); ke/we/fe: the 256-strip Exp(1) table."""
+    an, fn = np.empty(ZIG_NORMAL_LAYERS + 2), np.empty(ZIG_NORMAL_LAYERS + 2)
     ke = np.empty(256, dtype=np.uint64)
-    wn, fn = np.empty(ZIG_NORMAL_LAYERS), np.empty(ZIG_NORMAL_LAYERS)
     we, fe = np.empty(256), np.empty(256)
     u64 = C.POINTER(C.c_uint64)
-    lib().orc_zig_tables_copy(kn.ctypes.data_as(u64), _d(wn), _d(fn), ke.ctypes.data_as(u64), _d(we), _d(fe))
-    return {"kn": kn, "wn": wn, "fn": fn, "ke": ke, "we": we, "fe": fe}
+    lib().orc_zig_tables_copy(_d(an), _d(fn), ke.ctypes.data_as(u64), _d(we), _d(fe))
+    return {"an": an, "fn": fn, "ke": ke, "we": we, "fe": fe}
 
 
 def markstein_mismatches(b, x):

@@ -211,17 +211,21 @@ static inline double orc_log_1_2(double u) {
 }
 
 /* ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ----
- * N(0,1): 4096 strips, Exp(1): 256 strips, 52-bit magnitudes.  r and v of the 4096-strip normal table solve the M&T closure
- * (top strip area = v) to double precision. */
-#define ORC_ZN_L 4096
-#define ORC_ZN_R 4.3859450348713045
-#define ORC_ZN_V 3.061541032784645e-4
+ * N(0,1): 8192 strips, Exp(1): 256 strips, 52-bit magnitudes.  r and v of the
+ * 8192-strip normal table solve the M&T closure (top strip area = v) to double
+ * precision (tests/test_oracle.py checks it in 50-digit arithmetic). */
+#define ORC_ZN_L 8192
+#define ORC_ZN_R 4.548600609949139
+#define ORC_ZN_V 1.5303723494629906e-4
 #define ORC_ZE_R 7.69711747013104972
 #define ORC_ZE_V 3.949659822581572e-3
 
+/* N(0,1): an[0] = 0 (x_0), an[j] = x_j for 1 ≤ j < L (x_{L−1} = r), an[L] = q
+ * (base strip width), an[L+1] = 0; fn[j] = f(x_j), fn[0] = 1.  Layer ℓ of a
+ * draw is strip j = ℓ + 1 with (bound, width) = (an[j−1], an[j]): strip L is
+ * the base (bound r), strip 1 the top (bound 0). */
 typedef struct {
-    uint64_t kn[ORC_ZN_L];
-    double wn[ORC_ZN_L], fn[ORC_ZN_L];
+    double an[ORC_ZN_L + 2], fn[ORC_ZN_L + 2];
     uint64_t ke[256];
     double we[256], fe[256];
 } orc_zig_tables;
@@ -229,21 +233,20 @@ typedef struct {
 /* zigset (M&T Fig. 1): strip i ≥ 1 spans [0, x_i] × [f(x_i), f(x_{i−1})],
  * x_{L−1} = r; strip 0 is the base rectangle of width q = v/f(r) plus the tail */
 static inline void orc_zig_build(orc_zig_tables *t) {
-    const double mn = 4503599627370496.0; /* 2^52 */
-    double dn = ORC_ZN_R, tn = dn;
+    double dn = ORC_ZN_R;
     double q = ORC_ZN_V / orc_exp_nonpos(-0.5 * (dn * dn));
-    t->kn[0] = (uint64_t)((dn / q) * mn);
-    t->kn[1] = 0;
-    t->wn[0] = q / mn;
-    t->wn[ORC_ZN_L - 1] = dn / mn;
+    t->an[0] = 0.0;
+    t->an[ORC_ZN_L - 1] = dn;
+    t->an[ORC_ZN_L] = q;
+    t->an[ORC_ZN_L + 1] = 0.0;
     t->fn[0] = 1.0;
     t->fn[ORC_ZN_L - 1] = orc_exp_nonpos(-0.5 * (dn * dn));
+    t->fn[ORC_ZN_L] = t->fn[ORC_ZN_L - 1];
+    t->fn[ORC_ZN_L + 1] = 0.0;
     for (int i = ORC_ZN_L - 2; i >= 1; --i) {
         dn = sqrt(-2.0 * orc_log(ORC_ZN_V / dn + orc_exp_nonpos(-0.5 * (dn * dn))));
-        t->kn[i + 1] = (uint64_t)((dn / tn) * mn);
-        tn = dn;
         t->fn[i] = orc_exp_nonpos(-0.5 * (dn * dn));
-        t->wn[i] = dn / mn;
+        t->an[i] = dn;
     }
     const double me = 4503599627370496.0; /* 2^52 */
     double de = ORC_ZE_R, te = de;
@@ -269,11 +272,16 @@ typedef struct {
     uint64_t mag;
 } orc_zdraw;
 
-/* normal: layer = lo[11:0], magnitude = (hi:lo)[63:12] (52 bits), sign = lo[12]
- * (the magnitude's last bit; Julia's randn likewise reuses its layer bits) */
+/* normal: layer = lo[12:0], magnitude = (hi:lo)[63:12] (52 bits), sign = lo[13]
+ * (the magnitude's last two bits; Julia's randn likewise reuses its layer bits) */
 static inline orc_zdraw orc_zsplit_n(uint32_t hi, uint32_t lo) {
-    orc_zdraw d = {lo & 4095u, (lo >> 12) & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
+    orc_zdraw d = {lo & 8191u, (lo >> 13) & 1u, ((uint64_t)hi << 20) | (uint64_t)(lo >> 12)};
     return d;
+}
+/* |x| of a normal draw in its strip j = layer + 1: (double)mag · x_j / 2^52
+ * (one rounding), and the rectangle test |x| < x_{j−1} */
+static inline double orc_zx_n(const orc_zig_tables *t, orc_zdraw d) {
+    return (double)d.mag * (t->an[d.layer + 1] * 0x1p-52);
 }
 /* exponential: layer = lo[11:4], magnitude = (hi:lo)[63:12] (52 bits) */
 static inline orc_zdraw orc_zsplit_e(uint32_t hi, uint32_t lo) {
@@ -292,7 +300,8 @@ static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k
                                 uint32_t pidx0, uint32_t g, uint32_t *faults) {
     orc_u32x4 r0 = orc_draw(k0, k1, chain, iter, g >> 1, pidx0, 0);
     orc_zdraw d = (g & 1u) ? orc_zsplit_n(r0.v[2], r0.v[3]) : orc_zsplit_n(r0.v[0], r0.v[1]);
-    if (d.mag < t->kn[d.layer]) return orc_signed((double)d.mag * t->wn[d.layer], d.negative);
+    double x = orc_zx_n(t, d);
+    if (x < t->an[d.layer]) return orc_signed(x, d.negative);
     for (uint32_t step = 0;; ++step) {
         uint32_t attempt = 1u + 2u * step + (g & 1u);
         if (attempt > ORC_MAX_ATTEMPT) {
@@ -300,17 +309,18 @@ static inline double orc_normal(const orc_zig_tables *t, uint32_t k0, uint32_t k
             return 0.0;
         }
         orc_u32x4 b = orc_draw(k0, k1, chain, iter, g >> 1, pidx0, attempt);
-        if (d.layer == 0) { /* tail beyond r */
+        const uint32_t j = d.layer + 1u; /* strip */
+        if (j == ORC_ZN_L) { /* base strip: tail beyond r */
             double xx = -orc_log(orc_u01_open0(b.v[0], b.v[1])) * (1.0 / ORC_ZN_R);
             double yy = -orc_log(orc_u01_open0(b.v[2], b.v[3]));
             if (yy + yy > xx * xx) return orc_signed(ORC_ZN_R + xx, d.negative);
-        } else {
-            double x = (double)d.mag * t->wn[d.layer];
+        } else { /* wedge of strip j: y uniform on [f(x_j), f(x_{j−1})] */
             double u = orc_u01_closed0(b.v[0], b.v[1]);
-            if (fma(u, t->fn[d.layer - 1] - t->fn[d.layer], t->fn[d.layer]) < orc_exp_nonpos(-0.5 * (x * x)))
+            if (fma(u, t->fn[j - 1] - t->fn[j], t->fn[j]) < orc_exp_nonpos(-0.5 * (x * x)))
                 return orc_signed(x, d.negative);
             d = orc_zsplit_n(b.v[2], b.v[3]);
-            if (d.mag < t->kn[d.layer]) return orc_signed((double)d.mag * t->wn[d.layer], d.negative);
+            x = orc_zx_n(t, d);
+            if (x < t->an[d.layer]) return orc_signed(x, d.negative);
         }
     }
 }

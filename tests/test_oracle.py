@@ -1,7 +1,7 @@
 """Oracle self-checks (CPU): the shared variate stream and canonical arithmetic.
 
 Pins: Random123 Philox KATs (tests/golden/philox_kat.json); accuracy of the
-restated log / exp against numpy; the 256-strip ziggurat tables (equal strip
+restated log / exp against numpy; the 8192-strip N(0,1) and 256-strip Exp(1) ziggurat tables (equal strip
 areas) and the N(0,1) / Exp(1) distributions they produce; the canonical
 Cholesky and summation against LAPACK / math.fsum; and the claim the kernels
 rely on that the dense (general-L) formulas give the same bits as the diagonal
@@ -42,15 +42,33 @@ def test_exp_accuracy(oracle):
     assert y[x == 0.0][0] == 1.0
 
 
-def test_ziggurat_tables(oracle):
-    """Strips of equal area v (M&T construction) — 4096 for N(0,1), 256 for
-    Exp(1), 52-bit magnitudes: x_{L-1} = r, top strip
-    reaches x_0 ≈ 0, thresholds below 2^bits and increasing towards the base."""
+R_N, V_N = 4.548600609949139, 1.5303723494629906e-4  # 8192-strip normal table (oracle_math.h)
+
+
+def test_ziggurat_normal_table(oracle):
+    """8192 strips of equal area v (M&T construction) as 8-byte edges: an[0] = 0,
+    an[j] = x_j increasing to x_{L-1} = r, an[L] = q = v/f(r) (base strip); a
+    layer's (bound, width) pair is (an[j-1], an[j]), so every bound is below its
+    width (the top strip's bound is 0: it never fast-accepts)."""
     t = oracle.zig_tables()
-    for k, w, f, r, v, fx, L, m in ((t["kn"], t["wn"], t["fn"], 4.3859450348713045, 3.061541032784645e-4,
-                                     lambda x: np.exp(-0.5 * x * x), 4096, 2.0 ** 52),
-                                    (t["ke"], t["we"], t["fe"], 7.69711747013104972, 3.949659822581572e-3,
-                                     lambda x: np.exp(-x), 256, 2.0 ** 52)):
+    an, fn, L = t["an"], t["fn"], 8192
+    assert len(an) == L + 2 and an[0] == 0.0 and fn[0] == 1.0
+    x = an[1:L]  # x_1 .. x_{L-1}
+    assert x[-1] == R_N and np.all(np.diff(x) > 0)
+    assert np.allclose(fn[1:L], np.exp(-0.5 * x * x), rtol=1e-14)
+    areas = x * (fn[0:L - 1] - fn[1:L])  # strip j spans f(x_j)..f(x_{j-1})
+    assert np.allclose(areas, V_N, rtol=1e-9)
+    assert an[L] * np.exp(-0.5 * R_N * R_N) == pytest.approx(V_N, rel=1e-12)  # base width q
+    assert np.all(an[0:L] < an[1:L + 1])  # bound < width for every layer (base: r < q)
+
+
+def test_ziggurat_tables(oracle):
+    """Strips of equal area v (M&T construction) — 256 for Exp(1), 52-bit
+    magnitudes: x_{L-1} = r, top strip reaches x_0 ≈ 0, thresholds below 2^bits
+    and increasing towards the base."""
+    t = oracle.zig_tables()
+    for k, w, f, r, v, fx, L, m in ((t["ke"], t["we"], t["fe"], 7.69711747013104972, 3.949659822581572e-3,
+                                     lambda x: np.exp(-x), 256, 2.0 ** 52),):
         assert len(k) == L
         x = w * m  # x_i for i ≥ 1; base strip width for i = 0
         assert x[L - 1] == pytest.approx(r, rel=1e-15)
@@ -64,17 +82,17 @@ def test_ziggurat_tables(oracle):
 
 
 def test_ziggurat_normal_constants_close_the_table():
-    """r, v of the 4096-strip normal table: v = r·f(r) + ∫_r^∞ f, and the
+    """r, v of the 8192-strip normal table: v = r·f(r) + ∫_r^∞ f, and the
     recursion from x = r up through the strips ends with the top strip's area
     equal to v (checked in 50-digit arithmetic)."""
     import mpmath as mp
 
     mp.mp.dps = 50
-    r, v = mp.mpf(4.3859450348713045), mp.mpf(3.061541032784645e-4)
+    r, v = mp.mpf(R_N), mp.mpf(V_N)
     f = lambda x: mp.e ** (-x * x / 2)  # noqa: E731
     assert abs(r * f(r) + mp.sqrt(2 * mp.pi) * mp.ncdf(-r) - v) / v < 1e-14  # r, v rounded to double
     x = r
-    for _ in range(4096 - 2):
+    for _ in range(8192 - 2):
         x = mp.sqrt(-2 * mp.log(v / x + f(x)))
     assert abs(x * (1 - f(x)) - v) / v < 1e-9
 
@@ -85,9 +103,9 @@ def test_ziggurat_distributions(oracle):
     z = oracle.normals(W.SEED, 400_000)
     assert abs(z.mean()) < 0.006 and abs(z.std() - 1.0) < 0.006
     assert stats.kstest(z, "norm").pvalue > 1e-3
-    # tail beyond r = 4.386 is reached through the rare path and has the right mass
-    tail = (np.abs(z) > 4.3859450348713045).mean()
-    assert abs(tail - 2 * stats.norm.sf(4.3859450348713045)) < 4e-5
+    # tail beyond r = 4.55 is reached through the rare path and has the right mass
+    tail = (np.abs(z) > R_N).mean()
+    assert abs(tail - 2 * stats.norm.sf(R_N)) < 2e-5
     assert tail > 0
     e = oracle.exponentials(W.SEED, 200_000)
     assert abs(e.mean() - 1.0) < 0.01

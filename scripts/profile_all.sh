@@ -4,7 +4,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 for W in ${WORKLOADS:-cfg2 cfg4 cfg3}; do
   case $W in
-    cfg2) T=r1 B="" S=300 ;;
+    cfg2) T=r1 B="" S=1000 ;;
     cfg4) T=r1_cfg4 B="--workload cfg4" S=200 ;;
     cfg3) T=r1_cfg3 B="--workload cfg3" S=20; export WARMUP=5 ;;
   esac

@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2")
+    ap.add_argument("--shard", type=int, default=-1,
+                    help="single-process run of shard r: global chains [r·C, (r+1)·C) (default: this rank's)")
     ap.add_argument("--chains-per-gpu", type=int, default=0,
                     help="0: 65,536 (cfg2) / 32,768 (cfg3) / 131,072 (cfg4)")
     ap.add_argument("--haario-k", type=int, default=200)
@@ -137,7 +139,8 @@ def main():
     ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
     hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
     M = a.warmup + a.steps * a.reps
-    eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=rank * Cg,
+    first = (a.shard if a.shard >= 0 else rank) * Cg  # global id of this process's chain 0
+    eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=first,
                               device=local, history_mode=hist, lanes_per_chain=a.lpc,
                               steps_per_launch=a.steps_per_launch, history_ring=a.history_ring))
     stream_bufs = None
@@ -253,7 +256,7 @@ def main():
                          if cfg4 else
                          f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64"),
             "chains_per_gpu": Cg,
-            "total_chains": total_chains,
+            "total_chains": total_chains, "first_chain_id": first,
             "dim": w.D,
             "num_obs": w.nobs,
             "proposal": (f"MALA(ϵ={w.eps:.4g})" if cfg3 else
@@ -313,7 +316,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
         if not a.history_ring:
             try:
-                out["parity"] = parity_sample(eng, w, a, ll_mode)
+                out["parity"] = parity_sample(eng, w, a, ll_mode, first)
             except Exception as e:
                 out["parity"] = {"error": repr(e)}
     print(json.dumps(out))
@@ -322,8 +325,9 @@ def main():
         dist.destroy_process_group()
 
 
-def parity_sample(eng, w, a, ll_mode, n=8):
-    """Replay n random chains of the measured run on the oracle (bitwise)."""
+def parity_sample(eng, w, a, ll_mode, first=0, n=8):
+    """Replay n random chains of the measured run on the oracle (bitwise); local
+    chain c has the global id (RNG key) first + c."""
     from extensible_mcmc import _lib as L
     from oracle import oracle as O
 
@@ -340,7 +344,7 @@ def parity_sample(eng, w, a, ll_mode, n=8):
         hist_theta = eng.get_history(L.H_STATE, S, 1)[0, 0]
         for c in picks[:2]:
             st = O.MALAState(np.zeros((1, w.D)), w.X, w.y, nthreads=16)
-            h = O.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=1, nsteps=S, chain0=int(c), nthreads=16)
+            h = O.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=1, nsteps=S, chain0=first + int(c), nthreads=16)
             ok_acc &= bool(np.array_equal(acc[:, c], h["acc"][:, 0]))
             ok_th &= bool(np.array_equal(hist_theta[c], st.theta[0]))
         return {"chains_replayed": 2, "iterations": int(S), "accept_stream_bitwise": ok_acc,
@@ -349,11 +353,11 @@ def parity_sample(eng, w, a, ll_mode, n=8):
         if w.haario_k is not None:
             st = O.MixState(np.zeros((1, w.D)), sigma_b=w.sigma_b)
             h = O.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
-                          lam=w.lam, haario_k=w.haario_k, chain0=int(c), ll_mode=ll_mode)
+                          lam=w.lam, haario_k=w.haario_k, chain0=first + int(c), ll_mode=ll_mode)
         else:
             st = O.OracleState(np.zeros((1, w.D)))
             h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
-                          chain0=int(c), ll_mode=ll_mode, history=True)
+                          chain0=first + int(c), ll_mode=ll_mode, history=True)
         ok_acc &= bool(np.array_equal(acc[:, c], h["acc"][:, 0]))
         ok_th &= bool(np.array_equal(theta[c], st.theta[0]) and ll[c] == st.ll[0])
     return {"chains_replayed": int(n), "iterations": int(S), "accept_stream_bitwise": ok_acc,

@@ -39,6 +39,24 @@ def test_device_variates_match_oracle(oracle, D):
         assert E[i] == Eo
 
 
+def test_device_variates_cover_every_ziggurat_path(oracle):
+    """2M normals and 32k accept exponentials of one chain, all bitwise equal to the
+    oracle, including the rare paths: N(0,1) draws beyond the base strip's edge r
+    (tail, ≈ 5e-6 per draw), draws from wedges (≈ 6e-4) and Exp(1) draws past
+    its r."""
+    R_N, R_E = 4.548600609949139, 7.69711747013104972
+    n, D, chain, it0 = 32768, 64, 12345, 1000
+    z, E = L.probe_variates(W.SEED, np.full(n, chain, np.uint32), np.arange(it0, it0 + n, dtype=np.uint32), D)
+    zo = oracle.normals(W.SEED, n * D, chain=chain, iter0=it0).reshape(n, D)
+    assert np.array_equal(z, zo)
+    assert (np.abs(z) > R_N).sum() >= 2  # tail path taken (expected ≈ 11)
+    Eo = np.array([oracle.step_variates(W.SEED, chain, int(i), 1)[1] for i in range(it0, it0 + 2048)])
+    assert np.array_equal(E[:2048], Eo)
+    En = L.probe_variates(W.SEED, np.arange(1, 2 ** 20 + 1, dtype=np.uint32), np.full(2 ** 20, 7, np.uint32), 1)[1]
+    assert np.array_equal(En, oracle.exponentials(W.SEED, 2 ** 20, chain0=1, it=7))
+    assert (En > R_E).sum() > 0 and abs(En.mean() - 1.0) < 0.005  # Exp(1) tail path taken
+
+
 @pytest.mark.parametrize("lpc", [1, 2, 4])
 @pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
 def test_d32_headline_shape(oracle, lpc, ll_mode):

@@ -13,9 +13,9 @@
  *  - natural log: fdlibm e_log.c argument reduction + Lg1..Lg7 polynomial,
  *    evaluated with the single formula of its main branch.
  *  - exp on [-700, 0]: ln2 range reduction + degree-13 Taylor polynomial.
- *  - Marsaglia & Tsang's ziggurat, 256 strips (J. Stat. Softw. 5(8), 2000),
- *    for N(0,1) and Exp(1) — the sampler family Julia's randn/randexp use —
- *    with 52-bit magnitudes drawn from the Philox stream.
+ *  - Marsaglia & Tsang's ziggurat (J. Stat. Softw. 5(8), 2000), 8192 strips
+ *    for N(0,1) and 256 for Exp(1) — the sampler family Julia's randn/randexp
+ *    use — with 52-bit magnitudes drawn from the Philox stream.
  *
  * The reference (Julia) draws from Random.GLOBAL_RNG via Distributions
  * (src/transition_kernels/random_walk.jl:147, src/run.jl:278); that stream

@@ -1,0 +1,60 @@
+// Do fp64 MFMA and fp64 VALU overlap on one SIMD?  Blocks of 1024 threads, one
+// per CU (16 waves: 4 per SIMD).  MODE 1: waves 0–7 (2 per SIMD, enough to
+// saturate the f64 MFMA pipe) run 8 v_mfma_f64_16x16x4f64 chains, the rest
+// exit; MODE 2: waves 8–15 run 8 v_fma_f64 chains, the rest exit; MODE 3: both.  Overlap ⇔ t3 ≈ max(t1, t2); a shared fp64 datapath
+// ⇔ t3 ≈ t1 + t2.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#define CK(x) do { hipError_t e = (x); if (e) { printf("%s: %s\n", #x, hipGetErrorString(e)); exit(1);} } while (0)
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+template <int MODE>
+__global__ void __launch_bounds__(1024) k(double *out, int nm, int nv) {
+  const int wave = threadIdx.x >> 6;
+  const bool mf = wave < 8;  // 16 waves per CU: waves 0–7 (2 per SIMD) MFMA, 8–15 (2 per SIMD) VALU
+  double acc = 0.0;
+  if (mf && (MODE & 1)) {
+    d4 c[8];
+    for (int j = 0; j < 8; ++j) c[j] = d4{0, 0, 0, 0};
+    double a = 1.0 + threadIdx.x * 1e-9, b = 0.5;
+    for (int i = 0; i < nm; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) c[j] = __builtin_amdgcn_mfma_f64_16x16x4f64((j & 1) ? a : b, (j & 2) ? a : b, c[j], 0, 0, 0);
+    for (int j = 0; j < 8; ++j) acc += c[j][j & 3];
+  }
+  if (!mf && (MODE & 2)) {
+    double v[8];
+    for (int j = 0; j < 8; ++j) v[j] = 1.0 + threadIdx.x * 1e-9 + j;
+    for (int i = 0; i < nv; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = fma(v[j], 0.9999999, 1e-9);
+    for (int j = 0; j < 8; ++j) acc += v[j];
+  }
+  out[blockIdx.x * 1024 + threadIdx.x] = acc;
+}
+
+template <int MODE> float run(double *o, int nm, int nv) {
+  hipEvent_t a, b; CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
+  hipLaunchKernelGGL(k<MODE>, dim3(256), dim3(1024), 0, 0, o, nm, nv);
+  CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int r = 0; r < 5; ++r) {
+    CK(hipEventRecord(a));
+    hipLaunchKernelGGL(k<MODE>, dim3(256), dim3(1024), 0, 0, o, nm, nv);
+    CK(hipEventRecord(b)); CK(hipEventSynchronize(b));
+    float ms; CK(hipEventElapsedTime(&ms, a, b)); if (ms < best) best = ms;
+  }
+  return best;
+}
+
+int main() {
+  double *o; CK(hipMalloc(&o, 256 * 1024 * 8));
+  const int nm = 10000;
+  for (int nv : {10000, 20000, 40000}) {
+    const float t1 = run<1>(o, nm, nv), t2 = run<2>(o, nm, nv), t3 = run<3>(o, nm, nv);
+    printf("mfma %d×8, fma %d×8 per wave: mfma-only %.3f ms, valu-only %.3f ms, both %.3f ms "
+           "(max %.3f, sum %.3f)\n", nm, nv, t1, t2, t3, t1 > t2 ? t1 : t2, t1 + t2);
+  }
+  return 0;
+}

@@ -65,8 +65,10 @@ struct MathLds {
     double invc[128];
     double logc[128];
 };
+// exp_le0 without its NaN select: a NaN η still makes ℓ_n = y·η − … NaN, so the
+// chain's ll° is NaN (fault bit, rejected) with the same bits everywhere else.
 __device__ __forceinline__ void logistic_terms(double eta, double y, double &ell, double &r, const MathLds &mt) {
-    const double t = exp_le0(-fabs(eta), mt.exp2_64);
+    const double t = exp_le0<false>(-fabs(eta), mt.exp2_64);
     const double u = 1.0 + t;
     const double v = 1.0 / u;
     const double lp1 = (u == 1.0) ? t : log_1_2(u, mt.invc, mt.logc) - ((u - 1.0) - t) * v;
@@ -160,6 +162,8 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
         // the matrix pipe works while the VALU evaluates exp/log/σ (they are
         // independent); a region holds one block's temporaries.
         constexpr int NB = kMalaTileRows / 16;
+        // rows of this tile below N (all 64 but in the last tile)
+        const uint32_t rem = (uint32_t)(a.nrows - n0 < (uint64_t)kMalaTileRows ? a.nrows - n0 : kMalaTileRows);
         mala_d4 en = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int j = 0; j < J; ++j)
@@ -188,9 +192,10 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
 #else
                 logistic_terms(eta[q], ys[rb + row], ell, rr, mt);
 #endif
-                const bool in = n0 + rb + row < a.nrows;
-                if (in) S = S + ell;
-                r[q] = in ? rr : 0.0;
+                // rows past N are zero rows of X, so their r only meets zeros in the
+                // ∇ℓ MFMA (fma(0, r, G) = G for finite r); only ℓ is masked
+                if ((uint32_t)(rb + row) < rem) S = S + ell;
+                r[q] = rr;
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q)

@@ -252,6 +252,7 @@ EMCMC_HD double log_any(double x) {
 // polynomial (truncation < 3e-20); the table entry times (1 + p) in one fma,
 // the power of two by ldexp (IEEE: subnormal results rounded once, 0 below
 // −745.13).  ≤ 1 ulp (tests/test_oracle.py).  NaN → NaN.
+template <bool NANSEL = true>
 EMCMC_HD double exp_le0(double x, const double *exp2_64) {
     const double ln2_64_hi = 6.93147180369123816490e-01 / 64.0, ln2_64_lo = 1.90821492927058770002e-10 / 64.0;
     const double xc = fmax(x, -746.0);  // keeps k in int range (NaN → −746, selected away)
@@ -268,6 +269,7 @@ EMCMC_HD double exp_le0(double x, const double *exp2_64) {
     const double pm1 = fma(q * r, r, r);  // e^r − 1
     const double tj = exp2_64[j];
     const double e = ldexp(fma(tj, pm1, tj), m);
+    if constexpr (!NANSEL) return e;  // x must be a number (NaN gives ≈ 0, not NaN)
     return (x != x) ? x : e;
 }
 // log_1_2: u ∈ [1, 2]; u = 2^e·w, w ∈ [1, 2), w in interval j of 128 with

@@ -116,6 +116,7 @@ mutable struct MI355XGlobalWorkspace{T} <: eMCMC.GlobalWorkspace{T}
     dim::Int
     num_updates::Int
     num_locals::Int
+    num_coords::Vector{Int}   # per update: length(updt.coords)
 end
 
 struct MI355XLocalWorkspace{T} <: eMCMC.LocalWorkspace{T}
@@ -217,7 +218,8 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
     θ0 = repeat(Float64.(θinit), be.num_chains)                     # [C][D] row-major
     check(ccall((:emcmc_set_state, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), h[], θ0, C_NULL),
           h[], "emcmc_set_state")
-    ws = MI355XGlobalWorkspace{T}(h[], be, num_mcmc_steps, D, length(updates), 0)
+    ws = MI355XGlobalWorkspace{T}(h[], be, num_mcmc_steps, D, length(updates), 0,
+                                  [length(u.coords) for u in updates])
     finalizer(w -> ccall((:emcmc_destroy, LIB), Cvoid, (Ptr{Cvoid},), w.handle), ws)
     ws
 end
@@ -288,6 +290,154 @@ function state_history(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integ
     out
 end
 
-export MI355XBackend, state_history
+function _history(gws::MI355XGlobalWorkspace, which, out, iter_first, n)
+    check(ccall((:emcmc_get_history, LIB), Cint,
+                (Ptr{Cvoid}, UInt32, UInt64, UInt64, Ptr{Cvoid}, Csize_t),
+                gws.handle, which, iter_first, n, out, sizeof(out)), gws.handle, "emcmc_get_history")
+    out
+end
+
+"""
+    proposal_history(gws, iter_first, n) -> Array{Float64,4} (D, C, P, n)
+
+`state_proposal_history[iter][pidx]` (run.jl:237-239) of every chain.
+"""
+proposal_history(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integer) =
+    _history(gws, H_PROPOSAL, Array{Float64}(undef, gws.dim, gws.backend.num_chains, gws.num_updates, n),
+             iter_first, n)
+
+"""
+    ll_history(gws, iter_first, n) -> Array{Float64,3} (C, P, n)
+
+`local_wss[pidx].sub_ws.ll_history` (run.jl:333) of every chain.
+"""
+ll_history(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integer) =
+    _history(gws, H_LL, Array{Float64}(undef, gws.backend.num_chains, gws.num_updates, n), iter_first, n)
+
+"""
+    acceptance_history(gws, iter_first, n) -> Array{Bool,3} (C, P, n)
+
+`local_wss[pidx].acceptance_history` (run.jl:334) of every chain, unpacked
+from the device's one-bit-per-chain rows.
+"""
+function acceptance_history(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integer)
+    C = gws.backend.num_chains
+    words = _history(gws, H_ACCEPT, Array{UInt64}(undef, cld(C, 64), gws.num_updates, n), iter_first, n)
+    [((words[(c - 1) >> 6 + 1, p, i] >> ((c - 1) & 63)) & 1) == 1 for c in 1:C, p in 1:gws.num_updates, i in 1:n]
+end
+
+"""
+    rolling_acceptance(gws) -> (rolling_ar::Matrix{Float64} (C, P), accepted::Matrix{UInt64} (C, P))
+
+Current `GenericChainStats.rolling_ar[last iteration][pidx]` (chain_statistics.jl:51-65)
+and accepted counts of every chain.
+"""
+function rolling_acceptance(gws::MI355XGlobalWorkspace)
+    ra = Matrix{Float64}(undef, gws.backend.num_chains, gws.num_updates)
+    acc = Matrix{UInt64}(undef, gws.backend.num_chains, gws.num_updates)
+    check(ccall((:emcmc_get_chain_stats, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{UInt64}), gws.handle, ra, acc),
+          gws.handle, "emcmc_get_chain_stats")
+    ra, acc
+end
+
+"""
+    adaptation_state(gws, pidx) -> (ϵ::Matrix{Float64} (C, k), proposed::Vector{UInt32}, accepted::Vector{UInt32})
+
+UniformRandomWalk ϵ as adapted and AdaptationUnifRW's counters
+(adaptation.jl:51-70, 273-329) of update `pidx` for every chain.
+"""
+function adaptation_state(gws::MI355XGlobalWorkspace, pidx::Integer)
+    C, k = gws.backend.num_chains, gws.num_coords[pidx]
+    ϵ = Matrix{Float64}(undef, k, C)
+    prop, acc = Vector{UInt32}(undef, C), Vector{UInt32}(undef, C)
+    check(ccall((:emcmc_get_update_state, LIB), Cint, (Ptr{Cvoid}, UInt32, Ptr{Float64}, Ptr{UInt32}, Ptr{UInt32}),
+                gws.handle, UInt32(pidx), ϵ, prop, acc), gws.handle, "emcmc_get_update_state")
+    permutedims(ϵ), prop, acc
+end
+
+"""
+    chain_moments(gws) -> (mean::Matrix{Float64} (C, D), cov::Array{Float64,3} (D, D, C))
+
+GenericChainStats running mean/cov of every chain (chain_statistics.jl:46-49).
+"""
+function chain_moments(gws::MI355XGlobalWorkspace)
+    C, D = gws.backend.num_chains, gws.dim
+    m = Matrix{Float64}(undef, D, C)
+    cov = Array{Float64}(undef, D, D, C)   # symmetric blocks: row- and column-major agree
+    check(ccall((:emcmc_get_chain_moments, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), gws.handle, m, cov),
+          gws.handle, "emcmc_get_chain_moments")
+    permutedims(m), cov
+end
+
+"""
+    mix_state(gws, pidx) -> (L_B::Array{Float64,3} (D, D, C), M::Int)
+
+GaussianRandomWalkMix: lower Cholesky factor of every chain's Σ_B and
+HaarioTypeAdaptation's own-turn count since the last readjust (adaptation.jl:399-426).
+"""
+function mix_state(gws::MI355XGlobalWorkspace, pidx::Integer)
+    C, D = gws.backend.num_chains, gws.dim
+    L = Array{Float64}(undef, D, D, C)     # [C][D][D] row-major, transposed below
+    M = Ref{UInt32}(0)                     # the same for every chain
+    check(ccall((:emcmc_get_mix_state, LIB), Cint, (Ptr{Cvoid}, UInt32, Ptr{Float64}, Ref{UInt32}),
+                gws.handle, UInt32(pidx), L, M), gws.handle, "emcmc_get_mix_state")
+    permutedims(L, (2, 1, 3)), Int(M[])
+end
+
+"""
+    faults(gws) -> Vector{UInt32}
+
+Per-chain fault bits: 1 non-finite proposal log-likelihood, 2 RNG retry cap,
+4 Haario readjust not positive definite.
+"""
+function faults(gws::MI355XGlobalWorkspace)
+    f = Vector{UInt32}(undef, gws.backend.num_chains)
+    check(ccall((:emcmc_get_faults, LIB), Cint, (Ptr{Cvoid}, Ptr{UInt32}), gws.handle, f), gws.handle,
+          "emcmc_get_faults")
+    f
+end
+
+struct EmcmcMoments
+    num_chains::UInt64
+    num_draws::UInt64
+    accepted::UInt64
+    proposed::UInt64
+end
+
+"""
+    moments_window(gws, iter_first, n; split=true) -> (sums::Matrix{Float64} (D, 3), info::EmcmcMoments)
+
+Per-dimension sums over this shard's (split) chains of the window means, squared
+means and variances: the input of split-R̂.  Shards combine by summation
+(MPI/RCCL all-reduce across processes).
+"""
+function moments_window(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integer; split::Bool=true)
+    out = Matrix{Float64}(undef, gws.dim, 3)
+    info = Ref{EmcmcMoments}()
+    check(ccall((:emcmc_moments_window, LIB), Cint, (Ptr{Cvoid}, UInt64, UInt64, Cint, Ptr{Float64}, Ref{EmcmcMoments}),
+                gws.handle, iter_first, n, Cint(split), out, info), gws.handle, "emcmc_moments_window")
+    out, info[]
+end
+
+"""
+    kernel_name(gws) -> String
+
+The device kernel variant `__run!` dispatches to.
+"""
+function kernel_name(gws::MI355XGlobalWorkspace)
+    buf = Vector{UInt8}(undef, 256)
+    check(ccall((:emcmc_kernel_name, LIB), Cint, (Ptr{Cvoid}, Ptr{UInt8}, Csize_t), gws.handle, buf, length(buf)),
+          gws.handle, "emcmc_kernel_name")
+    unsafe_string(pointer(buf))
+end
+
+function device_count()
+    n = Ref{Cint}(0)
+    check(ccall((:emcmc_device_count, LIB), Cint, (Ref{Cint},), n), C_NULL, "emcmc_device_count")
+    Int(n[])
+end
+
+export MI355XBackend, state_history, proposal_history, ll_history, acceptance_history, rolling_acceptance,
+       adaptation_state, chain_moments, mix_state, faults, moments_window, kernel_name, device_count
 
 end # module

@@ -36,6 +36,16 @@ def test_library_exports_every_declared_symbol():
         assert getattr(lib, name) is not None
 
 
+def test_julia_shim_binds_only_declared_symbols():
+    """Every ccall of the Julia MI355XBackend shim names a function the header
+    declares (the shim is not executed here: no Julia in the image)."""
+    jl = (ROOT / "extensiblemcmc.jl_amd" / "julia" / "ExtensibleMCMCHip.jl").read_text()
+    called = set(re.findall(r"ccall\(\(:(emcmc_\w+), LIB\)", jl))
+    assert called and called <= set(declared_functions()), called - set(declared_functions())
+    for name in ("emcmc_create", "emcmc_run", "emcmc_get_history", "emcmc_get_chain_stats", "emcmc_moments_window"):
+        assert name in called
+
+
 def test_struct_layout_matches_header(tmp_path):
     src = textwrap.dedent(
         """

@@ -96,6 +96,7 @@ struct UpdateHost {
     std::vector<uint32_t> coords;
     std::vector<double> sigma, L, invdiag;  // GaussianRandomWalk
     std::vector<double> eps;                // UniformRandomWalk ϵ
+    std::vector<uint8_t> pos;               // UniformRandomWalk positivity flags (random_walk.jl:45-52)
     emcmc_unifrw_adaptation adpt{};         // AdaptationUnifRW (scalar form)
     bool diag = false;
     double c0 = 0.0;
@@ -425,6 +426,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
         for (uint32_t j = 0; j < m.nc; ++j) m.coords[j] = u.coords[j];
         if (u.kernel == EMCMC_RW_UNIFORM) {
             for (uint32_t j = 0; j < m.nc; ++j) m.eps0[j] = u.eps[j];
+            for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1u << j) : 0u;
             if (u.adaptation == EMCMC_ADPT_UNIF_RW) {
                 m.k = u.adpt.adapt_every_k_steps;
                 m.target = u.adpt.target_accpt_rate;
@@ -1199,15 +1201,21 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
         !(u->adaptation == EMCMC_ADPT_HAARIO && u->kernel == EMCMC_RW_GAUSSIAN_MIX))
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "adaptation %u has no device plugin for kernel %u yet",
                     u->adaptation, u->kernel);
+    std::vector<uint8_t> pos(u->num_coords, 0);
     if (u->pos)
-        for (uint32_t i = 0; i < u->num_coords; ++i)
-            if (u->pos[i]) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "positivity-restricted coordinates not on device yet");
+        for (uint32_t i = 0; i < u->num_coords; ++i) {
+            pos[i] = u->pos[i] ? 1 : 0;
+            if (pos[i] && u->kernel != EMCMC_RW_UNIFORM)
+                return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                            "positivity-restricted coordinates are on device for UniformRandomWalk only");
+        }
     if (h->updates.size() >= 64) return fail(h, EMCMC_INVALID_ARG, "at most 64 updates");
     UpdateHost uh;
     uh.kernel = u->kernel;
     uh.prior = u->prior;
     uh.adaptation = u->adaptation;
     uh.coords.assign(u->coords, u->coords + u->num_coords);
+    uh.pos = pos;
     const int n = (int)u->num_coords;
     if (u->kernel == EMCMC_RW_GAUSSIAN || u->kernel == EMCMC_RW_GAUSSIAN_MIX) {
         if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");

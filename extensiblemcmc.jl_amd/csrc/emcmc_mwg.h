@@ -10,8 +10,11 @@
 // (orc_run_mwg) and oracle/literal.py (run_mwg_chain):
 //   update_workspaces!  θ_local ← θ[coords]; ll carried from the previous step
 //                       (−Inf before the first)                       run.jl:101-112
-//   UniformRandomWalk   U = a + (b − a)·u (a = −ϵ, b = ϵ), θ° = θ·1 + U (pos
-//                       false), logpdf = 0                       random_walk.jl:63-94
+//   UniformRandomWalk   U = a + (b − a)·u (a = −ϵ, b = ϵ), θ° = θ·(e^U·pos + 1·!pos)
+//                       + U·!pos, i.e. θ·1 + U, or θ·e^U + copysign(0, U) where
+//                       pos; logpdf(θ, θ°) = Σ_i (pos_i ? −log(2ϵ_i) − log θ°_i
+//                       : 0.0) folded left over the update's coordinates
+//                                                                random_walk.jl:63-94
 //   GaussianRandomWalk  θ°_local = θ_local + L z over the update's coordinates
 //                                                                random_walk.jl:145-171
 //   set_parameters!(::Proposal)  P°.θ[coords] ← θ°; P° persists across updates
@@ -43,7 +46,7 @@ struct MwgUpdate {
     double L[kMwgMaxD * kMwgMaxD];  // GaussianRandomWalk: lower Cholesky factor, row-major, local indices
     double iL[kMwgMaxD];            // 1 / L_ii
     double c0;                      // −(nc·log2π + logdet Σ)/2
-    uint32_t diag, pad;
+    uint32_t diag, posmask;          // posmask bit j: UniformRandomWalk coordinate j positivity-restricted
     double target, scale, amin, amax, offset;  // AdaptationUnifRW (scalar form)
 };
 
@@ -166,18 +169,35 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         }
         // ---- proposal!
         double ltd_fwd = 0.0, ltd_rev = 0.0;
-        if (u.kind == 1) {  // UniformRandomWalk (pos = false): θ° = θ·1 + U
+        if (u.kind == 1) {  // UniformRandomWalk: θ° = θ·1 + U, or θ·e^U where pos
+            double ev[D];
 #pragma unroll
             for (int j = 0; j < D; j += 2) {
                 if ((uint32_t)j < n) {
                     const u32x4 r = draw(a.key0, a.key1, gid, iter, (uint32_t)j >> 1, p, 0);
                     const double e0 = u.adapt ? a.eps[((uint64_t)p * kMwgMaxD + j) * C + chain] : u.eps0[j];
-                    const double u0 = u01_closed0(r.x, r.y);
-                    tp[j] = tl[j] * 1.0 + ((-e0) + (e0 - (-e0)) * u0);
+                    const double U0 = (-e0) + (e0 - (-e0)) * u01_closed0(r.x, r.y);
+                    tp[j] = ((u.posmask >> j) & 1u) ? tl[j] * exp_any(U0) + copysign(0.0, U0) : tl[j] * 1.0 + U0;
+                    ev[j] = e0;
                     if (j + 1 < D && (uint32_t)(j + 1) < n) {
                         const double e1 = u.adapt ? a.eps[((uint64_t)p * kMwgMaxD + j + 1) * C + chain] : u.eps0[j + 1];
-                        const double u1 = u01_closed0(r.z, r.w);
-                        tp[j + 1] = tl[j + 1] * 1.0 + ((-e1) + (e1 - (-e1)) * u1);
+                        const double U1 = (-e1) + (e1 - (-e1)) * u01_closed0(r.z, r.w);
+                        tp[j + 1] = ((u.posmask >> (j + 1)) & 1u) ? tl[j + 1] * exp_any(U1) + copysign(0.0, U1)
+                                                                  : tl[j + 1] * 1.0 + U1;
+                        ev[j + 1] = e1;
+                    }
+                }
+            }
+            if (u.posmask) {  // uniform branch: the mask is the update's
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    if ((uint32_t)j < n) {
+                        const bool pj = (u.posmask >> j) & 1u;
+                        const double c = pj ? -log_any(2.0 * ev[j]) : 0.0;
+                        const double f = pj ? c - log_any(tp[j]) : 0.0;  // logpdf(rw, θ, θ°) term
+                        const double g = pj ? c - log_any(tl[j]) : 0.0;  // logpdf(rw, θ°, θ) term
+                        ltd_fwd = (j == 0) ? f : ltd_fwd + f;
+                        ltd_rev = (j == 0) ? g : ltd_rev + g;
                     }
                 }
             }

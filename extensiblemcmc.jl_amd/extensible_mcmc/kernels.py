@@ -350,8 +350,8 @@ class RandomWalkUpdate(MCMCParamUpdate):
         pos = getattr(self.rw, "pos", None)
         if isinstance(self.rw, GaussianRandomWalkMix):
             pos = np.concatenate([self.rw.gsn_A.pos, self.rw.gsn_B.pos])
-        if np.any(pos if pos is not None else False):
-            raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin yet")
+        if np.any(pos if pos is not None else False) and not isinstance(self.rw, UniformRandomWalk):
+            raise UnsupportedPlugin("positivity-restricted coordinates are on device for UniformRandomWalk only")
         if isinstance(self.rw, GaussianRandomWalkMix):
             engine.add_gaussian_rw_mix_update(coords0, self.rw.gsn_A.Sigma, self.rw.gsn_B.Sigma, lam=self.rw.lam,
                                               haario_k=None if adapt is None else adapt["k"],
@@ -360,7 +360,8 @@ class RandomWalkUpdate(MCMCParamUpdate):
         elif isinstance(self.rw, GaussianRandomWalk):
             engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior)
         elif isinstance(self.rw, UniformRandomWalk):
-            engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior)
+            engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior,
+                                         pos=self.rw.pos if np.any(self.rw.pos) else None)
         else:
             raise UnsupportedPlugin(f"transition kernel {type(self.rw).__name__} has no device plugin yet")
 

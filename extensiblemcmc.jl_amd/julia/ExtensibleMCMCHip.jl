@@ -165,10 +165,10 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
         return EmcmcUpdateDesc(RW_GAUSSIAN_MIX, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords),
                                pointer(ΣA), C_NULL, C_NULL, adptp, pointer(ΣB), (C_NULL, C_NULL), updt.rw.λ,
                                (0.0, 0.0, 0.0))
-    elseif updt.rw isa eMCMC.UniformRandomWalk
-        any(updt.rw.pos) && error("positivity-restricted coordinates are not on device yet")
+    elseif updt.rw isa eMCMC.UniformRandomWalk                      # random_walk.jl:45-94, pos included
         ϵ = Float64.(collect(updt.rw.ϵ))
-        push!(keep, ϵ)
+        pos = UInt8.(collect(updt.rw.pos) .!= 0)
+        push!(keep, ϵ, pos)
         if updt.adpt isa eMCMC.AdaptationUnifRW{Float64}      # scalar form (adaptation.jl:162-169)
             a = updt.adpt
             p = Ref(EmcmcUnifRWAdaptation(UInt32(a.adapt_every_k_steps), UInt32(0), a.target_accpt_rate, a.scale,
@@ -179,7 +179,7 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
             error("no device plugin for $(typeof(updt.adpt))")
         end
         return EmcmcUpdateDesc(RW_UNIFORM, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords), C_NULL,
-                               pointer(ϵ), C_NULL, adptp, C_NULL, (C_NULL, C_NULL), 0.0, (0.0, 0.0, 0.0))
+                               pointer(ϵ), pointer(pos), adptp, C_NULL, (C_NULL, C_NULL), 0.0, (0.0, 0.0, 0.0))
     end
     error("no device plugin for $(typeof(updt.rw))")
 end

@@ -170,7 +170,8 @@ typedef struct emcmc_update_desc {
     const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based), any order */
     const double *sigma;      /* GaussianRandomWalk Σ, GaussianRandomWalkMix Σ_A: num_coords² column-major */
     const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
-    const uint8_t *pos;       /* positivity flags or NULL (all false; true is not on device yet) */
+    const uint8_t *pos;       /* positivity flags or NULL (all false); true on device for UniformRandomWalk
+                                 (θ° = θ·e^U, random_walk.jl:63-94), not yet for the Gaussian walks */
     const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW) or
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
     const double *sigma_b;    /* GaussianRandomWalkMix Σ_B: num_coords² column-major */

@@ -437,9 +437,11 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
  *   update_workspaces!: θ_local ← θ[coords]; ll ← ll of the previous step's
  *     local workspace at its iteration (−Inf before the first step) .. run.jl:101-112
  *   UniformRandomWalk rand: U = a + (b − a)·u, a = −ϵ, b = ϵ (Distributions'
- *     Uniform), θ° = θ·(e^U·pos + 1·!pos) + U·!pos; pos = false ⇒ θ + U
- *                                                           random_walk.jl:63-73
- *   UniformRandomWalk logpdf (pos = false) = 0.0 ......... random_walk.jl:88-94
+ *     Uniform), θ° = θ·(e^U·pos + 1·!pos) + U·!pos with Julia's Bool products
+ *     (x·true = x, x·false = copysign(0, x)): pos = false ⇒ θ·1 + U,
+ *     pos = true ⇒ θ·e^U + copysign(0, U) ............... random_walk.jl:63-73
+ *   UniformRandomWalk logpdf(θ, θ°) = mapreduce(i → pos_i ? −log(2ϵ_i) −
+ *     log θ°_i : 0.0, +, 1:n), a left fold ............... random_walk.jl:88-94
  *   GaussianRandomWalk over the update's coordinates ..... random_walk.jl:145-171
  *   set_parameters!(::Proposal): P°.θ[coords] ← θ°; P° persists across updates
  *     and starts as deepcopy(data.P) — the target's μ, not θinit
@@ -464,6 +466,7 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
 typedef struct {
     uint32_t kind; /* 1 uniform, 2 gaussian */
     uint32_t nc;
+    uint8_t pos[ORC_MWG_MAXD]; /* uniform: positivity flags */
     uint32_t coords[ORC_MWG_MAXD];
     double eps0[ORC_MWG_MAXD];
     double L[ORC_MWG_MAXD * ORC_MWG_MAXD], iL[ORC_MWG_MAXD], c0;
@@ -474,10 +477,10 @@ typedef struct {
 
 /* table layout from Python (per update p, 64 doubles of params + 16 coords):
  *   kind[P], nc[P], coords[P*16], eps[P*16], sigma[P*256] (nc×nc column-major),
- *   adapt[P], k[P], aparams[P*5] = (target, scale, min, max, offset) */
+ *   pos[P*16] (uint8), adapt[P], k[P], aparams[P*5] = (target, scale, min, max, offset) */
 ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, uint32_t P, const uint32_t *kind,
                            const uint32_t *nc, const uint32_t *coords, const double *eps, const double *sigma,
-                           const uint32_t *adapt, const uint32_t *adapt_k, const double *aparams,
+                           const uint8_t *pos, const uint32_t *adapt, const uint32_t *adapt_k, const double *aparams,
                            const double *t_sigma, uint64_t nobs, const double *obs, int ll_mode,
                            uint32_t W, uint32_t nsteps, const uint32_t *step_iter, const uint32_t *step_pidx,
                            uint64_t *N_io, uint32_t *last_iter_io, double *theta, double *mu_p, double *ll,
@@ -509,6 +512,7 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         for (uint32_t j = 0; j < u->nc; ++j) {
             u->coords[j] = coords[p * ORC_MWG_MAXD + j];
             u->eps0[j] = eps[p * ORC_MWG_MAXD + j];
+            u->pos[j] = (pos && pos[p * ORC_MWG_MAXD + j]) ? 1 : 0;
             if (u->coords[j] >= (uint32_t)D) {
                 free(g);
                 free(U);
@@ -558,14 +562,22 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             double tl[ORC_MWG_MAXD], tp[ORC_MWG_MAXD];
             for (uint32_t j = 0; j < n; ++j) tl[j] = th[u->coords[j]];
             double ltd_fwd = 0.0, ltd_rev = 0.0;
-            if (u->kind == 1) { /* UniformRandomWalk, pos = false */
+            if (u->kind == 1) { /* UniformRandomWalk */
                 for (uint32_t j = 0; j < n; ++j) {
                     const orc_u32x4 r = orc_draw(k0, k1, chain_id, iter, j >> 1, p, 0);
                     const double uu = (j & 1u) ? orc_u01_closed0(r.v[2], r.v[3]) : orc_u01_closed0(r.v[0], r.v[1]);
                     const double e = ep[j];
                     const double a = -e, b = e;
                     const double Uv = a + (b - a) * uu;
-                    tp[j] = tl[j] * 1.0 + Uv;
+                    tp[j] = u->pos[j] ? tl[j] * orc_exp_any(Uv) + copysign(0.0, Uv) : tl[j] * 1.0 + Uv;
+                }
+                /* logpdf(rw, θ, θ°) (subtracted) and logpdf(rw, θ°, θ) (added), left folds */
+                for (uint32_t j = 0; j < n; ++j) {
+                    const double c = u->pos[j] ? -orc_log_any(2.0 * ep[j]) : 0.0;
+                    const double f = u->pos[j] ? c - orc_log_any(tp[j]) : 0.0;
+                    const double g2 = u->pos[j] ? c - orc_log_any(tl[j]) : 0.0;
+                    ltd_fwd = (j == 0) ? f : ltd_fwd + f;
+                    ltd_rev = (j == 0) ? g2 : ltd_rev + g2;
                 }
             } else { /* GaussianRandomWalk over the update's coordinates */
                 double z[ORC_MWG_MAXD];

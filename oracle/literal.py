@@ -96,13 +96,19 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
         u = updates[p]
         cs = u["coords"]
         tl = th[cs].copy()
-        if u["kind"] == 1:                     # UniformRandomWalk, pos = false
+        if u["kind"] == 1:                     # UniformRandomWalk (random_walk.jl:63-94)
+            pos = [bool(x) for x in u["pos"]] if u.get("pos") is not None else [False] * len(cs)
             tp = np.empty_like(tl)
             for j in range(len(cs)):
                 a, b = -eps[p][j], eps[p][j]
                 U = a + (b - a) * _oracle.uniform01(seed, chain, it, p, j)
-                tp[j] = tl[j] * (np.exp(U) * False + 1.0 * True) + U * True
-            ltd_fwd = ltd_rev = 0.0
+                tp[j] = tl[j] * (np.exp(U) * pos[j] + 1.0 * (not pos[j])) + U * (not pos[j])
+            # logpdf(rw, θ, θ°) = mapreduce(i -> pos[i] ? -log(2ϵ_i) - log(θ°_i) : 0.0, +, 1:n)
+            fwd = [(-np.log(2.0 * eps[p][j]) - np.log(tp[j])) if pos[j] else 0.0 for j in range(len(cs))]
+            rev = [(-np.log(2.0 * eps[p][j]) - np.log(tl[j])) if pos[j] else 0.0 for j in range(len(cs))]
+            ltd_fwd, ltd_rev = fwd[0], rev[0]
+            for j in range(1, len(cs)):
+                ltd_fwd, ltd_rev = ltd_fwd + fwd[j], ltd_rev + rev[j]
         else:                                  # GaussianRandomWalk
             Lr = np.linalg.cholesky(np.asarray(u["sigma"], dtype=float))
             z, _, _ = _oracle.step_variates(seed, chain, it, len(cs), pidx0=p)

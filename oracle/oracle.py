@@ -256,11 +256,13 @@ MWG_MAXD = 16
 KIND_UNIFORM, KIND_GAUSSIAN = 1, 2
 
 
-def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None):
+def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None):
     """One RandomWalkUpdate for run_mwg.  coords0: 0-based coordinates.
-    adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW)."""
+    adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW).
+    pos: None or per-coordinate positivity flags (UniformRandomWalk)."""
     return {"kind": kind, "coords": [int(c) for c in coords0], "eps": None if eps is None else list(eps),
-            "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt}
+            "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt,
+            "pos": None if pos is None else [bool(x) for x in pos]}
 
 
 class MWGState:
@@ -295,6 +297,7 @@ def _mwg_tables(updates):
     adapt = np.zeros(P, dtype=np.uint32)
     ak = np.ones(P, dtype=np.uint32)
     ap = np.zeros((P, 5))
+    pos = np.zeros((P, MWG_MAXD), dtype=np.uint8)
     for p, u in enumerate(updates):
         n = len(u["coords"])
         kind[p], nc[p] = u["kind"], n
@@ -307,7 +310,9 @@ def _mwg_tables(updates):
             a = u["adapt"]
             adapt[p], ak[p] = 1, a["k"]
             ap[p] = (a["target"], a["scale"], a["min"], a["max"], a["offset"])
-    return kind, nc, coords, eps, sigma, adapt, ak, ap
+        if u.get("pos") is not None:
+            pos[p, :n] = np.asarray(u["pos"], dtype=bool)
+    return kind, nc, coords, eps, sigma, adapt, ak, ap, pos
 
 
 def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll_mode=0, W=100, history=True,
@@ -319,12 +324,12 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
                                C.POINTER(C.c_uint8))
         L.orc_run_mwg.restype = C.c_int
         L.orc_run_mwg.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, u32p, u32p, u32p, dp, dp,
-                                  u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
+                                  u8p, u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
                                   u64p, u32p, dp, dp, dp, dp, u64p, u32p, u32p, u32p, dp, u32p, dp, dp, dp, u8p,
                                   C.c_int]
         L._mwg_ready = True
     Cn, D = state.C, state.D
-    kind, nc, coords, eps, sigma, adapt, ak, ap = _mwg_tables(updates)
+    kind, nc, coords, eps, sigma, adapt, ak, ap, pos = _mwg_tables(updates)
     steps = np.asarray(steps, dtype=np.uint32).reshape(-1, 2)
     si = np.ascontiguousarray(steps[:, 0])
     sp = np.ascontiguousarray(steps[:, 1])
@@ -336,7 +341,7 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
     u64 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint64))  # noqa: E731
     rc = L.orc_run_mwg(
         D, Cn, chain0, seed & 0xFFFFFFFFFFFFFFFF, len(updates), u32(kind), u32(nc), u32(coords), _d(eps), _d(sigma),
-        u32(adapt), u32(ak), _d(ap), _d(_colmajor(t_sigma, D)), X.shape[0], _d(X), ll_mode, W, n, u32(si), u32(sp),
+        pos.ctypes.data_as(C.POINTER(C.c_uint8)), u32(adapt), u32(ak), _d(ap), _d(_colmajor(t_sigma, D)), X.shape[0], _d(X), ll_mode, W, n, u32(si), u32(sp),
         u64(state.N), u32(state.last_iter), _d(state.theta), _d(state.mu_p), _d(state.ll), _d(state.ra),
         u64(state.ring), u32(state.nacc), u32(state.aprop), u32(state.aacc), _d(state.eps), u32(state.faults),
         _d(hist.get("theta")), _d(hist.get("prop")), _d(hist.get("ll")),

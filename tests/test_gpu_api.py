@@ -47,10 +47,25 @@ def test_unsupported_plugins_raise_not_fallback():
                  RandomWalkUpdate(GaussianRandomWalk(np.eye(1)), [2])], backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
-    mcmc = MCMC([RandomWalkUpdate(UniformRandomWalk([1.0], [True]), [1]),
+    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalk(np.eye(1), [True]), [1]),
                  RandomWalkUpdate(UniformRandomWalk([1.0]), [2])], backend=MI355XBackend(num_chains=8))
-    with pytest.raises(UnsupportedPlugin):  # positivity-restricted coordinates
-        run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
+    with pytest.raises(UnsupportedPlugin):  # positivity-restricted Gaussian walk
+        run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [1.0, 0.0])
+
+
+def test_positive_uniform_walk_through_the_api(oracle):
+    """UniformRandomWalk([0.5], [true]) on coordinate 1 through MCMC/run: the
+    device run equals the oracle's, and the restricted coordinate stays positive."""
+    w = W.ref_test()
+    mcmc = MCMC([RandomWalkUpdate(UniformRandomWalk([0.5], [True]), [1]),
+                 RandomWalkUpdate(UniformRandomWalk([1.0]), [2])], backend=MI355XBackend(num_chains=64, seed=w.seed))
+    gws, _ = run(mcmc, 200, dict(P=GsnTargetLaw([1.0, 2.0], w.t_sigma), obs=w.obs), [1.0, 0.0])
+    ups = [oracle.mwg_update(1, [0], eps=[0.5], pos=[True]), oracle.mwg_update(1, [1], eps=[1.0])]
+    st = oracle.MWGState(np.tile([1.0, 0.0], (64, 1)), [1.0, 2.0], ups)
+    oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs,
+                   steps=[(i, p) for i in range(1, 201) for p in (1, 2)], history=False)
+    th = gws.state
+    assert np.array_equal(th, st.theta) and np.all(th[:, 0] > 0)
 
 
 def test_haario_mix_through_the_api(oracle):

@@ -29,7 +29,7 @@ def make_engine(D, C, M, ups, mu, t_sigma, obs, seed, ll_mode=L.LL_PER_OBS, hist
                               steps_per_launch=spl))
     for u in ups:
         if u["kind"] == 1:
-            eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"])
+            eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"], pos=u.get("pos"))
         else:
             eng.add_gaussian_rw_update(u["coords"], u["sigma"])
     eng.set_gsn_target(mu, t_sigma, obs, ll_mode=ll_mode)
@@ -68,7 +68,8 @@ def check(oracle, eng, st, h, steps, ups, P, full=True):
 def run_both(oracle, D, C, M, ups, mu, t_sigma, obs, steps, seed, **kw):
     eng = make_engine(D, C, M, ups, mu, t_sigma, obs, seed, **kw)
     eng.run(steps)
-    st = oracle.MWGState(np.zeros((C, D)), mu, ups)
+    th0 = kw.get("theta0")
+    st = oracle.MWGState(np.zeros((C, D)) if th0 is None else np.array(th0, dtype=np.float64), mu, ups)
     h = oracle.run_mwg(st, ups, seed=seed, t_sigma=t_sigma, obs=obs, steps=steps,
                        ll_mode=kw.get("ll_mode", 0), nthreads=8)
     return eng, st, h
@@ -138,3 +139,24 @@ def test_dimensions_and_canonical_blocks(oracle, D, split):
     steps = full_steps(120, len(ups))
     eng, st, h = run_both(oracle, D, 256, 120, ups, mu, ts, obs, steps, w.seed)
     check(oracle, eng, st, h, steps, ups, len(ups))
+
+
+@pytest.mark.parametrize("adapt", [False, True])
+def test_uniform_rw_positivity_restricted(oracle, adapt):
+    """UniformRandomWalk(ϵ, pos) (random_walk.jl:63-94): θ° = θ·e^U on the restricted
+    coordinates, θ + U on the others, and the transition densities
+    Σ_pos −log(2ϵ) − log θ no longer cancel in the MH ratio; with and without
+    AdaptationUnifRW, a block mixing restricted and free coordinates."""
+    w = W.ref_test()
+    D, C, M = 3, 300, 120
+    mu = np.array([1.0, 2.0, 0.5])
+    t_sigma = np.array([[1.0, 0.3, 0.0], [0.3, 1.0, 0.0], [0.0, 0.0, 0.25]])
+    obs = np.random.default_rng(5).multivariate_normal(mu, t_sigma, 10)
+    ups = [oracle.mwg_update(1, [0, 2], eps=[0.4, 0.3], pos=[True, False], adapt=ADAPT if adapt else None),
+           oracle.mwg_update(1, [1], eps=[0.6], pos=[True])]
+    theta0 = np.tile([1.5, 0.7, 0.2], (C, 1))
+    steps = full_steps(M, 2)
+    eng, st, h = run_both(oracle, D, C, M, ups, mu, t_sigma, obs, steps, w.seed, theta0=theta0)
+    check(oracle, eng, st, h, steps, ups, 2)
+    th, _ = eng.get_state()
+    assert np.all(th[:, :2] > 0) and 0.05 < h["acc"].mean() < 0.95

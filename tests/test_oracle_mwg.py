@@ -124,3 +124,26 @@ def test_posterior_mean_single_site(oracle):
     draws = h["theta"][M:].reshape(-1, 2)
     se = np.sqrt(np.diag(np.asarray(w.t_sigma)) / len(w.obs) / (C * 10))  # ≥ 10 draws/chain of information
     assert np.all(np.abs(draws.mean(axis=0) - xbar) < 6 * se)
+
+
+def test_uniform_rw_positivity_restricted_against_literal(oracle):
+    """UniformRandomWalk(ϵ, pos) (random_walk.jl:63-94): θ° = θ·e^U where pos
+    (θ + U elsewhere) and logpdf(θ, θ°) = Σ_pos −log(2ϵ) − log θ°, which no longer
+    cancels between the two directions.  The literal restatement uses numpy's
+    exp/log, the oracle its own: θ within 1e-14 relative, the accept stream equal."""
+    w = W.ref_test()
+    ups = [oracle.mwg_update(1, [0], eps=[0.5], pos=[True]), oracle.mwg_update(1, [1], eps=[0.8], pos=[False])]
+    C, theta0 = 6, [1.5, 0.5]
+    steps = full_steps(300, 2)
+    st = oracle.MWGState(np.tile(theta0, (C, 1)), [1.0, 2.0], ups)
+    h = oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs, steps=steps)
+    for c in range(C):
+        o = LT.run_mwg_chain(w.seed, c, list(theta0), [1.0, 2.0], ups, w.t_sigma, w.obs, steps)
+        assert np.array_equal(np.array(o["acc"]), h["acc"][:, c]), f"chain {c}: accept stream"
+        np.testing.assert_allclose(np.array(o["theta"]), h["theta"][:, c], rtol=1e-14)
+        np.testing.assert_allclose(np.array(o["prop"]), h["prop"][:, c], rtol=1e-14)
+    assert np.all(h["theta"][:, :, 0] > 0)  # the restricted coordinate stays positive
+    # the restricted coordinate's moves are multiplicative: log θ° − log θ = U ∈ [−ϵ, ϵ]
+    lr = np.log(h["prop"][1:, :, 0]) - np.log(h["theta"][:-1, :, 0])
+    moved = np.array([p == 1 for _, p in steps])[1:]
+    assert np.all(np.abs(lr[moved]) <= 0.5 + 1e-12)

@@ -442,6 +442,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
             for (int i = 0; i < n; ++i) m.iL[i] = u.invdiag[i];
             m.c0 = u.c0;
             m.diag = u.diag ? 1u : 0u;
+            for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1u << j) : 0u;
         }
     }
     if (h->d_mwg) (void)hipFree(h->d_mwg);
@@ -471,6 +472,8 @@ emcmc_status select_mwg(emcmc_handle *h) {
 bool fused_eligible(const emcmc_handle *h) {
     if (!joint_all_coords(h) || h->cfg.chain_moments) return false;
     const UpdateHost &u = h->updates[0];
+    for (uint8_t f : u.pos)
+        if (f) return false;  // positivity-restricted coordinates: general schedule kernel (D ≤ 16)
     return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
 }
 
@@ -1205,9 +1208,10 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     if (u->pos)
         for (uint32_t i = 0; i < u->num_coords; ++i) {
             pos[i] = u->pos[i] ? 1 : 0;
-            if (pos[i] && u->kernel != EMCMC_RW_UNIFORM)
+            if (pos[i] && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN)
                 return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                            "positivity-restricted coordinates are on device for UniformRandomWalk only");
+                            "positivity-restricted coordinates are on device for UniformRandomWalk and "
+                            "GaussianRandomWalk only");
         }
     if (h->updates.size() >= 64) return fail(h, EMCMC_INVALID_ARG, "at most 64 updates");
     UpdateHost uh;

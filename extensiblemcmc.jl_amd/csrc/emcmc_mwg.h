@@ -15,8 +15,9 @@
 //                       pos; logpdf(θ, θ°) = Σ_i (pos_i ? −log(2ϵ_i) − log θ°_i
 //                       : 0.0) folded left over the update's coordinates
 //                                                                random_walk.jl:63-94
-//   GaussianRandomWalk  θ°_local = θ_local + L z over the update's coordinates
-//                                                                random_walk.jl:145-171
+//   GaussianRandomWalk  θ°_local = θ_local + L z over the update's coordinates; with
+//                       pos, on the log scale with the reference's in-place
+//                       exp/log round trips (see the kernel)   random_walk.jl:136-171
 //   set_parameters!(::Proposal)  P°.θ[coords] ← θ°; P° persists across updates
 //                       and starts at the target's μ          updates.jl:198-205,
 //                                                             workspaces.jl:225-233
@@ -46,7 +47,7 @@ struct MwgUpdate {
     double L[kMwgMaxD * kMwgMaxD];  // GaussianRandomWalk: lower Cholesky factor, row-major, local indices
     double iL[kMwgMaxD];            // 1 / L_ii
     double c0;                      // −(nc·log2π + logdet Σ)/2
-    uint32_t diag, posmask;          // posmask bit j: UniformRandomWalk coordinate j positivity-restricted
+    uint32_t diag, posmask;          // posmask bit j: coordinate j positivity-restricted
     double target, scale, amin, amax, offset;  // AdaptationUnifRW (scalar form)
 };
 
@@ -156,7 +157,7 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + p;
         const uint64_t pc = (uint64_t)p * C + chain;
         // ---- update_workspaces!: θ_local ← θ[coords] (uniform coordinate indices)
-        double tl[D], tp[D];
+        double tl[D], tp[D], ta[D];  // local θ, θ° (history / P°), θ° as stored on accept
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             double v = 0.0;
@@ -202,6 +203,8 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
                 }
             }
         } else {  // GaussianRandomWalk over the update's coordinates
+            const uint32_t pm = u.posmask;  // positivity-restricted coordinates (log scale)
+            auto isp = [&](int i) { return ((pm >> i) & 1u) != 0u; };
             double z[D];
 #pragma unroll
             for (int j = 0; j < D; ++j)
@@ -217,23 +220,79 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 #pragma unroll
                         for (int j = 1; j <= i; ++j) lz = fma(u.L[i * kMwgMaxD + j], z[j], lz);
                     }
-                    tp[i] = tl[i] + lz;
+                    // remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136, 145-147)
+                    tp[i] = (isp(i) ? log_any(tl[i]) : tl[i]) + lz;
                 } else {
                     tp[i] = 0.0;
                 }
             }
             double r[D];
+            if (pm == 0u) {
 #pragma unroll
-            for (int i = 0; i < D; ++i) r[i] = tp[i] - tl[i];
-            ltd_fwd = u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0;
+                for (int i = 0; i < D; ++i) r[i] = tp[i] - tl[i];
+                ltd_fwd = u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0;
 #pragma unroll
-            for (int i = 0; i < D; ++i) r[i] = tl[i] - tp[i];
-            ltd_rev = u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0;
+                for (int i = 0; i < D; ++i) r[i] = tl[i] - tp[i];
+                ltd_rev = u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0;
+            } else {
+                // The reference's in-place round trips, step by step (random_walk.jl:136-171):
+                //   rand:   θ° ← exp(log θ + Lz), θ ← exp(log θ)               (θ°₁, θ₁)
+                //   logpdf(θ°₁, θ₁): logJ = −Σ_pos log θ₁; MvNormal(log θ°₁) at log θ₁;
+                //           then θ°₂ = exp(log θ°₁), θ₂ = exp(log θ₁)
+                //   logpdf(θ₂, θ°₂): logJ = −Σ_pos log θ°₂; MvNormal(log θ₂) at log θ°₂;
+                //           then θ°₃ = exp(log θ°₂) — the value an accept stores
+                double t1[D], a1[D], b1[D];
+                double lj = 0.0;
+                bool first = true;
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    if ((uint32_t)i < n) {
+                        tp[i] = isp(i) ? exp_any(tp[i]) : tp[i];              // θ°₁
+                        t1[i] = isp(i) ? exp_any(log_any(tl[i])) : tl[i];     // θ₁
+                        if (isp(i)) {
+                            const double v = log_any(t1[i]);
+                            lj = first ? v : lj + v;
+                            first = false;
+                        }
+                        a1[i] = isp(i) ? log_any(tp[i]) : tp[i];             // μ = log θ°₁
+                        b1[i] = isp(i) ? log_any(t1[i]) : t1[i];             // x = log θ₁
+                        r[i] = b1[i] - a1[i];
+                    } else {
+                        t1[i] = a1[i] = b1[i] = r[i] = 0.0;
+                    }
+                }
+                ltd_rev = (u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0) + (-lj);
+                lj = 0.0;
+                first = true;
+#pragma unroll
+                for (int i = 0; i < D; ++i) {
+                    if ((uint32_t)i < n) {
+                        const double p2 = isp(i) ? exp_any(a1[i]) : a1[i];  // θ°₂
+                        const double l2 = isp(i) ? exp_any(b1[i]) : b1[i];  // θ₂
+                        if (isp(i)) {
+                            const double v = log_any(p2);
+                            lj = first ? v : lj + v;
+                            first = false;
+                        }
+                        const double a2 = isp(i) ? log_any(l2) : l2;        // μ = log θ₂
+                        const double b2 = isp(i) ? log_any(p2) : p2;        // x = log θ°₂
+                        r[i] = b2 - a2;
+                        ta[i] = isp(i) ? exp_any(b2) : p2;                  // θ°₃
+                    } else {
+                        r[i] = 0.0;
+                    }
+                }
+                ltd_fwd = (u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0) + (-lj);
+            }
+        }
+        if (!(u.kind == 2 && u.posmask != 0u)) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) ta[j] = tp[j];
         }
         // ---- set_proposal!: proposal history and P°.θ[coords] ← θ°
-        double prop[D];
+        double prop[D], nst[D];
 #pragma unroll
-        for (int d = 0; d < D; ++d) prop[d] = th[d];
+        for (int d = 0; d < D; ++d) prop[d] = nst[d] = th[d];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             if ((uint32_t)j < n) {
@@ -242,6 +301,7 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
                 for (int d = 0; d < D; ++d) {
                     prop[d] = (cj == (uint32_t)d) ? tp[j] : prop[d];
                     mp[d] = (cj == (uint32_t)d) ? tp[j] : mp[d];
+                    nst[d] = (cj == (uint32_t)d) ? ta[j] : nst[d];
                 }
             }
         }
@@ -271,9 +331,9 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 #pragma unroll
             for (int d = 0; d < D; ++d) __builtin_nontemporal_store(prop[d], a.hist_prop + slot * D * C + state_pos(d, chain, C, D));
         }
-        if (acc) {
+        if (acc) {  // set_chain_param!: θ[coords] ← θ° (run.jl:312-318)
 #pragma unroll
-            for (int d = 0; d < D; ++d) th[d] = prop[d];
+            for (int d = 0; d < D; ++d) th[d] = nst[d];
             ll = llp;
         }
         if constexpr (FULL) {

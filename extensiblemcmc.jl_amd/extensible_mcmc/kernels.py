@@ -350,15 +350,17 @@ class RandomWalkUpdate(MCMCParamUpdate):
         pos = getattr(self.rw, "pos", None)
         if isinstance(self.rw, GaussianRandomWalkMix):
             pos = np.concatenate([self.rw.gsn_A.pos, self.rw.gsn_B.pos])
-        if np.any(pos if pos is not None else False) and not isinstance(self.rw, UniformRandomWalk):
-            raise UnsupportedPlugin("positivity-restricted coordinates are on device for UniformRandomWalk only")
+        if np.any(pos if pos is not None else False) and isinstance(self.rw, GaussianRandomWalkMix):
+            raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin for "
+                                    "GaussianRandomWalkMix yet")
         if isinstance(self.rw, GaussianRandomWalkMix):
             engine.add_gaussian_rw_mix_update(coords0, self.rw.gsn_A.Sigma, self.rw.gsn_B.Sigma, lam=self.rw.lam,
                                               haario_k=None if adapt is None else adapt["k"],
                                               haario_scale=2.38 ** 2 if adapt is None else adapt["scale"],
                                               prior=prior)
         elif isinstance(self.rw, GaussianRandomWalk):
-            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior)
+            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior,
+                                          pos=self.rw.pos if np.any(self.rw.pos) else None)
         elif isinstance(self.rw, UniformRandomWalk):
             engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior,
                                          pos=self.rw.pos if np.any(self.rw.pos) else None)

@@ -144,11 +144,12 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
     adpt, adptp = ADPT_NONE, C_NULL
     if updt.rw isa eMCMC.GaussianRandomWalk
         updt.adpt isa eMCMC.NoAdaptation || error("no device plugin for $(typeof(updt.adpt)) with GaussianRandomWalk")
-        any(updt.rw.pos) && error("positivity-restricted coordinates are not on device yet")
         Σ = Matrix{Float64}(updt.rw.Σ)                         # column-major already
-        push!(keep, Σ)
+        pos = UInt8.(updt.rw.pos)                               # log-scale coordinates (random_walk.jl:136-171)
+        push!(keep, Σ, pos)
         return EmcmcUpdateDesc(RW_GAUSSIAN, PRIOR_IMPROPER, ADPT_NONE, UInt32(length(coords)), pointer(coords),
-                               pointer(Σ), C_NULL, C_NULL, C_NULL, C_NULL, (C_NULL, C_NULL), 0.0, (0.0, 0.0, 0.0))
+                               pointer(Σ), C_NULL, pointer(pos), C_NULL, C_NULL, (C_NULL, C_NULL), 0.0,
+                               (0.0, 0.0, 0.0))
     elseif updt.rw isa eMCMC.GaussianRandomWalkMix                # random_walk.jl:193-232
         (any(updt.rw.gsn_A.pos) || any(updt.rw.gsn_B.pos)) &&
             error("positivity-restricted coordinates are not on device yet")

@@ -171,7 +171,8 @@ typedef struct emcmc_update_desc {
     const double *sigma;      /* GaussianRandomWalk Σ, GaussianRandomWalkMix Σ_A: num_coords² column-major */
     const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
     const uint8_t *pos;       /* positivity flags or NULL (all false); true on device for UniformRandomWalk
-                                 (θ° = θ·e^U, random_walk.jl:63-94), not yet for the Gaussian walks */
+                                 (θ° = θ·e^U, random_walk.jl:63-94) and GaussianRandomWalk (log scale,
+                                 random_walk.jl:136-171; D ≤ 16), not for GaussianRandomWalkMix */
     const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW) or
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
     const double *sigma_b;    /* GaussianRandomWalkMix Σ_B: num_coords² column-major */

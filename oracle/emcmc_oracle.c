@@ -443,6 +443,9 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
  *   UniformRandomWalk logpdf(θ, θ°) = mapreduce(i → pos_i ? −log(2ϵ_i) −
  *     log θ°_i : 0.0, +, 1:n), a left fold ............... random_walk.jl:88-94
  *   GaussianRandomWalk over the update's coordinates ..... random_walk.jl:145-171
+ *     with pos: on the log scale, with the in-place exp/log round trips of
+ *     remove_/reimpose_constraints! in rand and both logpdf calls, and the
+ *     log-Jacobian −sum(log θ[pos]) (see the code) ....... random_walk.jl:136-171
  *   set_parameters!(::Proposal): P°.θ[coords] ← θ°; P° persists across updates
  *     and starts as deepcopy(data.P) — the target's μ, not θinit
  *                                         updates.jl:198-205, workspaces.jl:225-233
@@ -559,7 +562,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             const orc_mwg_update *u = &U[p];
             const uint32_t n = u->nc;
             double *ep = eps_state + ((size_t)p * C + c) * ORC_MWG_MAXD;
-            double tl[ORC_MWG_MAXD], tp[ORC_MWG_MAXD];
+            double tl[ORC_MWG_MAXD], tp[ORC_MWG_MAXD], ta[ORC_MWG_MAXD];
+            int accept_ta = 0; /* accepted values differ from the proposal (Gaussian with pos) */
             for (uint32_t j = 0; j < n; ++j) tl[j] = th[u->coords[j]];
             double ltd_fwd = 0.0, ltd_rev = 0.0;
             if (u->kind == 1) { /* UniformRandomWalk */
@@ -580,6 +584,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                     ltd_rev = (j == 0) ? g2 : ltd_rev + g2;
                 }
             } else { /* GaussianRandomWalk over the update's coordinates */
+                int anypos = 0;
+                for (uint32_t j = 0; j < n; ++j) anypos |= u->pos[j];
                 double z[ORC_MWG_MAXD];
                 for (uint32_t j = 0; j < n; ++j) z[j] = orc_normal(zt, k0, k1, chain_id, iter, p, j, &f);
                 for (uint32_t i = 0; i < n; ++i) {
@@ -590,13 +596,55 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                         lz = u->L[(size_t)i * n] * z[0];
                         for (uint32_t j = 1; j <= i; ++j) lz = fma(u->L[(size_t)i * n + j], z[j], lz);
                     }
-                    tp[i] = tl[i] + lz;
+                    /* remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136) */
+                    tp[i] = (u->pos[i] ? orc_log_any(tl[i]) : tl[i]) + lz;
                 }
                 double r[ORC_MWG_MAXD];
-                for (uint32_t i = 0; i < n; ++i) r[i] = tp[i] - tl[i];
-                ltd_fwd = u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0;
-                for (uint32_t i = 0; i < n; ++i) r[i] = tl[i] - tp[i];
-                ltd_rev = u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0;
+                if (!anypos) {
+                    for (uint32_t i = 0; i < n; ++i) r[i] = tp[i] - tl[i];
+                    ltd_fwd = u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0;
+                    for (uint32_t i = 0; i < n; ++i) r[i] = tl[i] - tp[i];
+                    ltd_rev = u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0;
+                } else {
+                    /* rand (random_walk.jl:145-151): θ°₁ = exp(log θ + Lz), θ₁ = exp(log θ)
+                     * (reimpose_constraints! on both, in place);
+                     * logpdf(rw, θ°₁, θ₁) (:166-171): logJ = −sum(log θ₁[pos]),
+                     * logpdf(MvNormal(log θ°₁, Σ), log θ₁) + logJ, then θ°₂ = exp(log θ°₁),
+                     * θ₂ = exp(log θ₁); logpdf(rw, θ₂, θ°₂) likewise, then
+                     * θ°₃ = exp(log θ°₂), the value set_chain_param! copies on accept */
+                    double t1[ORC_MWG_MAXD], a1[ORC_MWG_MAXD], b1[ORC_MWG_MAXD], lj = 0.0;
+                    int first = 1;
+                    for (uint32_t i = 0; i < n; ++i) {
+                        tp[i] = u->pos[i] ? orc_exp_any(tp[i]) : tp[i];
+                        t1[i] = u->pos[i] ? orc_exp_any(orc_log_any(tl[i])) : tl[i];
+                        if (u->pos[i]) {
+                            const double v = orc_log_any(t1[i]);
+                            lj = first ? v : lj + v;
+                            first = 0;
+                        }
+                        a1[i] = u->pos[i] ? orc_log_any(tp[i]) : tp[i];
+                        b1[i] = u->pos[i] ? orc_log_any(t1[i]) : t1[i];
+                        r[i] = b1[i] - a1[i];
+                    }
+                    ltd_rev = (u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0) + (-lj);
+                    lj = 0.0;
+                    first = 1;
+                    for (uint32_t i = 0; i < n; ++i) {
+                        const double p2 = u->pos[i] ? orc_exp_any(a1[i]) : a1[i];
+                        const double l2 = u->pos[i] ? orc_exp_any(b1[i]) : b1[i];
+                        if (u->pos[i]) {
+                            const double v = orc_log_any(p2);
+                            lj = first ? v : lj + v;
+                            first = 0;
+                        }
+                        const double a2 = u->pos[i] ? orc_log_any(l2) : l2;
+                        const double b2 = u->pos[i] ? orc_log_any(p2) : p2;
+                        r[i] = b2 - a2;
+                        ta[i] = u->pos[i] ? orc_exp_any(b2) : p2;
+                    }
+                    ltd_fwd = (u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0) + (-lj);
+                    accept_ta = 1;
+                }
             }
             /* set_proposal!: history θ with coords ← θ°; P°.θ[coords] ← θ° */
             double prop[ORC_MWG_MAXD];
@@ -623,8 +671,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             const double E = orc_exponential(zt, k0, k1, chain_id, iter, p, &f);
             const int acc = E > -llr;
             if (hist_prop) memcpy(hist_prop + ((uint64_t)s * C + c) * D, prop, sizeof(double) * D);
-            if (acc) {
-                for (uint32_t j = 0; j < n; ++j) th[u->coords[j]] = tp[j];
+            if (acc) { /* set_chain_param!: θ[coords] ← θ° of the local workspace (run.jl:312-318) */
+                for (uint32_t j = 0; j < n; ++j) th[u->coords[j]] = accept_ta ? ta[j] : tp[j];
                 cll = llp;
                 nacc[(size_t)p * C + c] += 1;
             }

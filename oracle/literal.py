@@ -96,6 +96,7 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
         u = updates[p]
         cs = u["coords"]
         tl = th[cs].copy()
+        ta = None
         if u["kind"] == 1:                     # UniformRandomWalk (random_walk.jl:63-94)
             pos = [bool(x) for x in u["pos"]] if u.get("pos") is not None else [False] * len(cs)
             tp = np.empty_like(tl)
@@ -112,9 +113,32 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
         else:                                  # GaussianRandomWalk
             Lr = np.linalg.cholesky(np.asarray(u["sigma"], dtype=float))
             z, _, _ = _oracle.step_variates(seed, chain, it, len(cs), pidx0=p)
-            tp = tl + Lr @ z
-            ltd_fwd = mvnormal_logpdf(tp, tl, Lr)
-            ltd_rev = mvnormal_logpdf(tl, tp, Lr)
+            pos = np.array(u["pos"], dtype=bool) if u.get("pos") is not None else np.zeros(len(cs), dtype=bool)
+            if not pos.any():
+                tp = tl + Lr @ z
+                ltd_fwd = mvnormal_logpdf(tp, tl, Lr)
+                ltd_rev = mvnormal_logpdf(tl, tp, Lr)
+            else:                              # random_walk.jl:136-171, in-place as written
+                th_l = tl.copy()               # state(ws)
+                th_l[pos] = np.log(th_l[pos])  # remove_constraints!(rw, θ)
+                th_o = th_l + Lr @ z           # rand(MvNormal(θ, Σ))
+                th_o[pos] = np.exp(th_o[pos])  # reimpose_constraints!(rw, θ°)
+                th_l[pos] = np.exp(th_l[pos])  # reimpose_constraints!(rw, θ)
+                tp = th_o.copy()               # state°(ws) as set_proposal! sees it
+
+                def rw_logpdf(a, b):           # logpdf(rw, a, b), mutating a and b
+                    logJ = -sum(np.log(b[pos]))
+                    a[pos] = np.log(a[pos])
+                    b[pos] = np.log(b[pos])
+                    lp = mvnormal_logpdf(b, a, Lr) + logJ
+                    a[pos] = np.exp(a[pos])
+                    b[pos] = np.exp(b[pos])
+                    return lp
+                ltd_rev = rw_logpdf(th_o, th_l)  # log_transition_density(__PROPOSAL): θ° → θ
+                ltd_fwd = rw_logpdf(th_l, th_o)  # log_transition_density(__PREVIOUS): θ → θ°
+                ta = th_o.copy()                 # what set_chain_param! copies on accept
+        if ta is None:
+            ta = tp
         prop = th.copy()
         prop[cs] = tp
         mp[cs] = tp                            # set_parameters!(P°, coords, θ°)
@@ -125,7 +149,7 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
         llr = llp - ll + ltd_rev - ltd_fwd + 0.0 - 0.0
         acc = bool(E > -llr)
         if acc:
-            th[cs] = tp
+            th[cs] = ta
             ll = llp
         acc_hist[(it, p)] = acc
         prev = ra.get((it - 1, p), 0.0) if it > 1 else 0.0

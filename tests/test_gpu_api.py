@@ -47,9 +47,9 @@ def test_unsupported_plugins_raise_not_fallback():
                  RandomWalkUpdate(GaussianRandomWalk(np.eye(1)), [2])], backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
-    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalk(np.eye(1), [True]), [1]),
-                 RandomWalkUpdate(UniformRandomWalk([1.0]), [2])], backend=MI355XBackend(num_chains=8))
-    with pytest.raises(UnsupportedPlugin):  # positivity-restricted Gaussian walk
+    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(np.eye(2), 2 * np.eye(2), pos=[True, False]), [1, 2])],
+                backend=MI355XBackend(num_chains=8))
+    with pytest.raises(UnsupportedPlugin):  # positivity-restricted mixture walk
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [1.0, 0.0])
 
 

@@ -31,7 +31,7 @@ def make_engine(D, C, M, ups, mu, t_sigma, obs, seed, ll_mode=L.LL_PER_OBS, hist
         if u["kind"] == 1:
             eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"], pos=u.get("pos"))
         else:
-            eng.add_gaussian_rw_update(u["coords"], u["sigma"])
+            eng.add_gaussian_rw_update(u["coords"], u["sigma"], pos=u.get("pos"))
     eng.set_gsn_target(mu, t_sigma, obs, ll_mode=ll_mode)
     eng.set_state(np.zeros((C, D)) if theta0 is None else theta0)
     return eng
@@ -160,3 +160,27 @@ def test_uniform_rw_positivity_restricted(oracle, adapt):
     check(oracle, eng, st, h, steps, ups, 2)
     th, _ = eng.get_state()
     assert np.all(th[:, :2] > 0) and 0.05 < h["acc"].mean() < 0.95
+
+
+@pytest.mark.parametrize("joint", [False, True])
+def test_gaussian_rw_positivity_restricted(oracle, joint):
+    """GaussianRandomWalk(Σ, pos) (random_walk.jl:136-171) on device: the log-scale
+    walk, the log-Jacobian terms and the reference's in-place exp/log round trips
+    (accepted states are θ° after two more round trips), bit for bit.  joint: one
+    update on all coordinates (not the fused kernel: positivity routes it here)."""
+    w = W.ref_test()
+    D, C, M = 3, 300, 120
+    mu = np.array([1.0, 2.0, 0.5])
+    t_sigma = np.array([[1.0, 0.3, 0.0], [0.3, 1.0, 0.0], [0.0, 0.0, 0.25]])
+    obs = np.random.default_rng(6).multivariate_normal(mu, t_sigma, 10)
+    if joint:
+        ups = [oracle.mwg_update(2, [0, 1, 2], sigma=0.02 * np.eye(3) + 0.005, pos=[True, False, True])]
+    else:
+        ups = [oracle.mwg_update(2, [2, 0], sigma=[[0.05, 0.01], [0.01, 0.04]], pos=[True, False]),
+               oracle.mwg_update(1, [1], eps=[0.6], pos=[True])]
+    theta0 = np.tile([1.5, 0.7, 0.2], (C, 1))
+    steps = full_steps(M, len(ups))
+    eng, st, h = run_both(oracle, D, C, M, ups, mu, t_sigma, obs, steps, w.seed, theta0=theta0)
+    assert "mwg" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, len(ups))
+    assert h["acc"][len(ups):].sum() > 10  # moves beyond the first step's auto-accepts

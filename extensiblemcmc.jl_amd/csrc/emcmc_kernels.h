@@ -123,16 +123,19 @@ constexpr bool kSerialPairs = EMCMC_SERIAL_PAIRS != 0;
 // a wave-uniform loop resolves the ≈1% wedge/tail draws one per lane per trip
 // (with 64 lanes × N draws per wave most steps take one trip, so the trip only
 // fixes z[i]; the proposal arithmetic runs once, after it).
-template <int N>
+template <int N, bool VK = false>
 __device__ __forceinline__ void propose_diag(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain,
                                              uint32_t iter, uint32_t pidx0, uint32_t g0, const double (&base)[N],
-                                             const double *scale, double (&out)[N], uint32_t &faults) {
+                                             const double *scale, double (&out)[N], uint32_t &faults,
+                                             const PhiloxVKeys &vk = PhiloxVKeys{}) {
     constexpr int NP = (N + 1) / 2;
     uint32_t pend = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         if constexpr (kSerialPairs) __builtin_amdgcn_sched_barrier(0);
-        const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
+        u32x4 r;
+        if constexpr (VK) r = draw_vk(vk, chain, iter, (g0 >> 1) + j, pidx0);
+        else r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
         if (!zig_normal_fast(zig_split_n(r.x, r.y), zt.n, out[2 * j])) pend |= 1u << (2 * j);
         if (2 * j + 1 < N)
             if (!zig_normal_fast(zig_split_n(r.z, r.w), zt.n, out[2 * j + 1])) pend |= 1u << (2 * j + 1);
@@ -352,9 +355,14 @@ __device__ __forceinline__ void normals(const ZigTabs &zt, uint32_t key0, uint32
 // half a block per step.  `first` forces the block at the launch's first step.
 struct AcceptStream {
     u32x4 r;
+    template <bool VK = false>
     __device__ __forceinline__ double next(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain,
-                                           uint32_t iter, uint32_t pidx0, bool first, uint32_t &faults) {
-        if (first || (iter & 1u) == 0) r = draw(key0, key1, chain, iter >> 1, kBlockAccept, pidx0, 0);
+                                           uint32_t iter, uint32_t pidx0, bool first, uint32_t &faults,
+                                           const PhiloxVKeys &vk = PhiloxVKeys{}) {
+        if (first || (iter & 1u) == 0) {
+            if constexpr (VK) r = draw_vk(vk, chain, iter >> 1, kBlockAccept, pidx0);
+            else r = draw(key0, key1, chain, iter >> 1, kBlockAccept, pidx0, 0);
+        }
         const ZigDraw d = accept_split(r, iter);
         double e;
         if (!zig_exp_fast(d, zt.e, e) && (EMCMC_ABLATE & 2) == 0) e = zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
@@ -403,6 +411,9 @@ __device__ __forceinline__ double tree_inplace(double (&b)[N]) {
     return b[0];
 }
 
+#ifndef EMCMC_VKEYS
+#define EMCMC_VKEYS 1  // Philox round keys precomputed once into VGPRs (diag kernel); 0: derived per call (SALU)
+#endif
 #ifndef EMCMC_SUMSQ_BARRIER
 #define EMCMC_SUMSQ_BARRIER 1
 #endif
@@ -649,6 +660,11 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     const uint32_t wave_gid0 = a.chain0 + (uint32_t)((tid & ~(uint64_t)63) / LPC);
     if constexpr (kBatched) ws.fl[__lane_id()] = 0;
     AcceptStream accs;
+#if EMCMC_VKEYS
+    const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
+#else
+    const PhiloxVKeys vkeys{};
+#endif
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
@@ -665,7 +681,8 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
             propose_diag_batched<DPL, LPC>(zt, ws, a.key0, a.key1, gid, wave_gid0, iter, a.pidx0, (uint32_t)d0, th,
                                            Lrw + d0, thp);
         else
-            propose_diag<DPL>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults);
+            propose_diag<DPL, EMCMC_VKEYS != 0>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0,
+                                                thp, faults, vkeys);
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
         const double ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
@@ -731,7 +748,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
         // ---- accept_reject! (run.jl:271-278), left-associative as written
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
-        const double E = accs.next(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults);
+        const double E = accs.next<EMCMC_VKEYS != 0>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
         const bool acc = E > -llr;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
         if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);

@@ -50,10 +50,11 @@ struct u32x4 {
 #if defined(__HIP_DEVICE_COMPILE__)
 // a ^ b ^ k in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); k is a
 // round key derived from the seed, wave-uniform, so it sits in an SGPR
+// (the builtin, not inline asm: the compiler must otherwise assume the worst
+// hazard after every asm block and pads each following v_mad_u64_u32 with an
+// s_nop — ≈ 75 wasted issue slots per wave-step of the step kernel)
 __device__ __forceinline__ uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "s"(k));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 }
 #else
 static inline uint32_t xor3_key(uint32_t a, uint32_t b, uint32_t k) { return a ^ b ^ k; }
@@ -129,9 +130,7 @@ EMCMC_HD PhiloxVKeys philox_vkeys(uint32_t k0, uint32_t k1) {
 }
 EMCMC_HD uint32_t xor3_vkey(uint32_t a, uint32_t b, uint32_t k) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(k));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(a, b, k, 0x96);
 #else
     return a ^ b ^ k;
 #endif

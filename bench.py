@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
-    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4"], default="cfg2")
+    ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "cfg5"], default="cfg2",
+                    help="cfg2 at N=1; with N>1 GPUs cfg2 means cfg5 (131,072 chains per GPU)")
     ap.add_argument("--shard", type=int, default=-1,
                     help="single-process run of shard r: global chains [r·C, (r+1)·C) (default: this rank's)")
     ap.add_argument("--chains-per-gpu", type=int, default=0,
@@ -57,61 +58,105 @@ def parse():
     ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
     ap.add_argument("--lpc", type=int, default=0)
     ap.add_argument("--steps-per-launch", type=int, default=100)
-    ap.add_argument("--reps", type=int, default=1, help="repeat the timed region; report the median")
+    ap.add_argument("--reps", type=int, default=0,
+                    help="repeat the timed region, report the median (0: 5 when the histories fit in 96 GB, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def cpu_baseline(w, seconds, ll_mode):
-    """The oracle (C restatement, OpenMP over chains) on a bounded sample of the
-    same workload, histories included, on this host's cores."""
-    from oracle import oracle as O
+def host_info():
+    """Host CPU facts for the baseline line: model, nproc, the cores this process may run on."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cores": affinity,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    C = 256 * threads
-    chunk = 50
-    mix = getattr(w, "haario_k", None) is not None
-    if hasattr(w, "X"):  # cfg 3: MALA on the logistic target
-        C = threads
-        chunk = 2
-        st = O.MALAState(np.zeros((C, w.D)), w.X, w.y, nthreads=threads)
 
-        def step(it):
-            O.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=it, nsteps=chunk, nthreads=threads)
-    elif mix:
-        st = O.MixState(np.zeros((C, w.D)), sigma_b=w.sigma_b)
-
-        def step(it):
-            O.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
-                      lam=w.lam, haario_k=w.haario_k, ll_mode=ll_mode, nthreads=threads)
-    else:
-        st = O.OracleState(np.zeros((C, w.D)))
-        hist = O.alloc_history(C, w.D, chunk)
-
-        def step(it):
-            O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
-                      ll_mode=ll_mode, nthreads=threads, hist=hist)
-    it = 1
-    step(it)  # warm (page faults, caches)
-    it += chunk
-    steps = 0
+def _time_oracle(step, chunk, seconds):
+    step(1)  # warm (page faults, caches)
+    it, steps = 1 + chunk, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         step(it)
         it += chunk
         steps += chunk
-    dt = time.perf_counter() - t0
-    if hasattr(w, "X"):
-        return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
-                "sample": f"{C} chains x {steps} iterations of the same MALA logistic workload (N={w.nobs}, "
-                          f"D={w.D}), oracle/liboracle.so, {dt:.1f} s"}
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(w, seconds, ll_mode):
+    """The oracle (C restatement, OpenMP over chains) on a bounded sample of the
+    same workload, histories included.  Threads = this GPU's CPU share: the
+    OMP_NUM_THREADS the box sets (16 per GPU), else the cores in this process's
+    affinity mask.  Also timed on 1 core, and (cfg 2) in the "faithful" variant
+    that re-factorises Σ at every MvNormal construction like the reference
+    (random_walk.jl:147,167; gsn_target.jl:20)."""
+    from oracle import oracle as O
+
+    hi = host_info()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or hi["affinity_cores"] or 1
+    mix = getattr(w, "haario_k", None) is not None
+    mala = hasattr(w, "X")
+
+    def make(T, faithful=False):
+        if mala:  # cfg 3: MALA on the logistic target
+            C, chunk = T, 2
+            st = O.MALAState(np.zeros((C, w.D)), w.X, w.y, nthreads=T)
+
+            def step(it):
+                O.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=it, nsteps=chunk, nthreads=T)
+        elif mix:
+            C, chunk = 256 * T, 50
+            st = O.MixState(np.zeros((C, w.D)), sigma_b=w.sigma_b)
+
+            def step(it):
+                O.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
+                          lam=w.lam, haario_k=w.haario_k, ll_mode=ll_mode, nthreads=T)
+        else:
+            C, chunk = 256 * T, (10 if faithful else 50)
+            st = O.OracleState(np.zeros((C, w.D)))
+            hist = O.alloc_history(C, w.D, chunk)
+            mode = ll_mode | (0x200 if faithful else 0)
+
+            def step(it):
+                O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=it, nsteps=chunk,
+                          ll_mode=mode, nthreads=T, hist=hist)
+        return C, chunk, step
+
+    def rate(T, secs, faithful=False):
+        C, chunk, step = make(T, faithful)
+        steps, dt = _time_oracle(step, chunk, secs)
+        return C * steps / dt, C, steps, dt
+
+    v, C, steps, dt = rate(threads, 0.5 * seconds)
+    v1, C1, steps1, dt1 = rate(1, 0.2 * seconds)
+    out = {"value": v, "unit": "chain-steps/s", "cores": threads, "kind": "port", **hi,
+           "single_core": {"value": v1, "sample": f"{C1} chains x {steps1} iterations, {dt1:.1f} s"}}
+    if mala:
+        out["sample"] = (f"{C} chains x {steps} iterations of the same MALA logistic workload (N={w.nobs}, D={w.D}), "
+                         f"oracle/liboracle.so, {threads} threads, {dt:.1f} s")
+        return out
+    if not mix:
+        vf, Cf, stepsf, dtf = rate(threads, 0.3 * seconds, faithful=True)
+        out["faithful"] = {"value": vf, "cores": threads,
+                           "sample": f"{Cf} chains x {stepsf} iterations, {dtf:.1f} s: a Cholesky of Σ at every "
+                                     "MvNormal construction (rand, both logpdfs, P° and P set_parameters!) and a "
+                                     "logdet per logpdf, as the reference; same bits as the factor-once oracle"}
     what = ("GaussianRandomWalkMix + HaarioTypeAdaptation(k=%d) + chain mean/cov" % w.haario_k) if mix else "RWM"
-    return {"value": C * steps / dt, "unit": "chain-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{C} chains x {steps} iterations of the same D=32 {what} workload ({w.nobs} obs, "
-                      f"{'per-observation' if ll_mode == 0 else 'sufficient-statistic'} log-likelihood, "
-                      f"full histories), oracle/liboracle.so, {dt:.1f} s"}
+    out["sample"] = (f"{C} chains x {steps} iterations of the same D=32 {what} workload ({w.nobs} obs, "
+                     f"{'per-observation' if ll_mode == 0 else 'sufficient-statistic'} log-likelihood, "
+                     f"full histories), oracle/liboracle.so factor-once, {threads} threads, {dt:.1f} s")
+    return out
 
 
 def main():
@@ -119,13 +164,22 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # EMCMC_BENCH_SHARED_DEVICE=1: every rank on device 0 with gloo (a rehearsal of
+    # the torchrun path on a one-GPU box; RCCL needs one GPU per rank)
+    shared = os.environ.get("EMCMC_BENCH_SHARED_DEVICE") == "1"
+    device = 0 if shared else local
     dist = None
+    dev = None  # where the diagnostics all-gather runs
     if world > 1:
         import torch
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dev = f"cuda:{local}"
 
     from extensible_mcmc import _lib as L
     from extensible_mcmc import diagnostics as DG
@@ -134,14 +188,30 @@ def main():
 
     cfg4 = a.workload == "cfg4"
     cfg3 = a.workload == "cfg3"
-    Cg = a.chains_per_gpu or (131072 if cfg4 else 32768 if cfg3 else 65536)
-    w = W.cfg4(Cg, k=a.haario_k) if cfg4 else W.cfg3(Cg) if cfg3 else W.cfg2(Cg)
+    # N > 1 GPUs: BASELINE cfg 5, 131,072 chains per GPU (1,048,576 over 8), overdispersed θinit
+    cfg5 = a.workload == "cfg5" or (a.workload == "cfg2" and world > 1)
+    Cg = a.chains_per_gpu or (131072 if (cfg4 or cfg5) else 32768 if cfg3 else 65536)
+    first = (a.shard if a.shard >= 0 else rank) * Cg  # global id of this process's chain 0
+    if cfg4:
+        w = W.cfg4(Cg, k=a.haario_k)
+    elif cfg3:
+        w = W.cfg3(Cg)
+    elif cfg5:
+        w = W.cfg5(first + Cg)  # rows [first, first + Cg) are this shard's θinit whatever the world size
+        w.theta_init = w.theta_init[first:]
+        w.num_chains = Cg
+    else:
+        w = W.cfg2(Cg)
+    theta0 = np.broadcast_to(np.asarray(w.theta_init, dtype=np.float64), (Cg, w.D))
     ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
     hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
-    M = a.warmup + a.steps * a.reps
-    first = (a.shard if a.shard >= 0 else rank) * Cg  # global id of this process's chain 0
+    reps = a.reps
+    if reps <= 0:  # median of 5 timed repetitions when their full histories fit in 96 GB of HBM
+        per_iter = Cg * (16 * w.D + 8.125) if (hist == L.HIST_FULL and not a.history_ring) else 0
+        reps = 5 if (a.warmup + 5 * a.steps) * per_iter <= 96e9 else 1
+    M = a.warmup + a.steps * reps
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=first,
-                              device=local, history_mode=hist, lanes_per_chain=a.lpc,
+                              device=device, history_mode=hist, lanes_per_chain=a.lpc,
                               steps_per_launch=a.steps_per_launch, history_ring=a.history_ring))
     stream_bufs = None
     if a.stream_thin:
@@ -157,46 +227,47 @@ def main():
         eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
     if not cfg3:
         eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
-    eng.set_state(np.zeros((Cg, w.D)))
+    eng.set_state(np.ascontiguousarray(theta0))
     if a.warmup:
         eng.run_iters(1, a.warmup)
     eng.synchronize(allow_faults=cfg4)  # cfg 4: PosDef faults are counted and reported
 
     def barrier():
         if dist is not None:
-            dist.barrier(device_ids=[local])
+            if shared:
+                dist.barrier()
+            else:
+                dist.barrier(device_ids=[local])
 
     times, kern = [], []
     it = a.warmup + 1
-    for _ in range(a.reps):
+    for _ in range(reps):
+        # the rep's (mcmciter, pidx) schedule is built before the clock starts
+        steps = np.stack([np.arange(it, it + a.steps, dtype=np.uint32), np.ones(a.steps, dtype=np.uint32)], axis=1)
         eng.set_timing(True)
         barrier()
         eng.synchronize()
-        if dist is not None:
-            import torch
-
-            torch.cuda.synchronize()
         t0 = time.perf_counter()
         if stream_bufs is None:
-            eng.run_iters(it, a.steps)
+            eng.run(steps)
         else:  # half a ring per chunk: a chunk's thinned θ history leaves while the next chunk runs
             ch = a.history_ring // 2 if a.history_ring >= 2 * a.stream_thin else a.history_ring
             for c0 in range(0, a.steps, ch):
-                eng.run_iters(it + c0, ch)
+                eng.run(steps[c0:c0 + ch])
                 k0 = c0 // a.stream_thin
                 eng.stream_history(L.H_STATE, it + c0 + a.stream_thin - 1, ch // a.stream_thin, thin=a.stream_thin,
                                    out=stream_bufs[k0:k0 + ch // a.stream_thin])
             eng.stream_wait()
-        eng.synchronize(allow_faults=cfg4)
-        if dist is not None:
-            torch.cuda.synchronize()
+        eng.synchronize(allow_faults=cfg4)  # hipStreamSynchronize of the engine's stream (+ a 4-byte fault flag)
         barrier()
         dt = time.perf_counter() - t0
         ms, launches, nbytes = eng.get_timing(reset=True)
         eng.set_timing(False)
         kern.append((ms, launches, nbytes))
         if dist is not None:
-            t = torch.tensor([dt], dtype=torch.float64, device=f"cuda:{local}")
+            import torch
+
+            t = torch.tensor([dt], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dt = float(t.item())
         times.append(dt)
@@ -206,12 +277,12 @@ def main():
     dt = times[mid]
     ms, launches, nbytes = kern[mid]
 
-    # diagnostics over the timed window: one all-reduce of 3·D+3 doubles
+    # diagnostics over the first timed window: one all-gather of 3·D+3 doubles per rank, Chan-merged
     mom = eng.moments_window(a.warmup + 1, a.steps, split=True) if hist == L.HIST_FULL and not a.history_ring \
-        else None
+        and a.steps >= 4 else None
     if mom is not None and dist is not None:
-        mom = DG.allreduce_sums(mom, w.D, device=f"cuda:{local}")
-    diag = DG.rhat_from_sums(mom) if mom is not None else None
+        mom = DG.allgather_moments(mom, w.D, device=dev)
+    diag = DG.rhat_from_moments(mom) if mom is not None else None
 
     if rank != 0:
         dist.destroy_process_group()
@@ -247,14 +318,19 @@ def main():
         "dtype": "f64",
         "data": ("synthetic (X ~ N(0, 1/D), θ* ~ N(0, I), y ~ Bernoulli(σ(Xθ*)), numpy default_rng(20261018)), "
                  "θinit = 0" if cfg3 else
-                 "synthetic (GsnTargetLaw(μ*, I32), 10 obs from numpy default_rng(20261015)), θinit = 0"),
+                 "synthetic (GsnTargetLaw(μ*, I32), 10 obs from numpy default_rng(20261015)), " +
+                 ("θinit = x̄ + 3z/√n overdispersed (z from default_rng(20261016), row = global chain id)" if cfg5
+                  else "θinit = 0")),
         "config": {
             "workload": (f"BASELINE cfg 3: {Cg} MALA chains per GPU on a logistic-regression log-likelihood, "
                          f"N={w.nobs}, D={w.D}, fp64" if cfg3 else
                          f"BASELINE cfg 4: {Cg} adaptive RWM chains per GPU (GaussianRandomWalkMix + "
                          f"HaarioTypeAdaptation, per-chain running mean/cov on device), D=32 Gaussian target, fp64"
                          if cfg4 else
-                         f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64"),
+                         (f"BASELINE cfg 5: chains sharded over MI355X GPUs, {Cg} per GPU (1,048,576 at 8 GPUs), "
+                          f"here {world} GPU(s) = {Cg * world} chains, D=32 Gaussian target, fp64; cross-chain "
+                          "split-R̂ moments all-gathered once after the timed region" if cfg5 else
+                          f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64")),
             "chains_per_gpu": Cg,
             "total_chains": total_chains, "first_chain_id": first,
             "dim": w.D,
@@ -286,7 +362,13 @@ def main():
             "bytes_per_chain_step": bytes_per_launch / (Cg * a.steps / launches),
         },
         "kernel_chain_steps_per_s": Cg * a.steps / (ms / 1e3),
+        "reps": reps,
+        "times_s": times,
     }
+    # the same bytes on the wall clock of the timed region (host launch + synchronize included)
+    e2e = bytes_per_launch * launches / dt / 1e9
+    out["roofline"]["end_to_end"] = {"achieved": e2e, "frac": e2e / HBM_PEAK_GBS,
+                                     "note": "this rank's algorithmic bytes over the timed region's wall clock"}
     if cfg4:  # HIP events bracket the launch group, and its bytes cover all three kernels
         out["roofline"]["timed_region"] = ("per launch group: mix_gsn_kernel (steps) + mix_moments_kernel (batched "
                                            "GenericChainStats mean/cov) + mix_readjust_kernel when Haario is due")
@@ -316,7 +398,7 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
         if not a.history_ring:
             try:
-                out["parity"] = parity_sample(eng, w, a, ll_mode, first)
+                out["parity"] = parity_sample(eng, w, a, ll_mode, first, reps)
             except Exception as e:
                 out["parity"] = {"error": repr(e)}
     print(json.dumps(out))
@@ -325,7 +407,7 @@ def main():
         dist.destroy_process_group()
 
 
-def parity_sample(eng, w, a, ll_mode, first=0, n=8):
+def parity_sample(eng, w, a, ll_mode, first=0, reps=1, n=8):
     """Replay n random chains of the measured run on the oracle (bitwise); local
     chain c has the global id (RNG key) first + c."""
     from extensible_mcmc import _lib as L
@@ -333,7 +415,8 @@ def parity_sample(eng, w, a, ll_mode, first=0, n=8):
 
     rng = np.random.default_rng(123)
     picks = np.sort(rng.choice(w.num_chains, n, replace=False))
-    S = a.warmup + a.steps * a.reps
+    S = a.warmup + a.steps * reps
+    init = np.broadcast_to(np.asarray(w.theta_init, dtype=np.float64), (w.num_chains, w.D))
     acc = eng.get_history(L.H_ACCEPT, 1, S)[:, 0]
     theta, ll = eng.get_state()
     ok_acc = ok_th = True
@@ -355,7 +438,7 @@ def parity_sample(eng, w, a, ll_mode, first=0, n=8):
             h = O.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
                           lam=w.lam, haario_k=w.haario_k, chain0=first + int(c), ll_mode=ll_mode)
         else:
-            st = O.OracleState(np.zeros((1, w.D)))
+            st = O.OracleState(np.array(init[c:c + 1]))
             h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
                           chain0=first + int(c), ll_mode=ll_mode, history=True)
         ok_acc &= bool(np.array_equal(acc[:, c], h["acc"][:, 0]))

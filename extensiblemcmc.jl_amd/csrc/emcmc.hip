@@ -20,11 +20,13 @@
 #include <utility>
 #include <vector>
 
+#define EMCMC_HOST_UNIT 1  // this unit compiles the diagnostics / probe kernels
 #include "../../include/emcmc.h"
 #include "emcmc_kernels.h"
 #include "emcmc_mala.h"
 #include "emcmc_mix.h"
 #include "emcmc_mwg.h"
+#include "emcmc_dispatch.h"
 
 using namespace emcmc;
 
@@ -116,12 +118,6 @@ struct TargetHost {
     double c0 = 0.0, S_c = 0.0;
 };
 
-using KernelFn = void (*)(StepParams);
-using MwgFn = void (*)(MwgParams);
-using MixFn = void (*)(MixParams);
-using ReadjustFn = void (*)(MixReadjustParams);
-using MalaFn = void (*)(MalaParams);
-using MomentsFn = void (*)(MixMomentsParams);
 
 struct Variant {
     KernelFn fn = nullptr;
@@ -153,6 +149,10 @@ struct emcmc_handle {
     double *d_theta = nullptr, *d_ll = nullptr, *d_ra = nullptr;
     uint64_t *d_ring = nullptr;
     uint32_t *d_nacc = nullptr, *d_faults = nullptr;
+    // any-fault word, written by the kernels only when a chain ends a launch faulted:
+    // host-mapped pinned memory, so emcmc_synchronize reads 4 B after the stream
+    // drains instead of copying and scanning C fault words
+    uint32_t *h_fault_flag = nullptr, *d_fault_flag = nullptr;
     double *d_hist_theta = nullptr, *d_hist_prop = nullptr, *d_hist_ll = nullptr;
     uint8_t *d_hist_acc = nullptr;
     double *d_consts = nullptr, *d_obs = nullptr;
@@ -227,59 +227,8 @@ emcmc_status fail(emcmc_handle *h, emcmc_status st, const char *fmt, ...) {
                         "%s failed: %s", #expr, hipGetErrorString(e_));                       \
     } while (0)
 
-// ---- kernel table -----------------------------------------------------------
-struct Key {
-    int D, lpc, full, ll, dense, unit, occ;
-};
-
-template <int D, int LPC, bool FULL, int LL, bool UNIT, int MINW = 1>
-KernelFn diag_fn() {
-    return &rwm_gsn_diag_kernel<D, LPC, FULL, LL, UNIT, MINW>;
-}
-template <int D, bool FULL, int LL>
-KernelFn dense_fn() {
-    return &rwm_gsn_dense_kernel<D, FULL, LL>;
-}
-
-#define DIAGU(D, LPC, U)                                                                          \
-    {{D, LPC, 1, 0, 0, U, 0}, diag_fn<D, LPC, true, 0, U>()},                                        \
-        {{D, LPC, 1, 1, 0, U, 0}, diag_fn<D, LPC, true, 1, U>()},                                    \
-        {{D, LPC, 0, 0, 0, U, 0}, diag_fn<D, LPC, false, 0, U>()},                                   \
-        {{D, LPC, 0, 1, 0, U, 0}, diag_fn<D, LPC, false, 1, U>()}
-#define DIAG4(D, LPC) DIAGU(D, LPC, false), DIAGU(D, LPC, true)
-#define DIAGO(D, LPC, U)                                                                          \
-    {{D, LPC, 1, 0, 0, U, 4}, diag_fn<D, LPC, true, 0, U, 4>()},                                     \
-        {{D, LPC, 1, 1, 0, U, 4}, diag_fn<D, LPC, true, 1, U, 4>()},                                 \
-        {{D, LPC, 0, 0, 0, U, 4}, diag_fn<D, LPC, false, 0, U, 4>()},                                \
-        {{D, LPC, 0, 1, 0, U, 4}, diag_fn<D, LPC, false, 1, U, 4>()}
-#define DIAGO3(D, LPC, U)                                                                         \
-    {{D, LPC, 1, 0, 0, U, 3}, diag_fn<D, LPC, true, 0, U, 3>()},                                     \
-        {{D, LPC, 1, 1, 0, U, 3}, diag_fn<D, LPC, true, 1, U, 3>()},                                 \
-        {{D, LPC, 0, 0, 0, U, 3}, diag_fn<D, LPC, false, 0, U, 3>()},                                \
-        {{D, LPC, 0, 1, 0, U, 3}, diag_fn<D, LPC, false, 1, U, 3>()}
-#define DENSE4(D)                                                                                    \
-    {{D, 1, 1, 0, 1, 0, 0}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1, 0, 0}, dense_fn<D, true, 1>()},   \
-        {{D, 1, 0, 0, 1, 0, 0}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1, 0, 0}, dense_fn<D, false, 1>()}
-
-struct Entry {
-    Key k;
-    KernelFn fn;
-};
-
-const std::vector<Entry> &kernel_table() {
-    static const std::vector<Entry> t = {
-        DIAG4(1, 1),  DIAG4(2, 1),  DIAG4(3, 1),  DIAG4(4, 1),  DIAG4(8, 1),
-        DIAG4(16, 1), DIAG4(16, 2), DIAG4(32, 1), DIAG4(32, 2), DIAG4(32, 4),
-        DIAG4(64, 2), DIAG4(64, 4), DIAGO(32, 4, true), DIAGO(32, 4, false), DIAGO(32, 2, true),
-        DIAGO3(32, 2, true), DIAGO3(32, 4, true), DIAGO3(32, 1, true),
-        DENSE4(1),    DENSE4(2),    DENSE4(3),
-        DENSE4(4),    DENSE4(8),
-    };
-    return t;
-}
-
 KernelFn lookup(int D, int lpc, bool full, int ll, bool dense, bool unit, int occ = 0) {
-    for (const auto &e : kernel_table())
+    for (const auto &e : diag_table())
         if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == (int)dense &&
             e.k.unit == (int)unit && e.k.occ == occ)
             return e.fn;
@@ -336,6 +285,9 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
     HIPCHK(h, hipMalloc(&h->d_ring, 2 * P * C * sizeof(uint64_t)));
     HIPCHK(h, hipMalloc(&h->d_nacc, P * C * sizeof(uint32_t)));
     HIPCHK(h, hipMalloc(&h->d_faults, C * sizeof(uint32_t)));
+    HIPCHK(h, hipHostMalloc(reinterpret_cast<void **>(&h->h_fault_flag), sizeof(uint32_t), hipHostMallocMapped));
+    HIPCHK(h, hipHostGetDevicePointer(reinterpret_cast<void **>(&h->d_fault_flag), h->h_fault_flag, 0));
+    *h->h_fault_flag = 0u;
     // general schedule path: P° mean, AdaptationUnifRW state, step lists
     HIPCHK(h, hipMalloc(&h->d_mu_p, C * D * sizeof(double)));
     HIPCHK(h, hipMalloc(&h->d_aprop, P * C * sizeof(uint32_t)));
@@ -375,22 +327,6 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
     }
     h->allocated = true;
     return EMCMC_OK;
-}
-
-// ---- general schedule kernel table ----------------------------------------
-template <int D, bool FULL, int LL>
-MwgFn mwg_fn() {
-    return &mwg_gsn_kernel<D, FULL, LL>;
-}
-#define MWG4(D) \
-    {D, mwg_fn<D, true, 0>(), mwg_fn<D, true, 1>(), mwg_fn<D, false, 0>(), mwg_fn<D, false, 1>()}
-struct MwgEntry {
-    int D;
-    MwgFn full_perobs, full_suff, acc_perobs, acc_suff;
-};
-const std::vector<MwgEntry> &mwg_table() {
-    static const std::vector<MwgEntry> t = {MWG4(1), MWG4(2), MWG4(3), MWG4(4), MWG4(8), MWG4(16)};
-    return t;
 }
 
 // Every schedule but one joint GaussianRandomWalk update on coords 1:D runs on
@@ -477,67 +413,12 @@ bool fused_eligible(const emcmc_handle *h) {
     return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
 }
 
-// ---- mix kernel table -------------------------------------------------------
-template <int D, bool FULL, int LL, bool MIX, bool ADIAG>
-MixFn mix_fn() {
-    return &mix_gsn_kernel<D, FULL, LL, MIX, ADIAG>;
-}
-struct MixEntry {
-    int D, full, ll, mix, adiag;
-    MixFn fn;
-};
-#define MIXV(D, F, L, M, A) {D, F, L, M, A, mix_fn<D, F, L, M, A>()}
-#define MIX8(D, A)                                                                                         \
-    MIXV(D, true, 0, true, A), MIXV(D, true, 1, true, A), MIXV(D, false, 0, true, A),                     \
-        MIXV(D, false, 1, true, A), MIXV(D, true, 0, false, A), MIXV(D, true, 1, false, A),                \
-        MIXV(D, false, 0, false, A), MIXV(D, false, 1, false, A)
-const std::vector<MixEntry> &mix_table() {
-    // dense Σ_A / Σ_t for D ≤ 8; D = 16, 32 take diagonal ones (cfg 4: σ²I, I)
-    static const std::vector<MixEntry> t = {MIX8(1, true),  MIX8(2, true),  MIX8(2, false), MIX8(3, true),
-                                            MIX8(3, false), MIX8(4, true),  MIX8(4, false), MIX8(8, true),
-                                            MIX8(8, false), MIX8(16, true), MIX8(32, true)};
-    return t;
-}
-template <int D>
-ReadjustFn readjust_fn() {
-    return &mix_readjust_kernel<D>;
-}
-template <int D>
-std::pair<MomentsFn, int> moments_fn() {
-    return {&mix_moments_kernel<D>, MomentTiles<D>::WPB};
-}
-std::pair<MomentsFn, int> moments_lookup(int D) {
-    switch (D) {
-    case 1: return moments_fn<1>();
-    case 2: return moments_fn<2>();
-    case 3: return moments_fn<3>();
-    case 4: return moments_fn<4>();
-    case 8: return moments_fn<8>();
-    case 16: return moments_fn<16>();
-    case 32: return moments_fn<32>();
-    default: return {nullptr, 0};
-    }
-}
-
 // chains per 256-thread block of mix_readjust_kernel<D> (R lanes per chain)
 int readjust_chains_per_block(int D) {
     int r = 1;
     while (r < D) r <<= 1;
     return 4 * (64 / r);
 }
-ReadjustFn readjust_lookup(int D) {
-    switch (D) {
-    case 1: return readjust_fn<1>();
-    case 2: return readjust_fn<2>();
-    case 3: return readjust_fn<3>();
-    case 4: return readjust_fn<4>();
-    case 8: return readjust_fn<8>();
-    case 16: return readjust_fn<16>();
-    case 32: return readjust_fn<32>();
-    default: return nullptr;
-    }
-}
-
 emcmc_status select_mix(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
     const UpdateHost &u = h->updates[0];
@@ -593,10 +474,6 @@ emcmc_status select_mix(emcmc_handle *h) {
 }
 
 // ---- MALA kernel table ---------------------------------------------------------
-template <int DB, bool FULL, int MODE>
-MalaFn mala_fn() {
-    return &mala_logistic_kernel<DB, FULL, MODE>;
-}
 emcmc_status select_mala(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
     if (!joint_all_coords(h))
@@ -605,14 +482,10 @@ emcmc_status select_mala(emcmc_handle *h) {
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA on device needs the logistic-regression target");
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     Variant v;
-    switch (D) {
-    case 16: v.afn = full ? mala_fn<1, true, 0>() : mala_fn<1, false, 0>(); v.ainit = mala_fn<1, true, 1>(); break;
-    case 32: v.afn = full ? mala_fn<2, true, 0>() : mala_fn<2, false, 0>(); v.ainit = mala_fn<2, true, 1>(); break;
-    case 48: v.afn = full ? mala_fn<3, true, 0>() : mala_fn<3, false, 0>(); v.ainit = mala_fn<3, true, 1>(); break;
-    case 64: v.afn = full ? mala_fn<4, true, 0>() : mala_fn<4, false, 0>(); v.ainit = mala_fn<4, true, 1>(); break;
-    default:
+    v.afn = mala_lookup(D, full, 0);
+    v.ainit = mala_lookup(D, true, 1);
+    if (!v.afn || !v.ainit)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no MALA kernel for D=%d (instantiated: D ∈ {16,32,48,64})", D);
-    }
     char nm[160];
     snprintf(nm, sizeof nm, "mala_logistic_kernel<D=%d,%s>", D, full ? "FULL" : "ACCEPT_ONLY");
     v.name = nm;
@@ -839,6 +712,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     p.ring = h->d_ring;
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
+    p.fault_flag = h->d_fault_flag;
     p.mom_theta = h->d_mom_scratch;
     p.LB = h->d_LB;
     p.iLB = h->d_iLB;
@@ -872,6 +746,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     r.iLB = h->d_iLB;
     r.c0B = h->d_c0B;
     r.faults = h->d_faults;
+    r.fault_flag = h->d_fault_flag;
     r.C = C;
     r.sB = (2.38 * 2.38) / (double)h->cfg.dim;  // 2.38^2/length(rw), adaptation.jl:423
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
@@ -971,6 +846,7 @@ emcmc_status run_mala(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
     p.ring = h->d_ring;
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
+    p.fault_flag = h->d_fault_flag;
     p.hist_theta = h->d_hist_theta;
     p.hist_prop = h->d_hist_prop;
     p.hist_ll = h->d_hist_ll;
@@ -1068,6 +944,7 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.aacc = h->d_aacc;
     a.eps = h->d_eps;
     a.faults = h->d_faults;
+    a.fault_flag = h->d_fault_flag;
     a.hist_theta = h->d_hist_theta;
     a.hist_prop = h->d_hist_prop;
     a.hist_ll = h->d_hist_ll;
@@ -1363,6 +1240,7 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
             if (st) return st;
         }
         HIPCHK(h, hipStreamSynchronize(h->stream));  // host vectors go out of scope
+        *static_cast<volatile uint32_t *>(h->h_fault_flag) = 0u;  // fault words were cleared above
     }
     if (h->d_mean) {  // GenericChainStats: mean = 0, cov = 0, N = 1 (chain_statistics.jl:30-35)
         const uint64_t DP = (uint64_t)packed_n((int)D);
@@ -1421,6 +1299,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     p.ring = h->d_ring;
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
+    p.fault_flag = h->d_fault_flag;
     p.hist_theta = h->d_hist_theta;
     p.hist_prop = h->d_hist_prop;
     p.hist_ll = h->d_hist_ll;
@@ -1495,10 +1374,9 @@ emcmc_status emcmc_synchronize(emcmc_handle *h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->steps_staging.clear();
     if (!h->allocated) return EMCMC_OK;
-    std::vector<uint32_t> f(h->cfg.num_chains);
-    HIPCHK(h, hipMemcpy(f.data(), h->d_faults, f.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    for (uint32_t x : f)
-        if (x) return fail(h, EMCMC_CHAIN_FAULT, "at least one chain raised a fault (emcmc_get_faults)");
+    // O(1): the kernels set the mapped flag when a chain ends a launch with a fault bit
+    if (*static_cast<volatile uint32_t *>(h->h_fault_flag))
+        return fail(h, EMCMC_CHAIN_FAULT, "at least one chain raised a fault (emcmc_get_faults)");
     return EMCMC_OK;
 }
 
@@ -1523,6 +1401,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (h->h_fault_flag) (void)hipHostFree(h->h_fault_flag);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
 }

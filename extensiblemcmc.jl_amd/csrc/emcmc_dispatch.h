@@ -1,0 +1,53 @@
+// emcmc_dispatch.h — kernel tables shared by the host ABI (emcmc.hip) and the
+// per-family instantiation units (inst_*.hip).  Each unit instantiates one
+// family of step kernels for gfx950; splitting them lets make build the
+// families in parallel.
+#pragma once
+
+#include <utility>
+#include <vector>
+
+#include "emcmc_kernels.h"
+#include "emcmc_mala.h"
+#include "emcmc_mix.h"
+#include "emcmc_mwg.h"
+
+namespace emcmc {
+
+using KernelFn = void (*)(StepParams);
+using MwgFn = void (*)(MwgParams);
+using MixFn = void (*)(MixParams);
+using ReadjustFn = void (*)(MixReadjustParams);
+using MalaFn = void (*)(MalaParams);
+using MomentsFn = void (*)(MixMomentsParams);
+
+// fused single-update kernels (rwm_gsn_diag_kernel / rwm_gsn_dense_kernel)
+struct Key {
+    int D, lpc, full, ll, dense, unit, occ;
+};
+struct Entry {
+    Key k;
+    KernelFn fn;
+};
+const std::vector<Entry> &diag_table();
+
+// general schedule kernel (mwg_gsn_kernel)
+struct MwgEntry {
+    int D;
+    MwgFn full_perobs, full_suff, acc_perobs, acc_suff;
+};
+const std::vector<MwgEntry> &mwg_table();
+
+// GaussianRandomWalkMix / chain moments (mix_gsn_kernel, mix_moments_kernel, mix_readjust_kernel)
+struct MixEntry {
+    int D, full, ll, mix, adiag;
+    MixFn fn;
+};
+const std::vector<MixEntry> &mix_table();
+std::pair<MomentsFn, int> moments_lookup(int D);
+ReadjustFn readjust_lookup(int D);
+
+// MALA on the logistic target (mala_logistic_kernel); mode 1 = ∇ℓ initialisation
+MalaFn mala_lookup(int D, bool full, int mode);
+
+}  // namespace emcmc

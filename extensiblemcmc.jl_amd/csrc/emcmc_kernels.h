@@ -42,6 +42,7 @@ struct StepParams {
     uint64_t *ring;    // [C][2] acceptance bits of the last 128 iterations
     uint32_t *nacc;    // [C] accepted proposals
     uint32_t *faults;  // [C]
+    uint32_t *fault_flag;  // set to 1 by any lane that ends a launch with a fault bit (emcmc_synchronize)
     // history streams (FULL mode), slot = (mcmciter-1)*P + pidx0
     double *hist_theta;  // [M*P][C][D]
     double *hist_prop;   // [M*P][C][D]
@@ -784,6 +785,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         chain_elem(a.ring, 2 * c32 + 1) = r1;
         chain_elem(a.nacc, c32) = nacc;
         chain_elem(a.faults, c32) = faults;
+        if (faults) *a.fault_flag = 1u;
     }
     store_slot_cached<D>(a.theta, soff, th);
 }
@@ -898,9 +900,12 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     a.ring[2 * chain + 1] = r1;
     a.nacc[chain] = nacc;
     a.faults[chain] = faults;
+    if (faults) *a.fault_flag = 1u;
     store_state<D>(a.theta, C, chain, 0, th, false);
 }
 
+// Host-unit kernels (diagnostics, gathers, probes): compiled once, in emcmc.hip.
+#ifdef EMCMC_HOST_UNIT
 // ---------------------------------------------------------------------------
 // Diagnostics: per-(half-)chain mean and unbiased variance of θ over a window
 // of history slots, then a deterministic tree reduction over chains.
@@ -929,39 +934,63 @@ chain_moments_kernel(const double *__restrict__ hist, uint64_t C, uint32_t D, ui
     var_out[t] = (len > 1) ? q / (double)(len - 1) : 0.0;
 }
 
-// out[d] = Σ over (half-)chains of f(x), f ∈ {x, x², y}: one block per d,
-// fixed chunking → deterministic for a given (C, halves).
+// out = [mean of the (half-)chain means | M2 = Σ (m_c − m̄)² | Σ var_c], per d:
+// one block per d.  Each thread runs Welford over its strided rows; the block
+// combines them by Chan's pairwise merge in a fixed tree, so the result is
+// deterministic for a given (C, halves) and M2 does not cancel at 1M chains the
+// way Σm² − (Σm)²/m does.  Shards merge the same way (diagnostics.py).
+__device__ __forceinline__ void chan_merge(double &na, double &ma, double &qa, double nb, double mb, double qb) {
+    const double n = na + nb;
+    if (nb == 0.0) return;
+    if (na == 0.0) {
+        na = nb;
+        ma = mb;
+        qa = qb;
+        return;
+    }
+    const double dl = mb - ma;
+    ma = ma + dl * (nb / n);
+    qa = (qa + qb) + dl * dl * (na * nb / n);
+    na = n;
+}
+
 __global__ void __launch_bounds__(256)
 moments_reduce_kernel(const double *__restrict__ mean_in, const double *__restrict__ var_in, uint64_t C,
                       uint32_t D, uint32_t halves, double *__restrict__ out3d) {
     const uint32_t d = blockIdx.x;
-    __shared__ double sm[3][256];
-    double a = 0.0, b = 0.0, c = 0.0;
+    __shared__ double sm[4][256];
+    double n = 0.0, mu = 0.0, q = 0.0, c = 0.0;
     const uint64_t rows = C * halves;
     for (uint64_t r = threadIdx.x; r < rows; r += blockDim.x) {
         const uint64_t h = r / C, ch = r % C;
         const uint64_t idx = h * C * D + state_pos(d, ch, C, D);
         const double m = mean_in[idx];
-        a = a + m;
-        b = b + m * m;
+        n = n + 1.0;
+        const double dl = m - mu;
+        mu = mu + dl / n;
+        q = q + dl * (m - mu);
         c = c + var_in[idx];
     }
-    sm[0][threadIdx.x] = a;
-    sm[1][threadIdx.x] = b;
-    sm[2][threadIdx.x] = c;
+    sm[0][threadIdx.x] = n;
+    sm[1][threadIdx.x] = mu;
+    sm[2][threadIdx.x] = q;
+    sm[3][threadIdx.x] = c;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) {
-            sm[0][threadIdx.x] = sm[0][threadIdx.x] + sm[0][threadIdx.x + w];
-            sm[1][threadIdx.x] = sm[1][threadIdx.x] + sm[1][threadIdx.x + w];
-            sm[2][threadIdx.x] = sm[2][threadIdx.x] + sm[2][threadIdx.x + w];
+            double na = sm[0][threadIdx.x], ma = sm[1][threadIdx.x], qa = sm[2][threadIdx.x];
+            chan_merge(na, ma, qa, sm[0][threadIdx.x + w], sm[1][threadIdx.x + w], sm[2][threadIdx.x + w]);
+            sm[0][threadIdx.x] = na;
+            sm[1][threadIdx.x] = ma;
+            sm[2][threadIdx.x] = qa;
+            sm[3][threadIdx.x] = sm[3][threadIdx.x] + sm[3][threadIdx.x + w];
         }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        out3d[d] = sm[0][0];
-        out3d[D + d] = sm[1][0];
-        out3d[2 * D + d] = sm[2][0];
+        out3d[d] = sm[1][0];
+        out3d[D + d] = sm[2][0];
+        out3d[2 * D + d] = sm[3][0];
     }
 }
 
@@ -1003,5 +1032,7 @@ __global__ void __launch_bounds__(256) probe_log_kernel(const double *__restrict
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) y[t] = log_pos(x[t]);
 }
+
+#endif  // EMCMC_HOST_UNIT
 
 }  // namespace emcmc

@@ -41,6 +41,7 @@ struct MalaParams {
     uint64_t *ring;  // [C][2]
     uint32_t *nacc;  // [C]
     uint32_t *faults;
+    uint32_t *fault_flag;
     double *hist_theta, *hist_prop, *hist_ll;
     uint8_t *hist_acc;
     const Ziggurat *zig;  // global memory (a few draws per lane per step)
@@ -272,6 +273,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
         a.ring[2 * chain + 1] = r1;
         a.nacc[chain] += acc ? 1u : 0u;
         a.faults[chain] = faults;
+        if (faults) *a.fault_flag = 1u;
     }
 }
 

@@ -48,6 +48,7 @@ struct MixParams {
     uint64_t *ring;  // [C][2]
     uint32_t *nacc;  // [C]
     uint32_t *faults;
+    uint32_t *fault_flag;
     double *mom_theta;  // ACCEPT_ONLY: θ after each step of the launch, [nsteps] slots (state_pos)
     const double *LB;   // [DP] packed lower, state_pos(q, c, C, DP)
     const double *iLB;  // [D][C]
@@ -302,6 +303,7 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
     a.ring[2 * chain + 1] = r1;
     a.nacc[chain] = nacc;
     a.faults[chain] = faults;
+    if (faults) *a.fault_flag = 1u;
     store_state<D>(a.theta, C, chain, 0, th, false);
 }
 
@@ -331,6 +333,7 @@ struct MixMomentsParams {
     uint32_t nsteps;
 };
 
+#ifdef EMCMC_HOST_UNIT
 // The step-dependent scalars of the recurrence, (N, N+1, (N−1)/N, N/(N+1),
 // (N+1)/N, 1/N, 1/(N+1)) for the launch's steps, computed once per launch
 // (the same IEEE divisions, so the same bits) instead of by every lane of
@@ -350,6 +353,8 @@ __global__ void __launch_bounds__(64) moments_consts_kernel(uint64_t N0, uint32_
     k[6] = 1.0 / N1d;
     k[7] = 0.0;
 }
+
+#endif  // EMCMC_HOST_UNIT
 
 template <int D>
 struct MomentTiles {
@@ -543,6 +548,7 @@ struct MixReadjustParams {
     double *iLB;        // [D][C]
     double *c0B;        // [C]
     uint32_t *faults;
+    uint32_t *fault_flag;
     uint64_t C;
     double sB;  // 2.38²/D
 };
@@ -619,7 +625,10 @@ __global__ void __launch_bounds__(256) mix_readjust_kernel(const MixReadjustPara
     const bool chain_ok = (okm & gm) == gm;
     if (chain >= C) return;
     if (!chain_ok) {
-        if (i == 0) a.faults[chain] |= 4u;  // EMCMC_FAULT_POSDEF
+        if (i == 0) {
+            a.faults[chain] |= 4u;  // EMCMC_FAULT_POSDEF
+            *a.fault_flag = 1u;
+        }
         return;
     }
     if (i >= D) return;

@@ -62,6 +62,7 @@ struct MwgParams {
     uint32_t *aacc;    // [P][C]
     double *eps;       // [P][kMwgMaxD][C]  per-chain ϵ of adaptive updates
     uint32_t *faults;  // [C]
+    uint32_t *fault_flag;
     double *hist_theta, *hist_prop, *hist_ll;
     uint8_t *hist_acc;
     const Ziggurat *zig;
@@ -396,6 +397,7 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
     }
     a.ll[chain] = ll;
     a.faults[chain] = faults;
+    if (faults) *a.fault_flag = 1u;
 }
 
 }  // namespace emcmc

@@ -1,0 +1,58 @@
+// inst_mix.hip — gfx950 instantiations of the GaussianRandomWalkMix / Haario / chain-moments
+// kernels (emcmc_mix.h).
+#include "emcmc_dispatch.h"
+
+namespace emcmc {
+
+template <int D, bool FULL, int LL, bool MIX, bool ADIAG>
+MixFn mix_fn() {
+    return &mix_gsn_kernel<D, FULL, LL, MIX, ADIAG>;
+}
+#define MIXV(D, F, L, M, A) {D, F, L, M, A, mix_fn<D, F, L, M, A>()}
+#define MIX8(D, A)                                                                                         \
+    MIXV(D, true, 0, true, A), MIXV(D, true, 1, true, A), MIXV(D, false, 0, true, A),                     \
+        MIXV(D, false, 1, true, A), MIXV(D, true, 0, false, A), MIXV(D, true, 1, false, A),                \
+        MIXV(D, false, 0, false, A), MIXV(D, false, 1, false, A)
+const std::vector<MixEntry> &mix_table() {
+    // dense Σ_A / Σ_t for D ≤ 8; D = 16, 32 take diagonal ones (cfg 4: σ²I, I)
+    static const std::vector<MixEntry> t = {MIX8(1, true),  MIX8(2, true),  MIX8(2, false), MIX8(3, true),
+                                            MIX8(3, false), MIX8(4, true),  MIX8(4, false), MIX8(8, true),
+                                            MIX8(8, false), MIX8(16, true), MIX8(32, true)};
+    return t;
+}
+template <int D>
+ReadjustFn readjust_fn() {
+    return &mix_readjust_kernel<D>;
+}
+template <int D>
+std::pair<MomentsFn, int> moments_fn() {
+    return {&mix_moments_kernel<D>, MomentTiles<D>::WPB};
+}
+std::pair<MomentsFn, int> moments_lookup(int D) {
+    switch (D) {
+    case 1: return moments_fn<1>();
+    case 2: return moments_fn<2>();
+    case 3: return moments_fn<3>();
+    case 4: return moments_fn<4>();
+    case 8: return moments_fn<8>();
+    case 16: return moments_fn<16>();
+    case 32: return moments_fn<32>();
+    default: return {nullptr, 0};
+    }
+}
+
+ReadjustFn readjust_lookup(int D) {
+    switch (D) {
+    case 1: return readjust_fn<1>();
+    case 2: return readjust_fn<2>();
+    case 3: return readjust_fn<3>();
+    case 4: return readjust_fn<4>();
+    case 8: return readjust_fn<8>();
+    case 16: return readjust_fn<16>();
+    case 32: return readjust_fn<32>();
+    default: return nullptr;
+    }
+}
+
+
+}  // namespace emcmc

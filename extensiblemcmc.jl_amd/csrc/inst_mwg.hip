@@ -1,0 +1,18 @@
+// inst_mwg.hip — gfx950 instantiations of the general schedule kernel (emcmc_mwg.h).
+#include "emcmc_dispatch.h"
+
+namespace emcmc {
+
+template <int D, bool FULL, int LL>
+MwgFn mwg_fn() {
+    return &mwg_gsn_kernel<D, FULL, LL>;
+}
+#define MWG4(D) \
+    {D, mwg_fn<D, true, 0>(), mwg_fn<D, true, 1>(), mwg_fn<D, false, 0>(), mwg_fn<D, false, 1>()}
+const std::vector<MwgEntry> &mwg_table() {
+    static const std::vector<MwgEntry> t = {MWG4(1), MWG4(2), MWG4(3), MWG4(4), MWG4(8), MWG4(16)};
+    return t;
+}
+
+
+}  // namespace emcmc

@@ -6,7 +6,7 @@ Names follow the reference's exports (src/ExtensibleMCMC.jl:31-41); Julia's
 mcmciter, pidx) stay 1-based as in the reference.
 """
 from .callbacks import Callback, REPLCallback, SavingCallback
-from .diagnostics import allreduce_sums, rhat_from_sums
+from .diagnostics import allgather_moments, merge as merge_moments, rhat_from_moments
 from .engine import Engine, EngineConfig
 from .kernels import (AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMix, HaarioTypeAdaptation,
                       HamiltonianMCUpdate, ImproperPosPrior, ImproperPrior, MALAUpdate, MCMCBackend,
@@ -23,5 +23,5 @@ __all__ = [
     "HaarioTypeAdaptation", "NoAdaptation", "RandomWalkUpdate", "GenericMCMCBackend", "MI355XBackend",
     "GsnTargetLaw", "run", "run_", "get_decorators", "isdecorator", "ImproperPosPrior", "ImproperPrior",
     "SavingCallback", "REPLCallback", "MCMCSchedule", "JRange", "reschedule", "Engine", "EngineConfig",
-    "EMCMCError", "device_count", "rhat_from_sums", "allreduce_sums", "MALAUpdate", "LogisticRegressionLaw",
+    "EMCMCError", "device_count", "rhat_from_moments", "allgather_moments", "merge_moments", "MALAUpdate", "LogisticRegressionLaw",
 ]

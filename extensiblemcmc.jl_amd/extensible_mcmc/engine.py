@@ -368,8 +368,8 @@ class Engine:
         )
         D = self.cfg.dim
         return {
-            "sum_mean": out[:D].copy(),
-            "sum_mean_sq": out[D : 2 * D].copy(),
+            "mean": out[:D].copy(),
+            "m2": out[D : 2 * D].copy(),
             "sum_var": out[2 * D :].copy(),
             "num_chains": int(info.num_chains),
             "num_draws": int(info.num_draws),

@@ -319,9 +319,11 @@ emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dp
 
 /* ---- diagnostics (new; BASELINE cfg 5) --------------------------------- */
 
-/* Per-dimension sums over the chains of this handle of the (split) chain means,
- * squared means and unbiased variances of θ over iterations
- * [iter_first, iter_first+num_iters).  out3d = [Σ mean | Σ mean² | Σ var], 3·D doubles.
+/* Per-dimension moments over the chains of this handle of the (split) chain
+ * means and unbiased variances of θ over iterations [iter_first, iter_first+num_iters):
+ * out3d = [m̄ = mean of the chain means | M2 = Σ_c (m_c − m̄)² | Σ_c var_c], 3·D doubles,
+ * with info->num_chains (half-)chains.  M2 comes from a Welford/Chan reduction, so
+ * shards merge without cancellation (Chan et al. 1979; extensible_mcmc/diagnostics.py).
  * split != 0 treats each chain as two halves (split-R̂). */
 emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t num_iters,
                                   int split, double *out3d, emcmc_moments *info);

@@ -155,6 +155,13 @@ static int is_diag_upper(const double *S, int D) {
 
 typedef struct {
     int D, diag, ll_mode;
+    /* faithful (ll_mode bit 9, CPU baseline only): every MvNormal construction
+     * factorises its Σ again, as the reference does (random_walk.jl:147,167 for
+     * rand and both logpdfs; gsn_target.jl:20 for set_parameters! of P° and of P),
+     * and every logpdf recomputes its log-determinant.  Same bits as the
+     * factor-once path (the same deterministic Cholesky of the same Σ). */
+    int faithful;
+    const double *rw_sigma, *t_sigma;
     uint64_t nobs;
     const double *obs;
     double Lrw[64 * 64], iLrw[64], Lt[64 * 64], iLt[64], xbar[64];
@@ -169,11 +176,14 @@ static int gsn_prepare(orc_gsn *g, int D, const double *rw_sigma, const double *
     g->nobs = nobs;
     g->obs = obs;
     g->ll_mode = ll_mode & 0xFF;
+    g->faithful = (ll_mode & 0x200) != 0;
+    g->rw_sigma = rw_sigma;
+    g->t_sigma = t_sigma;
     if (orc_cholesky(rw_sigma, D, g->Lrw)) return -1;
     if (orc_cholesky(t_sigma, D, g->Lt)) return -1;
     /* ll_mode bit 8 forces the dense (general Cholesky) formulas even for a
      * diagonal Σ — used by tests to show both formulas give the same bits. */
-    g->diag = !(ll_mode & 0x100) && is_diag_upper(rw_sigma, D) && is_diag_upper(t_sigma, D);
+    g->diag = !(ll_mode & 0x300) && is_diag_upper(rw_sigma, D) && is_diag_upper(t_sigma, D);
     for (int i = 0; i < D; ++i) {
         g->iLrw[i] = 1.0 / g->Lrw[(size_t)i * D + i];
         g->iLt[i] = 1.0 / g->Lt[(size_t)i * D + i];
@@ -223,6 +233,93 @@ typedef struct {
     uint32_t *faults;
 } orc_chain;
 
+/* A fresh MvNormal(·, Σ): Cholesky factor, 1/L_ii and c0 (PDMat construction +
+ * mvnormal_c0's logdetcov at every logpdf call). */
+typedef struct {
+    double L[64 * 64], iL[64], c0;
+} orc_mvn;
+static void mvn_build(orc_mvn *m, const double *S, int D) {
+    (void)orc_cholesky(S, D, m->L);
+    for (int i = 0; i < D; ++i) m->iL[i] = 1.0 / m->L[(size_t)i * D + i];
+    m->c0 = mvnormal_c0(D, logdet_chol(m->L, D));
+}
+
+/* The reference's per-step work without the factor-once shortcut (CPU baseline
+ * "faithful" variant; iterations consecutive from iter0; dense formulas). */
+static void run_chain_faithful(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t key1, uint32_t chain_id,
+                               uint32_t iter0, uint32_t nsteps, uint64_t N0, uint32_t W, uint64_t C, uint64_t c,
+                               double *hist_theta, double *hist_prop, double *hist_ll, uint8_t *hist_acc) {
+    const int D = g->D;
+    const orc_zig_tables *zt = zig();
+    orc_mvn *m = (orc_mvn *)malloc(sizeof(orc_mvn));
+    double th[64], thp[64], z[64], r[64];
+    memcpy(th, st.theta, sizeof(double) * D);
+    double ll = *st.ll, ra = *st.ra;
+    uint64_t ring0 = st.ring[0], ring1 = st.ring[1];
+    uint32_t nacc = *st.nacc, faults = *st.faults;
+    volatile double sink = 0.0;
+    for (uint32_t s = 0; s < nsteps; ++s) {
+        const uint32_t iter = iter0 + s;
+        mvn_build(m, g->rw_sigma, D); /* rand(MvNormal(θ, Σ)) */
+        for (int j = 0; j < D; ++j) z[j] = orc_normal(zt, key0, key1, chain_id, iter, 0, (uint32_t)j, &faults);
+        for (int i = 0; i < D; ++i) {
+            double lz = m->L[(size_t)i * D] * z[0];
+            for (int j = 1; j <= i; ++j) lz = fma(m->L[(size_t)i * D + j], z[j], lz);
+            thp[i] = th[i] + lz;
+        }
+        mvn_build(m, g->t_sigma, D); /* set_parameters!(P°, …): MvNormal(μ, Symmetric(triu(Σ))) */
+        double llp = 0.0;
+        for (uint64_t k = 0; k < g->nobs; ++k) {
+            for (int i = 0; i < D; ++i) r[i] = g->obs[k * D + i] - thp[i];
+            const double c0 = mvnormal_c0(D, logdet_chol(m->L, D));
+            llp = llp + (c0 - sqmahal(m->L, m->iL, r, D, 0) / 2.0);
+        }
+        if (!isfinite(llp)) faults |= 1u;
+        mvn_build(m, g->rw_sigma, D); /* logpdf(MvNormal(θ°, Σ), θ) */
+        for (int i = 0; i < D; ++i) r[i] = th[i] - thp[i];
+        const double ltd_rev = m->c0 - sqmahal(m->L, m->iL, r, D, 0) / 2.0;
+        mvn_build(m, g->rw_sigma, D); /* logpdf(MvNormal(θ, Σ), θ°) */
+        for (int i = 0; i < D; ++i) r[i] = thp[i] - th[i];
+        const double ltd_fwd = m->c0 - sqmahal(m->L, m->iL, r, D, 0) / 2.0;
+        const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + 0.0) - 0.0;
+        const double E = orc_exponential(zt, key0, key1, chain_id, iter, 0, &faults);
+        const int acc = E > -llr;
+        if (hist_prop) memcpy(hist_prop + ((uint64_t)s * C + c) * D, thp, sizeof(double) * D);
+        if (acc) {
+            memcpy(th, thp, sizeof(double) * D);
+            ll = llp;
+            nacc += 1;
+        }
+        mvn_build(m, g->t_sigma, D); /* set_parameters!(::Previous): P rebuilt (dead work, kept) */
+        sink = sink + m->L[(size_t)D * D - 1];
+        if (hist_theta) memcpy(hist_theta + ((uint64_t)s * C + c) * D, th, sizeof(double) * D);
+        if (hist_ll) hist_ll[(uint64_t)s * C + c] = ll;
+        if (hist_acc) hist_acc[(uint64_t)s * C + c] = (uint8_t)acc;
+        const uint64_t N = N0 + s;
+        int outside = 0;
+        if (iter > W) {
+            uint32_t j = (iter - W) & 127u;
+            outside = (int)((((j & 64u) ? ring1 : ring0) >> (j & 63u)) & 1u);
+        }
+        const uint64_t mn = N < (uint64_t)W ? N : (uint64_t)W;
+        ra = (ra * (double)W + (double)(acc - outside)) / (double)mn;
+        {
+            uint32_t j = iter & 127u;
+            uint64_t bit = 1ull << (j & 63u);
+            if (j & 64u) ring1 = acc ? (ring1 | bit) : (ring1 & ~bit);
+            else ring0 = acc ? (ring0 | bit) : (ring0 & ~bit);
+        }
+    }
+    memcpy(st.theta, th, sizeof(double) * D);
+    *st.ll = ll;
+    *st.ra = ra;
+    st.ring[0] = ring0;
+    st.ring[1] = ring1;
+    *st.nacc = nacc;
+    *st.faults = faults;
+    free(m);
+}
+
 static void run_chain(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t key1, uint32_t chain_id,
                       const uint32_t *iters, uint32_t iter0, uint32_t nsteps, uint64_t N0, uint32_t W,
                       uint64_t C, uint64_t c, double *hist_theta, double *hist_prop, double *hist_ll,
@@ -235,6 +332,11 @@ static void run_chain(const orc_gsn *g, orc_chain st, uint32_t key0, uint32_t ke
     uint64_t ring0 = st.ring[0], ring1 = st.ring[1];
     uint32_t nacc = *st.nacc, faults = *st.faults;
 
+    if (g->faithful) {
+        run_chain_faithful(g, st, key0, key1, chain_id, iter0, nsteps, N0, W, C, c, hist_theta, hist_prop, hist_ll,
+                           hist_acc);
+        return;
+    }
     for (uint32_t s = 0; s < nsteps; ++s) {
         const uint32_t iter = iters ? iters[s] : iter0 + s;
         /* proposal!  θ° = θ + L z  (random_walk.jl:147: rand(MvNormal(θ, Σ))) */

@@ -1,12 +1,13 @@
 """Multi-process chain sharding on CPU (torch.distributed gloo, world_size 2).
 
 The N>1 path of bench.py/extensible_mcmc shards chains by global id with no
-data-path collective and all-reduces the cross-chain diagnostics once.  Here
-each rank advances its shard with the oracle (the GPU engine is exercised by
-the gpu tests), reduces its shard's split-chain moments and all-reduces them
-through extensible_mcmc.diagnostics.allreduce_sums; the result must equal the
-single-process reduction, and per-chain states must equal the unsharded run
-(RNG keyed by global chain id)."""
+data-path collective and all-gathers the cross-chain diagnostics once.  Here
+each rank advances its shard with the oracle (no GPU in this container; the
+engine's shards are exercised by tests/test_gpu_cfg5.py), reduces its shard's
+split-chain moments and all-gathers them through
+extensible_mcmc.diagnostics.allgather_moments (Chan merge in rank order); the
+result must equal the single-process reduction, and per-chain states must equal
+the unsharded run (RNG keyed by global chain id)."""
 import os
 import socket
 import sys
@@ -19,16 +20,17 @@ ROOT = Path(__file__).resolve().parent.parent
 
 
 def shard_moments(hist_theta, split=True):
-    """Per-(half-)chain mean/var over the window, summed over chains — the
+    """Per-(half-)chain mean/var over the window, reduced over chains — the
     host restatement of chain_moments_kernel + moments_reduce_kernel."""
+    from extensible_mcmc import diagnostics as DG
+
     S, C, D = hist_theta.shape
     halves = 2 if split else 1
     ln = S // halves
     parts = [hist_theta[h * ln:(h + 1) * ln] for h in range(halves)]
     means = np.concatenate([p.mean(axis=0) for p in parts])  # [halves*C][D]
     vars_ = np.concatenate([p.var(axis=0, ddof=1) for p in parts])
-    return {"sum_mean": means.sum(0), "sum_mean_sq": (means * means).sum(0), "sum_var": vars_.sum(0),
-            "num_chains": C * halves, "num_draws": ln, "accepted": 0, "proposed": 0}
+    return DG.from_chain_moments(means, vars_, ln)
 
 
 def _free_port():
@@ -58,7 +60,7 @@ def _worker(rank, world, port, out_dir):
     m = shard_moments(h["theta"][20:])
     m["accepted"] = int(h["acc"][20:].sum())
     m["proposed"] = int(h["acc"][20:].size)
-    tot = DG.allreduce_sums(m, w.D)
+    tot = DG.allgather_moments(m, w.D)
     np.save(os.path.join(out_dir, f"theta_{rank}.npy"), st.theta)
     if rank == 0:
         np.save(os.path.join(out_dir, "reduced.npy"), DG.pack(tot))
@@ -83,9 +85,27 @@ def test_two_rank_sharding_and_diagnostics(tmp_path, oracle):
     ref = shard_moments(h["theta"][20:])
     ref["accepted"], ref["proposed"] = int(h["acc"][20:].sum()), int(h["acc"][20:].size)
     got = DG.unpack(np.load(tmp_path / "reduced.npy"), w.D, ref["num_draws"])
-    for k in ("sum_mean", "sum_mean_sq", "sum_var"):
+    for k in ("mean", "sum_var"):
         np.testing.assert_allclose(got[k], ref[k], rtol=1e-12)
+    np.testing.assert_allclose(got["m2"], ref["m2"], rtol=1e-10)
     assert got["num_chains"] == ref["num_chains"] and got["accepted"] == ref["accepted"]
-    r_got, r_ref = DG.rhat_from_sums(got), DG.rhat_from_sums(ref)
+    r_got, r_ref = DG.rhat_from_moments(got), DG.rhat_from_moments(ref)
     np.testing.assert_allclose(r_got["rhat"], r_ref["rhat"], rtol=1e-10)
     assert r_got["accept_rate"] == r_ref["accept_rate"]
+
+
+def test_chan_merge_does_not_cancel():
+    """1M chain means at 1e8 ± 1e-3: Σm² − (Σm)²/m loses every digit of M2, the
+    Chan merge of 8 shards keeps it (the cfg 5 shape)."""
+    from extensible_mcmc import diagnostics as DG
+
+    rng = np.random.default_rng(5)
+    means = 1e8 + 1e-3 * rng.standard_normal((1 << 20, 2))
+    vars_ = np.ones_like(means)
+    exact = ((means - means.mean(0)) ** 2).sum(0)
+    shards = [DG.from_chain_moments(m, v, 100) for m, v in zip(np.split(means, 8), np.split(vars_, 8))]
+    got = DG.merge(shards)
+    np.testing.assert_allclose(got["m2"], exact, rtol=1e-5)
+    naive = (means * means).sum(0) - means.sum(0) ** 2 / means.shape[0]
+    assert np.all(np.abs(naive - exact) > 1e3 * np.abs(got["m2"] - exact))
+    assert got["num_chains"] == 1 << 20

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from extensible_mcmc import _lib as L
-from extensible_mcmc import rhat_from_sums
+from extensible_mcmc import rhat_from_moments
 from extensible_mcmc import workloads as W
 
 from helpers import run_engine
@@ -59,7 +59,7 @@ def test_posterior_matches_analytic(require_gpu):
     e = run_engine(w, 8192, 4000, fetch=False)
     eng = e["engine"]
     m = eng.moments_window(2001, 2000, split=True)
-    r = rhat_from_sums(m)
+    r = rhat_from_moments(m)
     xbar = w.obs.mean(axis=0)
     assert np.abs(r["mean"] - xbar).max() < 0.01
     post_var = r["W"] + r["B"] / m["num_draws"]

@@ -231,3 +231,21 @@ def test_log_1_2_table_driven(oracle):
     assert np.all(err[far] <= 1.5 * np.spacing(ref[far]))
     assert np.all(err <= 2.0 ** -60 + 1.5 * np.spacing(ref))
     assert oracle.log_1_2_vec(np.array([1.0]))[0] == 0.0 or abs(oracle.log_1_2_vec(np.array([1.0]))[0]) < 2 ** -60
+
+
+def test_faithful_refactor_variant_has_the_same_bits(oracle):
+    """The CPU baseline's "faithful" variant (a Cholesky per MvNormal construction,
+    random_walk.jl:147,167, gsn_target.jl:20) gives the factor-once path's bits."""
+    from extensible_mcmc import workloads as W
+
+    w = W.cfg2(64, D=32)
+    runs = []
+    for mode in (0, 0x200):
+        st = oracle.OracleState(np.zeros((64, w.D)))
+        h = oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=60,
+                           ll_mode=mode)
+        runs.append((st, h))
+    (a, ha), (b, hb) = runs
+    assert np.array_equal(a.theta, b.theta) and np.array_equal(a.ll, b.ll) and np.array_equal(a.ra, b.ra)
+    for k in ("theta", "prop", "ll", "acc"):
+        assert np.array_equal(ha[k], hb[k]), k

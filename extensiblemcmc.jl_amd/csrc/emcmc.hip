@@ -106,6 +106,10 @@ struct UpdateHost {
     std::vector<double> sigma_b, LB, invdiagB;
     double c0B = 0.0, lam = 0.0;
     emcmc_haario_adaptation haario{};
+    // prior (priors.jl) per local coordinate: family, parameters, host constant; factor starts
+    std::vector<uint32_t> pfam;
+    std::vector<double> pa, pb, pc;
+    uint32_t pstart = 0;
 };
 
 struct TargetHost {
@@ -153,6 +157,7 @@ struct emcmc_handle {
     // host-mapped pinned memory, so emcmc_synchronize reads 4 B after the stream
     // drains instead of copying and scanning C fault words
     uint32_t *h_fault_flag = nullptr, *d_fault_flag = nullptr;
+    double *d_ll_prop = nullptr;  // [P][C] sub_ws°.ll of each update's latest proposal
     double *d_hist_theta = nullptr, *d_hist_prop = nullptr, *d_hist_ll = nullptr;
     uint8_t *d_hist_acc = nullptr;
     double *d_consts = nullptr, *d_obs = nullptr;
@@ -292,6 +297,7 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
     HIPCHK(h, hipMalloc(&h->d_mu_p, C * D * sizeof(double)));
     HIPCHK(h, hipMalloc(&h->d_aprop, P * C * sizeof(uint32_t)));
     HIPCHK(h, hipMalloc(&h->d_aacc, P * C * sizeof(uint32_t)));
+    HIPCHK(h, hipMalloc(&h->d_ll_prop, P * C * sizeof(double)));
     HIPCHK(h, hipMalloc(&h->d_eps, P * kMwgMaxD * C * sizeof(double)));
     HIPCHK(h, hipMalloc(&h->d_steps, M * P * 4 * sizeof(uint32_t)));
     {
@@ -345,12 +351,19 @@ emcmc_status select_mwg(emcmc_handle *h) {
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     const int ll = (int)h->target.ll_mode;
     Variant v;
-    for (const auto &e : mwg_table())
-        if (e.D == D) v.mfn = full ? (ll == LL_PER_OBS ? e.full_perobs : e.full_suff)
-                                   : (ll == LL_PER_OBS ? e.acc_perobs : e.acc_suff);
+    size_t nmax = 1;  // largest update: the wide kernel's local vector length
+    for (const auto &u : h->updates) nmax = std::max(nmax, u.coords.size());
+    int best_nu = 1 << 30;
+    for (const auto &e : mwg_table()) {
+        if (e.D != D) continue;
+        if (e.nu != 0 && ((size_t)e.nu < nmax || e.nu >= best_nu)) continue;  // smallest NU that fits
+        if (e.nu != 0) best_nu = e.nu;
+        v.mfn = full ? (ll == LL_PER_OBS ? e.full_perobs : e.full_suff)
+                     : (ll == LL_PER_OBS ? e.acc_perobs : e.acc_suff);
+    }
     if (!v.mfn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                    "no general-schedule device kernel for D=%d (instantiated: D ∈ {1,2,3,4,8,16})", D);
+                    "no general-schedule device kernel for D=%d (instantiated: D ∈ {1,2,3,4,8,16,32})", D);
     std::vector<MwgUpdate> tab(h->updates.size());
     for (size_t p = 0; p < h->updates.size(); ++p) {
         const UpdateHost &u = h->updates[p];
@@ -380,6 +393,14 @@ emcmc_status select_mwg(emcmc_handle *h) {
             m.diag = u.diag ? 1u : 0u;
             for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1u << j) : 0u;
         }
+        m.prior = u.prior;
+        m.pstart = u.pstart;
+        for (size_t j = 0; j < u.pfam.size(); ++j) {
+            m.pfam[j] = u.pfam[j];
+            m.pa[j] = u.pa[j];
+            m.pb[j] = u.pb[j];
+            m.pc[j] = u.pc[j];
+        }
     }
     if (h->d_mwg) (void)hipFree(h->d_mwg);
     HIPCHK(h, hipMalloc(&h->d_mwg, tab.size() * sizeof(MwgUpdate)));
@@ -397,8 +418,12 @@ emcmc_status select_mwg(emcmc_handle *h) {
         (st = upload(h->d_obs, t.obs)))
         return st;
     char nm[160];
-    snprintf(nm, sizeof nm, "mwg_gsn_kernel<D=%d,P=%zu,%s,%s>", D, h->updates.size(), full ? "FULL" : "ACCEPT_ONLY",
-             ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
+    if (best_nu < (1 << 30))
+        snprintf(nm, sizeof nm, "mwg_wide_kernel<D=%d,NU=%d,P=%zu,%s,%s>", D, best_nu, h->updates.size(),
+                 full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
+    else
+        snprintf(nm, sizeof nm, "mwg_gsn_kernel<D=%d,P=%zu,%s,%s>", D, h->updates.size(),
+                 full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
     v.name = nm;
     h->lds_bytes = 0;  // tables only, in static LDS
     h->var = v;
@@ -408,8 +433,9 @@ emcmc_status select_mwg(emcmc_handle *h) {
 bool fused_eligible(const emcmc_handle *h) {
     if (!joint_all_coords(h) || h->cfg.chain_moments) return false;
     const UpdateHost &u = h->updates[0];
+    if (u.prior != EMCMC_PRIOR_IMPROPER) return false;  // priors and proposal! resampling: general kernel
     for (uint8_t f : u.pos)
-        if (f) return false;  // positivity-restricted coordinates: general schedule kernel (D ≤ 16)
+        if (f) return false;  // positivity-restricted coordinates: general schedule kernel (D ≤ 32)
     return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
 }
 
@@ -526,6 +552,9 @@ emcmc_status select_variant(emcmc_handle *h) {
     if (!fused_eligible(h)) return select_mwg(h);
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
+    // a correlated Σ (proposal or target) beyond the fused dense kernel's D ≤ 8
+    // runs on the general kernel: forward substitutions from the factors, D ≤ 32
+    if (!(u.diag && h->target.diag) && D > 8) return select_mwg(h);
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     const int ll = (int)h->target.ll_mode;
     const bool diag = u.diag && h->target.diag;
@@ -713,6 +742,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
     p.fault_flag = h->d_fault_flag;
+    p.ll_prop = h->d_ll_prop;
     p.mom_theta = h->d_mom_scratch;
     p.LB = h->d_LB;
     p.iLB = h->d_iLB;
@@ -847,6 +877,7 @@ emcmc_status run_mala(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
     p.fault_flag = h->d_fault_flag;
+    p.ll_prop = h->d_ll_prop;
     p.hist_theta = h->d_hist_theta;
     p.hist_prop = h->d_hist_prop;
     p.hist_ll = h->d_hist_ll;
@@ -945,6 +976,7 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.eps = h->d_eps;
     a.faults = h->d_faults;
     a.fault_flag = h->d_fault_flag;
+    a.ll_prop = h->d_ll_prop;
     a.hist_theta = h->d_hist_theta;
     a.hist_prop = h->d_hist_prop;
     a.hist_ll = h->d_hist_ll;
@@ -1074,8 +1106,11 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN_MIX &&
         u->kernel != EMCMC_MALA)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "transition kernel %u has no device plugin yet", u->kernel);
-    if (u->prior != EMCMC_PRIOR_IMPROPER)
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin yet", u->prior);
+    if (u->prior > EMCMC_PRIOR_STANDARD)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin", u->prior);
+    if (u->prior != EMCMC_PRIOR_IMPROPER && (u->kernel == EMCMC_RW_GAUSSIAN_MIX || u->kernel == EMCMC_MALA))
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "priors other than ImproperPrior run on device with Gaussian/Uniform random walks only");
     if (u->adaptation != EMCMC_ADPT_NONE &&
         !(u->adaptation == EMCMC_ADPT_UNIF_RW && u->kernel == EMCMC_RW_UNIFORM) &&
         !(u->adaptation == EMCMC_ADPT_HAARIO && u->kernel == EMCMC_RW_GAUSSIAN_MIX))
@@ -1097,6 +1132,49 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     uh.adaptation = u->adaptation;
     uh.coords.assign(u->coords, u->coords + u->num_coords);
     uh.pos = pos;
+    if (u->prior == EMCMC_PRIOR_PRODUCT || u->prior == EMCMC_PRIOR_STANDARD) {
+        // priors.jl:35-88 over the update's local coordinates; constants as the
+        // Distributions/StatsFuns forms need them (see emcmc_mwg.h univariate_logpdf)
+        const emcmc_prior_desc *pd = u->prior_params;
+        if (!pd || !pd->factors || pd->num_factors == 0)
+            return fail(h, EMCMC_INVALID_ARG, "ProductPrior/StandardPrior needs prior_params factors");
+        uint32_t j = 0;
+        for (uint32_t f = 0; f < pd->num_factors; ++f) {
+            const emcmc_prior_factor &fa = pd->factors[f];
+            if (fa.count == 0 || j + fa.count > u->num_coords)
+                return fail(h, EMCMC_INVALID_ARG, "prior factor counts must sum to num_coords");
+            double a = fa.a, b = fa.b, c = 0.0;
+            switch (fa.family) {
+            case EMCMC_DIST_NORMAL:
+                if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Normal prior: σ must be > 0");
+                c = log_pos(b);
+                break;
+            case EMCMC_DIST_UNIFORM:
+                if (!(a < b)) return fail(h, EMCMC_INVALID_ARG, "Uniform prior: a < b");
+                c = -log_pos(b - a);
+                break;
+            case EMCMC_DIST_EXPONENTIAL:
+                if (!(a > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Exponential prior: θ must be > 0");
+                b = 1.0 / a;
+                c = log_pos(b);
+                break;
+            case EMCMC_DIST_GAMMA:
+                if (!(a > 0.0 && b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Gamma prior: α, θ must be > 0");
+                c = (-std::lgamma(a)) - a * log_pos(b);
+                break;
+            default:
+                return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior family %u has no device plugin", fa.family);
+            }
+            if (u->prior == EMCMC_PRIOR_PRODUCT && j > 0) uh.pstart |= 1u << j;
+            for (uint32_t k = 0; k < fa.count; ++k, ++j) {
+                uh.pfam.push_back(fa.family);
+                uh.pa.push_back(a);
+                uh.pb.push_back(b);
+                uh.pc.push_back(c);
+            }
+        }
+        if (j != u->num_coords) return fail(h, EMCMC_INVALID_ARG, "prior factor counts must sum to num_coords");
+    }
     const int n = (int)u->num_coords;
     if (u->kernel == EMCMC_RW_GAUSSIAN || u->kernel == EMCMC_RW_GAUSSIAN_MIX) {
         if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");
@@ -1229,6 +1307,7 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
     HIPCHK(h, hipMemsetAsync(h->d_faults, 0, C * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_aprop, 0, P * C * sizeof(uint32_t), h->stream));
     HIPCHK(h, hipMemsetAsync(h->d_aacc, 0, P * C * sizeof(uint32_t), h->stream));
+    HIPCHK(h, hipMemsetAsync(h->d_ll_prop, 0xFF, P * C * sizeof(double), h->stream));  // NaN until an update runs
     {  // per-chain ϵ of every update starts at the update's ϵ
         std::vector<double> e(P * kMwgMaxD * C, 0.0);
         for (uint64_t q = 0; q < P; ++q)
@@ -1300,6 +1379,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     p.nacc = h->d_nacc;
     p.faults = h->d_faults;
     p.fault_flag = h->d_fault_flag;
+    p.ll_prop = h->d_ll_prop;
     p.hist_theta = h->d_hist_theta;
     p.hist_prop = h->d_hist_prop;
     p.hist_ll = h->d_hist_ll;
@@ -1398,7 +1478,8 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_scratch,   h->d_gather,    h->d_zig,     h->d_mu_p,     h->d_eps,   h->d_tL,
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
-                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts};
+                    h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts,
+                    h->d_ll_prop};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->h_fault_flag) (void)hipHostFree(h->h_fault_flag);
@@ -1512,6 +1593,15 @@ emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults) {
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(faults, h->d_faults, h->cfg.num_chains * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_proposal_ll(emcmc_handle *h, double *ll_prop) {
+    if (!h || !ll_prop) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(ll_prop, h->d_ll_prop, h->updates.size() * h->cfg.num_chains * sizeof(double),
+                        hipMemcpyDeviceToHost));
     return EMCMC_OK;
 }
 

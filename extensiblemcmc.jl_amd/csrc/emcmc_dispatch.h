@@ -34,6 +34,7 @@ const std::vector<Entry> &diag_table();
 // general schedule kernel (mwg_gsn_kernel)
 struct MwgEntry {
     int D;
+    int nu;  // 0: mwg_gsn_kernel<D> (registers, D ≤ 16); else mwg_wide_kernel<D, nu>
     MwgFn full_perobs, full_suff, acc_perobs, acc_suff;
 };
 const std::vector<MwgEntry> &mwg_table();

@@ -43,6 +43,7 @@ struct StepParams {
     uint32_t *nacc;    // [C] accepted proposals
     uint32_t *faults;  // [C]
     uint32_t *fault_flag;  // set to 1 by any lane that ends a launch with a fault bit (emcmc_synchronize)
+    double *ll_prop;       // [C] sub_ws°.ll: log-likelihood of the launch's last proposal (update pidx0)
     // history streams (FULL mode), slot = (mcmciter-1)*P + pidx0
     double *hist_theta;  // [M*P][C][D]
     double *hist_prop;   // [M*P][C][D]
@@ -756,6 +757,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)
 #pragma unroll
         for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
+        if (s + 1 == a.nsteps && sub == 0) chain_elem(a.ll_prop, c32) = llp;  // sub_ws°.ll after the launch
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {
@@ -882,6 +884,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
         if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
 #pragma unroll
         for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        if (s + 1 == a.nsteps) a.ll_prop[chain] = llp;
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {

@@ -42,6 +42,7 @@ struct MalaParams {
     uint32_t *nacc;  // [C]
     uint32_t *faults;
     uint32_t *fault_flag;
+    double *ll_prop;  // [C] sub_ws°.ll
     double *hist_theta, *hist_prop, *hist_ll;
     uint8_t *hist_acc;
     const Ziggurat *zig;  // global memory (a few draws per lane per step)
@@ -265,6 +266,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
     }
     if (valid && g == 0) {
         const double lln = acc ? llp : ll;
+        a.ll_prop[chain] = llp;
         a.ll[chain] = lln;
         if constexpr (FULL) __builtin_nontemporal_store(lln, a.hist_ll + slot * C + chain);
         uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];

@@ -49,6 +49,7 @@ struct MixParams {
     uint32_t *nacc;  // [C]
     uint32_t *faults;
     uint32_t *fault_flag;
+    double *ll_prop;  // [C] sub_ws°.ll after the launch
     double *mom_theta;  // ACCEPT_ONLY: θ after each step of the launch, [nsteps] slots (state_pos)
     const double *LB;   // [DP] packed lower, state_pos(q, c, C, DP)
     const double *iLB;  // [D][C]
@@ -282,6 +283,7 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
         if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
 #pragma unroll
         for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        if (s + 1 == a.nsteps) a.ll_prop[chain] = llp;
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {

@@ -28,13 +28,28 @@
 //                       (0.0 when (iter−1, p) did not run)   chain_statistics.jl:42-66
 //   AdaptationUnifRW    register on own turn, readjust at k proposals
 //                                                   run.jl:136-178, adaptation.jl:273-329
+//   proposal! resample  θ° is drawn again while logpdf(prior, θ°) === −Inf
+//                       (resample r uses counter blocks (r << 16) | j/2; capped at
+//                       kMaxResample with fault bit 8)                  updates.jl:191-196
+//   log_prior           logpdf(prior, θ_local) of ImproperPrior, ImproperPosPrior,
+//                       StandardPrior / ProductPrior of univariate Normal, Uniform,
+//                       Exponential, Gamma factors; llr adds lp(θ°) − lp(θ)
+//                                                   priors.jl:18-88, run.jl:374-385
+//   loglikelihood       a target policy: GsnTargetLaw (gsn_target.jl:23-29) or a
+//                       user device function compiled at run time (emcmc_user.h)
 #pragma once
 
 #include "emcmc_kernels.h"
 
 namespace emcmc {
 
-constexpr int kMwgMaxD = 16;
+constexpr int kMwgMaxD = 32;
+constexpr uint32_t kMaxResample = 0xFFFEu;          // proposal! resamples before fault bit 8
+constexpr uint32_t kFaultPriorResample = 8u;       // EMCMC_FAULT_PRIOR_RESAMPLES
+
+// prior kinds / univariate families (include/emcmc.h EMCMC_PRIOR_*, EMCMC_DIST_*)
+constexpr uint32_t kPriorImproper = 0u, kPriorImproperPos = 1u, kPriorProduct = 2u, kPriorStandard = 3u;
+constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, kDistGamma = 4u;
 
 // One RandomWalkUpdate, host-built; read with scalar (uniform) loads.
 struct MwgUpdate {
@@ -49,6 +64,12 @@ struct MwgUpdate {
     double c0;                      // −(nc·log2π + logdet Σ)/2
     uint32_t diag, posmask;          // posmask bit j: coordinate j positivity-restricted
     double target, scale, amin, amax, offset;  // AdaptationUnifRW (scalar form)
+    // prior over the update's local coordinates (priors.jl): kind, and for
+    // Product/Standard priors one univariate family per coordinate, with
+    // bit j of pstart set where coordinate j starts a new ProductPrior factor
+    uint32_t prior, pstart;
+    uint32_t pfam[kMwgMaxD];
+    double pa[kMwgMaxD], pb[kMwgMaxD], pc[kMwgMaxD];  // family parameters + host-computed constants
 };
 
 struct MwgParams {
@@ -63,6 +84,8 @@ struct MwgParams {
     double *eps;       // [P][kMwgMaxD][C]  per-chain ϵ of adaptive updates
     uint32_t *faults;  // [C]
     uint32_t *fault_flag;
+    double *ll_prop;   // [P][C] sub_ws°.ll: log-likelihood of the update's latest proposal
+    const double *user_params;  // user target: opaque parameters (emcmc_target_desc.user_params)
     double *hist_theta, *hist_prop, *hist_ll;
     uint8_t *hist_acc;
     const Ziggurat *zig;
@@ -79,16 +102,75 @@ struct MwgParams {
     double t_c0, n_tc0, S_c, nobs_d;
 };
 
+// log of any real: NaN below 0 (Julia's log throws DomainError there), −Inf at 0
+__device__ __forceinline__ double log_real(double x) { return (x < 0.0) ? __builtin_nan("") : log_any(x); }
+
+// logpdf of one univariate prior factor at x (Distributions.jl / StatsFuns
+// forms; a, b the parameters, c a constant computed once on the host):
+//   Normal(μ=a, σ=b), c = log σ:      −(z² + log2π)/2 − c, z = (x − μ)/σ
+//   Uniform(a, b), c = −log(b − a):   c on [a, b], else −Inf
+//   Exponential(θ), b = 1/θ, c = log(1/θ):   x < 0 ? −Inf : c − b·x
+//   Gamma(α=a, θ=b), c = −lgamma(α) − α·log θ:  x < 0 ? −Inf : (c + (α − 1)·log x) − x/θ
+__device__ __forceinline__ double univariate_logpdf(uint32_t fam, double a, double b, double c, double x) {
+    if (fam == kDistNormal) {
+        const double z = (x - a) / b;
+        return -(z * z + kLog2Pi) / 2.0 - c;
+    }
+    if (fam == kDistUniform) return (x >= a && x <= b) ? c : -__builtin_inf();
+    if (fam == kDistExponential) return (x < 0.0) ? -__builtin_inf() : c - b * x;
+    // Gamma
+    return (x < 0.0) ? -__builtin_inf() : (c + (a - 1.0) * log_real(x)) - x / b;
+}
+
+// logpdf(prior, θ_local) (priors.jl:18-88) over the first n of D local entries.
+//   ImproperPrior: 0.0.  ImproperPosPrior: −sum(log.(θ)), the sum folded left
+//   from θ_1.  ProductPrior: lp = 0.0; lp += logpdf(factor) in order, each
+//   factor's own coordinates folded left.  StandardPrior of a product of
+//   univariates: the left fold alone.
+template <int D, bool ROLL = false>
+__device__ __forceinline__ double mwg_log_prior(const MwgUpdate &u, uint32_t n, const double (&x)[D]) {
+    constexpr int UJ = ROLL ? 1 : D;
+    if (u.prior == kPriorImproper) return 0.0;
+    if (u.prior == kPriorImproperPos) {
+        double s = 0.0;
+#pragma unroll UJ
+        for (int j = 0; j < D; ++j) {
+            if ((uint32_t)j < n) {
+                const double v = log_real(x[j]);
+                s = (j == 0) ? v : s + v;
+            }
+        }
+        return -s;
+    }
+    double lp = 0.0, s = 0.0;
+#pragma unroll UJ
+    for (int j = 0; j < D; ++j) {
+        if ((uint32_t)j < n) {
+            const double v = univariate_logpdf(u.pfam[j], u.pa[j], u.pb[j], u.pc[j], x[j]);
+            if (j == 0) {
+                s = v;
+            } else if ((u.pstart >> j) & 1u) {
+                lp = lp + s;
+                s = v;
+            } else {
+                s = s + v;
+            }
+        }
+    }
+    return (u.prior == kPriorProduct) ? lp + s : s;
+}
+
 // ‖L⁻¹ r‖² for a D-vector (target Σ; dense forward substitution unless
 // diagonal), canonical order (SumShape<D>).
-template <int D>
+template <int D, bool ROLL = false>
 __device__ __forceinline__ double mwg_sqmahal_t(const MwgParams &a, const double (&r)[D]) {
+    constexpr int UJ = ROLL ? 1 : D;
     double y[D];
-#pragma unroll
+#pragma unroll UJ
     for (int i = 0; i < D; ++i) {
         double acc = r[i];
         if (!a.tdiag) {
-#pragma unroll
+#pragma unroll UJ
             for (int j = 0; j < i; ++j) acc = fma(-a.Lt[i * D + j], y[j], acc);
         }
         y[i] = acc * a.iLt[i];
@@ -98,15 +180,16 @@ __device__ __forceinline__ double mwg_sqmahal_t(const MwgParams &a, const double
 
 // ‖L⁻¹ r‖² over the first n of D local entries (the update's Σ), canonical
 // order of an n-vector: blocks of 8 when n % 8 == 0 and n ≥ 16, else one block.
-template <int D>
+template <int D, bool ROLL = false>
 __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, const double (&r)[D]) {
+    constexpr int UJ = ROLL ? 1 : D;
     double y[D];
-#pragma unroll
+#pragma unroll UJ
     for (int i = 0; i < D; ++i) {
         if ((uint32_t)i < n) {
             double acc = r[i];
             if (!u.diag) {
-#pragma unroll
+#pragma unroll UJ
                 for (int j = 0; j < i; ++j) acc = fma(-u.L[i * kMwgMaxD + j], y[j], acc);
             }
             y[i] = acc * u.iL[i];
@@ -117,24 +200,276 @@ __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, 
     const bool blocks = (n % 8 == 0 && n >= 16);
     if (!blocks) {
         double s = y[0] * y[0];
-#pragma unroll
+#pragma unroll UJ
         for (int i = 1; i < D; ++i)
             if ((uint32_t)i < n) s = fma(y[i], y[i], s);
         return s;
     }
-    // n = 16 (D = 16): two blocks of 8, one pairwise add
-    double b0 = y[0] * y[0], b1 = y[8 % D] * y[8 % D];
-#pragma unroll
-    for (int i = 1; i < 8 && i < D; ++i) b0 = fma(y[i], y[i], b0);
-#pragma unroll
-    for (int i = 9; i < 16 && i < D; ++i) b1 = fma(y[i], y[i], b1);
-    return b0 + b1;
+    // n ∈ {16, 24, 32}: blocks of 8, pairwise tree over the n/8 blocks
+    constexpr int NBMAX = D / 8 > 0 ? D / 8 : 1;
+    double b[NBMAX];
+#pragma unroll UJ
+    for (int k = 0; k < NBMAX; ++k) {
+        b[k] = y[8 * k] * y[8 * k];
+#pragma unroll UJ
+        for (int i = 1; i < 8; ++i) b[k] = fma(y[8 * k + i], y[8 * k + i], b[k]);
+    }
+    const uint32_t nb = n / 8;
+    if (nb == 2) return b[0] + b[1 % NBMAX];
+    if (nb == 3) return (b[0] + b[1 % NBMAX]) + b[2 % NBMAX];
+    return (b[0] + b[1 % NBMAX]) + (b[2 % NBMAX] + b[3 % NBMAX]);
 }
 
-template <int D, bool FULL, int LLMODE>
+// The built-in target: loglikelihood(P°::GsnTargetLaw, obs) (gsn_target.jl:23-29),
+// per observation or through the sufficient statistics.
+struct GsnTarget {
+    template <int D, int LLMODE, bool ROLL = false>
+    __device__ __forceinline__ static double loglik(const MwgParams &a, const double (&mp)[D]) {
+        constexpr int UJ = ROLL ? 1 : D;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            double llp = 0.0;
+            for (uint32_t k = 0; k < a.nobs; ++k) {
+                double r[D];
+#pragma unroll UJ
+                for (int i = 0; i < D; ++i) r[i] = a.obs[(size_t)k * D + i] - mp[i];
+                llp = llp + (a.t_c0 - mwg_sqmahal_t<D, ROLL>(a, r) / 2.0);
+            }
+            return llp;
+        } else {
+            double r[D];
+#pragma unroll UJ
+            for (int i = 0; i < D; ++i) r[i] = a.xbar[i] - mp[i];
+            const double qv = mwg_sqmahal_t<D, ROLL>(a, r);
+            return a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+    }
+};
+
+// ---- one update step on the update's local coordinates (shared by both kernels)
+// proposal! with resampling, log_transition_density both ways, and the two
+// log-priors of the MH ratio.  tl: θ_local in (pos Gaussian: left as the
+// reference's in-place round trips leave it); tp: θ° (proposal history, P°);
+// ta: θ° as set_chain_param! copies it on accept.
+template <int NU, bool ROLL = false>
+__device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs &zt, const MwgUpdate &u, uint32_t n,
+                                               uint64_t chain, uint32_t gid, uint32_t iter, uint32_t p,
+                                               double (&tl)[NU], double (&tp)[NU], double (&ta)[NU], double &ltd_fwd,
+                                               double &ltd_rev, double &lpp, double &lpc, uint32_t &faults) {
+    constexpr int UJ = ROLL ? 1 : NU;
+    const uint64_t C = a.C;
+    double t3[NU];  // θ as log_prior(::Previous) sees it (pos GaussianRandomWalk: after the round trips)
+    // ---- proposal!: draw θ°; draw again while logpdf(prior, θ°) === −Inf
+    // (updates.jl:191-196).  Resample r reads counter blocks (r << 16) | j/2.
+    ltd_fwd = 0.0;
+    ltd_rev = 0.0;
+    double ev[NU];  // UniformRandomWalk ϵ of each local coordinate
+    const uint32_t pm = u.posmask;  // positivity-restricted coordinates
+    auto isp = [&](int i) { return ((pm >> i) & 1u) != 0u; };
+    for (uint32_t rs = 0;; ++rs) {
+        if (u.kind == 1) {  // UniformRandomWalk: θ° = θ·1 + U, or θ·e^U where pos
+#pragma unroll UJ
+            for (int j = 0; j < NU; j += 2) {
+                if ((uint32_t)j < n) {
+                    const u32x4 r = draw(a.key0, a.key1, gid, iter, (rs << 16) | ((uint32_t)j >> 1), p, 0);
+                    const double e0 = u.adapt ? a.eps[((uint64_t)p * kMwgMaxD + j) * C + chain] : u.eps0[j];
+                    const double U0 = (-e0) + (e0 - (-e0)) * u01_closed0(r.x, r.y);
+                    tp[j] = isp(j) ? tl[j] * exp_any(U0) + copysign(0.0, U0) : tl[j] * 1.0 + U0;
+                    ev[j] = e0;
+                    if (j + 1 < NU && (uint32_t)(j + 1) < n) {
+                        const double e1 =
+                            u.adapt ? a.eps[((uint64_t)p * kMwgMaxD + j + 1) * C + chain] : u.eps0[j + 1];
+                        const double U1 = (-e1) + (e1 - (-e1)) * u01_closed0(r.z, r.w);
+                        tp[j + 1] = isp(j + 1) ? tl[j + 1] * exp_any(U1) + copysign(0.0, U1) : tl[j + 1] * 1.0 + U1;
+                        ev[j + 1] = e1;
+                    }
+                }
+            }
+        } else {  // GaussianRandomWalk over the update's coordinates
+            if (rs > 0 && pm != 0u) {  // the previous rand! left θ ← exp(log θ) where pos
+#pragma unroll UJ
+                for (int i = 0; i < NU; ++i)
+                    if ((uint32_t)i < n && isp(i)) tl[i] = exp_any(log_any(tl[i]));
+            }
+            double z[NU];
+#pragma unroll UJ
+            for (int j = 0; j < NU; ++j)
+                z[j] = ((uint32_t)j < n) ? normal_draw(zt, a.key0, a.key1, gid, iter, p, (rs << 17) | (uint32_t)j,
+                                                       faults)
+                                         : 0.0;
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) {
+                if ((uint32_t)i < n) {
+                    double lz;
+                    if (u.diag) {
+                        lz = u.L[i * kMwgMaxD + i] * z[i];
+                    } else {
+                        lz = u.L[i * kMwgMaxD] * z[0];
+#pragma unroll UJ
+                        for (int j = 1; j <= i; ++j) lz = fma(u.L[i * kMwgMaxD + j], z[j], lz);
+                    }
+                    // remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136, 145-147);
+                    // reimpose_constraints!: θ°_i ← exp(θ°_i) (θ°₁)
+                    const double v = (isp(i) ? log_any(tl[i]) : tl[i]) + lz;
+                    tp[i] = isp(i) ? exp_any(v) : v;
+                } else {
+                    tp[i] = 0.0;
+                }
+            }
+        }
+        if (u.prior == kPriorImproper) break;
+        if (!(mwg_log_prior<NU, ROLL>(u, n, tp) == -__builtin_inf())) break;
+        if (rs >= kMaxResample) {
+            faults |= kFaultPriorResample;
+            break;
+        }
+    }
+      // θ as log_prior(::Previous) sees it (pos GaussianRandomWalk: after the round trips)
+    if (u.kind == 1) {
+        if (pm) {  // uniform branch: the mask is the update's
+#pragma unroll UJ
+            for (int j = 0; j < NU; ++j) {
+                if ((uint32_t)j < n) {
+                    const bool pj = isp(j);
+                    const double c = pj ? -log_any(2.0 * ev[j]) : 0.0;
+                    const double f = pj ? c - log_any(tp[j]) : 0.0;  // logpdf(rw, θ, θ°) term
+                    const double g = pj ? c - log_any(tl[j]) : 0.0;  // logpdf(rw, θ°, θ) term
+                    ltd_fwd = (j == 0) ? f : ltd_fwd + f;
+                    ltd_rev = (j == 0) ? g : ltd_rev + g;
+                }
+            }
+        }
+    } else {
+        double r[NU];
+        if (pm == 0u) {
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) r[i] = tp[i] - tl[i];
+            ltd_fwd = u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0;
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) r[i] = tl[i] - tp[i];
+            ltd_rev = u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0;
+        } else {
+            // The reference's in-place round trips, step by step (random_walk.jl:136-171):
+            //   rand:   θ° ← exp(log θ + Lz), θ ← exp(log θ)               (θ°₁, θ₁)
+            //   logpdf(θ°₁, θ₁): logJ = −Σ_pos log θ₁; MvNormal(log θ°₁) at log θ₁;
+            //           then θ°₂ = exp(log θ°₁), θ₂ = exp(log θ₁)
+            //   logpdf(θ₂, θ°₂): logJ = −Σ_pos log θ°₂; MvNormal(log θ₂) at log θ°₂;
+            //           then θ°₃ = exp(log θ°₂) — the value an accept stores — and
+            //           θ₃ = exp(log θ₂), the θ log_prior(::Previous) reads
+            double t1[NU], a1[NU], b1[NU];
+            double lj = 0.0;
+            bool first = true;
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) {
+                if ((uint32_t)i < n) {
+                    t1[i] = isp(i) ? exp_any(log_any(tl[i])) : tl[i];     // θ₁
+                    if (isp(i)) {
+                        const double v = log_any(t1[i]);
+                        lj = first ? v : lj + v;
+                        first = false;
+                    }
+                    a1[i] = isp(i) ? log_any(tp[i]) : tp[i];             // μ = log θ°₁
+                    b1[i] = isp(i) ? log_any(t1[i]) : t1[i];             // x = log θ₁
+                    r[i] = b1[i] - a1[i];
+                } else {
+                    t1[i] = a1[i] = b1[i] = r[i] = 0.0;
+                }
+            }
+            ltd_rev = (u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0) + (-lj);
+            lj = 0.0;
+            first = true;
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) {
+                if ((uint32_t)i < n) {
+                    const double p2 = isp(i) ? exp_any(a1[i]) : a1[i];  // θ°₂
+                    const double l2 = isp(i) ? exp_any(b1[i]) : b1[i];  // θ₂
+                    if (isp(i)) {
+                        const double v = log_any(p2);
+                        lj = first ? v : lj + v;
+                        first = false;
+                    }
+                    const double a2 = isp(i) ? log_any(l2) : l2;        // μ = log θ₂
+                    const double b2 = isp(i) ? log_any(p2) : p2;        // x = log θ°₂
+                    r[i] = b2 - a2;
+                    ta[i] = isp(i) ? exp_any(b2) : p2;                  // θ°₃
+                    t3[i] = isp(i) ? exp_any(a2) : l2;                  // θ₃
+                } else {
+                    r[i] = 0.0;
+                    t3[i] = 0.0;
+                }
+            }
+            ltd_fwd = (u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0) + (-lj);
+        }
+    }
+    if (!(u.kind == 2 && pm != 0u)) {
+#pragma unroll UJ
+        for (int j = 0; j < NU; ++j) ta[j] = tp[j];
+    }
+    lpp = 0.0;
+    lpc = 0.0;
+    if (u.prior != kPriorImproper) {
+        const bool rt = (u.kind == 2 && pm != 0u);  // after the pos round trips: θ°₃, θ₃
+        lpp = mwg_log_prior<NU, ROLL>(u, n, rt ? ta : tp);
+        lpc = mwg_log_prior<NU, ROLL>(u, n, rt ? t3 : tl);
+    }
+}
+
+// ---- accept bits, accept counts, rolling acceptance, AdaptationUnifRW of update p
+__device__ __forceinline__ void mwg_register_step(const MwgParams &a, const MwgUpdate &u, uint32_t n, uint64_t chain,
+                                                  uint32_t iter, uint32_t p, uint32_t s, uint32_t flags, uint64_t slot,
+                                                  bool acc) {
+    const uint64_t C = a.C;
+    const uint64_t pc = (uint64_t)p * C + chain;
+    {
+        const uint64_t m = __ballot(acc);
+        if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
+    }
+    a.nacc[pc] += acc ? 1u : 0u;
+    // update_stats!: rolling acceptance of update p (chain_statistics.jl:51-65)
+    {
+        const uint64_t N = a.N0 + s;
+        uint64_t r0 = a.ring[2 * pc], r1 = a.ring[2 * pc + 1];
+        const double ra_prev = (flags & 1u) ? a.ra[pc] : 0.0;
+        int out = 0;
+        if (iter > a.W) {
+            const uint32_t j = (iter - a.W) & 127u;
+            out = (int)((((j & 64u) ? r1 : r0) >> (j & 63u)) & 1ull);
+        }
+        const uint64_t mn = (N < (uint64_t)a.W) ? N : (uint64_t)a.W;
+        a.ra[pc] = (ra_prev * (double)a.W + (double)((int)acc - out)) / (double)mn;
+        const uint32_t jw = iter & 127u;
+        const uint64_t bit = 1ull << (jw & 63u);
+        if (jw & 64u) r1 = acc ? (r1 | bit) : (r1 & ~bit);
+        else r0 = acc ? (r0 | bit) : (r0 & ~bit);
+        a.ring[2 * pc] = r0;
+        a.ring[2 * pc + 1] = r1;
+    }
+    // update_adaptation!: AdaptationUnifRW on its own turn (run.jl:136-178, adaptation.jl:273-329)
+    if (u.adapt == 1) {
+        const uint32_t pr = a.aprop[pc] + 1, ac = a.aacc[pc] + (acc ? 1u : 0u);
+        if (pr >= u.k) {  // proposed counts are equal across chains: uniform branch
+            const double delta = u.scale / sqrt(fmax(1.0, (double)iter / (double)u.k - u.offset));
+            const double a_r = (double)ac / (double)pr;
+            const double stp = (a_r > u.target) ? delta : -delta;
+            for (uint32_t j = 0; j < n; ++j) {
+                double *ep = a.eps + ((uint64_t)p * kMwgMaxD + j) * C + chain;
+                double e = *ep + stp;
+                e = (e < u.amax) ? e : u.amax;
+                *ep = (e > u.amin) ? e : u.amin;
+            }
+            a.aprop[pc] = 0;
+            a.aacc[pc] = 0;
+        } else {
+            a.aprop[pc] = pr;
+            a.aacc[pc] = ac;
+        }
+    }
+}
+
+// One lane per chain; θ and P°.θ in registers, coordinates moved between global
+// and update-local order by selects over the compile-time D (D ≤ 16).
+template <int D, bool FULL, int LLMODE, class TGT = GsnTarget>
 __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
-    static_assert(D <= kMwgMaxD, "MWG kernel supports D ≤ 16");
-    // ziggurat tables → static LDS (the only lane-indexed constants)
+    static_assert(D <= 16, "register-state MWG kernel: D ≤ 16 (mwg_wide_kernel below for larger D)");
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
@@ -156,9 +491,8 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         const MwgUpdate &u = a.updates[p];
         const uint32_t n = u.nc;
         const uint64_t slot = (uint64_t)(iter - 1) * a.P + p;
-        const uint64_t pc = (uint64_t)p * C + chain;
         // ---- update_workspaces!: θ_local ← θ[coords] (uniform coordinate indices)
-        double tl[D], tp[D], ta[D];  // local θ, θ° (history / P°), θ° as stored on accept
+        double tl[D], tp[D], ta[D];
 #pragma unroll
         for (int j = 0; j < D; ++j) {
             double v = 0.0;
@@ -169,127 +503,8 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
             }
             tl[j] = v;
         }
-        // ---- proposal!
-        double ltd_fwd = 0.0, ltd_rev = 0.0;
-        if (u.kind == 1) {  // UniformRandomWalk: θ° = θ·1 + U, or θ·e^U where pos
-            double ev[D];
-#pragma unroll
-            for (int j = 0; j < D; j += 2) {
-                if ((uint32_t)j < n) {
-                    const u32x4 r = draw(a.key0, a.key1, gid, iter, (uint32_t)j >> 1, p, 0);
-                    const double e0 = u.adapt ? a.eps[((uint64_t)p * kMwgMaxD + j) * C + chain] : u.eps0[j];
-                    const double U0 = (-e0) + (e0 - (-e0)) * u01_closed0(r.x, r.y);
-                    tp[j] = ((u.posmask >> j) & 1u) ? tl[j] * exp_any(U0) + copysign(0.0, U0) : tl[j] * 1.0 + U0;
-                    ev[j] = e0;
-                    if (j + 1 < D && (uint32_t)(j + 1) < n) {
-                        const double e1 = u.adapt ? a.eps[((uint64_t)p * kMwgMaxD + j + 1) * C + chain] : u.eps0[j + 1];
-                        const double U1 = (-e1) + (e1 - (-e1)) * u01_closed0(r.z, r.w);
-                        tp[j + 1] = ((u.posmask >> (j + 1)) & 1u) ? tl[j + 1] * exp_any(U1) + copysign(0.0, U1)
-                                                                  : tl[j + 1] * 1.0 + U1;
-                        ev[j + 1] = e1;
-                    }
-                }
-            }
-            if (u.posmask) {  // uniform branch: the mask is the update's
-#pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    if ((uint32_t)j < n) {
-                        const bool pj = (u.posmask >> j) & 1u;
-                        const double c = pj ? -log_any(2.0 * ev[j]) : 0.0;
-                        const double f = pj ? c - log_any(tp[j]) : 0.0;  // logpdf(rw, θ, θ°) term
-                        const double g = pj ? c - log_any(tl[j]) : 0.0;  // logpdf(rw, θ°, θ) term
-                        ltd_fwd = (j == 0) ? f : ltd_fwd + f;
-                        ltd_rev = (j == 0) ? g : ltd_rev + g;
-                    }
-                }
-            }
-        } else {  // GaussianRandomWalk over the update's coordinates
-            const uint32_t pm = u.posmask;  // positivity-restricted coordinates (log scale)
-            auto isp = [&](int i) { return ((pm >> i) & 1u) != 0u; };
-            double z[D];
-#pragma unroll
-            for (int j = 0; j < D; ++j)
-                z[j] = ((uint32_t)j < n) ? normal_draw(zt, a.key0, a.key1, gid, iter, p, (uint32_t)j, faults) : 0.0;
-#pragma unroll
-            for (int i = 0; i < D; ++i) {
-                if ((uint32_t)i < n) {
-                    double lz;
-                    if (u.diag) {
-                        lz = u.L[i * kMwgMaxD + i] * z[i];
-                    } else {
-                        lz = u.L[i * kMwgMaxD] * z[0];
-#pragma unroll
-                        for (int j = 1; j <= i; ++j) lz = fma(u.L[i * kMwgMaxD + j], z[j], lz);
-                    }
-                    // remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136, 145-147)
-                    tp[i] = (isp(i) ? log_any(tl[i]) : tl[i]) + lz;
-                } else {
-                    tp[i] = 0.0;
-                }
-            }
-            double r[D];
-            if (pm == 0u) {
-#pragma unroll
-                for (int i = 0; i < D; ++i) r[i] = tp[i] - tl[i];
-                ltd_fwd = u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0;
-#pragma unroll
-                for (int i = 0; i < D; ++i) r[i] = tl[i] - tp[i];
-                ltd_rev = u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0;
-            } else {
-                // The reference's in-place round trips, step by step (random_walk.jl:136-171):
-                //   rand:   θ° ← exp(log θ + Lz), θ ← exp(log θ)               (θ°₁, θ₁)
-                //   logpdf(θ°₁, θ₁): logJ = −Σ_pos log θ₁; MvNormal(log θ°₁) at log θ₁;
-                //           then θ°₂ = exp(log θ°₁), θ₂ = exp(log θ₁)
-                //   logpdf(θ₂, θ°₂): logJ = −Σ_pos log θ°₂; MvNormal(log θ₂) at log θ°₂;
-                //           then θ°₃ = exp(log θ°₂) — the value an accept stores
-                double t1[D], a1[D], b1[D];
-                double lj = 0.0;
-                bool first = true;
-#pragma unroll
-                for (int i = 0; i < D; ++i) {
-                    if ((uint32_t)i < n) {
-                        tp[i] = isp(i) ? exp_any(tp[i]) : tp[i];              // θ°₁
-                        t1[i] = isp(i) ? exp_any(log_any(tl[i])) : tl[i];     // θ₁
-                        if (isp(i)) {
-                            const double v = log_any(t1[i]);
-                            lj = first ? v : lj + v;
-                            first = false;
-                        }
-                        a1[i] = isp(i) ? log_any(tp[i]) : tp[i];             // μ = log θ°₁
-                        b1[i] = isp(i) ? log_any(t1[i]) : t1[i];             // x = log θ₁
-                        r[i] = b1[i] - a1[i];
-                    } else {
-                        t1[i] = a1[i] = b1[i] = r[i] = 0.0;
-                    }
-                }
-                ltd_rev = (u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0) + (-lj);
-                lj = 0.0;
-                first = true;
-#pragma unroll
-                for (int i = 0; i < D; ++i) {
-                    if ((uint32_t)i < n) {
-                        const double p2 = isp(i) ? exp_any(a1[i]) : a1[i];  // θ°₂
-                        const double l2 = isp(i) ? exp_any(b1[i]) : b1[i];  // θ₂
-                        if (isp(i)) {
-                            const double v = log_any(p2);
-                            lj = first ? v : lj + v;
-                            first = false;
-                        }
-                        const double a2 = isp(i) ? log_any(l2) : l2;        // μ = log θ₂
-                        const double b2 = isp(i) ? log_any(p2) : p2;        // x = log θ°₂
-                        r[i] = b2 - a2;
-                        ta[i] = isp(i) ? exp_any(b2) : p2;                  // θ°₃
-                    } else {
-                        r[i] = 0.0;
-                    }
-                }
-                ltd_fwd = (u.c0 - mwg_sqmahal_u<D>(u, n, r) / 2.0) + (-lj);
-            }
-        }
-        if (!(u.kind == 2 && u.posmask != 0u)) {
-#pragma unroll
-            for (int j = 0; j < D; ++j) ta[j] = tp[j];
-        }
+        double ltd_fwd, ltd_rev, lpp, lpc;
+        mwg_local_step<D>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
         // ---- set_proposal!: proposal history and P°.θ[coords] ← θ°
         double prop[D], nst[D];
 #pragma unroll
@@ -307,30 +522,17 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
             }
         }
         // ---- compute_ll!: loglikelihood(P°, obs)
-        double llp;
-        if constexpr (LLMODE == LL_PER_OBS) {
-            llp = 0.0;
-            for (uint32_t k = 0; k < a.nobs; ++k) {
-                double r[D];
-#pragma unroll
-                for (int i = 0; i < D; ++i) r[i] = a.obs[(size_t)k * D + i] - mp[i];
-                llp = llp + (a.t_c0 - mwg_sqmahal_t<D>(a, r) / 2.0);
-            }
-        } else {
-            double r[D];
-#pragma unroll
-            for (int i = 0; i < D; ++i) r[i] = a.xbar[i] - mp[i];
-            const double qv = mwg_sqmahal_t<D>(a, r);
-            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
-        }
+        const double llp = TGT::template loglik<D, LLMODE>(a, mp);
         if (!(llp - llp == 0.0)) faults |= 1u;
-        // ---- accept_reject!
-        const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + 0.0) - 0.0;
+        a.ll_prop[(uint64_t)p * C + chain] = llp;
+        // ---- accept_reject! (run.jl:268-281)
+        const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + lpp) - lpc;
         const double E = exp_draw(zt, a.key0, a.key1, gid, iter, p, faults);
         const bool acc = E > -llr;
         if constexpr (FULL) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) __builtin_nontemporal_store(prop[d], a.hist_prop + slot * D * C + state_pos(d, chain, C, D));
+            for (int d = 0; d < D; ++d)
+                __builtin_nontemporal_store(prop[d], a.hist_prop + slot * D * C + state_pos(d, chain, C, D));
         }
         if (acc) {  // set_chain_param!: θ[coords] ← θ° (run.jl:312-318)
 #pragma unroll
@@ -339,61 +541,83 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         }
         if constexpr (FULL) {
 #pragma unroll
-            for (int d = 0; d < D; ++d) __builtin_nontemporal_store(th[d], a.hist_theta + slot * D * C + state_pos(d, chain, C, D));
+            for (int d = 0; d < D; ++d)
+                __builtin_nontemporal_store(th[d], a.hist_theta + slot * D * C + state_pos(d, chain, C, D));
             __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
         }
-        {
-            const uint64_t m = __ballot(acc);
-            if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
-        }
-        a.nacc[pc] += acc ? 1u : 0u;
-        // ---- update_stats!: rolling acceptance of update p
-        {
-            const uint64_t N = a.N0 + s;
-            uint64_t r0 = a.ring[2 * pc], r1 = a.ring[2 * pc + 1];
-            const double ra_prev = (flags & 1u) ? a.ra[pc] : 0.0;
-            int out = 0;
-            if (iter > a.W) {
-                const uint32_t j = (iter - a.W) & 127u;
-                out = (int)((((j & 64u) ? r1 : r0) >> (j & 63u)) & 1ull);
-            }
-            const uint64_t mn = (N < (uint64_t)a.W) ? N : (uint64_t)a.W;
-            a.ra[pc] = (ra_prev * (double)a.W + (double)((int)acc - out)) / (double)mn;
-            const uint32_t jw = iter & 127u;
-            const uint64_t bit = 1ull << (jw & 63u);
-            if (jw & 64u) r1 = acc ? (r1 | bit) : (r1 & ~bit);
-            else r0 = acc ? (r0 | bit) : (r0 & ~bit);
-            a.ring[2 * pc] = r0;
-            a.ring[2 * pc + 1] = r1;
-        }
-        // ---- update_adaptation!: AdaptationUnifRW on its own turn
-        if (u.adapt == 1) {
-            const uint32_t pr = a.aprop[pc] + 1, ac = a.aacc[pc] + (acc ? 1u : 0u);
-            if (pr >= u.k) {  // proposed counts are equal across chains: uniform branch
-                const double delta = u.scale / sqrt(fmax(1.0, (double)iter / (double)u.k - u.offset));
-                const double a_r = (double)ac / (double)pr;
-                const double stp = (a_r > u.target) ? delta : -delta;
-#pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    if ((uint32_t)j < n) {
-                        double *ep = a.eps + ((uint64_t)p * kMwgMaxD + j) * C + chain;
-                        double e = *ep + stp;
-                        e = (e < u.amax) ? e : u.amax;
-                        *ep = (e > u.amin) ? e : u.amin;
-                    }
-                }
-                a.aprop[pc] = 0;
-                a.aacc[pc] = 0;
-            } else {
-                a.aprop[pc] = pr;
-                a.aacc[pc] = ac;
-            }
-        }
+        mwg_register_step(a, u, n, chain, iter, p, s, flags, slot, acc);
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         a.theta[state_pos(d, chain, C, D)] = th[d];
         a.mu_p[state_pos(d, chain, C, D)] = mp[d];
+    }
+    a.ll[chain] = ll;
+    a.faults[chain] = faults;
+    if (faults) *a.fault_flag = 1u;
+}
+
+// One lane per chain for larger D: θ and P°.θ stay in HBM (SoA state_pos layout,
+// L2/MALL-resident) and are read and written at the update's coordinates with
+// wave-uniform indices, so no select network over D is needed; only the
+// update's NU-sized local vectors and, for the likelihood, P°.θ live in
+// registers.  The arithmetic is mwg_gsn_kernel's.
+template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget>
+__global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
+    static_assert(NU <= D && D <= kMwgMaxD, "NU ≤ D ≤ 32");
+    const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint64_t C = a.C;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+    double ll = a.ll[chain];
+    uint32_t faults = a.faults[chain];
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.steps[4 * s], pidx = a.steps[4 * s + 1], flags = a.steps[4 * s + 2];
+        const uint32_t p = pidx - 1;
+        const MwgUpdate &u = a.updates[p];
+        const uint32_t n = u.nc;
+        const uint64_t slot = (uint64_t)(iter - 1) * a.P + p;
+        // ---- update_workspaces!: θ_local ← θ[coords]
+        double tl[NU], tp[NU], ta[NU];
+        for (int j = 0; j < NU; ++j) tl[j] = ((uint32_t)j < n) ? a.theta[state_pos(u.coords[j], chain, C, D)] : 0.0;
+        double ltd_fwd, ltd_rev, lpp, lpc;
+        mwg_local_step<NU, true>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
+        // ---- set_proposal!: P°.θ[coords] ← θ°, then all of P°.θ for the likelihood
+        for (int j = 0; j < NU; ++j)
+            if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tp[j];
+        double mp[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) mp[d] = a.mu_p[state_pos(d, chain, C, D)];
+        // ---- compute_ll!
+        const double llp = TGT::template loglik<D, LLMODE, true>(a, mp);
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        a.ll_prop[(uint64_t)p * C + chain] = llp;
+        // ---- accept_reject! (run.jl:268-281)
+        const double llr = ((((llp - ll) + ltd_rev) - ltd_fwd) + lpp) - lpc;
+        const double E = exp_draw(zt, a.key0, a.key1, gid, iter, p, faults);
+        const bool acc = E > -llr;
+        if constexpr (FULL) {  // proposal history: θ with coords ← θ° (run.jl:237-239)
+            double *hp = a.hist_prop + slot * D * C;
+#pragma unroll
+            for (int d = 0; d < D; ++d) hp[state_pos(d, chain, C, D)] = a.theta[state_pos(d, chain, C, D)];
+            for (int j = 0; j < NU; ++j)
+                if ((uint32_t)j < n) hp[state_pos(u.coords[j], chain, C, D)] = tp[j];
+        }
+        if (acc) {  // set_chain_param!: θ[coords] ← θ° (run.jl:312-318)
+            for (int j = 0; j < NU; ++j)
+                if ((uint32_t)j < n) a.theta[state_pos(u.coords[j], chain, C, D)] = ta[j];
+            ll = llp;
+        }
+        if constexpr (FULL) {
+            double *ht = a.hist_theta + slot * D * C;
+#pragma unroll
+            for (int d = 0; d < D; ++d)
+                __builtin_nontemporal_store(a.theta[state_pos(d, chain, C, D)], ht + state_pos(d, chain, C, D));
+            __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
+        }
+        mwg_register_step(a, u, n, chain, iter, p, s, flags, slot, acc);
     }
     a.ll[chain] = ll;
     a.faults[chain] = faults;

@@ -38,7 +38,8 @@ STATUS_NAMES = {
 }
 
 RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA = 1, 2, 3, 4
-PRIOR_IMPROPER, PRIOR_IMPROPER_POS = 0, 1
+PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
+DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
 ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO = 0, 1, 2
 TARGET_GSN, TARGET_LOGISTIC = 1, 2
 LL_PER_OBS, LL_SUFFSTAT = 0, 1
@@ -47,6 +48,7 @@ H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
 FAULT_NONFINITE_LL = 1
 FAULT_RNG_RETRIES = 2
 FAULT_POSDEF = 4
+FAULT_PRIOR_RESAMPLES = 8
 VARIANT_HIGH_OCCUPANCY = 1
 VARIANT_OCCUPANCY3 = 2
 
@@ -83,10 +85,22 @@ class EmcmcUpdateDesc(C.Structure):
         ("pos", C.POINTER(C.c_uint8)),
         ("adaptation_params", C.c_void_p),
         ("sigma_b", C.POINTER(C.c_double)),
-        ("reserved_ptr", C.c_void_p * 2),
+        ("prior_params", C.c_void_p),
+        ("reserved_ptr", C.c_void_p),
         ("mix_lambda", C.c_double),
         ("reserved_f64", C.c_double * 3),
     ]
+
+
+class EmcmcPriorFactor(C.Structure):
+    """One ProductPrior / StandardPrior factor (include/emcmc.h emcmc_prior_factor)."""
+    _fields_ = [("family", C.c_uint32), ("count", C.c_uint32), ("a", C.c_double), ("b", C.c_double)]
+
+
+class EmcmcPriorDesc(C.Structure):
+    """emcmc_update_desc.prior_params (include/emcmc.h emcmc_prior_desc)."""
+    _fields_ = [("num_factors", C.c_uint32), ("reserved", C.c_uint32),
+                ("factors", C.POINTER(EmcmcPriorFactor))]
 
 
 class EmcmcHaarioAdaptation(C.Structure):
@@ -157,6 +171,7 @@ SIGNATURES = {
         _ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     ),
     "emcmc_get_faults": (_ST, [_H, C.POINTER(C.c_uint32)]),
+    "emcmc_get_proposal_ll": (_ST, [_H, C.POINTER(C.c_double)]),
     "emcmc_get_chain_moments": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_get_mix_state": (_ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
     "emcmc_get_history": (_ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]),

@@ -106,13 +106,26 @@ class Engine:
             pass
 
     # -- setup ------------------------------------------------------------------
-    def add_gaussian_rw_update(self, coords0, sigma, prior=L.PRIOR_IMPROPER, adaptation=L.ADPT_NONE, pos=None):
+    @staticmethod
+    def _prior_desc(u, prior, factors, keep):
+        """emcmc_update_desc.prior/prior_params; factors: [(EMCMC_DIST_*, count, a, b), ...]."""
+        u.prior = prior
+        if factors:
+            arr = (L.EmcmcPriorFactor * len(factors))(*[L.EmcmcPriorFactor(int(f), int(c), float(a), float(b))
+                                                       for f, c, a, b in factors])
+            pd = L.EmcmcPriorDesc(len(factors), 0, C.cast(arr, C.POINTER(L.EmcmcPriorFactor)))
+            keep += [arr, pd]
+            u.prior_params = C.cast(C.pointer(pd), C.c_void_p)
+
+    def add_gaussian_rw_update(self, coords0, sigma, prior=L.PRIOR_IMPROPER, adaptation=L.ADPT_NONE, pos=None,
+                               prior_factors=None):
+        keep = []
         coords = np.ascontiguousarray(coords0, dtype=np.uint32)
         S = np.asfortranarray(np.asarray(sigma, dtype=np.float64).reshape(len(coords), len(coords)))
         Sf = np.ascontiguousarray(S.ravel(order="F"))
         u = L.EmcmcUpdateDesc()
         u.kernel = L.RW_GAUSSIAN
-        u.prior = prior
+        self._prior_desc(u, prior, prior_factors, keep)
         u.adaptation = adaptation
         u.num_coords = len(coords)
         u.coords = L.u32ptr(coords)
@@ -123,14 +136,15 @@ class Engine:
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
 
-    def add_uniform_rw_update(self, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None):
+    def add_uniform_rw_update(self, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):
         """UniformRandomWalk(ϵ) on coords0 (0-based); adapt: None or a dict with
         AdaptationUnifRW's k, target, scale, min, max, offset."""
+        keep = []
         coords = np.ascontiguousarray(coords0, dtype=np.uint32)
         e = np.ascontiguousarray(np.broadcast_to(np.asarray(eps, dtype=np.float64), (len(coords),)))
         u = L.EmcmcUpdateDesc()
         u.kernel = L.RW_UNIFORM
-        u.prior = prior
+        self._prior_desc(u, prior, prior_factors, keep)
         u.num_coords = len(coords)
         u.coords = L.u32ptr(coords)
         u.epsilon = L.dptr(e)
@@ -240,6 +254,12 @@ class Engine:
         it = np.arange(iter_first, iter_first + n, dtype=np.uint32)
         steps = np.stack([it, np.full(n, pidx, dtype=np.uint32)], axis=1)
         self.run(steps)
+
+    def get_proposal_ll(self):
+        """sub_ws°.ll of every update (the log-likelihood of its latest proposal), [P][C]."""
+        out = np.empty((max(1, self.num_updates), self.cfg.num_chains))
+        self._check(self._lib.emcmc_get_proposal_ll(self._h, L.dptr(out)), "emcmc_get_proposal_ll")
+        return out
 
     def synchronize(self, allow_faults=False):
         st = self._lib.emcmc_synchronize(self._h)

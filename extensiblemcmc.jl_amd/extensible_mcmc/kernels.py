@@ -114,6 +114,74 @@ class ImproperPosPrior(Prior):
         return -float(np.sum(np.log(theta)))
 
 
+# univariate prior families with a device plugin (Distributions.jl parameterisations);
+# logpdf here is the host restatement (StatsFuns forms), the device computes the same
+class Normal:
+    family = L.DIST_NORMAL
+
+    def __init__(self, mu=0.0, sigma=1.0):
+        assert sigma > 0
+        self.a, self.b = float(mu), float(sigma)
+
+    def logpdf(self, x):
+        z = (np.asarray(x, dtype=float) - self.a) / self.b
+        return -(z * z + np.log(2 * np.pi)) / 2.0 - np.log(self.b)
+
+
+class Uniform:
+    family = L.DIST_UNIFORM
+
+    def __init__(self, a=0.0, b=1.0):
+        assert a < b
+        self.a, self.b = float(a), float(b)
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        return np.where((x >= self.a) & (x <= self.b), -np.log(self.b - self.a), -np.inf)
+
+
+class Exponential:
+    family = L.DIST_EXPONENTIAL
+
+    def __init__(self, theta=1.0):
+        assert theta > 0
+        self.a, self.b = float(theta), 0.0
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        lam = 1.0 / self.a
+        return np.where(x < 0, -np.inf, np.log(lam) - lam * x)
+
+
+class Gamma:
+    family = L.DIST_GAMMA
+
+    def __init__(self, alpha=1.0, theta=1.0):
+        assert alpha > 0 and theta > 0
+        self.a, self.b = float(alpha), float(theta)
+
+    def logpdf(self, x):
+        from math import lgamma
+
+        x = np.asarray(x, dtype=float)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            v = -lgamma(self.a) - self.a * np.log(self.b) + (self.a - 1) * np.log(x) - x / self.b
+        return np.where(x < 0, -np.inf, v)
+
+
+class Product:
+    """Distributions.Product of univariates (a StandardPrior argument)."""
+
+    def __init__(self, dists):
+        self.v = list(dists)
+
+    def logpdf(self, x):
+        return sum(float(d.logpdf(xi)) for d, xi in zip(self.v, np.atleast_1d(x)))
+
+
+_UNIVARIATE = (Normal, Uniform, Exponential, Gamma)
+
+
 class StandardPrior(Prior):
     """StandardPrior(dist) with a scipy-like ``logpdf`` (priors.jl:35-39)."""
 
@@ -308,6 +376,33 @@ class HaarioTypeAdaptation(Adaptation):
         self.f = f if f is not None else (lambda x, y, z: x)
 
 
+def prior_to_device(prior, n):
+    """(EMCMC_PRIOR_*, factors) of a prior over an update's n coordinates (priors.jl).
+    ProductPrior(dists, dims): one factor per dist, dims[i] iid coordinates each;
+    StandardPrior(univariate) on n = 1, or StandardPrior(Product([...]))."""
+    if isinstance(prior, ImproperPrior):
+        return L.PRIOR_IMPROPER, None
+    if isinstance(prior, ImproperPosPrior):
+        return L.PRIOR_IMPROPER_POS, None
+    if isinstance(prior, ProductPrior):
+        fs = []
+        for dist, ix in zip(prior.dists, prior.idx):
+            if not isinstance(dist, _UNIVARIATE):
+                raise UnsupportedPlugin(f"ProductPrior factor {type(dist).__name__} has no device plugin")
+            fs.append((dist.family, ix.stop - ix.start, dist.a, dist.b))
+        if sum(f[1] for f in fs) != n:
+            raise ValueError("ProductPrior dims must cover the update's coordinates")
+        return L.PRIOR_PRODUCT, fs
+    if isinstance(prior, StandardPrior):
+        d = prior.dist
+        if isinstance(d, _UNIVARIATE) and n == 1:
+            return L.PRIOR_STANDARD, [(d.family, 1, d.a, d.b)]
+        if isinstance(d, Product) and len(d.v) == n and all(isinstance(x, _UNIVARIATE) for x in d.v):
+            return L.PRIOR_STANDARD, [(x.family, 1, x.a, x.b) for x in d.v]
+        raise UnsupportedPlugin(f"StandardPrior({type(d).__name__}) has no device plugin")
+    raise UnsupportedPlugin(f"prior {type(prior).__name__} has no device plugin")
+
+
 # ---------------------------------------------------------------------------
 # updates (src/updates.jl)
 @dataclass
@@ -327,10 +422,7 @@ class RandomWalkUpdate(MCMCParamUpdate):
     def to_device(self, engine):
         """Register this update with the engine (emcmc_add_update)."""
         coords0 = np.asarray(self.coords, dtype=np.int64) - 1
-        if isinstance(self.prior, ImproperPrior):
-            prior = L.PRIOR_IMPROPER
-        else:
-            raise UnsupportedPlugin(f"prior {type(self.prior).__name__} has no device plugin yet")
+        prior, factors = prior_to_device(self.prior, len(self.coords))
         adapt = None
         if isinstance(self.adpt, NoAdaptation):
             pass
@@ -359,10 +451,10 @@ class RandomWalkUpdate(MCMCParamUpdate):
                                               haario_scale=2.38 ** 2 if adapt is None else adapt["scale"],
                                               prior=prior)
         elif isinstance(self.rw, GaussianRandomWalk):
-            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior,
+            engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior, prior_factors=factors,
                                           pos=self.rw.pos if np.any(self.rw.pos) else None)
         elif isinstance(self.rw, UniformRandomWalk):
-            engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior,
+            engine.add_uniform_rw_update(coords0, self.rw.eps, adapt=adapt, prior=prior, prior_factors=factors,
                                          pos=self.rw.pos if np.any(self.rw.pos) else None)
         else:
             raise UnsupportedPlugin(f"transition kernel {type(self.rw).__name__} has no device plugin yet")

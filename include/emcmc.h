@@ -19,8 +19,8 @@
  *    `emcmc_step`, which are 1-based exactly as `MCMCSchedule` yields them
  *    (src/schedule.jl:56-66).
  *  - Matrices Σ are column-major (Julia layout); only the upper triangle is
- *    read, like `Symmetric(Σ)` (uplo = :U) in src/transition_kernels/random_walk.jl:358
- *    and src/example/gsn_target.jl:173.
+ *    read, like `Symmetric(Σ)` (uplo = :U) in src/transition_kernels/random_walk.jl:132
+ *    and `Symmetric(triu(Σ))` in src/example/gsn_target.jl:19.
  *  - Chain state crossing the ABI is row-major [C][D] (chain-major).
  *  - Ownership: the library owns all device memory; the caller owns host
  *    buffers and keeps them alive for the duration of the call.
@@ -61,9 +61,22 @@ typedef enum emcmc_status {
 #define EMCMC_MALA 4u             /* MALAUpdate: a stub in the reference (updates.jl:216-218); the engine's
                                      definition is in DESIGN.md §2.  epsilon[0] = step size ϵ. */
 
-/* Priors — src/priors.jl */
-#define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior    priors.jl:18-19 */
-#define EMCMC_PRIOR_IMPROPER_POS 1u /* ImproperPosPrior priors.jl:25-26 (reserved) */
+/* Priors — src/priors.jl.  Evaluated on the update's local coordinates
+ * (log_prior, updates.jl:104; run.jl:374-385); proposal! draws θ° again while
+ * logpdf(prior, θ°) === −Inf (updates.jl:191-196).  Non-improper priors run on
+ * the general schedule kernel (D ≤ 32). */
+#define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior     priors.jl:18-19: 0.0 */
+#define EMCMC_PRIOR_IMPROPER_POS 1u /* ImproperPosPrior  priors.jl:25-26: −sum(log.(θ)) */
+#define EMCMC_PRIOR_PRODUCT 2u      /* ProductPrior(dists, dims) priors.jl:60-88: lp = 0.0; lp += logpdf(dist, θ[idx])
+                                       per factor; a factor over k > 1 coordinates is k iid copies
+                                       (Product(fill(dist, k))) */
+#define EMCMC_PRIOR_STANDARD 3u     /* StandardPrior(dist) priors.jl:35-39 with dist a univariate on a 1-coordinate
+                                       update or a Product of univariates: one left fold, no leading 0.0 */
+/* Univariate families of a prior factor (Distributions.jl parameterisations) */
+#define EMCMC_DIST_NORMAL 1u        /* Normal(μ = a, σ = b) */
+#define EMCMC_DIST_UNIFORM 2u       /* Uniform(a, b) */
+#define EMCMC_DIST_EXPONENTIAL 3u   /* Exponential(θ = a), the scale */
+#define EMCMC_DIST_GAMMA 4u         /* Gamma(α = a, θ = b), shape and scale */
 
 /* Adaptation — src/transition_kernels/adaptation.jl */
 #define EMCMC_ADPT_NONE 0u      /* NoAdaptation          adaptation.jl:26 */
@@ -98,6 +111,9 @@ typedef enum emcmc_status {
 #define EMCMC_FAULT_POSDEF 4u        /* Haario readjust: 2.38²/D·cov not positive definite.  The reference
                                         throws PosDefException at the next MvNormal(θ, Σ_B)
                                         (random_walk.jl:147,167); the chain keeps its previous Σ_B factor */
+#define EMCMC_FAULT_PRIOR_RESAMPLES 8u /* proposal! drew 65,535 proposals outside the prior's support
+                                          (the reference loops forever, updates.jl:193-195); the last
+                                          draw is kept and rejected (llr = NaN or −Inf) */
 
 typedef struct emcmc_handle emcmc_handle;
 
@@ -153,6 +169,22 @@ typedef struct emcmc_haario_adaptation {
     double scale;
 } emcmc_haario_adaptation;
 
+/* One factor of a ProductPrior / StandardPrior: `count` consecutive local
+ * coordinates with the same univariate family EMCMC_DIST_* and parameters (a, b). */
+typedef struct emcmc_prior_factor {
+    uint32_t family;
+    uint32_t count;
+    double a, b;
+} emcmc_prior_factor;
+
+/* emcmc_update_desc.prior_params for EMCMC_PRIOR_PRODUCT / EMCMC_PRIOR_STANDARD:
+ * the factors in coordinate order, their counts summing to num_coords. */
+typedef struct emcmc_prior_desc {
+    uint32_t num_factors;
+    uint32_t reserved;
+    const emcmc_prior_factor *factors;
+} emcmc_prior_desc;
+
 /* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183).
  * Any number of updates, each on any coordinate subset (Metropolis-within-Gibbs,
  * BASELINE cfg 1 and the reference's own test, test/runtests.jl:87-114).  A single
@@ -160,10 +192,10 @@ typedef struct emcmc_haario_adaptation {
  * kernels; a single GaussianRandomWalkMix update on coords 1:D (optionally with
  * HaarioTypeAdaptation, BASELINE cfg 4) runs on the mix kernels, which also keep
  * the chain moments; every other schedule runs on the general schedule kernel
- * (D ≤ 16). */
+ * (D ≤ 32). */
 typedef struct emcmc_update_desc {
     uint32_t kernel;          /* EMCMC_RW_UNIFORM, EMCMC_RW_GAUSSIAN or EMCMC_RW_GAUSSIAN_MIX */
-    uint32_t prior;           /* EMCMC_PRIOR_IMPROPER */
+    uint32_t prior;           /* EMCMC_PRIOR_* */
     uint32_t adaptation;      /* EMCMC_ADPT_NONE, EMCMC_ADPT_UNIF_RW (UniformRandomWalk) or
                                  EMCMC_ADPT_HAARIO (GaussianRandomWalkMix) */
     uint32_t num_coords;      /* length(coords) */
@@ -172,11 +204,12 @@ typedef struct emcmc_update_desc {
     const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
     const uint8_t *pos;       /* positivity flags or NULL (all false); true on device for UniformRandomWalk
                                  (θ° = θ·e^U, random_walk.jl:63-94) and GaussianRandomWalk (log scale,
-                                 random_walk.jl:136-171; D ≤ 16), not for GaussianRandomWalkMix */
+                                 random_walk.jl:136-171; D ≤ 32), not for GaussianRandomWalkMix */
     const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW) or
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
     const double *sigma_b;    /* GaussianRandomWalkMix Σ_B: num_coords² column-major */
-    const void *reserved_ptr[2];
+    const emcmc_prior_desc *prior_params; /* EMCMC_PRIOR_PRODUCT / EMCMC_PRIOR_STANDARD factors, else NULL */
+    const void *reserved_ptr;
     double mix_lambda;        /* GaussianRandomWalkMix λ ∈ [0, 1] (B is picked iff rand() ≤ λ) */
     double reserved_f64[3];
 } emcmc_update_desc;
@@ -279,6 +312,12 @@ emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_si
 
 /* Per-chain fault bits (EMCMC_FAULT_*), [C] uint32. */
 emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults);
+
+/* `ll°(local_ws)` = sub_ws°.ll of every update (workspaces.jl:316-337): the
+ * log-likelihood of the update's most recent proposal, per chain: [P][C]
+ * (NaN for an update that has not run since emcmc_set_state).  REPLCallback's
+ * ll° and llr (callbacks.jl:305-307, workspaces.jl:378) read it. */
+emcmc_status emcmc_get_proposal_ll(emcmc_handle *h, double *ll_prop);
 
 /* Copies iterations [iter_first, iter_first+num_iters) (1-based) of one history
  * to host.  Layout per EMCMC_H_* above, restricted to the window. */

@@ -567,7 +567,55 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
  * to the update); the accept exponential as orc_exponential with pidx0 = p.
  * ========================================================================== */
 
-#define ORC_MWG_MAXD 16
+#define ORC_MWG_MAXD 32
+#define ORC_MAX_RESAMPLE 0xFFFEu
+#define ORC_FAULT_PRIOR_RESAMPLES 8u
+
+/* priors.jl, restated: EMCMC_PRIOR_* kinds, EMCMC_DIST_* families */
+enum { ORC_PRIOR_IMPROPER = 0, ORC_PRIOR_IMPROPER_POS = 1, ORC_PRIOR_PRODUCT = 2, ORC_PRIOR_STANDARD = 3 };
+enum { ORC_DIST_NORMAL = 1, ORC_DIST_UNIFORM = 2, ORC_DIST_EXPONENTIAL = 3, ORC_DIST_GAMMA = 4 };
+
+static double orc_log_real(double x) { return (x < 0.0) ? NAN : orc_log_any(x); }
+
+/* logpdf of one univariate factor (Distributions.jl / StatsFuns forms):
+ *   Normal(μ, σ): normlogpdf(z) − log σ = −(z² + log2π)/2 − log σ, z = (x − μ)/σ
+ *   Uniform(a, b): −log(b − a) on [a, b], else −Inf
+ *   Exponential(θ): x < 0 ? −Inf : log λ − λx, λ = 1/θ
+ *   Gamma(α, θ): x < 0 ? −Inf : −loggamma(α) − α log θ + (α − 1) log x − x/θ (left to right)
+ * (a, b) are the parameters as the device holds them (Exponential: b = 1/θ),
+ * c the constant the host computes once. */
+static double orc_univariate_logpdf(uint32_t fam, double a, double b, double c, double x) {
+    if (fam == ORC_DIST_NORMAL) {
+        const double z = (x - a) / b;
+        return -(z * z + ORC_LOG2PI) / 2.0 - c;
+    }
+    if (fam == ORC_DIST_UNIFORM) return (x >= a && x <= b) ? c : -INFINITY;
+    if (fam == ORC_DIST_EXPONENTIAL) return (x < 0.0) ? -INFINITY : c - b * x;
+    return (x < 0.0) ? -INFINITY : (c + (a - 1.0) * orc_log_real(x)) - x / b;
+}
+
+/* (family, a, b) of a factor → device parameters and constant (engine host code) */
+static int orc_prior_factor_consts(uint32_t fam, double a, double b, double *pa, double *pb, double *pc) {
+    switch (fam) {
+    case ORC_DIST_NORMAL:
+        if (!(b > 0.0)) return -1;
+        *pa = a, *pb = b, *pc = orc_log(b);
+        return 0;
+    case ORC_DIST_UNIFORM:
+        if (!(a < b)) return -1;
+        *pa = a, *pb = b, *pc = -orc_log(b - a);
+        return 0;
+    case ORC_DIST_EXPONENTIAL:
+        if (!(a > 0.0)) return -1;
+        *pa = a, *pb = 1.0 / a, *pc = orc_log(1.0 / a);
+        return 0;
+    case ORC_DIST_GAMMA:
+        if (!(a > 0.0 && b > 0.0)) return -1;
+        *pa = a, *pb = b, *pc = (-lgamma(a)) - a * orc_log(b);
+        return 0;
+    }
+    return -2;
+}
 typedef struct {
     uint32_t kind; /* 1 uniform, 2 gaussian */
     uint32_t nc;
@@ -578,11 +626,49 @@ typedef struct {
     int diag;
     uint32_t adapt, k;
     double target, scale, amin, amax, offset;
+    uint32_t prior, pstart, pfam[ORC_MWG_MAXD];
+    double pa[ORC_MWG_MAXD], pb[ORC_MWG_MAXD], pc[ORC_MWG_MAXD];
 } orc_mwg_update;
 
-/* table layout from Python (per update p, 64 doubles of params + 16 coords):
- *   kind[P], nc[P], coords[P*16], eps[P*16], sigma[P*256] (nc×nc column-major),
- *   pos[P*16] (uint8), adapt[P], k[P], aparams[P*5] = (target, scale, min, max, offset) */
+/* logpdf(prior, x) over the update's n local coordinates (priors.jl:18-88):
+ * ImproperPosPrior −(x₁ + x₂ + …) of the logs; ProductPrior lp = 0.0; lp += factor
+ * (each factor folded left); StandardPrior of univariates: the left fold alone. */
+static double orc_mwg_log_prior(const orc_mwg_update *u, uint32_t n, const double *x) {
+    if (u->prior == ORC_PRIOR_IMPROPER) return 0.0;
+    if (u->prior == ORC_PRIOR_IMPROPER_POS) {
+        double s = 0.0;
+        for (uint32_t j = 0; j < n; ++j) {
+            const double v = orc_log_real(x[j]);
+            s = (j == 0) ? v : s + v;
+        }
+        return -s;
+    }
+    double lp = 0.0, s = 0.0;
+    for (uint32_t j = 0; j < n; ++j) {
+        const double v = orc_univariate_logpdf(u->pfam[j], u->pa[j], u->pb[j], u->pc[j], x[j]);
+        if (j == 0) {
+            s = v;
+        } else if ((u->pstart >> j) & 1u) {
+            lp = lp + s;
+            s = v;
+        } else {
+            s = s + v;
+        }
+    }
+    return (u->prior == ORC_PRIOR_PRODUCT) ? lp + s : s;
+}
+
+/* user target (EMCMC_TARGET_USER): loglikelihood(P°, obs) of a user function,
+ * the same source the engine compiles for the device (tests/user_targets/) */
+typedef double (*orc_user_loglik_fn)(const double *theta, int D, const double *obs, uint64_t nobs,
+                                     const double *params);
+
+/* table layout from Python (ORC_MWG_MAXD = 32 slots per update):
+ *   kind[P], nc[P], coords[P*32], eps[P*32], sigma[P*1024] (nc×nc column-major),
+ *   pos[P*32] (uint8), adapt[P], k[P], aparams[P*5] = (target, scale, min, max, offset),
+ *   prior[P], factor tables per update: nfac[P], ffam[P*32], fcnt[P*32], fa[P*32], fb[P*32];
+ * ll_prop [P][C] out: sub_ws°.ll of each update's latest proposal (NULL: skip);
+ * user_ll: NULL for GsnTargetLaw, else the user target (user_params its parameters). */
 ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, uint32_t P, const uint32_t *kind,
                            const uint32_t *nc, const uint32_t *coords, const double *eps, const double *sigma,
                            const uint8_t *pos, const uint32_t *adapt, const uint32_t *adapt_k, const double *aparams,
@@ -591,7 +677,10 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                            uint64_t *N_io, uint32_t *last_iter_io, double *theta, double *mu_p, double *ll,
                            double *ra, uint64_t *ring, uint32_t *nacc, uint32_t *aprop, uint32_t *aacc,
                            double *eps_state, uint32_t *faults, double *hist_theta, double *hist_prop,
-                           double *hist_ll, uint8_t *hist_acc, int nthreads) {
+                           double *hist_ll, uint8_t *hist_acc, int nthreads, const uint32_t *prior_kind,
+                           const uint32_t *nfac, const uint32_t *ffam, const uint32_t *fcnt, const double *fa,
+                           const double *fb, double *ll_prop, orc_user_loglik_fn user_ll,
+                           const double *user_params) {
     if (D < 1 || D > ORC_MWG_MAXD || P < 1 || P > 64) return -2;
     (void)zig();
     orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
@@ -626,14 +715,14 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         }
         if (u->kind == 2) {
             const int n = (int)u->nc;
-            if (orc_cholesky(sigma + (size_t)p * 256, n, u->L)) {
+            if (orc_cholesky(sigma + (size_t)p * 1024, n, u->L)) {
                 free(g);
                 free(U);
                 return -1;
             }
             for (int i = 0; i < n; ++i) u->iL[i] = 1.0 / u->L[(size_t)i * n + i];
             u->c0 = mvnormal_c0(n, logdet_chol(u->L, n));
-            u->diag = is_diag_upper(sigma + (size_t)p * 256, n);
+            u->diag = is_diag_upper(sigma + (size_t)p * 1024, n);
         }
         u->adapt = adapt[p];
         u->k = adapt_k[p];
@@ -642,6 +731,32 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         u->amin = aparams[p * 5 + 2];
         u->amax = aparams[p * 5 + 3];
         u->offset = aparams[p * 5 + 4];
+        u->prior = prior_kind ? prior_kind[p] : ORC_PRIOR_IMPROPER;
+        if (u->prior == ORC_PRIOR_PRODUCT || u->prior == ORC_PRIOR_STANDARD) {
+            uint32_t j = 0;
+            for (uint32_t f = 0; f < nfac[p]; ++f) {
+                const uint32_t fam = ffam[p * ORC_MWG_MAXD + f], cnt = fcnt[p * ORC_MWG_MAXD + f];
+                double a, b, cc;
+                if (cnt == 0 || j + cnt > u->nc ||
+                    orc_prior_factor_consts(fam, fa[p * ORC_MWG_MAXD + f], fb[p * ORC_MWG_MAXD + f], &a, &b, &cc)) {
+                    free(g);
+                    free(U);
+                    return -2;
+                }
+                if (u->prior == ORC_PRIOR_PRODUCT && j > 0) u->pstart |= 1u << j;
+                for (uint32_t k = 0; k < cnt; ++k, ++j) {
+                    u->pfam[j] = fam;
+                    u->pa[j] = a;
+                    u->pb[j] = b;
+                    u->pc[j] = cc;
+                }
+            }
+            if (j != u->nc) {
+                free(g);
+                free(U);
+                return -2;
+            }
+        }
     }
     const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
     const orc_zig_tables *zt = zig();
@@ -668,39 +783,58 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             int accept_ta = 0; /* accepted values differ from the proposal (Gaussian with pos) */
             for (uint32_t j = 0; j < n; ++j) tl[j] = th[u->coords[j]];
             double ltd_fwd = 0.0, ltd_rev = 0.0;
-            if (u->kind == 1) { /* UniformRandomWalk */
-                for (uint32_t j = 0; j < n; ++j) {
-                    const orc_u32x4 r = orc_draw(k0, k1, chain_id, iter, j >> 1, p, 0);
-                    const double uu = (j & 1u) ? orc_u01_closed0(r.v[2], r.v[3]) : orc_u01_closed0(r.v[0], r.v[1]);
-                    const double e = ep[j];
-                    const double a = -e, b = e;
-                    const double Uv = a + (b - a) * uu;
-                    tp[j] = u->pos[j] ? tl[j] * orc_exp_any(Uv) + copysign(0.0, Uv) : tl[j] * 1.0 + Uv;
+            int anypos = 0;
+            for (uint32_t j = 0; j < n; ++j) anypos |= u->pos[j];
+            /* proposal! (updates.jl:191-196): rand!, again while logpdf(prior, θ°) === −Inf;
+             * resample r reads counter blocks (r << 16) | j/2 */
+            for (uint32_t rs = 0;; ++rs) {
+                if (u->kind == 1) { /* UniformRandomWalk */
+                    for (uint32_t j = 0; j < n; ++j) {
+                        const orc_u32x4 r = orc_draw(k0, k1, chain_id, iter, (rs << 16) | (j >> 1), p, 0);
+                        const double uu = (j & 1u) ? orc_u01_closed0(r.v[2], r.v[3]) : orc_u01_closed0(r.v[0], r.v[1]);
+                        const double e = ep[j];
+                        const double a = -e, b = e;
+                        const double Uv = a + (b - a) * uu;
+                        tp[j] = u->pos[j] ? tl[j] * orc_exp_any(Uv) + copysign(0.0, Uv) : tl[j] * 1.0 + Uv;
+                    }
+                } else { /* GaussianRandomWalk over the update's coordinates */
+                    if (rs > 0) /* the previous rand! left θ ← exp(log θ) where pos */
+                        for (uint32_t i = 0; i < n; ++i)
+                            if (u->pos[i]) tl[i] = orc_exp_any(orc_log_any(tl[i]));
+                    double z[ORC_MWG_MAXD];
+                    for (uint32_t j = 0; j < n; ++j) z[j] = orc_normal(zt, k0, k1, chain_id, iter, p, (rs << 17) | j, &f);
+                    for (uint32_t i = 0; i < n; ++i) {
+                        double lz;
+                        if (u->diag) {
+                            lz = u->L[(size_t)i * n + i] * z[i];
+                        } else {
+                            lz = u->L[(size_t)i * n] * z[0];
+                            for (uint32_t j = 1; j <= i; ++j) lz = fma(u->L[(size_t)i * n + j], z[j], lz);
+                        }
+                        /* remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136);
+                         * reimpose_constraints!: θ°_i ← exp θ°_i (θ°₁) */
+                        const double v = (u->pos[i] ? orc_log_any(tl[i]) : tl[i]) + lz;
+                        tp[i] = u->pos[i] ? orc_exp_any(v) : v;
+                    }
                 }
+                if (u->prior == ORC_PRIOR_IMPROPER) break;
+                if (!(orc_mwg_log_prior(u, n, tp) == -INFINITY)) break;
+                if (rs >= ORC_MAX_RESAMPLE) {
+                    f |= ORC_FAULT_PRIOR_RESAMPLES;
+                    break;
+                }
+            }
+            double t3[ORC_MWG_MAXD]; /* θ as log_prior(::Previous) reads it */
+            if (u->kind == 1) {
                 /* logpdf(rw, θ, θ°) (subtracted) and logpdf(rw, θ°, θ) (added), left folds */
                 for (uint32_t j = 0; j < n; ++j) {
                     const double c = u->pos[j] ? -orc_log_any(2.0 * ep[j]) : 0.0;
-                    const double f = u->pos[j] ? c - orc_log_any(tp[j]) : 0.0;
+                    const double f1 = u->pos[j] ? c - orc_log_any(tp[j]) : 0.0;
                     const double g2 = u->pos[j] ? c - orc_log_any(tl[j]) : 0.0;
-                    ltd_fwd = (j == 0) ? f : ltd_fwd + f;
+                    ltd_fwd = (j == 0) ? f1 : ltd_fwd + f1;
                     ltd_rev = (j == 0) ? g2 : ltd_rev + g2;
                 }
-            } else { /* GaussianRandomWalk over the update's coordinates */
-                int anypos = 0;
-                for (uint32_t j = 0; j < n; ++j) anypos |= u->pos[j];
-                double z[ORC_MWG_MAXD];
-                for (uint32_t j = 0; j < n; ++j) z[j] = orc_normal(zt, k0, k1, chain_id, iter, p, j, &f);
-                for (uint32_t i = 0; i < n; ++i) {
-                    double lz;
-                    if (u->diag) {
-                        lz = u->L[(size_t)i * n + i] * z[i];
-                    } else {
-                        lz = u->L[(size_t)i * n] * z[0];
-                        for (uint32_t j = 1; j <= i; ++j) lz = fma(u->L[(size_t)i * n + j], z[j], lz);
-                    }
-                    /* remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136) */
-                    tp[i] = (u->pos[i] ? orc_log_any(tl[i]) : tl[i]) + lz;
-                }
+            } else {
                 double r[ORC_MWG_MAXD];
                 if (!anypos) {
                     for (uint32_t i = 0; i < n; ++i) r[i] = tp[i] - tl[i];
@@ -713,11 +847,11 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                      * logpdf(rw, θ°₁, θ₁) (:166-171): logJ = −sum(log θ₁[pos]),
                      * logpdf(MvNormal(log θ°₁, Σ), log θ₁) + logJ, then θ°₂ = exp(log θ°₁),
                      * θ₂ = exp(log θ₁); logpdf(rw, θ₂, θ°₂) likewise, then
-                     * θ°₃ = exp(log θ°₂), the value set_chain_param! copies on accept */
+                     * θ°₃ = exp(log θ°₂), the value set_chain_param! copies on accept,
+                     * and θ₃ = exp(log θ₂), the θ log_prior(::Previous) reads */
                     double t1[ORC_MWG_MAXD], a1[ORC_MWG_MAXD], b1[ORC_MWG_MAXD], lj = 0.0;
                     int first = 1;
                     for (uint32_t i = 0; i < n; ++i) {
-                        tp[i] = u->pos[i] ? orc_exp_any(tp[i]) : tp[i];
                         t1[i] = u->pos[i] ? orc_exp_any(orc_log_any(tl[i])) : tl[i];
                         if (u->pos[i]) {
                             const double v = orc_log_any(t1[i]);
@@ -743,10 +877,17 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                         const double b2 = u->pos[i] ? orc_log_any(p2) : p2;
                         r[i] = b2 - a2;
                         ta[i] = u->pos[i] ? orc_exp_any(b2) : p2;
+                        t3[i] = u->pos[i] ? orc_exp_any(a2) : l2;
                     }
                     ltd_fwd = (u->c0 - sqmahal(u->L, u->iL, r, (int)n, u->diag) / 2.0) + (-lj);
                     accept_ta = 1;
                 }
+            }
+            /* log_prior(::Proposal) − log_prior(::Previous) of the local states (run.jl:374-385) */
+            double lpp = 0.0, lpc = 0.0;
+            if (u->prior != ORC_PRIOR_IMPROPER) {
+                lpp = orc_mwg_log_prior(u, n, accept_ta ? ta : tp);
+                lpc = orc_mwg_log_prior(u, n, accept_ta ? t3 : tl);
             }
             /* set_proposal!: history θ with coords ← θ°; P°.θ[coords] ← θ° */
             double prop[ORC_MWG_MAXD];
@@ -757,7 +898,9 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             }
             /* compute_ll!: loglikelihood(P°, obs) */
             double llp, r[ORC_MWG_MAXD];
-            if (g->ll_mode == 0) {
+            if (user_ll) {
+                llp = user_ll(mp, D, obs, nobs, user_params);
+            } else if (g->ll_mode == 0) {
                 llp = 0.0;
                 for (uint64_t kk = 0; kk < nobs; ++kk) {
                     for (int i = 0; i < D; ++i) r[i] = obs[kk * D + i] - mp[i];
@@ -769,7 +912,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 llp = (double)nobs * g->t_c0 - (g->S_c + (double)nobs * qv) * 0.5;
             }
             if (!isfinite(llp)) f |= 1u;
-            const double llr = ((((llp - cll) + ltd_rev) - ltd_fwd) + 0.0) - 0.0;
+            if (ll_prop) ll_prop[(size_t)p * C + c] = llp;
+            const double llr = ((((llp - cll) + ltd_rev) - ltd_fwd) + lpp) - lpc;
             const double E = orc_exponential(zt, k0, k1, chain_id, iter, p, &f);
             const int acc = E > -llr;
             if (hist_prop) memcpy(hist_prop + ((uint64_t)s * C + c) * D, prop, sizeof(double) * D);

@@ -252,17 +252,23 @@ def markstein_mismatches(b, x):
 
 
 # ---- general schedule path (P ≥ 1 updates, Metropolis-within-Gibbs) ---------
-MWG_MAXD = 16
+MWG_MAXD = 32
 KIND_UNIFORM, KIND_GAUSSIAN = 1, 2
 
 
-def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None):
+PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
+DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
+
+
+def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=PRIOR_IMPROPER, factors=None):
     """One RandomWalkUpdate for run_mwg.  coords0: 0-based coordinates.
     adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW).
-    pos: None or per-coordinate positivity flags (UniformRandomWalk)."""
+    pos: None or per-coordinate positivity flags (UniformRandomWalk).
+    prior: PRIOR_*; factors: [(family, count, a, b), ...] for PRIOR_PRODUCT / PRIOR_STANDARD."""
     return {"kind": kind, "coords": [int(c) for c in coords0], "eps": None if eps is None else list(eps),
             "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt,
-            "pos": None if pos is None else [bool(x) for x in pos]}
+            "pos": None if pos is None else [bool(x) for x in pos], "prior": int(prior),
+            "factors": [] if factors is None else [tuple(f) for f in factors]}
 
 
 class MWGState:
@@ -293,7 +299,7 @@ def _mwg_tables(updates):
     nc = np.zeros(P, dtype=np.uint32)
     coords = np.zeros((P, MWG_MAXD), dtype=np.uint32)
     eps = np.zeros((P, MWG_MAXD))
-    sigma = np.zeros((P, 256))
+    sigma = np.zeros((P, MWG_MAXD * MWG_MAXD))
     adapt = np.zeros(P, dtype=np.uint32)
     ak = np.ones(P, dtype=np.uint32)
     ap = np.zeros((P, 5))
@@ -315,9 +321,32 @@ def _mwg_tables(updates):
     return kind, nc, coords, eps, sigma, adapt, ak, ap, pos
 
 
+def _prior_tables(updates):
+    P = len(updates)
+    pk = np.zeros(P, dtype=np.uint32)
+    nf = np.zeros(P, dtype=np.uint32)
+    ffam = np.zeros((P, MWG_MAXD), dtype=np.uint32)
+    fcnt = np.zeros((P, MWG_MAXD), dtype=np.uint32)
+    fa = np.zeros((P, MWG_MAXD))
+    fb = np.zeros((P, MWG_MAXD))
+    for p, u in enumerate(updates):
+        pk[p] = u.get("prior", PRIOR_IMPROPER)
+        fs = u.get("factors", [])
+        nf[p] = len(fs)
+        for k, (fam, cnt, a, b) in enumerate(fs):
+            ffam[p, k], fcnt[p, k], fa[p, k], fb[p, k] = fam, cnt, a, b
+    return pk, nf, ffam, fcnt, fa, fb
+
+
+USER_LL_FN = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_uint64,
+                         C.POINTER(C.c_double))
+
+
 def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll_mode=0, W=100, history=True,
-            nthreads=1):
-    """Advance `state` over `steps` [(mcmciter, pidx 1-based), …]; histories per step."""
+            nthreads=1, user_ll=None, user_params=None):
+    """Advance `state` over `steps` [(mcmciter, pidx 1-based), …]; histories per step.
+    user_ll: a C function pointer (ctypes) of the user target's loglikelihood, or None
+    for GsnTargetLaw; state.ll_prop receives sub_ws°.ll of every update."""
     L = lib()
     if not hasattr(L, "_mwg_ready"):
         dp, u32p, u64p, u8p = (C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
@@ -326,10 +355,14 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         L.orc_run_mwg.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, u32p, u32p, u32p, dp, dp,
                                   u8p, u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
                                   u64p, u32p, dp, dp, dp, dp, u64p, u32p, u32p, u32p, dp, u32p, dp, dp, dp, u8p,
-                                  C.c_int]
+                                  C.c_int, u32p, u32p, u32p, u32p, dp, dp, dp, C.c_void_p, dp]
         L._mwg_ready = True
     Cn, D = state.C, state.D
     kind, nc, coords, eps, sigma, adapt, ak, ap, pos = _mwg_tables(updates)
+    pk, nf, ffam, fcnt, fa, fb = _prior_tables(updates)
+    if getattr(state, "ll_prop", None) is None:
+        state.ll_prop = np.full((len(updates), state.C), np.nan)
+    up = None if user_params is None else np.ascontiguousarray(user_params, dtype=np.float64)
     steps = np.asarray(steps, dtype=np.uint32).reshape(-1, 2)
     si = np.ascontiguousarray(steps[:, 0])
     sp = np.ascontiguousarray(steps[:, 1])
@@ -345,7 +378,9 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         u64(state.N), u32(state.last_iter), _d(state.theta), _d(state.mu_p), _d(state.ll), _d(state.ra),
         u64(state.ring), u32(state.nacc), u32(state.aprop), u32(state.aacc), _d(state.eps), u32(state.faults),
         _d(hist.get("theta")), _d(hist.get("prop")), _d(hist.get("ll")),
-        None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads)
+        None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads,
+        u32(pk), u32(nf), u32(ffam), u32(fcnt), _d(fa), _d(fb), _d(state.ll_prop),
+        None if user_ll is None else C.cast(user_ll, C.c_void_p), None if up is None else _d(up))
     if rc != 0:
         raise ValueError(f"orc_run_mwg failed: {rc}")
     if history:

@@ -28,10 +28,11 @@ def make_engine(D, C, M, ups, mu, t_sigma, obs, seed, ll_mode=L.LL_PER_OBS, hist
     eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
                               steps_per_launch=spl))
     for u in ups:
+        pr = dict(prior=u.get("prior", 0), prior_factors=u.get("factors") or None)
         if u["kind"] == 1:
-            eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"], pos=u.get("pos"))
+            eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"], pos=u.get("pos"), **pr)
         else:
-            eng.add_gaussian_rw_update(u["coords"], u["sigma"], pos=u.get("pos"))
+            eng.add_gaussian_rw_update(u["coords"], u["sigma"], pos=u.get("pos"), **pr)
     eng.set_gsn_target(mu, t_sigma, obs, ll_mode=ll_mode)
     eng.set_state(np.zeros((C, D)) if theta0 is None else theta0)
     return eng
@@ -46,6 +47,7 @@ def check(oracle, eng, st, h, steps, ups, P, full=True):
     assert np.array_equal(ra, st.ra)
     assert np.array_equal(nacc, st.nacc)
     assert np.array_equal(eng.get_faults(), st.faults)
+    assert np.array_equal(eng.get_proposal_ll(), st.ll_prop, equal_nan=True)
     iters = sorted({i for i, _ in steps})
     i0, n = iters[0], iters[-1] - iters[0] + 1
     acc = eng.get_history(L.H_ACCEPT, i0, n)

@@ -39,12 +39,51 @@ def find_available_name(path, filename, disambig_num="", extension=".csv"):
         disambig_num = "1" if disambig_num == "" else str(int(disambig_num) + 1)
 
 
+def julia_float_string(x: float) -> str:
+    """Julia's ``string(::Float64)`` (Base.Ryu.writeshortest as ``show`` calls it):
+    the shortest round-trip digits d₁…dₙ (Python's repr yields the same digit
+    string) of x = 0.d₁…dₙ × 10^pt, printed in plain decimal when −4 ≤ pt − 1 ≤ 5
+    (1.0e-5, 0.0001, 100000.0, 1.0e6) and as d₁.d₂…dₙe±k otherwise; integral
+    values keep a trailing ".0", a single digit gets ".0" in scientific form
+    ("1.0e-5"), and the exponent has no "+" or padding.  NaN, Inf, -Inf as Julia."""
+    x = float(x)
+    if x != x:
+        return "NaN"
+    if x in (float("inf"), float("-inf")):
+        return "Inf" if x > 0 else "-Inf"
+    if x == 0.0:
+        return "-0.0" if str(x).startswith("-") else "0.0"
+    sign = "-" if x < 0 else ""
+    r = repr(abs(x))
+    if "e" in r:
+        m, e = r.split("e")
+        e = int(e)
+    else:
+        m, e = r, 0
+    ip, _, fp = m.partition(".")
+    digits = (ip + fp).lstrip("0")
+    # position of the decimal point relative to the first significant digit
+    pt = len(ip.lstrip("0")) + e if ip.lstrip("0") else e - (len(fp) - len(fp.lstrip("0")))
+    digits = digits.rstrip("0") or "0"
+    n = len(digits)
+    k = pt - 1  # scientific exponent
+    if -4 <= k <= 5:
+        if pt <= 0:
+            body = "0." + "0" * (-pt) + digits
+        elif pt < n:
+            body = digits[:pt] + "." + digits[pt:]
+        else:
+            body = digits + "0" * (pt - n) + ".0"
+    else:
+        body = digits[0] + "." + (digits[1:] if n > 1 else "0") + f"e{k}"
+    return sign + body
+
+
 def _fmt(x) -> str:
-    # Julia's string(::Float64) shortest round-trip form, close to Python repr
+    """One CSV entry as Julia's string interpolation writes it (callbacks.jl:249-253)."""
     if isinstance(x, (bool, np.bool_)):
         return "true" if x else "false"
-    r = repr(float(x))
-    return r.replace("inf", "Inf").replace("nan", "NaN")
+    return julia_float_string(float(x))
 
 
 class SavingCallback(Callback):

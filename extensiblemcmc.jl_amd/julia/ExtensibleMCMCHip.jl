@@ -15,6 +15,7 @@
 module ExtensibleMCMCHip
 
 using ExtensibleMCMC
+import Distributions
 const eMCMC = ExtensibleMCMC
 
 const LIB = get(ENV, "EMCMC_LIB", joinpath(@__DIR__, "..", "lib", "libemcmc.so"))
@@ -50,7 +51,8 @@ struct EmcmcUpdateDesc
     pos::Ptr{UInt8}
     adaptation_params::Ptr{Cvoid}
     sigma_b::Ptr{Float64}
-    reserved_ptr::NTuple{2,Ptr{Cvoid}}
+    prior_params::Ptr{Cvoid}          # const emcmc_prior_desc* (ProductPrior / StandardPrior)
+    reserved_ptr::Ptr{Cvoid}
     mix_lambda::Float64
     reserved_f64::NTuple{3,Float64}
 end
@@ -70,6 +72,20 @@ struct EmcmcTargetDesc
     obs::Ptr{Float64}
     ll_mode::UInt32
     reserved::UInt32
+    labels::Ptr{Float64}              # EMCMC_TARGET_LOGISTIC: y
+end
+
+struct EmcmcPriorFactor
+    family::UInt32
+    count::UInt32
+    a::Float64
+    b::Float64
+end
+
+struct EmcmcPriorDesc
+    num_factors::UInt32
+    reserved::UInt32
+    factors::Ptr{EmcmcPriorFactor}
 end
 
 struct EmcmcStep
@@ -80,7 +96,8 @@ end
 const RW_GAUSSIAN = UInt32(2)
 const RW_GAUSSIAN_MIX = UInt32(3)
 const ADPT_HAARIO = UInt32(2)
-const PRIOR_IMPROPER = UInt32(0)
+const PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
+const DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = UInt32(1), UInt32(2), UInt32(3), UInt32(4)
 const ADPT_NONE = UInt32(0)
 const TARGET_GSN = UInt32(1)
 const H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
@@ -107,6 +124,7 @@ Base.@kwdef struct MI355XBackend <: eMCMC.MCMCBackend
     history::Symbol = :full
     ll_mode::Symbol = :per_obs
     chain_moments::Bool = false   # GenericChainStats mean/cov on device (chain_statistics.jl:46-49)
+    callback_chain::Int = 1       # the chain the reference's callbacks (SavingCallback, REPLCallback) observe
 end
 
 mutable struct MI355XGlobalWorkspace{T} <: eMCMC.GlobalWorkspace{T}
@@ -116,7 +134,11 @@ mutable struct MI355XGlobalWorkspace{T} <: eMCMC.GlobalWorkspace{T}
     dim::Int
     num_updates::Int
     num_locals::Int
-    num_coords::Vector{Int}   # per update: length(updt.coords)
+    num_coords::Vector{Int}        # per update: length(updt.coords)
+    coords::Vector{Vector{Int}}    # per update: updt.coords (1-based)
+    names::Vector{String}          # per update: string(remove_curly(typeof(updt))) (workspaces.jl:474)
+    last_iter::Vector{Int}         # per update: the last mcmciter __run! handed to the device (0: none)
+    θinit::Vector{T}
 end
 
 struct MI355XLocalWorkspace{T} <: eMCMC.LocalWorkspace{T}
@@ -137,9 +159,36 @@ end
 const RW_UNIFORM = UInt32(1)
 const ADPT_UNIF_RW = UInt32(1)
 
+# priors.jl:18-88 → (EMCMC_PRIOR_*, emcmc_prior_desc pointer or C_NULL)
+_dist_factor(d::Distributions.Normal, k) = EmcmcPriorFactor(DIST_NORMAL, UInt32(k), d.μ, d.σ)
+_dist_factor(d::Distributions.Uniform, k) = EmcmcPriorFactor(DIST_UNIFORM, UInt32(k), d.a, d.b)
+_dist_factor(d::Distributions.Exponential, k) = EmcmcPriorFactor(DIST_EXPONENTIAL, UInt32(k), d.θ, 0.0)
+_dist_factor(d::Distributions.Gamma, k) = EmcmcPriorFactor(DIST_GAMMA, UInt32(k), d.α, d.θ)
+_dist_factor(d, k) = error("no device plugin for prior distribution $(typeof(d))")
+
+function _prior_desc(prior, n, keep)
+    prior isa eMCMC.ImproperPrior && return PRIOR_IMPROPER, C_NULL
+    prior isa eMCMC.ImproperPosPrior && return PRIOR_IMPROPER_POS, C_NULL
+    if prior isa eMCMC.ProductPrior
+        fs = EmcmcPriorFactor[_dist_factor(d, length(ix)) for (d, ix) in zip(prior.dists, prior.idx)]
+        kind = PRIOR_PRODUCT
+    elseif prior isa eMCMC.StandardPrior && prior.dist isa Distributions.UnivariateDistribution && n == 1
+        fs = EmcmcPriorFactor[_dist_factor(prior.dist, 1)]
+        kind = PRIOR_STANDARD
+    elseif prior isa eMCMC.StandardPrior && prior.dist isa Distributions.Product
+        fs = EmcmcPriorFactor[_dist_factor(d, 1) for d in prior.dist.v]
+        kind = PRIOR_STANDARD
+    else
+        error("no device plugin for $(typeof(prior))")
+    end
+    pd = Ref(EmcmcPriorDesc(UInt32(length(fs)), UInt32(0), pointer(fs)))
+    push!(keep, fs, pd)
+    kind, Base.unsafe_convert(Ptr{Cvoid}, pd)
+end
+
 function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
-    updt.prior isa eMCMC.ImproperPrior || error("no device plugin for $(typeof(updt.prior))")
     coords = UInt32.(collect(updt.coords) .- 1)                 # 0-based across the ABI
+    pk, pp = _prior_desc(updt.prior, length(coords), keep)
     push!(keep, coords)
     adpt, adptp = ADPT_NONE, C_NULL
     if updt.rw isa eMCMC.GaussianRandomWalk
@@ -147,8 +196,8 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
         Σ = Matrix{Float64}(updt.rw.Σ)                         # column-major already
         pos = UInt8.(updt.rw.pos)                               # log-scale coordinates (random_walk.jl:136-171)
         push!(keep, Σ, pos)
-        return EmcmcUpdateDesc(RW_GAUSSIAN, PRIOR_IMPROPER, ADPT_NONE, UInt32(length(coords)), pointer(coords),
-                               pointer(Σ), C_NULL, pointer(pos), C_NULL, C_NULL, (C_NULL, C_NULL), 0.0,
+        return EmcmcUpdateDesc(RW_GAUSSIAN, pk, ADPT_NONE, UInt32(length(coords)), pointer(coords),
+                               pointer(Σ), C_NULL, pointer(pos), C_NULL, C_NULL, pp, C_NULL, 0.0,
                                (0.0, 0.0, 0.0))
     elseif updt.rw isa eMCMC.GaussianRandomWalkMix                # random_walk.jl:193-232
         (any(updt.rw.gsn_A.pos) || any(updt.rw.gsn_B.pos)) &&
@@ -163,8 +212,8 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
         elseif !(updt.adpt isa eMCMC.NoAdaptation)
             error("no device plugin for $(typeof(updt.adpt)) with GaussianRandomWalkMix")
         end
-        return EmcmcUpdateDesc(RW_GAUSSIAN_MIX, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords),
-                               pointer(ΣA), C_NULL, C_NULL, adptp, pointer(ΣB), (C_NULL, C_NULL), updt.rw.λ,
+        return EmcmcUpdateDesc(RW_GAUSSIAN_MIX, pk, adpt, UInt32(length(coords)), pointer(coords),
+                               pointer(ΣA), C_NULL, C_NULL, adptp, pointer(ΣB), pp, C_NULL, updt.rw.λ,
                                (0.0, 0.0, 0.0))
     elseif updt.rw isa eMCMC.UniformRandomWalk                      # random_walk.jl:45-94, pos included
         ϵ = Float64.(collect(updt.rw.ϵ))
@@ -179,8 +228,8 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
         elseif !(updt.adpt isa eMCMC.NoAdaptation)
             error("no device plugin for $(typeof(updt.adpt))")
         end
-        return EmcmcUpdateDesc(RW_UNIFORM, PRIOR_IMPROPER, adpt, UInt32(length(coords)), pointer(coords), C_NULL,
-                               pointer(ϵ), pointer(pos), adptp, C_NULL, (C_NULL, C_NULL), 0.0, (0.0, 0.0, 0.0))
+        return EmcmcUpdateDesc(RW_UNIFORM, pk, adpt, UInt32(length(coords)), pointer(coords), C_NULL,
+                               pointer(ϵ), pointer(pos), adptp, C_NULL, pp, C_NULL, 0.0, (0.0, 0.0, 0.0))
     end
     error("no device plugin for $(typeof(updt.rw))")
 end
@@ -212,7 +261,8 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
     Xrm = permutedims(X)                                           # row-major view for the ABI
     GC.@preserve μ Σ Xrm begin
         t = Ref(EmcmcTargetDesc(TARGET_GSN, UInt32(d), pointer(μ), pointer(Σ), UInt64(size(X, 1)),
-                                pointer(Xrm), be.ll_mode === :per_obs ? UInt32(0) : UInt32(1), UInt32(0)))
+                                pointer(Xrm), be.ll_mode === :per_obs ? UInt32(0) : UInt32(1), UInt32(0),
+                                Ptr{Float64}(C_NULL)))
         check(ccall((:emcmc_set_target, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcTargetDesc}), h[], t),
               h[], "emcmc_set_target")
     end
@@ -220,7 +270,9 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
     check(ccall((:emcmc_set_state, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), h[], θ0, C_NULL),
           h[], "emcmc_set_state")
     ws = MI355XGlobalWorkspace{T}(h[], be, num_mcmc_steps, D, length(updates), 0,
-                                  [length(u.coords) for u in updates])
+                                  [length(u.coords) for u in updates], [collect(Int, u.coords) for u in updates],
+                                  [string(eMCMC.remove_curly(typeof(u))) for u in updates],
+                                  zeros(Int, length(updates)), copy(θinit))
     finalizer(w -> ccall((:emcmc_destroy, LIB), Cvoid, (Ptr{Cvoid},), w.handle), ws)
     ws
 end
@@ -257,6 +309,7 @@ function eMCMC.__run!(gws::MI355XGlobalWorkspace, local_wss, updates, schedule, 
             eMCMC.update_callbacks!(callbacks, gws, local_wss, step, pre)
         end
         push!(steps, EmcmcStep(UInt32(step.mcmciter), UInt32(step.pidx)))   # both 1-based across the ABI
+        gws.last_iter[step.pidx] = step.mcmciter
         if wants(step, post)
             flush!()
             eMCMC.update_callbacks!(callbacks, gws, local_wss, step, post)
@@ -406,11 +459,12 @@ struct EmcmcMoments
 end
 
 """
-    moments_window(gws, iter_first, n; split=true) -> (sums::Matrix{Float64} (D, 3), info::EmcmcMoments)
+    moments_window(gws, iter_first, n; split=true) -> (moments::Matrix{Float64} (D, 3), info::EmcmcMoments)
 
-Per-dimension sums over this shard's (split) chains of the window means, squared
-means and variances: the input of split-R̂.  Shards combine by summation
-(MPI/RCCL all-reduce across processes).
+Per-dimension moments over this shard's (split) chains of the window means and
+variances: columns m̄ (mean of the chain means), M2 = Σ(m_c − m̄)² and Σ var_c,
+the input of split-R̂.  Shards combine by Chan's pairwise merge of (count, m̄, M2)
+after an all-gather (extensible_mcmc/diagnostics.py).
 """
 function moments_window(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Integer; split::Bool=true)
     out = Matrix{Float64}(undef, gws.dim, 3)
@@ -437,6 +491,155 @@ function device_count()
     check(ccall((:emcmc_device_count, LIB), Cint, (Ref{Cint},), n), C_NULL, "emcmc_device_count")
     Int(n[])
 end
+
+
+# ---- the reference's workspace accessors, for its own callbacks -----------------
+# SavingCallback reads ws.sub_ws.state_history[i][j], ws.sub_ws.state_proposal_history[i][j],
+# local_wss[j].sub_ws.ll_history[i], local_wss[j].sub_ws°.ll_history[i] and
+# local_wss[j].acceptance_history[i] (callbacks.jl:246-256); REPLCallback calls
+# summary(ws), name_of_update, ll, ll°, llr, accepted, state and state° (callbacks.jl:
+# 276-319, workspaces.jl:244-385).  With many chains these observe one chain,
+# MI355XBackend.callback_chain, through lazy views that copy single slots from the
+# device (emcmc_get_history_chains, emcmc_get_proposal_ll).
+
+_cbchain(gws::MI355XGlobalWorkspace) = gws.backend.callback_chain
+
+# θ of the callback chain at (iter, pidx) from history `which` (EMCMC_H_STATE / H_PROPOSAL)
+function _hist_slot(gws::MI355XGlobalWorkspace, which, iter::Integer, pidx::Integer)
+    out = Array{Float64}(undef, gws.dim, 1, gws.num_updates)        # [1][P][1][D] row-major
+    check(ccall((:emcmc_get_history_chains, LIB), Cint,
+                (Ptr{Cvoid}, UInt32, UInt64, UInt64, UInt64, UInt64, Ptr{Cvoid}, Csize_t),
+                gws.handle, which, iter, 1, _cbchain(gws) - 1, 1, out, sizeof(out)),
+          gws.handle, "emcmc_get_history_chains")
+    out[:, 1, pidx]
+end
+function _ll_slot(gws::MI355XGlobalWorkspace, iter::Integer, pidx::Integer)
+    out = Array{Float64}(undef, 1, gws.num_updates)
+    check(ccall((:emcmc_get_history_chains, LIB), Cint,
+                (Ptr{Cvoid}, UInt32, UInt64, UInt64, UInt64, UInt64, Ptr{Cvoid}, Csize_t),
+                gws.handle, H_LL, iter, 1, _cbchain(gws) - 1, 1, out, sizeof(out)),
+          gws.handle, "emcmc_get_history_chains")
+    out[1, pidx]
+end
+
+"`state_history` / `state_proposal_history` of the callback chain: h[i][j] is a Vector (workspaces.jl:157-160)."
+struct HistoryView{T}
+    gws::MI355XGlobalWorkspace{T}
+    which::UInt32
+end
+struct HistoryRow{T}
+    gws::MI355XGlobalWorkspace{T}
+    which::UInt32
+    iter::Int
+end
+Base.getindex(h::HistoryView, i::Integer) = HistoryRow(h.gws, h.which, Int(i))
+Base.length(h::HistoryView) = h.gws.num_mcmc_steps
+Base.getindex(r::HistoryRow, j::Integer) = _hist_slot(r.gws, r.which, r.iter, j)
+Base.length(r::HistoryRow) = r.gws.num_updates
+Base.iterate(r::HistoryRow, j=1) = j > length(r) ? nothing : (r[j], j + 1)
+
+"The global sub-workspace view: ws.sub_ws.state, .state_history, .state_proposal_history."
+struct GlobalSubView{T}
+    gws::MI355XGlobalWorkspace{T}
+end
+function Base.getproperty(v::GlobalSubView, s::Symbol)
+    gws = getfield(v, :gws)
+    s === :state && return _chain_state(gws)
+    s === :state_history && return HistoryView(gws, H_STATE)
+    s === :state_proposal_history && return HistoryView(gws, H_PROPOSAL)
+    s === :gws && return gws
+    error("MI355X global sub-workspace has no field $s")
+end
+
+function Base.getproperty(gws::MI355XGlobalWorkspace, s::Symbol)
+    s === :sub_ws && return GlobalSubView(gws)
+    getfield(gws, s)
+end
+
+# θ of the callback chain, now
+_chain_state(gws::MI355XGlobalWorkspace) = eMCMC.state(gws)[_cbchain(gws), :]
+
+"ll_history views: sub_ws.ll_history[i] = [ll] of (i, pidx); sub_ws°.ll_history[i] stays zeros (never written, run.jl:333)."
+struct LLHistoryView{T}
+    lws::MI355XLocalWorkspace{T}
+    proposal::Bool
+end
+Base.getindex(h::LLHistoryView, i::Integer) =
+    h.proposal ? zeros(Float64, 1) : [_ll_slot(h.lws.gws, i, h.lws.pidx)]
+Base.length(h::LLHistoryView) = h.lws.gws.num_mcmc_steps
+
+struct LocalSubView{T}
+    lws::MI355XLocalWorkspace{T}
+    proposal::Bool
+end
+function Base.getproperty(v::LocalSubView, s::Symbol)
+    lws, prop = getfield(v, :lws), getfield(v, :proposal)
+    s === :ll && return prop ? [_proposal_ll(lws)] : [_current_ll(lws)]
+    s === :ll_history && return LLHistoryView(lws, prop)
+    s === :state && return prop ? _proposal_state(lws) : _chain_state(lws.gws)[lws.gws.coords[lws.pidx]]
+    error("MI355X local sub-workspace has no field $s")
+end
+
+struct AcceptanceView{T}
+    lws::MI355XLocalWorkspace{T}
+end
+function Base.getindex(a::AcceptanceView, i::Integer)
+    gws, c = a.lws.gws, _cbchain(a.lws.gws)
+    words = _history(gws, H_ACCEPT, Array{UInt64}(undef, cld(gws.backend.num_chains, 64), gws.num_updates, 1), i, 1)
+    ((words[(c - 1) >> 6 + 1, a.lws.pidx, 1] >> ((c - 1) & 63)) & 1) == 1
+end
+Base.length(a::AcceptanceView) = a.lws.gws.num_mcmc_steps
+
+function Base.getproperty(lws::MI355XLocalWorkspace, s::Symbol)
+    s === :sub_ws && return LocalSubView(lws, false)
+    s === :sub_ws° && return LocalSubView(lws, true)
+    s === :acceptance_history && return AcceptanceView(lws)
+    s === :updt_name && return getfield(lws, :gws).names[getfield(lws, :pidx)]
+    getfield(lws, s)
+end
+
+function _current_ll(lws::MI355XLocalWorkspace)
+    ll = Vector{Float64}(undef, lws.gws.backend.num_chains)
+    check(ccall((:emcmc_get_state, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), lws.gws.handle, C_NULL, ll),
+          lws.gws.handle, "emcmc_get_state")
+    ll[_cbchain(lws.gws)]
+end
+function _proposal_ll(lws::MI355XLocalWorkspace)
+    gws = lws.gws
+    out = Matrix{Float64}(undef, gws.backend.num_chains, gws.num_updates)     # [P][C] row-major
+    check(ccall((:emcmc_get_proposal_ll, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}), gws.handle, out),
+          gws.handle, "emcmc_get_proposal_ll")
+    out[_cbchain(gws), lws.pidx]
+end
+# sub_ws°.state: θ° of the update's latest proposal (its coordinates of the proposal history slot)
+function _proposal_state(lws::MI355XLocalWorkspace)
+    gws = lws.gws
+    it = gws.last_iter[lws.pidx]
+    it == 0 && return gws.θinit[gws.coords[lws.pidx]]
+    _hist_slot(gws, H_PROPOSAL, it, lws.pidx)[gws.coords[lws.pidx]]
+end
+
+# workspaces.jl:91-136, 294-385 for this backend
+eMCMC.num_mcmc_steps(gws::MI355XGlobalWorkspace) = gws.num_mcmc_steps
+eMCMC.num_updt(gws::MI355XGlobalWorkspace) = gws.num_updates
+eMCMC.state(gws::MI355XGlobalWorkspace, step) = _hist_slot(gws, H_STATE, step.mcmciter, step.pidx)
+eMCMC.state°(gws::MI355XGlobalWorkspace, step) = _hist_slot(gws, H_PROPOSAL, step.mcmciter, step.pidx)
+function eMCMC.estim_mean(gws::MI355XGlobalWorkspace)
+    gws.backend.chain_moments || error("estim_mean needs MI355XBackend(chain_moments=true)")
+    chain_moments(gws)[1][_cbchain(gws), :]
+end
+function eMCMC.estim_cov(gws::MI355XGlobalWorkspace)
+    gws.backend.chain_moments || error("estim_cov needs MI355XBackend(chain_moments=true)")
+    chain_moments(gws)[2][:, :, _cbchain(gws)]
+end
+eMCMC.accepted(lws::MI355XLocalWorkspace, i::Int) = lws.acceptance_history[i]
+eMCMC.ll(lws::MI355XLocalWorkspace) = lws.sub_ws.ll
+eMCMC.ll°(lws::MI355XLocalWorkspace) = lws.sub_ws°.ll
+eMCMC.ll(lws::MI355XLocalWorkspace, i::Int) = lws.sub_ws.ll_history[i]
+eMCMC.ll°(lws::MI355XLocalWorkspace, i::Int) = lws.sub_ws°.ll      # workspaces.jl:337 reads the current ll°
+eMCMC.state(lws::MI355XLocalWorkspace) = lws.sub_ws.state
+eMCMC.state°(lws::MI355XLocalWorkspace) = lws.sub_ws°.state
+eMCMC.name_of_update(lws::MI355XLocalWorkspace) = lws.updt_name
 
 export MI355XBackend, state_history, proposal_history, ll_history, acceptance_history, rolling_acceptance,
        adaptation_state, chain_moments, mix_state, faults, moments_window, kernel_name, device_count

@@ -37,6 +37,13 @@ def test_run_bivariate_joint_gaussian_rw(oracle, tmp_path):
     assert rows[0].startswith("1, 1, !, ") and rows[0].count("!") == 5
     vals = rows[10].split(", ")
     assert float(vals[3]) == o["theta"][10, 0, 0]
+    # the whole row as Julia's "$x, " interpolation writes it (callbacks.jl:249-253)
+    from extensible_mcmc.callbacks import julia_float_string as J
+    k = 10
+    want = (f"{k + 1}, 1, !, " + "".join(f"{J(v)}, " for v in o["theta"][k, 0]) + "!, "
+            + "".join(f"{J(v)}, " for v in o["prop"][k, 0]) + f"!, {J(o['ll'][k, 0])}, !, 0.0, !,"
+            + ("true" if o["acc"][k, 0] else "false") + ", ")
+    assert rows[k] == want
     assert any("1000.1" in l for l in lines) and any("successful" in l for l in lines)
 
 

@@ -27,6 +27,7 @@
 #include "emcmc_mix.h"
 #include "emcmc_mwg.h"
 #include "emcmc_dispatch.h"
+#include "emcmc_rtc.h"
 
 using namespace emcmc;
 
@@ -120,12 +121,17 @@ struct TargetHost {
     std::vector<double> mu, sigma, L, invdiag, obs, xbar;
     bool diag = false;
     double c0 = 0.0, S_c = 0.0;
+    // EMCMC_TARGET_USER: the law's source, hiprtc options, constants, row width
+    std::string src, opts;
+    std::vector<double> params;
+    uint32_t obs_dim = 0;
 };
 
 
 struct Variant {
     KernelFn fn = nullptr;
     MwgFn mfn = nullptr;  // general schedule kernel (mwg_gsn_kernel) when set
+    hipFunction_t ufn = nullptr;  // the same kernel with a user law, compiled at run time (emcmc_rtc.hip)
     MixFn xfn = nullptr;  // mix / chain-moments kernel (mix_gsn_kernel) when set
     ReadjustFn rfn = nullptr;  // Haario readjust kernel
     MomentsFn mofn = nullptr;  // batched chain mean/cov (mix_moments_kernel)
@@ -171,6 +177,10 @@ struct emcmc_handle {
     double *d_mu_p = nullptr, *d_eps = nullptr, *d_tL = nullptr, *d_tiL = nullptr, *d_xbar = nullptr;
     uint32_t *d_aprop = nullptr, *d_aacc = nullptr, *d_steps = nullptr;
     MwgUpdate *d_mwg = nullptr;
+    // user target (EMCMC_TARGET_USER): the loaded code object and the law's constants
+    hipModule_t umod = nullptr;
+    std::string umod_key;
+    double *d_uparams = nullptr;
     std::vector<uint32_t> last_iter;                    // per update: last iteration it ran (uniform)
     std::vector<std::vector<uint32_t>> steps_staging;   // host step lists alive until synchronize
     uint64_t steps_used = 0;
@@ -269,7 +279,7 @@ bool mix_path(const emcmc_handle *h) {
 
 // P°.θ[1:d] ← μ for every chain (workspaces.jl:225-233: P° = deepcopy(data.P))
 emcmc_status reset_mu_p(emcmc_handle *h) {
-    if (h->target.kind != EMCMC_TARGET_GSN) return EMCMC_OK;
+    if (h->target.kind != EMCMC_TARGET_GSN && h->target.kind != EMCMC_TARGET_USER) return EMCMC_OK;
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
     std::vector<double> m(C * D);
     for (uint64_t c = 0; c < C; ++c)
@@ -354,16 +364,42 @@ emcmc_status select_mwg(emcmc_handle *h) {
     size_t nmax = 1;  // largest update: the wide kernel's local vector length
     for (const auto &u : h->updates) nmax = std::max(nmax, u.coords.size());
     int best_nu = 1 << 30;
+    const bool user = h->target.kind == EMCMC_TARGET_USER;
     for (const auto &e : mwg_table()) {
+        if (user) break;
         if (e.D != D) continue;
         if (e.nu != 0 && ((size_t)e.nu < nmax || e.nu >= best_nu)) continue;  // smallest NU that fits
         if (e.nu != 0) best_nu = e.nu;
         v.mfn = full ? (ll == LL_PER_OBS ? e.full_perobs : e.full_suff)
                      : (ll == LL_PER_OBS ? e.acc_perobs : e.acc_suff);
     }
-    if (!v.mfn)
+    // a user law, or a dimension without an ahead-of-time instantiation: the
+    // same kernel compiled at run time (emcmc_rtc.hip, cached per process)
+    if (user || (!v.mfn && D <= kMwgMaxD)) {
+        RtcKernel k;
+        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, k)
+                                     : rtc_compile_gsn(D, full, ll, k);
+        if (!log.empty()) {
+            h->err = std::string(user ? "user target does not compile:\n" : "run-time kernel build failed:\n") + log;
+            return user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
+        }
+        const std::string key = k.name + '|' + k.lowered + '|' + std::to_string(std::hash<std::string>{}(
+                                    std::string(k.code.begin(), k.code.end())));
+        if (key != h->umod_key) {
+            if (h->umod) (void)hipModuleUnload(h->umod);
+            h->umod = nullptr;
+            h->umod_key.clear();
+            HIPCHK(h, hipSetDevice(h->cfg.device));
+            HIPCHK(h, hipModuleLoadData(&h->umod, k.code.data()));
+            h->umod_key = key;
+        }
+        HIPCHK(h, hipModuleGetFunction(&v.ufn, h->umod, k.lowered.c_str()));
+        v.name = k.name;
+        best_nu = 1 << 30;
+    }
+    if (!v.mfn && !v.ufn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                    "no general-schedule device kernel for D=%d (instantiated: D ∈ {1,2,3,4,8,16,32})", D);
+                    "no general-schedule device kernel for D=%d (D ≤ 32)", D);
     std::vector<MwgUpdate> tab(h->updates.size());
     for (size_t p = 0; p < h->updates.size(); ++p) {
         const UpdateHost &u = h->updates[p];
@@ -415,10 +451,12 @@ emcmc_status select_mwg(emcmc_handle *h) {
     };
     emcmc_status st;
     if ((st = upload(h->d_tL, t.L)) || (st = upload(h->d_tiL, t.invdiag)) || (st = upload(h->d_xbar, t.xbar)) ||
-        (st = upload(h->d_obs, t.obs)))
+        (st = upload(h->d_obs, t.obs)) || (st = upload(h->d_uparams, t.params)))
         return st;
     char nm[160];
-    if (best_nu < (1 << 30))
+    if (v.ufn)
+        snprintf(nm, sizeof nm, "%s", v.name.c_str());
+    else if (best_nu < (1 << 30))
         snprintf(nm, sizeof nm, "mwg_wide_kernel<D=%d,NU=%d,P=%zu,%s,%s>", D, best_nu, h->updates.size(),
                  full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT");
     else
@@ -541,6 +579,14 @@ emcmc_status select_variant(emcmc_handle *h) {
         if (u.kernel == EMCMC_MALA) return select_mala(h);
     if (h->target.kind == EMCMC_TARGET_LOGISTIC)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "the logistic-regression target runs on device with MALA only");
+    if (h->target.kind == EMCMC_TARGET_USER) {
+        for (const auto &u : h->updates)
+            if (u.kernel == EMCMC_RW_GAUSSIAN_MIX)
+                return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "GaussianRandomWalkMix runs on device with GsnTargetLaw only");
+        if (h->cfg.chain_moments)
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "chain moments on device need GsnTargetLaw");
+        return select_mwg(h);
+    }
     if (mix_path(h)) return select_mix(h);
     for (const auto &u : h->updates)
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX)
@@ -987,6 +1033,7 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.iLt = h->d_tiL;
     a.xbar = h->d_xbar;
     a.obs = h->d_obs;
+    a.user_params = h->d_uparams;
     a.C = C;
     a.row_bytes = h->row_bytes;
     a.chain0 = (uint32_t)h->cfg.first_chain_id;
@@ -1030,8 +1077,12 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             HIPCHK(h, hipEventRecord(e0, h->stream));
         }
         void *args[] = {&a};
-        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mfn), grid, block, args, h->lds_bytes,
-                                  h->stream));
+        if (h->var.ufn)
+            HIPCHK(h, hipModuleLaunchKernel(h->var.ufn, grid.x, 1, 1, block.x, 1, 1, (unsigned)h->lds_bytes, h->stream,
+                                            args, nullptr));
+        else
+            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mfn), grid, block, args, h->lds_bytes,
+                                      h->stream));
         if (h->timing) {
             HIPCHK(h, hipEventRecord(e1, h->stream));
             h->ev.emplace_back(e0, e1);
@@ -1287,6 +1338,64 @@ emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t) {
     return select_variant(h);
 }
 
+emcmc_status emcmc_set_user_target(emcmc_handle *h, const emcmc_user_target_desc *t) {
+    if (!h || !t) return EMCMC_INVALID_ARG;
+    if (!t->source) return fail(h, EMCMC_INVALID_ARG, "user target: null source");
+    if (t->dim != h->cfg.dim)
+        return fail(h, EMCMC_INVALID_ARG, "user target: dim %u != D %u (the law's θ is the chain state)", t->dim,
+                    h->cfg.dim);
+    if (t->dim > (uint32_t)kMwgMaxD)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "user target: D=%u > %d (general schedule kernel)", t->dim, kMwgMaxD);
+    if ((t->num_obs && (!t->obs || t->obs_dim == 0)) || (t->num_params && !t->params))
+        return fail(h, EMCMC_INVALID_ARG, "user target: null obs / params");
+    if (t->num_obs > 0xFFFFFFFFull) return fail(h, EMCMC_INVALID_ARG, "user target: more than 2^32-1 observations");
+    TargetHost th;
+    th.kind = EMCMC_TARGET_USER;
+    th.dim = t->dim;
+    th.nobs = t->num_obs;
+    th.obs_dim = t->obs_dim;
+    th.mu.assign(t->dim, 0.0);
+    if (t->theta0) th.mu.assign(t->theta0, t->theta0 + t->dim);
+    if (t->num_obs) th.obs.assign(t->obs, t->obs + t->num_obs * t->obs_dim);
+    if (t->num_params) th.params.assign(t->params, t->params + t->num_params);
+    th.src = t->source;
+    th.opts = t->options ? t->options : "";
+    th.diag = true;
+    h->target = std::move(th);
+    h->target_set = true;
+    if (h->allocated) {  // P° = deepcopy(data.P)
+        emcmc_status st = reset_mu_p(h);
+        if (st) return st;
+    }
+    if (h->updates.empty()) {  // compile now, so errors surface here; select_variant reuses the cache
+        RtcKernel k;
+        const std::string log = rtc_compile_user(h->target.src, h->target.opts, (int)t->dim,
+                                                 h->cfg.history_mode == EMCMC_HIST_FULL, k);
+        if (!log.empty()) {
+            h->err = "user target does not compile:\n" + log;
+            h->target_set = false;
+            return EMCMC_INVALID_ARG;
+        }
+        return EMCMC_OK;
+    }
+    emcmc_status st = select_variant(h);
+    if (st == EMCMC_INVALID_ARG) h->target_set = false;
+    return st;
+}
+
+emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const char *options, char *log_out,
+                                     size_t log_len) {
+    if (!source) return EMCMC_INVALID_ARG;
+    RtcKernel k;
+    const std::string log = rtc_compile_user(source, options ? options : "", (int)dim, true, k);
+    if (log_out && log_len) {
+        const size_t n = std::min(log.size(), log_len - 1);
+        std::memcpy(log_out, log.data(), n);
+        log_out[n] = '\0';
+    }
+    return log.empty() ? EMCMC_OK : EMCMC_INVALID_ARG;
+}
+
 emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {
     if (!h || !theta) return EMCMC_INVALID_ARG;
     emcmc_status st = ensure_alloc(h);
@@ -1352,7 +1461,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     if (!h || (!steps && num_steps)) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
     if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
-    if (!h->var.fn && !h->var.mfn && !h->var.xfn && !h->var.afn)
+    if (!h->var.fn && !h->var.mfn && !h->var.ufn && !h->var.xfn && !h->var.afn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
     if (!h->d_zig) return fail(h, EMCMC_STATE_ERROR, "state not allocated");
     const uint32_t P = (uint32_t)h->updates.size();
@@ -1362,7 +1471,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
             return fail(h, EMCMC_INVALID_ARG, "step %llu: mcmciter %u outside 1..M", (unsigned long long)i,
                         steps[i].mcmciter);
     }
-    if (h->var.mfn) return run_mwg(h, steps, num_steps);
+    if (h->var.mfn || h->var.ufn) return run_mwg(h, steps, num_steps);
     if (h->var.xfn) return run_mix(h, steps, num_steps);
     if (h->var.afn) return run_mala(h, steps, num_steps);
     const uint64_t C = h->cfg.num_chains;
@@ -1479,9 +1588,10 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
                     h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts,
-                    h->d_ll_prop};
+                    h->d_ll_prop,   h->d_uparams};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    if (h->umod) (void)hipModuleUnload(h->umod);
     if (h->h_fault_flag) (void)hipHostFree(h->h_fault_flag);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;

@@ -27,8 +27,10 @@
 // pairwise tree over adjacent blocks (odd tail carried up).  See DESIGN.md.
 #pragma once
 
+#ifndef __HIPCC_RTC__
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#endif
 
 #include "emcmc_math.h"
 

@@ -20,9 +20,20 @@
 // "Hard parts" 1), so the stream is defined here and shared with oracle/.
 #pragma once
 
+#ifndef __HIPCC_RTC__  // hiprtc (user targets, emcmc_user.cpp) provides its own builtins
 #include <stddef.h>
 #include <stdint.h>
 #include <math.h>
+#else
+typedef unsigned char uint8_t;
+typedef unsigned short uint16_t;
+typedef unsigned int uint32_t;
+typedef unsigned long uint64_t;
+typedef int int32_t;
+typedef long int64_t;
+typedef __SIZE_TYPE__ size_t;
+#define offsetof(t, m) __builtin_offsetof(t, m)
+#endif
 
 #include "emcmc_tables.h"
 
@@ -399,6 +410,7 @@ struct ZigTabs {
     const double *ef;
 };
 EMCMC_HD ZigTabs zig_tabs(const Ziggurat &z) { return ZigTabs{z.n, z.nf, z.e, z.ef}; }
+#ifndef __HIPCC_RTC__  // host-side table construction
 inline void build_ziggurat(Ziggurat &z) {
     {  // N(0,1), f(x) = exp(−x²/2): strips x_{L−1} = r down to x_1, then x_0 = 0
         constexpr int L = kZigNL;
@@ -438,6 +450,7 @@ inline void build_ziggurat(Ziggurat &z) {
         }
     }
 }
+#endif
 
 struct ZigDraw {
     uint32_t off;   // byte offset of the layer's ZigEntry (layer · 16)

@@ -36,7 +36,7 @@
 //                       Exponential, Gamma factors; llr adds lp(θ°) − lp(θ)
 //                                                   priors.jl:18-88, run.jl:374-385
 //   loglikelihood       a target policy: GsnTargetLaw (gsn_target.jl:23-29) or a
-//                       user device function compiled at run time (emcmc_user.h)
+//                       user device function compiled at run time (emcmc_rtc.h)
 #pragma once
 
 #include "emcmc_kernels.h"

@@ -1,0 +1,44 @@
+// emcmc_rtc.h — run-time compilation of user log-likelihoods (hiprtc).
+//
+// The reference's plugin surface for a target is a Julia type with
+// `set_parameters!(P, idx, θ)` and `loglikelihood(P, obs)`
+// (src/example/gsn_target.jl:15-29, docs/src/get_started/basic_use.md:84-112);
+// any law the user writes drops into `compute_ll!` (run.jl:251-260).  On the
+// device the law is a function of P°.θ, written once in a C subset that both
+// hiprtc (here) and gcc (the oracle, oracle/user_prelude.h) compile:
+//
+//     EMCMC_USER_LOGLIK {            // theta[D], D, obs, nobs, params in scope
+//         double s = 0.0;
+//         for (uint64_t k = 0; k < nobs; ++k) s = s + em_log(obs[k] * theta[0]);
+//         return s;
+//     }
+//
+// with + − × ÷, fma, sqrt, fabs, copysign and em_exp / em_log (the engine's
+// own exp/log, restated bit for bit in oracle/oracle_math.h).  The source is
+// compiled into the general schedule kernel (emcmc_mwg.h) with TGT = the
+// user's law, so every update kind, prior and adaptation of that kernel runs
+// with it.
+#pragma once
+
+#include <string>
+#include <vector>
+
+namespace emcmc {
+
+struct RtcKernel {
+    std::vector<char> code;  // gfx950 code object
+    std::string lowered;     // mangled kernel name inside it
+    std::string name;        // readable name for emcmc_kernel_name
+};
+
+// Compile (or fetch from the process-wide cache) the general schedule kernel
+// for dimension D with the user's log-likelihood: mwg_gsn_kernel<D> for
+// D ≤ 16, mwg_wide_kernel<D, D> for 16 < D ≤ 32.  Returns "" on success,
+// else the compiler's log.
+std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, RtcKernel &out);
+
+// The same kernel with the built-in GsnTargetLaw (emcmc_mwg.h GsnTarget) for a
+// dimension the library has no ahead-of-time instantiation of (inst_mwg.hip).
+std::string rtc_compile_gsn(int D, bool full, int ll_mode, RtcKernel &out);
+
+}  // namespace emcmc

@@ -1,0 +1,140 @@
+// emcmc_rtc.hip — hiprtc driver for user log-likelihoods (see emcmc_rtc.h).
+//
+// The kernel headers are embedded at build time (build/gen/rtc_headers.inc,
+// scripts/embed_headers.py); the user's source is wrapped between a prelude
+// that defines EMCMC_USER_LOGLIK / em_exp / em_log and an epilogue that turns
+// the function into the kernel's target policy (emcmc_mwg.h GsnTarget's
+// interface).  Code objects are cached per (source, options, D, history mode)
+// for the life of the process, so shards and repeated runs compile once.
+#include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
+
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "emcmc_rtc.h"
+#include "rtc_headers.inc"
+
+namespace emcmc {
+namespace {
+
+const char *const kPrelude = R"EMCMC_RTC(#include "emcmc_mwg.h"
+#define EMCMC_USER_LOGLIK                                                                                  \
+    extern "C" __device__ __attribute__((always_inline)) inline double emcmc_user_loglik(                 \
+        const double *__restrict__ theta, int D, const double *__restrict__ obs, uint64_t nobs,            \
+        const double *__restrict__ params)
+#define em_exp(x) emcmc::exp_any(x)
+#define em_log(x) emcmc::log_any(x)
+#line 1 "user_target"
+)EMCMC_RTC";
+
+const char *const kEpilogue = R"EMCMC_RTC(
+namespace emcmc {
+// loglikelihood(P°, obs) of the user's law (gsn_target.jl:23-29's interface)
+struct UserTarget {
+    template <int D, int LLMODE, bool ROLL = false>
+    __device__ __forceinline__ static double loglik(const MwgParams &a, const double (&mp)[D]) {
+        return emcmc_user_loglik(mp, D, a.obs, (uint64_t)a.nobs, a.user_params);
+    }
+};
+}  // namespace emcmc
+)EMCMC_RTC";
+
+std::mutex g_mu;
+std::map<std::string, RtcKernel> g_cache;
+
+std::string program_log(hiprtcProgram p) {
+    size_t n = 0;
+    if (hiprtcGetProgramLogSize(p, &n) != HIPRTC_SUCCESS || n == 0) return "";
+    std::string s(n, '\0');
+    if (hiprtcGetProgramLog(p, &s[0]) != HIPRTC_SUCCESS) return "";
+    while (!s.empty() && s.back() == '\0') s.pop_back();
+    return s;
+}
+
+}  // namespace
+
+// src empty: the built-in GsnTarget with likelihood mode ll; else the user's law
+std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, RtcKernel &out) {
+    if (D < 1 || D > 32) return "the general schedule kernel runs 1 ≤ D ≤ 32";
+    const bool user = !src.empty();
+    std::ostringstream key;
+    key << D << '|' << full << '|' << ll << '|' << opts << '|' << src;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_cache.find(key.str());
+        if (it != g_cache.end()) {
+            out = it->second;
+            return "";
+        }
+    }
+    std::ostringstream expr, name;
+    const char *fl = full ? "true" : "false";
+    const char *tgt = user ? "emcmc::UserTarget" : "emcmc::GsnTarget";
+    if (D <= 16) {
+        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ">";
+        name << "mwg_gsn_kernel<D=" << D;
+    } else {
+        expr << "emcmc::mwg_wide_kernel<" << D << ", " << D << ", " << fl << ", " << ll << ", " << tgt << ">";
+        name << "mwg_wide_kernel<D=" << D << ",NU=" << D;
+    }
+    name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << "[hiprtc]>";
+    const std::string prog_src =
+        user ? std::string(kPrelude) + src + "\n" + kEpilogue : std::string("#include \"emcmc_mwg.h\"\n");
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, prog_src.c_str(), user ? "user_target.hip" : "gsn_target.hip", kRtcHeaderCount,
+                            kRtcHeaderSrc, kRtcHeaderNames) != HIPRTC_SUCCESS)
+        return "hiprtcCreateProgram failed";
+    const std::string ex = expr.str();
+    hiprtcAddNameExpression(prog, ex.c_str());
+    // -ffp-contract=off: the parity contract with oracle/ (no implicit fma)
+    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    {
+        std::istringstream is(opts);
+        for (std::string w; is >> w;) o.push_back(w);
+    }
+    std::vector<const char *> ov;
+    for (const auto &s : o) ov.push_back(s.c_str());
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)ov.size(), ov.data());
+    std::string log = program_log(prog);
+    if (rc != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        return std::string("hiprtc: ") + hiprtcGetErrorString(rc) + "\n" + log;
+    }
+    RtcKernel k;
+    const char *low = nullptr;
+    size_t n = 0;
+    if (hiprtcGetLoweredName(prog, ex.c_str(), &low) != HIPRTC_SUCCESS || !low ||
+        hiprtcGetCodeSize(prog, &n) != HIPRTC_SUCCESS || n == 0) {
+        hiprtcDestroyProgram(&prog);
+        return "hiprtc: no code object for " + ex;
+    }
+    k.lowered = low;
+    k.code.resize(n);
+    if (hiprtcGetCode(prog, k.code.data()) != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        return "hiprtcGetCode failed";
+    }
+    hiprtcDestroyProgram(&prog);
+    k.name = name.str();
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_cache[key.str()] = k;
+    }
+    out = std::move(k);
+    return "";
+}
+
+std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, RtcKernel &out) {
+    if (src.empty()) return "empty user source";
+    return rtc_compile(src, opts, D, full, 0, out);
+}
+
+std::string rtc_compile_gsn(int D, bool full, int ll_mode, RtcKernel &out) { return rtc_compile("", "", D, full, ll_mode, out); }
+
+}  // namespace emcmc

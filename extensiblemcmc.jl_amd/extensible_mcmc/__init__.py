@@ -16,7 +16,7 @@ from .kernels import (AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMi
 from .mcmc import (MCMC, GenericMCMCBackend, MI355XBackend, MI355XGlobalWorkspace, MI355XLocalWorkspace,
                    create_workspaces, get_decorators, init, run, run_)
 from .schedule import JRange, MCMCSchedule, Step, reschedule, reschedule_
-from .targets import GsnTargetLaw, LogisticRegressionLaw, make_data
+from .targets import GsnTargetLaw, LogisticRegressionLaw, UserTargetLaw, make_data
 from ._lib import EMCMCError, device_count
 
 __all__ = [
@@ -25,5 +25,5 @@ __all__ = [
     "GsnTargetLaw", "run", "run_", "get_decorators", "isdecorator", "ImproperPosPrior", "ImproperPrior",
     "SavingCallback", "REPLCallback", "MCMCSchedule", "JRange", "reschedule", "Engine", "EngineConfig",
     "EMCMCError", "device_count", "rhat_from_moments", "allgather_moments", "merge_moments", "MALAUpdate", "LogisticRegressionLaw",
-    "StandardPrior", "ProductPrior", "Normal", "Uniform", "Exponential", "Gamma", "Product",
+    "StandardPrior", "ProductPrior", "Normal", "Uniform", "Exponential", "Gamma", "Product", "UserTargetLaw",
 ]

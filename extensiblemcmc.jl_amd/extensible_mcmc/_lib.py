@@ -41,7 +41,7 @@ RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA = 1, 2, 3, 4
 PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
 DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
 ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO = 0, 1, 2
-TARGET_GSN, TARGET_LOGISTIC = 1, 2
+TARGET_GSN, TARGET_LOGISTIC, TARGET_USER = 1, 2, 3
 LL_PER_OBS, LL_SUFFSTAT = 0, 1
 HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
 H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = 0, 1, 2, 3
@@ -139,6 +139,21 @@ class EmcmcTargetDesc(C.Structure):
     ]
 
 
+class EmcmcUserTargetDesc(C.Structure):
+    """A user law compiled at run time (include/emcmc.h emcmc_user_target_desc)."""
+    _fields_ = [
+        ("dim", C.c_uint32),
+        ("obs_dim", C.c_uint32),
+        ("theta0", C.POINTER(C.c_double)),
+        ("num_obs", C.c_uint64),
+        ("obs", C.POINTER(C.c_double)),
+        ("num_params", C.c_uint64),
+        ("params", C.POINTER(C.c_double)),
+        ("source", C.c_char_p),
+        ("options", C.c_char_p),
+    ]
+
+
 class EmcmcStep(C.Structure):
     _fields_ = [("mcmciter", C.c_uint32), ("pidx", C.c_uint32)]
 
@@ -160,6 +175,8 @@ SIGNATURES = {
     "emcmc_create": (_ST, [C.POINTER(_H), C.POINTER(EmcmcConfig)]),
     "emcmc_add_update": (_ST, [_H, C.POINTER(EmcmcUpdateDesc)]),
     "emcmc_set_target": (_ST, [_H, C.POINTER(EmcmcTargetDesc)]),
+    "emcmc_set_user_target": (_ST, [_H, C.POINTER(EmcmcUserTargetDesc)]),
+    "emcmc_check_user_target": (_ST, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_size_t]),
     "emcmc_set_state": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_run": (_ST, [_H, C.POINTER(EmcmcStep), C.c_uint64]),
     "emcmc_synchronize": (_ST, [_H]),
@@ -264,6 +281,15 @@ def probe_log(x, device: int = 0):
     if st != OK:
         raise EMCMCError(st, "emcmc_probe_log")
     return y
+
+
+def check_user_target(source: str, dim: int, options: str = "") -> None:
+    """Compile-only check of a user log-likelihood (hiprtc; no device needed).
+    Raises EMCMCError(INVALID_ARG) carrying the compiler log."""
+    buf = C.create_string_buffer(1 << 16)
+    st = lib().emcmc_check_user_target(source.encode(), dim, options.encode(), buf, len(buf))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_check_user_target", buf.value.decode(errors="replace"))
 
 
 def device_count() -> int:

@@ -232,6 +232,26 @@ class Engine:
         t.ll_mode = ll_mode
         self._check(self._lib.emcmc_set_target(self._h, C.byref(t)), "emcmc_set_target")
 
+    def set_user_target(self, source: str, obs=None, params=None, theta0=None, options: str = ""):
+        """A user law: ``loglikelihood(P, obs)`` as an EMCMC_USER_LOGLIK source
+        compiled for the device (include/emcmc.h emcmc_user_target_desc)."""
+        D = self.cfg.dim
+        X = np.zeros((0, 1)) if obs is None else np.asarray(obs, dtype=np.float64)
+        X = np.ascontiguousarray(X.reshape(X.shape[0], max(1, int(np.prod(X.shape[1:])))) if X.ndim > 1 else X.reshape(-1, 1))
+        prm = np.ascontiguousarray(np.zeros(0) if params is None else np.asarray(params, dtype=np.float64).ravel())
+        th0 = np.ascontiguousarray(np.zeros(D) if theta0 is None else np.asarray(theta0, dtype=np.float64).ravel())
+        t = L.EmcmcUserTargetDesc()
+        t.dim = D
+        t.obs_dim = X.shape[1]
+        t.theta0 = L.dptr(th0)
+        t.num_obs = X.shape[0]
+        t.obs = L.dptr(X) if X.size else None
+        t.num_params = prm.size
+        t.params = L.dptr(prm) if prm.size else None
+        t.source = source.encode()
+        t.options = options.encode()
+        self._check(self._lib.emcmc_set_user_target(self._h, C.byref(t)), "emcmc_set_user_target")
+
     def set_state(self, theta, ll=None):
         th = np.ascontiguousarray(theta, dtype=np.float64).reshape(self.cfg.num_chains, self.cfg.dim)
         llp = None

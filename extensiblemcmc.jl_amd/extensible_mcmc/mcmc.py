@@ -22,7 +22,7 @@ from . import _lib as L
 from .engine import Engine, EngineConfig
 from .kernels import (MCMCBackend, MCMCUpdate, PostMCMCStep, PreMCMCStep, UnsupportedPlugin, isdecorator)
 from .schedule import MCMCSchedule, Step
-from .targets import GsnTargetLaw, LogisticRegressionLaw
+from .targets import GsnTargetLaw, LogisticRegressionLaw, UserTargetLaw
 
 _HIST = {"full": L.HIST_FULL, "accept_only": L.HIST_ACCEPT_ONLY}
 _LL = {"per_obs": L.LL_PER_OBS, "suffstat": L.LL_SUFFSTAT}
@@ -168,7 +168,7 @@ def init_global_workspace(backend: MCMCBackend, num_mcmc_steps: int, updates, da
         raise UnsupportedPlugin(
             f"backend {type(backend).__name__} has no device implementation; use MI355XBackend")
     P = data["P"]
-    if not isinstance(P, (GsnTargetLaw, LogisticRegressionLaw)):
+    if not isinstance(P, (GsnTargetLaw, LogisticRegressionLaw, UserTargetLaw)):
         raise UnsupportedPlugin(f"target law {type(P).__name__} has no device plugin yet")
     th0 = np.asarray(theta_init, dtype=float)
     D = th0.shape[-1]

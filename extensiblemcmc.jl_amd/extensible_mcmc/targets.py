@@ -58,6 +58,32 @@ class LogisticRegressionLaw:
         engine.set_logistic_target(X, y)
 
 
+class UserTargetLaw:
+    """A user-defined target law (the reference's plugin surface for laws:
+    ``set_parameters!(P, idx, θ)`` + ``loglikelihood(P, obs)``,
+    gsn_target.jl:15-29, docs/src/get_started/basic_use.md:84-112).
+
+    ``source`` is the law's log-likelihood as an ``EMCMC_USER_LOGLIK { … }``
+    function body over ``theta`` (P.θ, length d), ``obs``/``nobs`` and
+    ``params`` (include/emcmc.h emcmc_user_target_desc); the engine compiles it
+    for the device with hiprtc.  ``set_parameters`` keeps the reference's
+    meaning: P.θ[idx] ← θ (the device does the same on P° every update)."""
+
+    def __init__(self, source: str, theta, params=None, options: str = ""):
+        self.source = source
+        self.theta = np.atleast_1d(np.asarray(theta, dtype=float)).copy()
+        self.d = self.theta.size
+        self.params = None if params is None else np.asarray(params, dtype=float)
+        self.options = options
+
+    def set_parameters(self, loc2glob_idx, theta):
+        idx = np.asarray(loc2glob_idx, dtype=int) - 1
+        self.theta[idx] = theta
+
+    def to_device(self, engine, ll_mode, obs):
+        engine.set_user_target(self.source, obs=obs, params=self.params, theta0=self.theta, options=self.options)
+
+
 def make_data(P, obs):
     """The ``data = (P = …, obs = …)`` NamedTuple of the reference (basic_use.md:112)."""
     return {"P": P, "obs": np.asarray(obs, dtype=float)}

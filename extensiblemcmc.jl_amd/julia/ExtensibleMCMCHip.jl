@@ -75,6 +75,19 @@ struct EmcmcTargetDesc
     labels::Ptr{Float64}              # EMCMC_TARGET_LOGISTIC: y
 end
 
+# include/emcmc.h emcmc_user_target_desc: a user law compiled at run time (hiprtc)
+struct EmcmcUserTargetDesc
+    dim::UInt32
+    obs_dim::UInt32
+    theta0::Ptr{Float64}
+    num_obs::UInt64
+    obs::Ptr{Float64}
+    num_params::UInt64
+    params::Ptr{Float64}
+    source::Cstring
+    options::Cstring
+end
+
 struct EmcmcPriorFactor
     family::UInt32
     count::UInt32
@@ -101,6 +114,42 @@ const DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = UInt32(1), UInt3
 const ADPT_NONE = UInt32(0)
 const TARGET_GSN = UInt32(1)
 const H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
+
+"""
+    HipTargetLaw(source, θ; params = Float64[], options = "")
+
+A user-defined target law for `MI355XBackend`: the law's parameter vector θ
+(`set_parameters!(P, idx, θ)` writes into it, as for any law of the reference,
+src/example/gsn_target.jl:15-21) and its `loglikelihood(P, obs)` written as an
+`EMCMC_USER_LOGLIK { … }` body (include/emcmc.h emcmc_user_target_desc), which the
+engine compiles for the device.  `obs` is the `data.obs` vector of observation
+vectors (all of one length).
+"""
+struct HipTargetLaw{T}
+    θ::Vector{T}
+    source::String
+    params::Vector{Float64}
+    options::String
+end
+HipTargetLaw(source::String, θ::Vector{T}; params = Float64[], options = "") where {T} =
+    HipTargetLaw{T}(copy(θ), source, Float64.(params), options)
+function eMCMC.set_parameters!(P::HipTargetLaw, loc2glob_idx, θ)
+    P.θ[loc2glob_idx] .= θ
+end
+
+function _set_user_target(h, P::HipTargetLaw, obs)
+    X = isempty(obs) ? zeros(0, 1) : reduce(vcat, permutedims.(obs))   # n×w
+    Xrm = permutedims(X)                                                # row-major for the ABI
+    θ0 = Float64.(P.θ)
+    GC.@preserve X Xrm θ0 P begin
+        t = Ref(EmcmcUserTargetDesc(UInt32(length(θ0)), UInt32(size(X, 2)), pointer(θ0), UInt64(size(X, 1)),
+                                    isempty(Xrm) ? Ptr{Float64}(C_NULL) : pointer(Xrm), UInt64(length(P.params)),
+                                    isempty(P.params) ? Ptr{Float64}(C_NULL) : pointer(P.params),
+                                    Base.unsafe_convert(Cstring, P.source), Base.unsafe_convert(Cstring, P.options)))
+        check(ccall((:emcmc_set_user_target, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcUserTargetDesc}), h, t),
+              h, "emcmc_set_user_target")
+    end
+end
 
 function check(st, h, where)
     st == 0 && return nothing
@@ -254,6 +303,9 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
         end
     end
     P = data.P
+    if P isa HipTargetLaw
+        _set_user_target(h[], P, data.obs)
+    else
     d = length(P.θ) == 0 ? 0 : Int(round((sqrt(1 + 4length(P.θ)) - 1) / 2))  # θ = [μ; vec Σ]
     μ = P.θ[1:d]
     Σ = reshape(P.θ[(d+1):end], d, d)
@@ -265,6 +317,7 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
                                 Ptr{Float64}(C_NULL)))
         check(ccall((:emcmc_set_target, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcTargetDesc}), h[], t),
               h[], "emcmc_set_target")
+    end
     end
     θ0 = repeat(Float64.(θinit), be.num_chains)                     # [C][D] row-major
     check(ccall((:emcmc_set_state, LIB), Cint, (Ptr{Cvoid}, Ptr{Float64}, Ptr{Float64}), h[], θ0, C_NULL),

@@ -86,6 +86,7 @@ typedef enum emcmc_status {
 /* Targets — src/example/gsn_target.jl */
 #define EMCMC_TARGET_GSN 1u     /* GsnTargetLaw(μ, Σ) with coords ⊆ μ */
 #define EMCMC_TARGET_LOGISTIC 2u /* logistic regression: obs = X (n×d), labels = y (n), ℓ = Σ y·η − log(1+e^η) */
+#define EMCMC_TARGET_USER 3u     /* a user law compiled at run time (emcmc_set_user_target) */
 
 /* How the Gaussian log-likelihood Σ_k logpdf(N(μ,Σ), x_k) is evaluated. */
 #define EMCMC_LL_PER_OBS 0u   /* literal gsn_target.jl:23-29: one sqmahal per observation */
@@ -228,6 +229,35 @@ typedef struct emcmc_target_desc {
     const double *labels; /* EMCMC_TARGET_LOGISTIC: y, n doubles (0/1 or any real) */
 } emcmc_target_desc;
 
+/* A user-defined target law: `data = (P = MyLaw(θ), obs = …)` with the law's
+ * `set_parameters!(P, idx, θ)` + `loglikelihood(P, obs)` (the plugin surface of
+ * src/example/gsn_target.jl:15-29 and docs/src/get_started/basic_use.md:84-112).
+ * set_parameters! is the engine's P°.θ[coords] ← θ° (updates.jl:198-205, P°
+ * starting at theta0 as deepcopy(data.P), workspaces.jl:225-233); loglikelihood
+ * is `source`, compiled with hiprtc for gfx950 into the general schedule kernel:
+ *
+ *     EMCMC_USER_LOGLIK {   // in scope: const double *theta (P°.θ, D entries), int D,
+ *         …                 //   const double *obs (num_obs × obs_dim), uint64_t nobs,
+ *         return ll;        //   const double *params (num_params)
+ *     }
+ *
+ * in the C subset both hiprtc and a C compiler accept: + − × ÷, fma, sqrt, fabs,
+ * copysign, em_exp(x), em_log(x) (the engine's exp / log; oracle/user_prelude.h
+ * maps them to their CPU restatement).  Every update kind, prior and adaptation
+ * of the general kernel runs with it; D ≤ 32.  GaussianRandomWalkMix and MALA
+ * raise EMCMC_UNSUPPORTED_PLUGIN with a user target. */
+typedef struct emcmc_user_target_desc {
+    uint32_t dim;           /* length(P.θ) = D */
+    uint32_t obs_dim;       /* doubles per observation row (the source's business) */
+    const double *theta0;   /* P.θ at construction (NULL: zeros) */
+    uint64_t num_obs;
+    const double *obs;      /* num_obs × obs_dim, row-major */
+    uint64_t num_params;
+    const double *params;   /* constants of the law (NULL if none) */
+    const char *source;     /* EMCMC_USER_LOGLIK { … } */
+    const char *options;    /* extra hiprtc options (e.g. "-DN_FEATURES=4"), or NULL */
+} emcmc_user_target_desc;
+
 /* One element of the `MCMCSchedule` iteration (src/schedule.jl:56-66). */
 typedef struct emcmc_step {
     uint32_t mcmciter;  /* 1-based */
@@ -262,6 +292,19 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u);
 /* Replaces set_parameters!(P::GsnTargetLaw, …) + loglikelihood(P, obs)
  * (gsn_target.jl:15-29): uploads observations and the factorised Σ. */
 emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t);
+
+/* Replaces set_parameters!(P::MyLaw, …) + loglikelihood(P::MyLaw, obs) of a
+ * user-defined law (gsn_target.jl:15-29 is the reference's example of the
+ * interface): compiles `source` for gfx950 (hiprtc; cached per process) and
+ * uploads obs / params.  A compile error returns EMCMC_INVALID_ARG with the
+ * compiler log in emcmc_last_error. */
+emcmc_status emcmc_set_user_target(emcmc_handle *h, const emcmc_user_target_desc *t);
+
+/* Compile-only check of a user log-likelihood for dimension dim (no device
+ * needed): EMCMC_OK, or EMCMC_INVALID_ARG with the compiler log in log_out
+ * (truncated to log_len bytes, NUL-terminated; log_out may be NULL). */
+emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const char *options, char *log_out,
+                                     size_t log_len);
 
 /* θinit for every chain (row-major [C][D]); ll = NULL means the reference's
  * initial ll = -Inf (workspaces.jl:425), i.e. the first step always accepts.

@@ -687,7 +687,9 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
     orc_mwg_update *U = (orc_mwg_update *)calloc(P, sizeof(orc_mwg_update));
     if (!g || !U) return -3;
     /* target constants (the rw Σ argument is unused here: pass Σ_t twice) */
-    int rc = gsn_prepare(g, D, t_sigma, t_sigma, nobs, obs, ll_mode | 0x100);
+    /* a user target's observation rows have their own width: the Gaussian
+     * constants are not used then, so they are built over no observations */
+    int rc = gsn_prepare(g, D, t_sigma, t_sigma, user_ll ? 0 : nobs, obs, ll_mode | 0x100);
     if (rc) {
         free(g);
         free(U);

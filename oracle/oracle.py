@@ -367,7 +367,13 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
     si = np.ascontiguousarray(steps[:, 0])
     sp = np.ascontiguousarray(steps[:, 1])
     n = steps.shape[0]
-    X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
+    if user_ll is None:
+        X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
+    else:  # a user law's observation rows have their own width
+        X = np.zeros((0, 1)) if obs is None else np.asarray(obs, dtype=np.float64)
+        X = np.ascontiguousarray(X.reshape(X.shape[0], max(1, int(np.prod(X.shape[1:])))) if X.ndim > 1 else X.reshape(-1, 1))
+        if t_sigma is None:
+            t_sigma = np.eye(D)
     hist = {"theta": np.empty((n, Cn, D)), "prop": np.empty((n, Cn, D)), "ll": np.empty((n, Cn)),
             "acc": np.empty((n, Cn), dtype=np.uint8)} if history else {}
     u32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))  # noqa: E731
@@ -386,6 +392,20 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
     if history:
         hist["acc"] = hist["acc"].astype(bool)
     return hist
+
+
+def user_loglik(name):
+    """The oracle build of user target tests/user_targets/<name>.c (oracle/Makefile:
+    lib/user_<name>.so, compiled with oracle/user_prelude.h): (ctypes function,
+    source text).  The engine compiles the same source for the device."""
+    so = Path(__file__).resolve().parent / "lib" / f"user_{name}.so"
+    src = Path(__file__).resolve().parent.parent / "tests" / "user_targets" / f"{name}.c"
+    if not so.exists():
+        raise ImportError(f"{so} not built (make -C oracle)")
+    dll = C.CDLL(str(so))
+    fn = USER_LL_FN(("emcmc_user_loglik", dll))
+    fn._dll = dll  # keep the library loaded
+    return fn, src.read_text()
 
 
 def uniform01(seed, chain, it, pidx0, j):

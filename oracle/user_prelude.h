@@ -1,0 +1,26 @@
+/*
+ * user_prelude.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * Host side of the user-target source protocol (include/emcmc.h
+ * emcmc_user_target_desc): a C compiler sees the same EMCMC_USER_LOGLIK source
+ * the engine compiles for the device with hiprtc, with em_exp / em_log bound to
+ * the oracle's restatement of the engine's exp / log (oracle_math.h).  The
+ * resulting function is what orc_run_mwg calls as `user_ll`
+ * (oracle/emcmc_oracle.c, orc_user_loglik_fn).  Build: oracle/Makefile
+ * (lib/user_<name>.so from tests/user_targets/<name>.c).
+ */
+#ifndef ORACLE_USER_PRELUDE_H
+#define ORACLE_USER_PRELUDE_H
+
+#include <math.h>
+#include <stdint.h>
+
+#include "oracle_math.h"
+
+#define EMCMC_USER_LOGLIK                                                                              \
+    double emcmc_user_loglik(const double *restrict theta, int D, const double *restrict obs, uint64_t nobs, \
+                             const double *restrict params)
+#define em_exp(x) orc_exp_any(x)
+#define em_log(x) orc_log_any(x)
+
+#endif

@@ -186,3 +186,37 @@ def test_gaussian_rw_positivity_restricted(oracle, joint):
     assert "mwg" in eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, len(ups))
     assert h["acc"][len(ups):].sum() > 10  # moves beyond the first step's auto-accepts
+
+
+def test_reference_schedule_kat_on_device(oracle, golden_dir):
+    """The reference's schedule KAT (test/runtests.jl:5-31) driven through the
+    general kernel: 4 updates with exclusions [(1, 3:8), (2, 4:2:10)], and at
+    (5, 3) reschedule!(schedule, 2, [4], [(5, 8:9)]) grows the schedule to 6
+    updates.  The host walks the schedule exactly as __run! does (run.jl:64-83)
+    and hands each (iter, pidx) to emcmc_run; the step list must be the KAT's and
+    every written slot, the rolling acceptance across the skipped iterations
+    and the final state must equal the oracle's run of that list."""
+    import json
+    from extensible_mcmc import JRange, reschedule
+    k = json.loads((golden_dir / "schedule_kat.json").read_text())
+    jr = lambda t: JRange(t[0], t[1], t[2])  # noqa: E731
+    D, C, M = 6, 777, k["num_mcmc_iter"]
+    rng = np.random.default_rng(11)
+    obs = rng.normal(size=(8, D))
+    mu = np.zeros(D)
+    ups = [oracle.mwg_update(1 if p % 2 else 2, [p], eps=[0.7] if p % 2 else None,
+                             sigma=None if p % 2 else [[0.5]]) for p in range(D)]
+    eng = make_engine(D, C, M, ups, mu, np.eye(D), obs, 4242)
+    sched = MCMCSchedule(M, k["num_params"], [(i, jr(r)) for i, r in k["exclude_params"]])
+    ra = k["reschedule_args"]
+    steps = []
+    for s in sched:
+        steps.append((s.mcmciter, s.pidx))
+        eng.run([(s.mcmciter, s.pidx)])
+        if [s.mcmciter, s.pidx] == k["reschedule_at"]:
+            reschedule(sched, ra["num_new_updates"], ra["idxes_to_remove"],
+                       [(i, jr(r)) for i, r in ra["idxes_to_add"]])
+    assert [list(t) for t in steps] == k["expected"]
+    st = oracle.MWGState(np.zeros((C, D)), mu, ups)
+    h = oracle.run_mwg(st, ups, seed=4242, t_sigma=np.eye(D), obs=obs, steps=steps, nthreads=8)
+    check(oracle, eng, st, h, steps, ups, D)

@@ -20,7 +20,8 @@ SHIM = ROOT / "extensiblemcmc.jl_amd" / "julia" / "ExtensibleMCMCHip.jl"
 C_NAME = {"EmcmcConfig": "emcmc_config", "EmcmcUpdateDesc": "emcmc_update_desc",
           "EmcmcHaarioAdaptation": "emcmc_haario_adaptation", "EmcmcUnifRWAdaptation": "emcmc_unifrw_adaptation",
           "EmcmcTargetDesc": "emcmc_target_desc", "EmcmcStep": "emcmc_step", "EmcmcMoments": "emcmc_moments",
-          "EmcmcPriorFactor": "emcmc_prior_factor", "EmcmcPriorDesc": "emcmc_prior_desc"}
+          "EmcmcPriorFactor": "emcmc_prior_factor", "EmcmcPriorDesc": "emcmc_prior_desc",
+          "EmcmcUserTargetDesc": "emcmc_user_target_desc"}
 
 JL_SCALAR = {"UInt8": 1, "Int8": 1, "UInt16": 2, "Int16": 2, "UInt32": 4, "Int32": 4, "Cint": 4, "Float32": 4,
              "UInt64": 8, "Int64": 8, "Float64": 8, "Csize_t": 8, "Cstring": 8}

@@ -100,7 +100,8 @@ struct UpdateHost {
     std::vector<double> sigma, L, invdiag;  // GaussianRandomWalk
     std::vector<double> eps;                // UniformRandomWalk ϵ
     std::vector<uint8_t> pos;               // UniformRandomWalk positivity flags (random_walk.jl:45-52)
-    emcmc_unifrw_adaptation adpt{};         // AdaptationUnifRW (scalar form)
+    emcmc_unifrw_adaptation adpt{};         // AdaptationUnifRW: k and target
+    std::vector<double> ascale, amin, amax, aoff;  // its per-coordinate scale/min/max/offset
     bool diag = false;
     double c0 = 0.0;
     // GaussianRandomWalkMix: Σ_B, its factor, λ; HaarioTypeAdaptation
@@ -415,10 +416,12 @@ emcmc_status select_mwg(emcmc_handle *h) {
             if (u.adaptation == EMCMC_ADPT_UNIF_RW) {
                 m.k = u.adpt.adapt_every_k_steps;
                 m.target = u.adpt.target_accpt_rate;
-                m.scale = u.adpt.scale;
-                m.amin = u.adpt.min;
-                m.amax = u.adpt.max;
-                m.offset = u.adpt.offset;
+                for (uint32_t j = 0; j < m.nc; ++j) {
+                    m.ascale[j] = u.ascale[j];
+                    m.amin[j] = u.amin[j];
+                    m.amax[j] = u.amax[j];
+                    m.aoff[j] = u.aoff[j];
+                }
             }
         } else {
             const int n = (int)m.nc;
@@ -1163,7 +1166,8 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "priors other than ImproperPrior run on device with Gaussian/Uniform random walks only");
     if (u->adaptation != EMCMC_ADPT_NONE &&
-        !(u->adaptation == EMCMC_ADPT_UNIF_RW && u->kernel == EMCMC_RW_UNIFORM) &&
+        !((u->adaptation == EMCMC_ADPT_UNIF_RW || u->adaptation == EMCMC_ADPT_UNIF_RW_VEC) &&
+          u->kernel == EMCMC_RW_UNIFORM) &&
         !(u->adaptation == EMCMC_ADPT_HAARIO && u->kernel == EMCMC_RW_GAUSSIAN_MIX))
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "adaptation %u has no device plugin for kernel %u yet",
                     u->adaptation, u->kernel);
@@ -1268,6 +1272,22 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
             if (!ad) return fail(h, EMCMC_INVALID_ARG, "AdaptationUnifRW parameters missing (adaptation_params)");
             if (ad->adapt_every_k_steps == 0) return fail(h, EMCMC_INVALID_ARG, "adapt_every_k_steps must be ≥ 1");
             uh.adpt = *ad;
+            uh.ascale.assign(n, ad->scale);
+            uh.amin.assign(n, ad->min);
+            uh.amax.assign(n, ad->max);
+            uh.aoff.assign(n, ad->offset);
+        } else if (u->adaptation == EMCMC_ADPT_UNIF_RW_VEC) {  // the per-coordinate form
+            const auto *ad = static_cast<const emcmc_unifrw_adaptation_vec *>(u->adaptation_params);
+            if (!ad || !ad->scale || !ad->min || !ad->max || !ad->offset)
+                return fail(h, EMCMC_INVALID_ARG, "AdaptationUnifRW per-coordinate parameters missing");
+            if (ad->adapt_every_k_steps == 0) return fail(h, EMCMC_INVALID_ARG, "adapt_every_k_steps must be ≥ 1");
+            uh.adaptation = EMCMC_ADPT_UNIF_RW;  // one device form: per-coordinate arrays
+            uh.adpt.adapt_every_k_steps = ad->adapt_every_k_steps;
+            uh.adpt.target_accpt_rate = ad->target_accpt_rate;
+            uh.ascale.assign(ad->scale, ad->scale + n);
+            uh.amin.assign(ad->min, ad->min + n);
+            uh.amax.assign(ad->max, ad->max + n);
+            uh.aoff.assign(ad->offset, ad->offset + n);
         }
     }
     h->updates.push_back(std::move(uh));

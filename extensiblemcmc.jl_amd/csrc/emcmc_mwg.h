@@ -55,7 +55,7 @@ constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, k
 struct MwgUpdate {
     uint32_t kind;    // EMCMC_RW_UNIFORM (1) / EMCMC_RW_GAUSSIAN (2)
     uint32_t nc;      // number of coordinates
-    uint32_t adapt;   // EMCMC_ADPT_NONE (0) / EMCMC_ADPT_UNIF_RW (1)
+    uint32_t adapt;   // EMCMC_ADPT_NONE (0) / AdaptationUnifRW (1, scalar or per-coordinate form)
     uint32_t k;       // adapt_every_k_steps
     uint32_t coords[kMwgMaxD];
     double eps0[kMwgMaxD];          // UniformRandomWalk ϵ (initial for adaptive updates)
@@ -63,7 +63,9 @@ struct MwgUpdate {
     double iL[kMwgMaxD];            // 1 / L_ii
     double c0;                      // −(nc·log2π + logdet Σ)/2
     uint32_t diag, posmask;          // posmask bit j: coordinate j positivity-restricted
-    double target, scale, amin, amax, offset;  // AdaptationUnifRW (scalar form)
+    double target;                  // AdaptationUnifRW target_accpt_rate
+    double ascale[kMwgMaxD], amin[kMwgMaxD], amax[kMwgMaxD], aoff[kMwgMaxD];  // per coordinate (the scalar
+                                    // form repeats its values)
     // prior over the update's local coordinates (priors.jl): kind, and for
     // Product/Standard priors one univariate family per coordinate, with
     // bit j of pstart set where coordinate j starts a new ProductPrior factor
@@ -447,14 +449,14 @@ __device__ __forceinline__ void mwg_register_step(const MwgParams &a, const MwgU
     if (u.adapt == 1) {
         const uint32_t pr = a.aprop[pc] + 1, ac = a.aacc[pc] + (acc ? 1u : 0u);
         if (pr >= u.k) {  // proposed counts are equal across chains: uniform branch
-            const double delta = u.scale / sqrt(fmax(1.0, (double)iter / (double)u.k - u.offset));
             const double a_r = (double)ac / (double)pr;
-            const double stp = (a_r > u.target) ? delta : -delta;
+            const bool up = a_r > u.target;
             for (uint32_t j = 0; j < n; ++j) {
+                const double delta = u.ascale[j] / sqrt(fmax(1.0, (double)iter / (double)u.k - u.aoff[j]));
                 double *ep = a.eps + ((uint64_t)p * kMwgMaxD + j) * C + chain;
-                double e = *ep + stp;
-                e = (e < u.amax) ? e : u.amax;
-                *ep = (e > u.amin) ? e : u.amin;
+                double e = *ep + (up ? delta : -delta);
+                e = (e < u.amax[j]) ? e : u.amax[j];
+                *ep = (e > u.amin[j]) ? e : u.amin[j];
             }
             a.aprop[pc] = 0;
             a.aacc[pc] = 0;

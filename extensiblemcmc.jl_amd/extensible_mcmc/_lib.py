@@ -40,7 +40,7 @@ STATUS_NAMES = {
 RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA = 1, 2, 3, 4
 PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
 DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
-ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO = 0, 1, 2
+ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO, ADPT_UNIF_RW_VEC = 0, 1, 2, 3
 TARGET_GSN, TARGET_LOGISTIC, TARGET_USER = 1, 2, 3
 LL_PER_OBS, LL_SUFFSTAT = 0, 1
 HIST_FULL, HIST_ACCEPT_ONLY = 0, 1
@@ -122,6 +122,19 @@ class EmcmcUnifRWAdaptation(C.Structure):
         ("min", C.c_double),
         ("max", C.c_double),
         ("offset", C.c_double),
+    ]
+
+
+class EmcmcUnifRWAdaptationVec(C.Structure):
+    """AdaptationUnifRW per-coordinate form (include/emcmc.h emcmc_unifrw_adaptation_vec)."""
+    _fields_ = [
+        ("adapt_every_k_steps", C.c_uint32),
+        ("reserved", C.c_uint32),
+        ("target_accpt_rate", C.c_double),
+        ("scale", C.POINTER(C.c_double)),
+        ("min", C.POINTER(C.c_double)),
+        ("max", C.POINTER(C.c_double)),
+        ("offset", C.POINTER(C.c_double)),
     ]
 
 

@@ -150,9 +150,18 @@ class Engine:
         u.epsilon = L.dptr(e)
         ad = None
         if adapt is not None:
-            ad = L.EmcmcUnifRWAdaptation(int(adapt["k"]), 0, float(adapt["target"]), float(adapt["scale"]),
-                                         float(adapt["min"]), float(adapt["max"]), float(adapt["offset"]))
-            u.adaptation = L.ADPT_UNIF_RW
+            names = ("scale", "min", "max", "offset")
+            if all(np.ndim(adapt[k]) == 0 for k in names):
+                ad = L.EmcmcUnifRWAdaptation(int(adapt["k"]), 0, float(adapt["target"]), float(adapt["scale"]),
+                                             float(adapt["min"]), float(adapt["max"]), float(adapt["offset"]))
+                u.adaptation = L.ADPT_UNIF_RW
+            else:  # per-coordinate form (adaptation.jl:155-188)
+                arrs = [np.ascontiguousarray(np.broadcast_to(np.asarray(adapt[k], dtype=np.float64),
+                                                             (len(coords),))) for k in names]
+                keep.extend(arrs)
+                ad = L.EmcmcUnifRWAdaptationVec(int(adapt["k"]), 0, float(adapt["target"]),
+                                                *[L.dptr(a) for a in arrs])
+                u.adaptation = L.ADPT_UNIF_RW_VEC
             u.adaptation_params = C.cast(C.pointer(ad), C.c_void_p)
         if pos is not None:
             p = np.ascontiguousarray(pos, dtype=np.uint8)

@@ -431,8 +431,6 @@ class RandomWalkUpdate(MCMCParamUpdate):
                 raise UnsupportedPlugin("HaarioTypeAdaptation with a custom fλ has no device plugin (λ is fixed)")
             adapt = {"k": self.adpt.adapt_every_k_steps, "scale": self.adpt.scale}
         elif isinstance(self.adpt, AdaptationUnifRW) and isinstance(self.rw, UniformRandomWalk):
-            if self.adpt.kind != "scalar":
-                raise UnsupportedPlugin("AdaptationUnifRW with per-coordinate parameters has no device plugin yet")
             a = self.adpt
             adapt = {"k": a.adapt_every_k_steps, "target": a.target_accpt_rate, "scale": a.scale, "min": a.min,
                      "max": a.max, "offset": a.offset}

@@ -205,8 +205,20 @@ struct EmcmcUnifRWAdaptation
     offset::Float64
 end
 
+# include/emcmc.h emcmc_unifrw_adaptation_vec: the per-coordinate form
+struct EmcmcUnifRWAdaptationVec
+    adapt_every_k_steps::UInt32
+    reserved::UInt32
+    target_accpt_rate::Float64
+    scale::Ptr{Float64}
+    min::Ptr{Float64}
+    max::Ptr{Float64}
+    offset::Ptr{Float64}
+end
+
 const RW_UNIFORM = UInt32(1)
 const ADPT_UNIF_RW = UInt32(1)
+const ADPT_UNIF_RW_VEC = UInt32(3)
 
 # priors.jl:18-88 → (EMCMC_PRIOR_*, emcmc_prior_desc pointer or C_NULL)
 _dist_factor(d::Distributions.Normal, k) = EmcmcPriorFactor(DIST_NORMAL, UInt32(k), d.μ, d.σ)
@@ -274,6 +286,14 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
                                           a.min, a.max, a.offset))
             push!(keep, p)
             adpt, adptp = ADPT_UNIF_RW, Base.unsafe_convert(Ptr{Cvoid}, p)
+        elseif updt.adpt isa eMCMC.AdaptationUnifRW              # Vector / SVector form (adaptation.jl:171-188)
+            a = updt.adpt
+            v = [Float64.(collect(a.scale)), Float64.(collect(a.min)), Float64.(collect(a.max)),
+                 Float64.(collect(a.offset))]
+            p = Ref(EmcmcUnifRWAdaptationVec(UInt32(a.adapt_every_k_steps), UInt32(0), a.target_accpt_rate,
+                                             pointer(v[1]), pointer(v[2]), pointer(v[3]), pointer(v[4])))
+            push!(keep, v, p)
+            adpt, adptp = ADPT_UNIF_RW_VEC, Base.unsafe_convert(Ptr{Cvoid}, p)
         elseif !(updt.adpt isa eMCMC.NoAdaptation)
             error("no device plugin for $(typeof(updt.adpt))")
         end

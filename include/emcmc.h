@@ -82,6 +82,8 @@ typedef enum emcmc_status {
 #define EMCMC_ADPT_NONE 0u      /* NoAdaptation          adaptation.jl:26 */
 #define EMCMC_ADPT_UNIF_RW 1u   /* AdaptationUnifRW      adaptation.jl:51-329 */
 #define EMCMC_ADPT_HAARIO 2u    /* HaarioTypeAdaptation  adaptation.jl:372-426 (GaussianRandomWalkMix only) */
+#define EMCMC_ADPT_UNIF_RW_VEC 3u /* AdaptationUnifRW with per-coordinate scale/min/max/offset (its nonscalar
+                                     form, adaptation.jl:155-188); see emcmc_unifrw_adaptation_vec */
 
 /* Targets — src/example/gsn_target.jl */
 #define EMCMC_TARGET_GSN 1u     /* GsnTargetLaw(μ, Σ) with coords ⊆ μ */
@@ -159,6 +161,27 @@ typedef struct emcmc_unifrw_adaptation {
     double offset;
 } emcmc_unifrw_adaptation;
 
+/* `AdaptationUnifRW(θ; scale = [...], min = ..., ...)` in its per-coordinate
+ * form (AdaptationUnifRW{Vector{Float64}} / {SVector{N,Float64}},
+ * adaptation.jl:155-188; the reference's constructor test, test/runtests.jl:65-84).
+ * Each array has num_coords entries.  Passed as adaptation_params when
+ * adaptation == EMCMC_ADPT_UNIF_RW_VEC.  The reference's readjust! evaluates
+ * `scale/sqrt(max(1.0, iter/k - offset))` and `max.(min.(ϵ, max), min)`; with a
+ * vector offset `Float64 - Vector` has no method in Julia 1.x, so the reference
+ * stops with a MethodError at the first readjust.  The engine applies the
+ * formula coordinate by coordinate: δ_i = scale_i/√max(1, iter/k − offset_i),
+ * ϵ_i ← clamp(ϵ_i ± δ_i, min_i, max_i) — the scalar form's bits when all
+ * entries are equal. */
+typedef struct emcmc_unifrw_adaptation_vec {
+    uint32_t adapt_every_k_steps;
+    uint32_t reserved;
+    double target_accpt_rate;
+    const double *scale;
+    const double *min;
+    const double *max;
+    const double *offset;
+} emcmc_unifrw_adaptation_vec;
+
 /* `HaarioTypeAdaptation(θ; adapt_every_k_steps, scale, f)` (adaptation.jl:372-397,
  * defaults 100, 2.38², identity).  Passed as emcmc_update_desc.adaptation_params
  * when adaptation == EMCMC_ADPT_HAARIO.  `scale` is carried but, as in the
@@ -197,8 +220,8 @@ typedef struct emcmc_prior_desc {
 typedef struct emcmc_update_desc {
     uint32_t kernel;          /* EMCMC_RW_UNIFORM, EMCMC_RW_GAUSSIAN or EMCMC_RW_GAUSSIAN_MIX */
     uint32_t prior;           /* EMCMC_PRIOR_* */
-    uint32_t adaptation;      /* EMCMC_ADPT_NONE, EMCMC_ADPT_UNIF_RW (UniformRandomWalk) or
-                                 EMCMC_ADPT_HAARIO (GaussianRandomWalkMix) */
+    uint32_t adaptation;      /* EMCMC_ADPT_NONE, EMCMC_ADPT_UNIF_RW / EMCMC_ADPT_UNIF_RW_VEC
+                                 (UniformRandomWalk) or EMCMC_ADPT_HAARIO (GaussianRandomWalkMix) */
     uint32_t num_coords;      /* length(coords) */
     const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based), any order */
     const double *sigma;      /* GaussianRandomWalk Σ, GaussianRandomWalkMix Σ_A: num_coords² column-major */
@@ -206,7 +229,8 @@ typedef struct emcmc_update_desc {
     const uint8_t *pos;       /* positivity flags or NULL (all false); true on device for UniformRandomWalk
                                  (θ° = θ·e^U, random_walk.jl:63-94) and GaussianRandomWalk (log scale,
                                  random_walk.jl:136-171; D ≤ 32), not for GaussianRandomWalkMix */
-    const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW) or
+    const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW),
+                                      const emcmc_unifrw_adaptation_vec* (EMCMC_ADPT_UNIF_RW_VEC) or
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
     const double *sigma_b;    /* GaussianRandomWalkMix Σ_B: num_coords² column-major */
     const emcmc_prior_desc *prior_params; /* EMCMC_PRIOR_PRODUCT / EMCMC_PRIOR_STANDARD factors, else NULL */

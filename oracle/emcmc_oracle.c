@@ -625,7 +625,7 @@ typedef struct {
     double L[ORC_MWG_MAXD * ORC_MWG_MAXD], iL[ORC_MWG_MAXD], c0;
     int diag;
     uint32_t adapt, k;
-    double target, scale, amin, amax, offset;
+    double target, scale[ORC_MWG_MAXD], amin[ORC_MWG_MAXD], amax[ORC_MWG_MAXD], offset[ORC_MWG_MAXD];
     uint32_t prior, pstart, pfam[ORC_MWG_MAXD];
     double pa[ORC_MWG_MAXD], pb[ORC_MWG_MAXD], pc[ORC_MWG_MAXD];
 } orc_mwg_update;
@@ -665,7 +665,8 @@ typedef double (*orc_user_loglik_fn)(const double *theta, int D, const double *o
 
 /* table layout from Python (ORC_MWG_MAXD = 32 slots per update):
  *   kind[P], nc[P], coords[P*32], eps[P*32], sigma[P*1024] (nc×nc column-major),
- *   pos[P*32] (uint8), adapt[P], k[P], aparams[P*5] = (target, scale, min, max, offset),
+ *   pos[P*32] (uint8), adapt[P], k[P], aparams[P*129] = (target, scale[32], min[32], max[32], offset[32])
+ *   (AdaptationUnifRW per coordinate; the scalar form repeats its values),
  *   prior[P], factor tables per update: nfac[P], ffam[P*32], fcnt[P*32], fa[P*32], fb[P*32];
  * ll_prop [P][C] out: sub_ws°.ll of each update's latest proposal (NULL: skip);
  * user_ll: NULL for GsnTargetLaw, else the user target (user_params its parameters). */
@@ -728,11 +729,16 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         }
         u->adapt = adapt[p];
         u->k = adapt_k[p];
-        u->target = aparams[p * 5 + 0];
-        u->scale = aparams[p * 5 + 1];
-        u->amin = aparams[p * 5 + 2];
-        u->amax = aparams[p * 5 + 3];
-        u->offset = aparams[p * 5 + 4];
+        {
+            const double *ap = aparams + (size_t)p * (1 + 4 * ORC_MWG_MAXD);
+            u->target = ap[0];
+            for (int j = 0; j < ORC_MWG_MAXD; ++j) {
+                u->scale[j] = ap[1 + j];
+                u->amin[j] = ap[1 + ORC_MWG_MAXD + j];
+                u->amax[j] = ap[1 + 2 * ORC_MWG_MAXD + j];
+                u->offset[j] = ap[1 + 3 * ORC_MWG_MAXD + j];
+            }
+        }
         u->prior = prior_kind ? prior_kind[p] : ORC_PRIOR_IMPROPER;
         if (u->prior == ORC_PRIOR_PRODUCT || u->prior == ORC_PRIOR_STANDARD) {
             uint32_t j = 0;
@@ -951,15 +957,18 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 *ac += (uint32_t)acc;
                 *pr += 1;
                 if (*pr >= u->k) {
-                    const double delta = u->scale / sqrt(fmax(1.0, (double)iter / (double)u->k - u->offset));
+                    /* δ = scale/√max(1, iter/k − offset) and the clamp, per coordinate
+                     * (adaptation.jl:312-329; the scalar form repeats its values) */
                     const double a_r = (*pr == 0) ? 0.0 : (double)*ac / (double)*pr;
                     *pr = 0;
                     *ac = 0;
-                    const double step = (a_r > u->target) ? delta : -delta;
                     for (uint32_t j = 0; j < n; ++j) {
+                        const double delta =
+                            u->scale[j] / sqrt(fmax(1.0, (double)iter / (double)u->k - u->offset[j]));
+                        const double step = (a_r > u->target) ? delta : -delta;
                         double e = ep[j] + step;
-                        e = e < u->amax ? e : u->amax;
-                        ep[j] = e > u->amin ? e : u->amin;
+                        e = e < u->amax[j] ? e : u->amax[j];
+                        ep[j] = e > u->amin[j] ? e : u->amin[j];
                     }
                 }
             }

@@ -161,11 +161,16 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
             acc_c[p] += int(acc)
             prop_c[p] += 1
             if prop_c[p] >= ad["k"]:
-                delta = ad["scale"] / np.sqrt(max(1.0, it / ad["k"] - ad["offset"]))
+                # compute_δ / compute_ϵ (adaptation.jl:312-329), coordinate by
+                # coordinate for the per-coordinate form (scalars broadcast)
+                nj = len(eps[p])
+                vec = lambda v: [float(v)] * nj if np.ndim(v) == 0 else [float(x) for x in v]  # noqa: E731
+                sc, mn, mx, off = vec(ad["scale"]), vec(ad["min"]), vec(ad["max"]), vec(ad["offset"])
                 a_r = 0.0 if prop_c[p] == 0 else acc_c[p] / prop_c[p]
                 prop_c[p] = acc_c[p] = 0
-                eps[p] = [max(min(e + 1.0 * (2 * int(a_r > ad["target"]) - 1) * delta, ad["max"]), ad["min"])
-                          for e in eps[p]]
+                eps[p] = [max(min(e + 1.0 * (2 * int(a_r > ad["target"]) - 1) *
+                                  (sc[j] / np.sqrt(max(1.0, it / ad["k"] - off[j]))), mx[j]), mn[j])
+                          for j, e in enumerate(eps[p])]
         out["theta"].append(th.copy())
         out["prop"].append(prop)
         out["ll"].append(ll)

@@ -302,7 +302,7 @@ def _mwg_tables(updates):
     sigma = np.zeros((P, MWG_MAXD * MWG_MAXD))
     adapt = np.zeros(P, dtype=np.uint32)
     ak = np.ones(P, dtype=np.uint32)
-    ap = np.zeros((P, 5))
+    ap = np.zeros((P, 1 + 4 * MWG_MAXD))
     pos = np.zeros((P, MWG_MAXD), dtype=np.uint8)
     for p, u in enumerate(updates):
         n = len(u["coords"])
@@ -315,7 +315,12 @@ def _mwg_tables(updates):
         if u["adapt"] is not None:
             a = u["adapt"]
             adapt[p], ak[p] = 1, a["k"]
-            ap[p] = (a["target"], a["scale"], a["min"], a["max"], a["offset"])
+            ap[p, 0] = a["target"]
+            for f, name in enumerate(("scale", "min", "max", "offset")):  # per coordinate (scalars repeat)
+                v = np.atleast_1d(np.asarray(a[name], dtype=np.float64))
+                row = ap[p, 1 + f * MWG_MAXD: 1 + (f + 1) * MWG_MAXD]
+                row[:] = v[0]
+                row[:v.size] = v
         if u.get("pos") is not None:
             pos[p, :n] = np.asarray(u["pos"], dtype=bool)
     return kind, nc, coords, eps, sigma, adapt, ak, ap, pos

@@ -220,3 +220,16 @@ def test_reference_schedule_kat_on_device(oracle, golden_dir):
     st = oracle.MWGState(np.zeros((C, D)), mu, ups)
     h = oracle.run_mwg(st, ups, seed=4242, t_sigma=np.eye(D), obs=obs, steps=steps, nthreads=8)
     check(oracle, eng, st, h, steps, ups, D)
+
+
+def test_per_coordinate_adaptation(oracle):
+    """AdaptationUnifRW's per-coordinate form on a UniformRandomWalk block, with a
+    Gaussian single-site update beside it (include/emcmc.h
+    emcmc_unifrw_adaptation_vec): every chain's adapted ϵ bitwise."""
+    w = W.ref_test()
+    vec = {"k": 40, "target": 0.234, "scale": [0.05, 0.2], "min": [1e-12, 0.02], "max": [1e7, 0.5],
+           "offset": [1e2, 3.0]}
+    ups = [oracle.mwg_update(1, [0, 1], eps=[0.1, 0.3], adapt=vec)]
+    steps = full_steps(600, 1)
+    eng, st, h = run_both(oracle, 2, 1500, 600, ups, [1.0, 2.0], w.t_sigma, w.obs, steps, w.seed)
+    check(oracle, eng, st, h, steps, ups, 1)

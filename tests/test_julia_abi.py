@@ -19,6 +19,7 @@ SHIM = ROOT / "extensiblemcmc.jl_amd" / "julia" / "ExtensibleMCMCHip.jl"
 
 C_NAME = {"EmcmcConfig": "emcmc_config", "EmcmcUpdateDesc": "emcmc_update_desc",
           "EmcmcHaarioAdaptation": "emcmc_haario_adaptation", "EmcmcUnifRWAdaptation": "emcmc_unifrw_adaptation",
+          "EmcmcUnifRWAdaptationVec": "emcmc_unifrw_adaptation_vec",
           "EmcmcTargetDesc": "emcmc_target_desc", "EmcmcStep": "emcmc_step", "EmcmcMoments": "emcmc_moments",
           "EmcmcPriorFactor": "emcmc_prior_factor", "EmcmcPriorDesc": "emcmc_prior_desc",
           "EmcmcUserTargetDesc": "emcmc_user_target_desc"}

@@ -168,3 +168,35 @@ def test_gaussian_rw_positivity_restricted_against_literal(oracle):
         np.testing.assert_allclose(np.array(o["prop"]), h["prop"][:, c], rtol=1e-13)
     assert np.all(h["theta"][:, :, 0] > 0) and np.all(h["prop"][:, :, 0] > 0)
     assert 0.05 < h["acc"].mean() < 0.95
+
+
+VEC_ADAPT = {"k": 40, "target": 0.234, "scale": [0.05, 0.2], "min": [1e-12, 0.02], "max": [1e7, 0.5],
+             "offset": [1e2, 3.0]}
+
+
+def test_per_coordinate_adaptation_against_literal(oracle):
+    """AdaptationUnifRW in its per-coordinate form (adaptation.jl:155-188) on a
+    block UniformRandomWalk over both coordinates: δ_i = scale_i/√max(1, iter/k −
+    offset_i) and clamp(·, min_i, max_i) coordinate by coordinate (the reference's
+    readjust! has no method for `Float64 - Vector`; include/emcmc.h documents the
+    elementwise reading)."""
+    w = W.ref_test()
+    ups = [oracle.mwg_update(1, [0, 1], eps=[0.1, 0.3], adapt=VEC_ADAPT)]
+    st, _ = compare_with_literal(oracle, w, ups, full_steps(600, 1), 6, [1.0, 2.0])
+    e = st.eps[0, :, :2]
+    assert np.all(e[:, 1] <= 0.5) and np.all(e[:, 1] >= 0.02)  # per-coordinate clamp active
+    assert not np.allclose(e[:, 0], e[:, 1])
+
+
+def test_scalar_adaptation_equals_repeated_vector(oracle):
+    """The scalar form is the per-coordinate form with repeated entries, bit for bit."""
+    w = W.ref_test()
+    sc = dict(ADAPT)
+    vec = {k: ([v, v] if k in ("scale", "min", "max", "offset") else v) for k, v in sc.items()}
+    runs = []
+    for a in (sc, vec):
+        ups = [oracle.mwg_update(1, [0, 1], eps=[0.1, 0.2], adapt=a)]
+        st = oracle.MWGState(np.zeros((64, 2)), [1.0, 2.0], ups)
+        oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs, steps=full_steps(300, 1), history=False)
+        runs.append(st)
+    assert np.array_equal(runs[0].eps, runs[1].eps) and np.array_equal(runs[0].theta, runs[1].theta)

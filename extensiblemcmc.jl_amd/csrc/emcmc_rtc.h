@@ -14,7 +14,7 @@
 //     }
 //
 // with + − × ÷, fma, sqrt, fabs, copysign and em_exp / em_log (the engine's
-// own exp/log, restated bit for bit in oracle/oracle_math.h).  The source is
+// own exp/log — NaN below 0 — restated bit for bit in oracle/oracle_math.h).  The source is
 // compiled into the general schedule kernel (emcmc_mwg.h) with TGT = the
 // user's law, so every update kind, prior and adaptation of that kernel runs
 // with it.

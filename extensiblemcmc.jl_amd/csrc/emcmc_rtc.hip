@@ -28,7 +28,7 @@ const char *const kPrelude = R"EMCMC_RTC(#include "emcmc_mwg.h"
         const double *__restrict__ theta, int D, const double *__restrict__ obs, uint64_t nobs,            \
         const double *__restrict__ params)
 #define em_exp(x) emcmc::exp_any(x)
-#define em_log(x) emcmc::log_any(x)
+#define em_log(x) emcmc::log_real(x)
 #line 1 "user_target"
 )EMCMC_RTC";
 

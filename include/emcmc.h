@@ -266,8 +266,8 @@ typedef struct emcmc_target_desc {
  *     }
  *
  * in the C subset both hiprtc and a C compiler accept: + − × ÷, fma, sqrt, fabs,
- * copysign, em_exp(x), em_log(x) (the engine's exp / log; oracle/user_prelude.h
- * maps them to their CPU restatement).  Every update kind, prior and adaptation
+ * copysign, em_exp(x), em_log(x) (the engine's exp / log, NaN below 0;
+ * oracle/user_prelude.h maps them to their CPU restatement).  Every update kind, prior and adaptation
  * of the general kernel runs with it; D ≤ 32.  GaussianRandomWalkMix and MALA
  * raise EMCMC_UNSUPPORTED_PLUGIN with a user target. */
 typedef struct emcmc_user_target_desc {

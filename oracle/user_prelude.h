@@ -21,6 +21,8 @@
     double emcmc_user_loglik(const double *restrict theta, int D, const double *restrict obs, uint64_t nobs, \
                              const double *restrict params)
 #define em_exp(x) orc_exp_any(x)
-#define em_log(x) orc_log_any(x)
+/* log: NaN below 0 (Julia's log throws DomainError there), −Inf at 0 */
+static inline double orc_user_log(double x) { return (x < 0.0) ? NAN : orc_log_any(x); }
+#define em_log(x) orc_user_log(x)
 
 #endif

@@ -127,3 +127,49 @@ def test_user_law_through_the_api(oracle):
                    user_ll=fn, user_params=case.params, history=False)
     assert np.array_equal(gws.state, st.theta)
     assert np.array_equal(lws[0].ll, st.ll)
+
+
+def test_full_gsn_law_updates_sigma_entries(oracle):
+    """GsnTargetLaw with θ = [μ; vec Σ] (gsn_target.jl:1-29) as a user law: a joint
+    Gaussian walk on μ and UniformRandomWalks on Σ₁₁, Σ₁₂ (the upper entry, the
+    one Symmetric(triu(Σ)) reads) and Σ₂₂, the variances positivity-restricted;
+    the law refactorises Σ at every evaluation like set_parameters! does."""
+    case = U.gsn_full()
+    ups = [oracle.mwg_update(2, [0, 1], sigma=0.1 * np.eye(2)),
+           oracle.mwg_update(1, [2], eps=[0.2], pos=[True]),
+           oracle.mwg_update(1, [4], eps=[1.5]),  # wide: some proposals leave the PD cone
+           oracle.mwg_update(1, [5], eps=[0.2], pos=[True])]
+    steps = full_steps(300, 4)
+    eng, st, h = run_user(oracle, case, ups, steps, 1200, 300)
+    check(oracle, eng, st, h, steps, ups, 4)
+    th = eng.get_state()[0]
+    assert np.all(th[:, 2] > 0) and np.all(th[:, 5] > 0)
+    assert np.any(eng.get_faults() & L.FAULT_NONFINITE_LL)  # some Σ proposals were not positive definite
+
+
+def test_full_gsn_law_with_fixed_sigma_matches_builtin_device_run(oracle):
+    """μ-only updates of the θ = [μ; vec Σ] user law give the built-in
+    GsnTargetLaw(μ, Σ) chain on the device, bit for bit."""
+    case = U.gsn_full()
+    d, C, M = 2, 2048, 200
+    fn, src = oracle.user_loglik(case.name)
+    th0 = np.concatenate([np.zeros(d), case.extra["S"].ravel(order="F")])
+    steps = full_steps(M, 2)
+    outs = []
+    for user in (False, True):
+        D = d + d * d if user else d
+        eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=case.seed))
+        eng.add_gaussian_rw_update([0], [[0.4]])
+        eng.add_uniform_rw_update([1], [0.6])
+        if user:
+            eng.set_user_target(src, obs=case.obs, params=case.params, theta0=th0)
+            eng.set_state(np.tile(th0, (C, 1)))
+        else:
+            eng.set_gsn_target(th0[:d], case.extra["S"], case.obs)
+            eng.set_state(np.zeros((C, d)))
+        eng.run(steps)
+        eng.synchronize(allow_faults=True)
+        th, ll = eng.get_state()
+        outs.append((th[:, :d], ll, eng.get_history(L.H_ACCEPT, 1, M), eng.get_history(L.H_LL, 1, M)))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)

@@ -58,6 +58,17 @@ def gsn_identity(D=3, n=10):
     return UserCase("gsn_identity", D, obs, np.array([c0]), mu.copy())
 
 
+def gsn_full(d=2, n=10):
+    """GsnTargetLaw(μ, Σ) with θ = [μ; vec Σ] (gsn_target.jl:1-13): the reference
+    test's target (test/runtests.jl:94-111) with its 10 observations drawn here."""
+    rng = np.random.default_rng(4)
+    mu = np.array([1.0, 2.0, -1.0, 0.5][:d])
+    S = np.array([[1.0, 0.5, 0.0, 0.0], [0.5, 1.0, 0.2, 0.0], [0.0, 0.2, 1.5, 0.1], [0.0, 0.0, 0.1, 0.8]])[:d, :d]
+    obs = rng.multivariate_normal(mu, S, size=n)
+    theta0 = np.concatenate([np.zeros(d), np.eye(d).ravel(order="F")])
+    return UserCase("gsn_full", d + d * d, obs, np.array([float(d)]), theta0, extra={"d": d, "mu": mu, "S": S})
+
+
 def numpy_loglik(case: UserCase, theta):
     """The sources' formulas in numpy (libm exp/log: agree to ~1e-13 relative)."""
     th = np.asarray(theta, dtype=float)
@@ -74,6 +85,14 @@ def numpy_loglik(case: UserCase, theta):
         b = case.params[0]
         p2 = th[1] + b * th[0] ** 2 - 100 * b
         return float(-th[0] ** 2 / 200 - p2 ** 2 / 2 - np.sum(th[2:] ** 2) / 2)
+    if case.name == "gsn_full":
+        d = case.extra["d"]
+        mu, S = th[:d], th[d:].reshape(d, d, order="F")
+        U = np.triu(S)
+        S = U + np.triu(U, 1).T  # Symmetric(triu(Σ)) (gsn_target.jl:19)
+        Li = np.linalg.inv(np.linalg.cholesky(S))
+        r = (case.obs - mu) @ Li.T
+        return float(np.sum(-(d * LOG2PI + np.linalg.slogdet(S)[1]) / 2 - np.sum(r * r, axis=1) / 2))
     if case.name == "gsn_identity":
         return float(np.sum(case.params[0] - np.sum((case.obs - th) ** 2, axis=1) / 2))
     raise KeyError(case.name)

@@ -1313,8 +1313,31 @@ emcmc_status emcmc_set_target(emcmc_handle *h, const emcmc_target_desc *t) {
         h->grad_valid = false;
         return select_variant(h);
     }
+    if (d != h->cfg.dim && (uint64_t)d + (uint64_t)d * d == h->cfg.dim) {
+        // the state is GsnTargetLaw's whole θ = [μ; vec Σ] (gsn_target.jl:1-13):
+        // updates may write Σ entries, so the law refactorises Σ at every
+        // evaluation — the shipped law csrc/laws/gsn_full.c, compiled at run time
+        if (!t->mu || !t->sigma || !t->obs || t->num_obs == 0) return fail(h, EMCMC_INVALID_ARG, "null target arrays");
+        if (t->ll_mode != EMCMC_LL_PER_OBS)
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "GsnTargetLaw over [μ; vec Σ] evaluates per observation only");
+        std::vector<double> th0(t->mu, t->mu + d);
+        th0.insert(th0.end(), t->sigma, t->sigma + (size_t)d * d);
+        const double prm = (double)d;
+        emcmc_user_target_desc u{};
+        u.dim = h->cfg.dim;
+        u.obs_dim = d;
+        u.theta0 = th0.data();
+        u.num_obs = t->num_obs;
+        u.obs = t->obs;
+        u.num_params = 1;
+        u.params = &prm;
+        u.source = rtc_builtin_law("gsn_full.c");
+        if (!u.source) return fail(h, EMCMC_HIP_ERROR, "the shipped GsnTargetLaw source is missing");
+        return emcmc_set_user_target(h, &u);
+    }
     if (d != h->cfg.dim)
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "device GsnTargetLaw needs state = μ (d=%u, D=%u)", d, h->cfg.dim);
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "device GsnTargetLaw needs state = μ or state = [μ; vec Σ] (d=%u, D=%u)", d, h->cfg.dim);
     if (!t->mu || !t->sigma || (t->num_obs && !t->obs)) return fail(h, EMCMC_INVALID_ARG, "null target arrays");
     if (t->num_obs == 0) return fail(h, EMCMC_INVALID_ARG, "GsnTargetLaw needs observations");
     if (t->ll_mode > EMCMC_LL_SUFFSTAT) return fail(h, EMCMC_INVALID_ARG, "ll_mode");

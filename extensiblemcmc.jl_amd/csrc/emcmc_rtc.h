@@ -37,6 +37,10 @@ struct RtcKernel {
 // else the compiler's log.
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, RtcKernel &out);
 
+// The text of a law the library ships as an EMCMC_USER_LOGLIK source
+// (csrc/laws/<name>), or nullptr.
+const char *rtc_builtin_law(const char *name);
+
 // The same kernel with the built-in GsnTargetLaw (emcmc_mwg.h GsnTarget) for a
 // dimension the library has no ahead-of-time instantiation of (inst_mwg.hip).
 std::string rtc_compile_gsn(int D, bool full, int ll_mode, RtcKernel &out);

@@ -135,6 +135,12 @@ std::string rtc_compile_user(const std::string &src, const std::string &opts, in
     return rtc_compile(src, opts, D, full, 0, out);
 }
 
+const char *rtc_builtin_law(const char *name) {
+    for (int i = 0; i < kRtcHeaderCount; ++i)
+        if (std::string(kRtcHeaderNames[i]) == name) return kRtcHeaderSrc[i];
+    return nullptr;
+}
+
 std::string rtc_compile_gsn(int D, bool full, int ll_mode, RtcKernel &out) { return rtc_compile("", "", D, full, ll_mode, out); }
 
 }  // namespace emcmc

@@ -400,11 +400,15 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
 
 
 def user_loglik(name):
-    """The oracle build of user target tests/user_targets/<name>.c (oracle/Makefile:
+    """The oracle build of user target tests/user_targets/<name>.c or of a law the
+    library ships, extensiblemcmc.jl_amd/csrc/laws/<name>.c (oracle/Makefile:
     lib/user_<name>.so, compiled with oracle/user_prelude.h): (ctypes function,
     source text).  The engine compiles the same source for the device."""
     so = Path(__file__).resolve().parent / "lib" / f"user_{name}.so"
-    src = Path(__file__).resolve().parent.parent / "tests" / "user_targets" / f"{name}.c"
+    root = Path(__file__).resolve().parent.parent
+    src = root / "tests" / "user_targets" / f"{name}.c"
+    if not src.exists():
+        src = root / "extensiblemcmc.jl_amd" / "csrc" / "laws" / f"{name}.c"
     if not so.exists():
         raise ImportError(f"{so} not built (make -C oracle)")
     dll = C.CDLL(str(so))

@@ -108,6 +108,8 @@ struct UpdateHost {
     std::vector<double> sigma_b, LB, invdiagB;
     double c0B = 0.0, lam = 0.0;
     emcmc_haario_adaptation haario{};
+    emcmc_lambda_fn flam = nullptr;  // HaarioTypeAdaptation fλ (host callback; nullptr = identity)
+    void *flam_ctx = nullptr;
     // prior (priors.jl) per local coordinate: family, parameters, host constant; factor starts
     std::vector<uint32_t> pfam;
     std::vector<double> pa, pb, pc;
@@ -780,7 +782,7 @@ emcmc_status guard_ring(emcmc_handle *h, uint64_t a, uint64_t b) {
 emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_steps) {
     const uint64_t C = h->cfg.num_chains;
     const TargetHost &t = h->target;
-    const UpdateHost &u = h->updates[0];
+    UpdateHost &u = h->updates[0];
     const bool haario = u.adaptation == EMCMC_ADPT_HAARIO;
     const uint32_t k = haario ? u.haario.adapt_every_k_steps : 0;
     MixParams p{};
@@ -899,6 +901,11 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
                                           h->stream));
                 h->mix_M = 0;
                 readjusted = true;
+                if (u.flam) {  // rw.λ = adpt.fλ(rw.λ, adpt.N, mcmc_iter) (adaptation.jl:425)
+                    u.lam = u.flam(u.lam, (int64_t)h->stats_N, (int64_t)steps[j - 1].mcmciter, u.flam_ctx);
+                    p.lam = u.lam;
+                    p.oml = 1.0 - u.lam;
+                }
             }
         }
         if (h->timing) {  // the whole group: step kernel, mean/cov kernel, readjust
@@ -1738,6 +1745,23 @@ emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_si
                         (j <= i) ? v[state_pos((uint64_t)lo_idx(i, j), c, C, (uint32_t)DP)] : 0.0;
     }
     if (steps_since_adapt) *steps_since_adapt = h->mix_M;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_set_mix_lambda_fn(emcmc_handle *h, uint32_t pidx, emcmc_lambda_fn f, void *ctx) {
+    if (!h || pidx < 1 || pidx > h->updates.size()) return EMCMC_INVALID_ARG;
+    UpdateHost &u = h->updates[pidx - 1];
+    if (u.kernel != EMCMC_RW_GAUSSIAN_MIX || u.adaptation != EMCMC_ADPT_HAARIO)
+        return fail(h, EMCMC_INVALID_ARG, "fλ belongs to a GaussianRandomWalkMix update with HaarioTypeAdaptation");
+    u.flam = f;
+    u.flam_ctx = ctx;
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_get_mix_lambda(emcmc_handle *h, uint32_t pidx, double *lambda) {
+    if (!h || !lambda || pidx < 1 || pidx > h->updates.size()) return EMCMC_INVALID_ARG;
+    if (h->updates[pidx - 1].kernel != EMCMC_RW_GAUSSIAN_MIX) return fail(h, EMCMC_INVALID_ARG, "not a mix update");
+    *lambda = h->updates[pidx - 1].lam;
     return EMCMC_OK;
 }
 

@@ -180,6 +180,8 @@ class EmcmcMoments(C.Structure):
     ]
 
 
+LAMBDA_FN = C.CFUNCTYPE(C.c_double, C.c_double, C.c_int64, C.c_int64, C.c_void_p)  # emcmc_lambda_fn
+
 # every symbol declared in include/emcmc.h, with its ctypes signature
 _H = C.c_void_p
 _ST = C.c_int
@@ -201,6 +203,8 @@ SIGNATURES = {
         _ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     ),
     "emcmc_get_faults": (_ST, [_H, C.POINTER(C.c_uint32)]),
+    "emcmc_set_mix_lambda_fn": (_ST, [_H, C.c_uint32, LAMBDA_FN, C.c_void_p]),
+    "emcmc_get_mix_lambda": (_ST, [_H, C.c_uint32, C.POINTER(C.c_double)]),
     "emcmc_get_proposal_ll": (_ST, [_H, C.POINTER(C.c_double)]),
     "emcmc_get_chain_moments": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_get_mix_state": (_ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),

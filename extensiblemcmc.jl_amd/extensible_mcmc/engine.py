@@ -341,6 +341,18 @@ class Engine:
         self._check(self._lib.emcmc_get_mix_state(self._h, pidx, L.dptr(Lb), C.byref(M)), "emcmc_get_mix_state")
         return Lb, int(M.value)
 
+    def set_mix_lambda_fn(self, pidx: int, f):
+        """HaarioTypeAdaptation's fλ(λ, N, mcmc_iter) (adaptation.jl:425), called on the
+        host at each readjust; None restores the identity."""
+        cb = L.LAMBDA_FN(lambda lam, N, it, ctx: float(f(lam, int(N), int(it)))) if f is not None else L.LAMBDA_FN()
+        self._flam = cb  # keep the trampoline alive while the handle may call it
+        self._check(self._lib.emcmc_set_mix_lambda_fn(self._h, pidx, cb, None), "emcmc_set_mix_lambda_fn")
+
+    def get_mix_lambda(self, pidx: int = 1) -> float:
+        v = C.c_double()
+        self._check(self._lib.emcmc_get_mix_lambda(self._h, pidx, C.byref(v)), "emcmc_get_mix_lambda")
+        return float(v.value)
+
     def get_faults(self):
         f = np.empty(self.cfg.num_chains, dtype=np.uint32)
         self._check(self._lib.emcmc_get_faults(self._h, L.u32ptr(f)), "emcmc_get_faults")

@@ -427,8 +427,6 @@ class RandomWalkUpdate(MCMCParamUpdate):
         if isinstance(self.adpt, NoAdaptation):
             pass
         elif isinstance(self.adpt, HaarioTypeAdaptation) and isinstance(self.rw, GaussianRandomWalkMix):
-            if not self.adpt.identity_f:
-                raise UnsupportedPlugin("HaarioTypeAdaptation with a custom fλ has no device plugin (λ is fixed)")
             adapt = {"k": self.adpt.adapt_every_k_steps, "scale": self.adpt.scale}
         elif isinstance(self.adpt, AdaptationUnifRW) and isinstance(self.rw, UniformRandomWalk):
             a = self.adpt
@@ -448,6 +446,9 @@ class RandomWalkUpdate(MCMCParamUpdate):
                                               haario_k=None if adapt is None else adapt["k"],
                                               haario_scale=2.38 ** 2 if adapt is None else adapt["scale"],
                                               prior=prior)
+            if isinstance(self.adpt, HaarioTypeAdaptation) and not self.adpt.identity_f:
+                # fλ(λ, N, mcmc_iter): one λ for all chains, called on the host at each readjust
+                engine.set_mix_lambda_fn(engine.num_updates, self.adpt.f)
         elif isinstance(self.rw, GaussianRandomWalk):
             engine.add_gaussian_rw_update(coords0, self.rw.Sigma, prior=prior, prior_factors=factors,
                                           pos=self.rw.pos if np.any(self.rw.pos) else None)
@@ -469,6 +470,7 @@ class RandomWalkUpdate(MCMCParamUpdate):
             if isinstance(self.adpt, HaarioTypeAdaptation):
                 self.adpt.mean_chains, self.adpt.cov_chains = engine.get_chain_moments()
                 self.adpt.M = M
+            self.rw.lam = engine.get_mix_lambda(pidx)  # rw.λ after fλ (adaptation.jl:425)
         if isinstance(self.rw, UniformRandomWalk):
             eps, pr, ac = engine.get_update_state(pidx, len(self.rw.eps))
             self.rw.eps_chains = eps

@@ -303,6 +303,14 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
     error("no device plugin for $(typeof(updt.rw))")
 end
 
+# emcmc_lambda_fn trampoline: ctx is a HaarioTypeAdaptation, kept alive by the
+# MCMC object for the whole run!
+function _flam_trampoline(λ::Float64, N::Int64, it::Int64, ctx::Ptr{Cvoid})::Float64
+    adpt = unsafe_pointer_to_objref(ctx)::eMCMC.HaarioTypeAdaptation
+    Float64(adpt.fλ(λ, N, it))
+end
+_flam_cfunction() = @cfunction(_flam_trampoline, Float64, (Float64, Int64, Int64, Ptr{Cvoid}))
+
 # workspaces.jl:38 — init_global_workspace(::MCMCBackend, …)
 function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
                                      updates::Vector{<:eMCMC.MCMCUpdate}, data, θinit::Vector{T};
@@ -316,10 +324,17 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
     check(ccall((:emcmc_create, LIB), Cint, (Ref{Ptr{Cvoid}}, Ref{EmcmcConfig}), h, cfg), C_NULL, "emcmc_create")
     keep = Any[]
     GC.@preserve keep begin
-        for u in updates
+        for (i, u) in enumerate(updates)
             desc = Ref(_update_desc(u, keep))
             check(ccall((:emcmc_add_update, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcUpdateDesc}), h[], desc),
                   h[], "emcmc_add_update")
+            if u.rw isa eMCMC.GaussianRandomWalkMix && u.adpt isa eMCMC.HaarioTypeAdaptation
+                # fλ (adaptation.jl:425) runs in Julia at every readjust: the library
+                # calls back with (λ, N, mcmc_iter); ctx is the (mutable) adaptation
+                check(ccall((:emcmc_set_mix_lambda_fn, LIB), Cint, (Ptr{Cvoid}, UInt32, Ptr{Cvoid}, Ptr{Cvoid}),
+                            h[], UInt32(i), _flam_cfunction(), pointer_from_objref(u.adpt)),
+                      h[], "emcmc_set_mix_lambda_fn")
+            end
         end
     end
     P = data.P
@@ -389,6 +404,14 @@ function eMCMC.__run!(gws::MI355XGlobalWorkspace, local_wss, updates, schedule, 
         end
     end
     flush!()
+    for (i, u) in enumerate(updates)   # readjust! mutates rw.λ (adaptation.jl:425)
+        if u.rw isa eMCMC.GaussianRandomWalkMix
+            λ = Ref(0.0)
+            check(ccall((:emcmc_get_mix_lambda, LIB), Cint, (Ptr{Cvoid}, UInt32, Ref{Float64}), h, UInt32(i), λ),
+                  h, "emcmc_get_mix_lambda")
+            u.rw.λ = λ[]
+        end
+    end
     nothing
 end
 

@@ -186,7 +186,7 @@ typedef struct emcmc_unifrw_adaptation_vec {
  * defaults 100, 2.38², identity).  Passed as emcmc_update_desc.adaptation_params
  * when adaptation == EMCMC_ADPT_HAARIO.  `scale` is carried but, as in the
  * reference, readjust! uses the literal 2.38² (adaptation.jl:423); fλ is the
- * identity (λ stays at its initial value). */
+ * identity unless emcmc_set_mix_lambda_fn installs one. */
 typedef struct emcmc_haario_adaptation {
     uint32_t adapt_every_k_steps;
     uint32_t reserved;
@@ -376,6 +376,17 @@ emcmc_status emcmc_get_chain_moments(emcmc_handle *h, double *mean, double *cov)
  * and HaarioTypeAdaptation's M (own-turn steps since the last readjust).
  * Either may be NULL. */
 emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_sigma_b, uint32_t *steps_since_adapt);
+
+/* HaarioTypeAdaptation's fλ (adaptation.jl:372-397, 425: `rw.λ = adpt.fλ(rw.λ,
+ * adpt.N, mcmc_iter)` at every readjust!).  N and mcmc_iter are the same for
+ * every chain (P = 1: N = 1 + the iterations registered), so λ stays one
+ * number: the library calls f on the host, when emcmc_run enqueues the
+ * readjust, and the launches that follow use the new λ.  f = NULL restores the
+ * identity (the reference's default (x, y, z) -> x). */
+typedef double (*emcmc_lambda_fn)(double lambda, int64_t N, int64_t mcmciter, void *ctx);
+emcmc_status emcmc_set_mix_lambda_fn(emcmc_handle *h, uint32_t pidx, emcmc_lambda_fn f, void *ctx);
+/* The current λ of GaussianRandomWalkMix update `pidx` (rw.λ). */
+emcmc_status emcmc_get_mix_lambda(emcmc_handle *h, uint32_t pidx, double *lambda);
 
 /* Per-chain fault bits (EMCMC_FAULT_*), [C] uint32. */
 emcmc_status emcmc_get_faults(emcmc_handle *h, uint32_t *faults);

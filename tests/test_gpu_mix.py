@@ -194,3 +194,50 @@ def test_cfg4_shape_moments_match_oracle_on_sampled_chains(oracle, hist):
         assert np.array_equal(cov[c], st.cov[0]), c
         assert np.array_equal(Lb[c], st.LB[0]), c
         assert faults[c] == st.faults[0], c
+
+
+def _flam(lam, N, it):
+    """A custom HaarioTypeAdaptation fλ(λ, N, mcmc_iter) (adaptation.jl:425)."""
+    return 0.5 + 0.4 * np.sin(it / 37.0) * (N % 5) / 4.0
+
+
+def test_custom_flambda_matches_oracle(oracle):
+    """fλ called on the host at every readjust (emcmc_set_mix_lambda_fn): λ changes
+    every k = 40 steps; the oracle is run in readjust-sized pieces with the same
+    fλ applied to (λ, N, iter) between them."""
+    D, C, M, k = 8, 640, 240, 40
+    seed, mu, ts, obs, sa = _problem(D)
+    sb = 0.5 * sa
+    eng = _engine(D, C, M, seed, mu, ts, obs, sa, sb, 0.5, k, L.LL_PER_OBS, L.HIST_FULL)
+    eng.set_mix_lambda_fn(1, _flam)
+    eng.run_iters(1, M)
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=sb)
+    lam, hs = 0.5, []
+    for it0 in range(1, M + 1, k):
+        hs.append(oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=it0, nsteps=k, lam=lam,
+                                 haario_k=k, nthreads=8))
+        lam = _flam(lam, st.N, it0 + k - 1)  # rw.λ = fλ(rw.λ, adpt.N, mcmc_iter)
+    _check(eng, st, hs, list(range(1, M + 1)), True)
+    assert eng.get_mix_lambda(1) == lam
+
+
+def test_custom_flambda_through_the_api(oracle):
+    """HaarioTypeAdaptation(state; f = fλ) through MCMC / run: rw.λ is the adapted λ."""
+    from extensible_mcmc import (MCMC, GaussianRandomWalkMix, GsnTargetLaw, HaarioTypeAdaptation, MI355XBackend,
+                                 RandomWalkUpdate, run)
+    D, C, M, k = 4, 256, 160, 40
+    seed, mu, ts, obs, sa = _problem(D)
+    sb = 0.5 * sa
+    rw = GaussianRandomWalkMix(sa, sb, 0.5)
+    mcmc = MCMC([RandomWalkUpdate(rw, list(range(1, D + 1)),
+                                  adpt=HaarioTypeAdaptation(np.zeros(D), adapt_every_k_steps=k, f=_flam))],
+                backend=MI355XBackend(num_chains=C, seed=seed))
+    ws, _ = run(mcmc, M, dict(P=GsnTargetLaw(mu, ts), obs=obs), np.zeros(D))
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=sb)
+    lam = 0.5
+    for it0 in range(1, M + 1, k):
+        oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=it0, nsteps=k, lam=lam, haario_k=k,
+                       nthreads=8, history=False)
+        lam = _flam(lam, st.N, it0 + k - 1)
+    assert np.array_equal(ws.state, st.theta)
+    assert rw.lam == lam

@@ -567,6 +567,10 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget>
 __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
     static_assert(NU <= D && D <= kMwgMaxD, "NU ≤ D ≤ 32");
+    // loops over the update's NU coordinates and over the target's D stay rolled
+    // only for the largest updates: unrolled, the local vectors live in registers
+    constexpr bool RU = NU > 16;
+    constexpr bool RT = NU > 16;
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
@@ -585,7 +589,7 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
         double tl[NU], tp[NU], ta[NU];
         for (int j = 0; j < NU; ++j) tl[j] = ((uint32_t)j < n) ? a.theta[state_pos(u.coords[j], chain, C, D)] : 0.0;
         double ltd_fwd, ltd_rev, lpp, lpc;
-        mwg_local_step<NU, true>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
+        mwg_local_step<NU, RU>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
         // ---- set_proposal!: P°.θ[coords] ← θ°, then all of P°.θ for the likelihood
         for (int j = 0; j < NU; ++j)
             if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tp[j];
@@ -593,7 +597,7 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
 #pragma unroll
         for (int d = 0; d < D; ++d) mp[d] = a.mu_p[state_pos(d, chain, C, D)];
         // ---- compute_ll!
-        const double llp = TGT::template loglik<D, LLMODE, true>(a, mp);
+        const double llp = TGT::template loglik<D, LLMODE, RT>(a, mp);
         if (!(llp - llp == 0.0)) faults |= 1u;
         a.ll_prop[(uint64_t)p * C + chain] = llp;
         // ---- accept_reject! (run.jl:268-281)

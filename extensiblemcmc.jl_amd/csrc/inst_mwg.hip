@@ -17,7 +17,8 @@ MwgFn mwg_wide_fn() {
     {D, NU, mwg_wide_fn<D, NU, true, 0>(), mwg_wide_fn<D, NU, true, 1>(), mwg_wide_fn<D, NU, false, 0>(), \
      mwg_wide_fn<D, NU, false, 1>()}
 const std::vector<MwgEntry> &mwg_table() {
-    static const std::vector<MwgEntry> t = {MWG4(1), MWG4(2), MWG4(3), MWG4(4), MWG4(8), MWG4(16), MWGW4(32, 32)};
+    static const std::vector<MwgEntry> t = {MWG4(1),  MWG4(2),  MWG4(3),        MWG4(4),
+                                            MWG4(8),  MWG4(16), MWGW4(32, 16), MWGW4(32, 32)};
     return t;
 }
 

@@ -113,7 +113,7 @@ struct UpdateHost {
     // prior (priors.jl) per local coordinate: family, parameters, host constant; factor starts
     std::vector<uint32_t> pfam;
     std::vector<double> pa, pb, pc;
-    uint32_t pstart = 0;
+    uint64_t pstart = 0;
 };
 
 struct TargetHost {
@@ -380,8 +380,9 @@ emcmc_status select_mwg(emcmc_handle *h) {
     // same kernel compiled at run time (emcmc_rtc.hip, cached per process)
     if (user || (!v.mfn && D <= kMwgMaxD)) {
         RtcKernel k;
-        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, k)
-                                     : rtc_compile_gsn(D, full, ll, k);
+        const int nu = rtc_wide_nu(D, (int)nmax);
+        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k)
+                                     : rtc_compile_gsn(D, full, ll, nu, k);
         if (!log.empty()) {
             h->err = std::string(user ? "user target does not compile:\n" : "run-time kernel build failed:\n") + log;
             return user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
@@ -402,7 +403,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
     }
     if (!v.mfn && !v.ufn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                    "no general-schedule device kernel for D=%d (D ≤ 32)", D);
+                    "no general-schedule device kernel for D=%d (D ≤ 64)", D);
     std::vector<MwgUpdate> tab(h->updates.size());
     for (size_t p = 0; p < h->updates.size(); ++p) {
         const UpdateHost &u = h->updates[p];
@@ -414,7 +415,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
         for (uint32_t j = 0; j < m.nc; ++j) m.coords[j] = u.coords[j];
         if (u.kernel == EMCMC_RW_UNIFORM) {
             for (uint32_t j = 0; j < m.nc; ++j) m.eps0[j] = u.eps[j];
-            for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1u << j) : 0u;
+            for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1ull << j) : 0ull;
             if (u.adaptation == EMCMC_ADPT_UNIF_RW) {
                 m.k = u.adpt.adapt_every_k_steps;
                 m.target = u.adpt.target_accpt_rate;
@@ -432,7 +433,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
             for (int i = 0; i < n; ++i) m.iL[i] = u.invdiag[i];
             m.c0 = u.c0;
             m.diag = u.diag ? 1u : 0u;
-            for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1u << j) : 0u;
+            for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1ull << j) : 0ull;
         }
         m.prior = u.prior;
         m.pstart = u.pstart;
@@ -478,7 +479,7 @@ bool fused_eligible(const emcmc_handle *h) {
     const UpdateHost &u = h->updates[0];
     if (u.prior != EMCMC_PRIOR_IMPROPER) return false;  // priors and proposal! resampling: general kernel
     for (uint8_t f : u.pos)
-        if (f) return false;  // positivity-restricted coordinates: general schedule kernel (D ≤ 32)
+        if (f) return false;  // positivity-restricted coordinates: general schedule kernel (D ≤ 64)
     return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
 }
 
@@ -604,7 +605,7 @@ emcmc_status select_variant(emcmc_handle *h) {
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
     // a correlated Σ (proposal or target) beyond the fused dense kernel's D ≤ 8
-    // runs on the general kernel: forward substitutions from the factors, D ≤ 32
+    // runs on the general kernel: forward substitutions from the factors, D ≤ 64
     if (!(u.diag && h->target.diag) && D > 8) return select_mwg(h);
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     const int ll = (int)h->target.ll_mode;
@@ -1227,7 +1228,7 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
             default:
                 return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior family %u has no device plugin", fa.family);
             }
-            if (u->prior == EMCMC_PRIOR_PRODUCT && j > 0) uh.pstart |= 1u << j;
+            if (u->prior == EMCMC_PRIOR_PRODUCT && j > 0) uh.pstart |= 1ull << j;
             for (uint32_t k = 0; k < fa.count; ++k, ++j) {
                 uh.pfam.push_back(fa.family);
                 uh.pa.push_back(a);
@@ -1420,7 +1421,7 @@ emcmc_status emcmc_set_user_target(emcmc_handle *h, const emcmc_user_target_desc
     if (h->updates.empty()) {  // compile now, so errors surface here; select_variant reuses the cache
         RtcKernel k;
         const std::string log = rtc_compile_user(h->target.src, h->target.opts, (int)t->dim,
-                                                 h->cfg.history_mode == EMCMC_HIST_FULL, k);
+                                                 h->cfg.history_mode == EMCMC_HIST_FULL, (int)t->dim, k);
         if (!log.empty()) {
             h->err = "user target does not compile:\n" + log;
             h->target_set = false;
@@ -1437,7 +1438,7 @@ emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const cha
                                      size_t log_len) {
     if (!source) return EMCMC_INVALID_ARG;
     RtcKernel k;
-    const std::string log = rtc_compile_user(source, options ? options : "", (int)dim, true, k);
+    const std::string log = rtc_compile_user(source, options ? options : "", (int)dim, true, (int)dim, k);
     if (log_out && log_len) {
         const size_t n = std::min(log.size(), log_len - 1);
         std::memcpy(log_out, log.data(), n);

@@ -43,7 +43,7 @@
 
 namespace emcmc {
 
-constexpr int kMwgMaxD = 32;
+constexpr int kMwgMaxD = 64;  // largest D of the general kernel (D ≤ 32 instantiated ahead of time, the rest at run time)
 constexpr uint32_t kMaxResample = 0xFFFEu;          // proposal! resamples before fault bit 8
 constexpr uint32_t kFaultPriorResample = 8u;       // EMCMC_FAULT_PRIOR_RESAMPLES
 
@@ -62,14 +62,16 @@ struct MwgUpdate {
     double L[kMwgMaxD * kMwgMaxD];  // GaussianRandomWalk: lower Cholesky factor, row-major, local indices
     double iL[kMwgMaxD];            // 1 / L_ii
     double c0;                      // −(nc·log2π + logdet Σ)/2
-    uint32_t diag, posmask;          // posmask bit j: coordinate j positivity-restricted
+    uint32_t diag, reserved0;
+    uint64_t posmask;                // bit j: coordinate j positivity-restricted
     double target;                  // AdaptationUnifRW target_accpt_rate
     double ascale[kMwgMaxD], amin[kMwgMaxD], amax[kMwgMaxD], aoff[kMwgMaxD];  // per coordinate (the scalar
                                     // form repeats its values)
     // prior over the update's local coordinates (priors.jl): kind, and for
     // Product/Standard priors one univariate family per coordinate, with
     // bit j of pstart set where coordinate j starts a new ProductPrior factor
-    uint32_t prior, pstart;
+    uint32_t prior, reserved1;
+    uint64_t pstart;
     uint32_t pfam[kMwgMaxD];
     double pa[kMwgMaxD], pb[kMwgMaxD], pc[kMwgMaxD];  // family parameters + host-computed constants
 };
@@ -151,7 +153,7 @@ __device__ __forceinline__ double mwg_log_prior(const MwgUpdate &u, uint32_t n, 
             const double v = univariate_logpdf(u.pfam[j], u.pa[j], u.pb[j], u.pc[j], x[j]);
             if (j == 0) {
                 s = v;
-            } else if ((u.pstart >> j) & 1u) {
+            } else if ((u.pstart >> j) & 1ull) {
                 lp = lp + s;
                 s = v;
             } else {
@@ -207,7 +209,8 @@ __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, 
             if ((uint32_t)i < n) s = fma(y[i], y[i], s);
         return s;
     }
-    // n ∈ {16, 24, 32}: blocks of 8, pairwise tree over the n/8 blocks
+    // n ∈ {16, 24, …, 64}: blocks of 8, then the pairwise tree over the n/8
+    // blocks (tree_inplace's order with a run-time block count)
     constexpr int NBMAX = D / 8 > 0 ? D / 8 : 1;
     double b[NBMAX];
 #pragma unroll UJ
@@ -216,10 +219,23 @@ __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, 
 #pragma unroll UJ
         for (int i = 1; i < 8; ++i) b[k] = fma(y[8 * k + i], y[8 * k + i], b[k]);
     }
-    const uint32_t nb = n / 8;
-    if (nb == 2) return b[0] + b[1 % NBMAX];
-    if (nb == 3) return (b[0] + b[1 % NBMAX]) + b[2 % NBMAX];
-    return (b[0] + b[1 % NBMAX]) + (b[2 % NBMAX] + b[3 % NBMAX]);
+    uint32_t nb = n / 8;
+#pragma unroll
+    for (int lvl = 0; lvl < 3; ++lvl) {  // NBMAX ≤ 8
+        if (nb <= 1) break;
+        double last = b[0];
+#pragma unroll
+        for (int q = 1; q < NBMAX; ++q) last = ((uint32_t)q == nb - 1) ? b[q] : last;
+#pragma unroll
+        for (int i = 0; i < NBMAX / 2; ++i)
+            if ((uint32_t)i < nb / 2) b[i] = b[2 * i] + b[2 * i + 1];
+        if (nb & 1u) {
+#pragma unroll
+            for (int q = 0; q < NBMAX; ++q) b[q] = ((uint32_t)q == nb / 2) ? last : b[q];
+        }
+        nb = (nb + 1) / 2;
+    }
+    return b[0];
 }
 
 // The built-in target: loglikelihood(P°::GsnTargetLaw, obs) (gsn_target.jl:23-29),
@@ -265,8 +281,8 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
     ltd_fwd = 0.0;
     ltd_rev = 0.0;
     double ev[NU];  // UniformRandomWalk ϵ of each local coordinate
-    const uint32_t pm = u.posmask;  // positivity-restricted coordinates
-    auto isp = [&](int i) { return ((pm >> i) & 1u) != 0u; };
+    const uint64_t pm = u.posmask;  // positivity-restricted coordinates
+    auto isp = [&](int i) { return ((pm >> i) & 1ull) != 0ull; };
     for (uint32_t rs = 0;; ++rs) {
         if (u.kind == 1) {  // UniformRandomWalk: θ° = θ·1 + U, or θ·e^U where pos
 #pragma unroll UJ
@@ -287,7 +303,7 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
                 }
             }
         } else {  // GaussianRandomWalk over the update's coordinates
-            if (rs > 0 && pm != 0u) {  // the previous rand! left θ ← exp(log θ) where pos
+            if (rs > 0 && pm != 0ull) {  // the previous rand! left θ ← exp(log θ) where pos
 #pragma unroll UJ
                 for (int i = 0; i < NU; ++i)
                     if ((uint32_t)i < n && isp(i)) tl[i] = exp_any(log_any(tl[i]));
@@ -342,7 +358,7 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
         }
     } else {
         double r[NU];
-        if (pm == 0u) {
+        if (pm == 0ull) {
 #pragma unroll UJ
             for (int i = 0; i < NU; ++i) r[i] = tp[i] - tl[i];
             ltd_fwd = u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0;
@@ -402,14 +418,14 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
             ltd_fwd = (u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0) + (-lj);
         }
     }
-    if (!(u.kind == 2 && pm != 0u)) {
+    if (!(u.kind == 2 && pm != 0ull)) {
 #pragma unroll UJ
         for (int j = 0; j < NU; ++j) ta[j] = tp[j];
     }
     lpp = 0.0;
     lpc = 0.0;
     if (u.prior != kPriorImproper) {
-        const bool rt = (u.kind == 2 && pm != 0u);  // after the pos round trips: θ°₃, θ₃
+        const bool rt = (u.kind == 2 && pm != 0ull);  // after the pos round trips: θ°₃, θ₃
         lpp = mwg_log_prior<NU, ROLL>(u, n, rt ? ta : tp);
         lpc = mwg_log_prior<NU, ROLL>(u, n, rt ? t3 : tl);
     }
@@ -566,7 +582,7 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 // registers.  The arithmetic is mwg_gsn_kernel's.
 template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget>
 __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
-    static_assert(NU <= D && D <= kMwgMaxD, "NU ≤ D ≤ 32");
+    static_assert(NU <= D && D <= kMwgMaxD, "NU ≤ D ≤ 64");
     // loops over the update's NU coordinates and over the target's D stay rolled
     // only for the largest updates: unrolled, the local vectors live in registers
     constexpr bool RU = NU > 16;

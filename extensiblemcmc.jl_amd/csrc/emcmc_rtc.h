@@ -33,9 +33,12 @@ struct RtcKernel {
 
 // Compile (or fetch from the process-wide cache) the general schedule kernel
 // for dimension D with the user's log-likelihood: mwg_gsn_kernel<D> for
-// D ≤ 16, mwg_wide_kernel<D, D> for 16 < D ≤ 32.  Returns "" on success,
-// else the compiler's log.
-std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, RtcKernel &out);
+// D ≤ 16, mwg_wide_kernel<D, NU> for 16 < D ≤ 64 (NU = 16 when every update
+// has ≤ 16 coordinates — unrolled, in registers — else NU = D).  Returns "" on
+// success, else the compiler's log.
+int rtc_wide_nu(int D, int nmax);
+std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
+                             RtcKernel &out);
 
 // The text of a law the library ships as an EMCMC_USER_LOGLIK source
 // (csrc/laws/<name>), or nullptr.
@@ -43,6 +46,6 @@ const char *rtc_builtin_law(const char *name);
 
 // The same kernel with the built-in GsnTargetLaw (emcmc_mwg.h GsnTarget) for a
 // dimension the library has no ahead-of-time instantiation of (inst_mwg.hip).
-std::string rtc_compile_gsn(int D, bool full, int ll_mode, RtcKernel &out);
+std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out);
 
 }  // namespace emcmc

@@ -59,11 +59,15 @@ std::string program_log(hiprtcProgram p) {
 }  // namespace
 
 // src empty: the built-in GsnTarget with likelihood mode ll; else the user's law
-std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, RtcKernel &out) {
-    if (D < 1 || D > 32) return "the general schedule kernel runs 1 ≤ D ≤ 32";
+int rtc_wide_nu(int D, int nmax) { return (D > 16 && nmax <= 16) ? 16 : D; }
+
+std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
+                        RtcKernel &out) {
+    if (D < 1 || D > 64) return "the general schedule kernel runs 1 ≤ D ≤ 64";
+    if (nu < 1 || nu > D) nu = D;
     const bool user = !src.empty();
     std::ostringstream key;
-    key << D << '|' << full << '|' << ll << '|' << opts << '|' << src;
+    key << D << '|' << nu << '|' << full << '|' << ll << '|' << opts << '|' << src;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_cache.find(key.str());
@@ -79,8 +83,8 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
         expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ">";
         name << "mwg_gsn_kernel<D=" << D;
     } else {
-        expr << "emcmc::mwg_wide_kernel<" << D << ", " << D << ", " << fl << ", " << ll << ", " << tgt << ">";
-        name << "mwg_wide_kernel<D=" << D << ",NU=" << D;
+        expr << "emcmc::mwg_wide_kernel<" << D << ", " << nu << ", " << fl << ", " << ll << ", " << tgt << ">";
+        name << "mwg_wide_kernel<D=" << D << ",NU=" << nu;
     }
     name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << "[hiprtc]>";
@@ -130,9 +134,10 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     return "";
 }
 
-std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, RtcKernel &out) {
+std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
+                             RtcKernel &out) {
     if (src.empty()) return "empty user source";
-    return rtc_compile(src, opts, D, full, 0, out);
+    return rtc_compile(src, opts, D, full, 0, nu, out);
 }
 
 const char *rtc_builtin_law(const char *name) {
@@ -141,6 +146,8 @@ const char *rtc_builtin_law(const char *name) {
     return nullptr;
 }
 
-std::string rtc_compile_gsn(int D, bool full, int ll_mode, RtcKernel &out) { return rtc_compile("", "", D, full, ll_mode, out); }
+std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out) {
+    return rtc_compile("", "", D, full, ll_mode, nu, out);
+}
 
 }  // namespace emcmc

@@ -64,7 +64,7 @@ typedef enum emcmc_status {
 /* Priors — src/priors.jl.  Evaluated on the update's local coordinates
  * (log_prior, updates.jl:104; run.jl:374-385); proposal! draws θ° again while
  * logpdf(prior, θ°) === −Inf (updates.jl:191-196).  Non-improper priors run on
- * the general schedule kernel (D ≤ 32). */
+ * the general schedule kernel (D ≤ 64). */
 #define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior     priors.jl:18-19: 0.0 */
 #define EMCMC_PRIOR_IMPROPER_POS 1u /* ImproperPosPrior  priors.jl:25-26: −sum(log.(θ)) */
 #define EMCMC_PRIOR_PRODUCT 2u      /* ProductPrior(dists, dims) priors.jl:60-88: lp = 0.0; lp += logpdf(dist, θ[idx])
@@ -216,7 +216,7 @@ typedef struct emcmc_prior_desc {
  * kernels; a single GaussianRandomWalkMix update on coords 1:D (optionally with
  * HaarioTypeAdaptation, BASELINE cfg 4) runs on the mix kernels, which also keep
  * the chain moments; every other schedule runs on the general schedule kernel
- * (D ≤ 32). */
+ * (D ≤ 64). */
 typedef struct emcmc_update_desc {
     uint32_t kernel;          /* EMCMC_RW_UNIFORM, EMCMC_RW_GAUSSIAN or EMCMC_RW_GAUSSIAN_MIX */
     uint32_t prior;           /* EMCMC_PRIOR_* */
@@ -228,7 +228,7 @@ typedef struct emcmc_update_desc {
     const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
     const uint8_t *pos;       /* positivity flags or NULL (all false); true on device for UniformRandomWalk
                                  (θ° = θ·e^U, random_walk.jl:63-94) and GaussianRandomWalk (log scale,
-                                 random_walk.jl:136-171; D ≤ 32), not for GaussianRandomWalkMix */
+                                 random_walk.jl:136-171; D ≤ 64), not for GaussianRandomWalkMix */
     const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW),
                                       const emcmc_unifrw_adaptation_vec* (EMCMC_ADPT_UNIF_RW_VEC) or
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
@@ -268,7 +268,7 @@ typedef struct emcmc_target_desc {
  * in the C subset both hiprtc and a C compiler accept: + − × ÷, fma, sqrt, fabs,
  * copysign, em_exp(x), em_log(x) (the engine's exp / log, NaN below 0;
  * oracle/user_prelude.h maps them to their CPU restatement).  Every update kind, prior and adaptation
- * of the general kernel runs with it; D ≤ 32.  GaussianRandomWalkMix and MALA
+ * of the general kernel runs with it; D ≤ 64.  GaussianRandomWalkMix and MALA
  * raise EMCMC_UNSUPPORTED_PLUGIN with a user target. */
 typedef struct emcmc_user_target_desc {
     uint32_t dim;           /* length(P.θ) = D */

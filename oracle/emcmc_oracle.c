@@ -567,7 +567,7 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
  * to the update); the accept exponential as orc_exponential with pidx0 = p.
  * ========================================================================== */
 
-#define ORC_MWG_MAXD 32
+#define ORC_MWG_MAXD 64
 #define ORC_MAX_RESAMPLE 0xFFFEu
 #define ORC_FAULT_PRIOR_RESAMPLES 8u
 
@@ -663,11 +663,11 @@ static double orc_mwg_log_prior(const orc_mwg_update *u, uint32_t n, const doubl
 typedef double (*orc_user_loglik_fn)(const double *theta, int D, const double *obs, uint64_t nobs,
                                      const double *params);
 
-/* table layout from Python (ORC_MWG_MAXD = 32 slots per update):
- *   kind[P], nc[P], coords[P*32], eps[P*32], sigma[P*1024] (nc×nc column-major),
- *   pos[P*32] (uint8), adapt[P], k[P], aparams[P*129] = (target, scale[32], min[32], max[32], offset[32])
+/* table layout from Python (ORC_MWG_MAXD = 64 slots per update):
+ *   kind[P], nc[P], coords[P*64], eps[P*64], sigma[P*4096] (nc×nc column-major),
+ *   pos[P*64] (uint8), adapt[P], k[P], aparams[P*257] = (target, scale[64], min[64], max[64], offset[64])
  *   (AdaptationUnifRW per coordinate; the scalar form repeats its values),
- *   prior[P], factor tables per update: nfac[P], ffam[P*32], fcnt[P*32], fa[P*32], fb[P*32];
+ *   prior[P], factor tables per update: nfac[P], ffam[P*64], fcnt[P*64], fa[P*64], fb[P*64];
  * ll_prop [P][C] out: sub_ws°.ll of each update's latest proposal (NULL: skip);
  * user_ll: NULL for GsnTargetLaw, else the user target (user_params its parameters). */
 ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, uint32_t P, const uint32_t *kind,
@@ -718,14 +718,14 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         }
         if (u->kind == 2) {
             const int n = (int)u->nc;
-            if (orc_cholesky(sigma + (size_t)p * 1024, n, u->L)) {
+            if (orc_cholesky(sigma + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD, n, u->L)) {
                 free(g);
                 free(U);
                 return -1;
             }
             for (int i = 0; i < n; ++i) u->iL[i] = 1.0 / u->L[(size_t)i * n + i];
             u->c0 = mvnormal_c0(n, logdet_chol(u->L, n));
-            u->diag = is_diag_upper(sigma + (size_t)p * 1024, n);
+            u->diag = is_diag_upper(sigma + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD, n);
         }
         u->adapt = adapt[p];
         u->k = adapt_k[p];

@@ -252,7 +252,7 @@ def markstein_mismatches(b, x):
 
 
 # ---- general schedule path (P ≥ 1 updates, Metropolis-within-Gibbs) ---------
-MWG_MAXD = 32
+MWG_MAXD = 64
 KIND_UNIFORM, KIND_GAUSSIAN = 1, 2
 
 

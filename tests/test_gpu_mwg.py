@@ -233,3 +233,41 @@ def test_per_coordinate_adaptation(oracle):
     steps = full_steps(600, 1)
     eng, st, h = run_both(oracle, 2, 1500, 600, ups, [1.0, 2.0], w.t_sigma, w.obs, steps, w.seed)
     check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_d64_general_kernel_blocks_and_dense(oracle):
+    """D = 64 on the general kernel (compiled at run time): a diagonal Gaussian
+    block of 16, a correlated Gaussian block of 40 (five canonical 8-blocks: the
+    run-time tree 5 → 3 → 2 → 1) and a UniformRandomWalk block of 8 with a
+    Normal ProductPrior, against a dense D = 64 target."""
+    rng = np.random.default_rng(9)
+    D, C, M = 64, 700, 120
+    A = rng.standard_normal((D, D))
+    ts = A @ A.T / D + np.eye(D)
+    mu = rng.normal(size=D)
+    obs = mu + rng.normal(size=(6, D))
+    B = rng.standard_normal((40, 40))
+    S40 = 0.002 * (B @ B.T / 40 + np.eye(40))
+    ups = [oracle.mwg_update(2, range(0, 16), sigma=0.01 * np.eye(16)),
+           oracle.mwg_update(2, range(16, 56), sigma=S40),
+           oracle.mwg_update(1, range(56, 64), eps=[0.05] * 8, prior=L.PRIOR_PRODUCT,
+                             factors=[(L.DIST_NORMAL, 8, 0.0, 3.0)])]
+    steps = full_steps(M, 3)
+    eng, st, h = run_both(oracle, D, C, M, ups, mu, ts, obs, steps, 31)
+    assert "D=64" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 3)
+
+
+def test_d48_block_of_48(oracle):
+    """A joint GaussianRandomWalk block of all 48 coordinates (six 8-blocks, tree
+    6 → 3 → 2 → 1) beside nothing else, on a diagonal target: general kernel
+    NU = 48 compiled at run time."""
+    rng = np.random.default_rng(10)
+    D, C, M = 48, 512, 80
+    mu = rng.normal(size=D)
+    obs = mu + rng.normal(size=(5, D))
+    ups = [oracle.mwg_update(2, range(D), sigma=0.004 * np.eye(D), pos=[False] * D, prior=L.PRIOR_PRODUCT,
+                             factors=[(L.DIST_NORMAL, D, 0.0, 10.0)])]
+    steps = full_steps(M, 1)
+    eng, st, h = run_both(oracle, D, C, M, ups, mu, np.eye(D), obs, steps, 32)
+    check(oracle, eng, st, h, steps, ups, 1)

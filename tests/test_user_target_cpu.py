@@ -10,7 +10,8 @@ from extensible_mcmc import _lib as L
 
 
 @pytest.mark.parametrize("name,D", [("student_t_regression", 4), ("poisson_regression", 3), ("banana", 2),
-                                    ("banana", 24), ("gsn_identity", 3), ("gsn_full", 6), ("gsn_full", 20)])
+                                    ("banana", 24), ("banana", 64), ("gsn_identity", 3), ("gsn_full", 6),
+                                    ("gsn_full", 20)])
 def test_user_source_compiles_for_gfx950(oracle, name, D):
     _, src = oracle.user_loglik(name)
     L.check_user_target(src, D)  # raises with the hiprtc log on error
@@ -27,7 +28,7 @@ def test_user_source_compile_error_is_reported():
 def test_user_target_rejects_too_large_dim(oracle):
     _, src = oracle.user_loglik("banana")
     with pytest.raises(L.EMCMCError):
-        L.check_user_target(src, 33)
+        L.check_user_target(src, 65)
 
 
 @pytest.mark.parametrize("make", [U.student_t, U.poisson, U.banana, U.gsn_identity, U.gsn_full])

@@ -15,7 +15,10 @@ from pathlib import Path
 import numpy as np
 
 ORACLE_DIR = Path(__file__).resolve().parent
-LIB_PATH = ORACLE_DIR / "lib" / "liboracle.so"
+import os  # noqa: E402
+
+# EMCMC_ORACLE_LIB: an alternative build (tests/test_oracle_sanitized.py loads the ASan/UBSan one)
+LIB_PATH = Path(os.environ.get("EMCMC_ORACLE_LIB", ORACLE_DIR / "lib" / "liboracle.so"))
 
 _lib = None
 

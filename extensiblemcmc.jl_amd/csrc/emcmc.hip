@@ -142,7 +142,7 @@ struct Variant {
     MalaFn afn = nullptr, ainit = nullptr;  // MALA step / ∇ℓ initialisation kernels
     bool mix = false;
     int lpc = 1;
-    bool dense = false;
+    int dense = 0;  // 0 rwm_gsn_diag_kernel, 1 rwm_gsn_dense_kernel, 2 rwm_gsn_chol_kernel
     bool unit = false;
     int occ = 0;
     std::string name;
@@ -245,9 +245,9 @@ emcmc_status fail(emcmc_handle *h, emcmc_status st, const char *fmt, ...) {
                         "%s failed: %s", #expr, hipGetErrorString(e_));                       \
     } while (0)
 
-KernelFn lookup(int D, int lpc, bool full, int ll, bool dense, bool unit, int occ = 0) {
+KernelFn lookup(int D, int lpc, bool full, int ll, int dense, bool unit, int occ = 0) {
     for (const auto &e : diag_table())
-        if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == (int)dense &&
+        if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == dense &&
             e.k.unit == (int)unit && e.k.occ == occ)
             return e.fn;
     return nullptr;
@@ -604,11 +604,12 @@ emcmc_status select_variant(emcmc_handle *h) {
     if (!fused_eligible(h)) return select_mwg(h);
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
-    // a correlated Σ (proposal or target) beyond the fused dense kernel's D ≤ 8
-    // runs on the general kernel: forward substitutions from the factors, D ≤ 64
-    if (!(u.diag && h->target.diag) && D > 8) return select_mwg(h);
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     const int ll = (int)h->target.ll_mode;
+    // a correlated Σ (proposal or target) beyond the fused dense kernel's D ≤ 8:
+    // rwm_gsn_chol_kernel (factors through the scalar cache) where instantiated,
+    // else the general kernel (forward substitutions from the factors, D ≤ 64)
+    if (!(u.diag && h->target.diag) && D > 8 && !lookup(D, 1, full, ll, 2, false)) return select_mwg(h);
     const bool diag = u.diag && h->target.diag;
     Variant v;
     if (diag) {
@@ -632,17 +633,18 @@ emcmc_status select_variant(emcmc_handle *h) {
         v.lpc = lpc;
         v.dense = false;
     } else {
-        v.fn = lookup(D, 1, full, ll, true, false);
+        v.dense = D > 8 ? 2 : 1;
+        v.fn = lookup(D, 1, full, ll, v.dense, false);
         v.lpc = 1;
-        v.dense = true;
     }
     if (!v.fn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "no device kernel for D=%d (%s, lanes_per_chain=%u); instantiated: diag D∈{1,2,3,4,8,16,32,64}, "
-                    "dense D∈{1,2,3,4,8}",
+                    "dense D∈{1,2,3,4,8,16,24,32}",
                     D, diag ? "diagonal" : "dense", h->cfg.lanes_per_chain);
     char nm[160];
-    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>", v.dense ? "dense" : "diag", D, v.lpc,
+    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>",
+             v.dense == 2 ? "chol" : v.dense ? "dense" : "diag", D, v.lpc,
              full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
              v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : "");
     v.name = nm;
@@ -657,6 +659,21 @@ emcmc_status select_variant(emcmc_handle *h) {
             c[2 * D + i] = t.invdiag[i];
             c[3 * D + i] = t.xbar[i];
         }
+    } else if (v.dense == 2) {
+        // packed column-major lower factors (emcmc_kernels.h, rwm_gsn_chol_kernel):
+        // L_rw with its diagonal, L_rw and L_t with 1/L_jj in place of L_jj, x̄, the
+        // observations row-major
+        const size_t P = (size_t)D * (D + 1) / 2;
+        c.resize(3 * P + (size_t)D + (ll == LL_PER_OBS ? t.nobs * (size_t)D : 0));
+        for (int j = 0; j < D; ++j)
+            for (int i = j; i < D; ++i) {
+                const size_t e = (size_t)chol_col(D, j) + (size_t)(i - j);
+                c[e] = u.L[(size_t)i * D + j];
+                c[P + e] = (i == j) ? u.invdiag[j] : u.L[(size_t)i * D + j];
+                c[2 * P + e] = (i == j) ? t.invdiag[j] : t.L[(size_t)i * D + j];
+            }
+        std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 3 * P);
+        if (ll == LL_PER_OBS) std::copy(t.obs.begin(), t.obs.end(), c.begin() + 3 * P + D);
     } else {
         const size_t DD = (size_t)D * D;
         c.resize(2 * DD + 3 * (size_t)D);
@@ -666,8 +683,9 @@ emcmc_status select_variant(emcmc_handle *h) {
         std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
         std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     }
-    const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    size_t lds = (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
+    const size_t obs_doubles = (ll == LL_PER_OBS && v.dense != 2) ? t.nobs * (size_t)D : 0;
+    // (the chol kernel reads its constants through the scalar cache: no dynamic LDS)
+    size_t lds = v.dense == 2 ? 0 : (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
     if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc, diag_block(v.occ) / 64);
     if (kZigLdsBytes + lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,

@@ -329,15 +329,18 @@ __device__ __forceinline__ void propose_diag_batched(const ZigTabs &zt, const Wa
 }
 
 // The N standard normals themselves (dense-L proposals).
-template <int N>
+template <int N, bool VK = false>
 __device__ __forceinline__ void normals(const ZigTabs &zt, uint32_t key0, uint32_t key1, uint32_t chain,
-                                        uint32_t iter, uint32_t pidx0, double (&z)[N], uint32_t &faults) {
+                                        uint32_t iter, uint32_t pidx0, double (&z)[N], uint32_t &faults,
+                                        const PhiloxVKeys &vk = PhiloxVKeys{}) {
     constexpr int NP = (N + 1) / 2;
     uint64_t pend = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
         if constexpr (N > 8) __builtin_amdgcn_sched_barrier(0);  // one Philox block at a time
-        const u32x4 r = draw(key0, key1, chain, iter, j, pidx0, 0);
+        u32x4 r;
+        if constexpr (VK) r = draw_vk(vk, chain, iter, j, pidx0);
+        else r = draw(key0, key1, chain, iter, j, pidx0, 0);
         if (!zig_normal_fast(zig_split_n(r.x, r.y), zt.n, z[2 * j])) pend |= 1ull << (2 * j);
         if (2 * j + 1 < N)
             if (!zig_normal_fast(zig_split_n(r.z, r.w), zt.n, z[2 * j + 1])) pend |= 1ull << (2 * j + 1);
@@ -907,6 +910,266 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     a.faults[chain] = faults;
     if (faults) *a.fault_flag = 1u;
     store_state<D>(a.theta, C, chain, 0, th, false);
+}
+
+// ---------------------------------------------------------------------------
+// Correlated Σ at D ≥ 16 (rows a5/a10 at the headline D): the same proposal,
+// transition densities and per-observation solves as rwm_gsn_dense_kernel, one
+// lane per chain, but the factors are read through the SCALAR cache: Σ_rw and
+// Σ_t are the same for every chain, so every factor element is wave-uniform and
+// enters v_fma_f64 as an SGPR operand (no per-lane LDS traffic: an LDS
+// broadcast would still return 8 B per lane per fma).  The sweeps run column by
+// column (forward substitution as column updates acc_i −= L_ij·y_j, i > j, and
+// the proposal L·z as acc_i += L_ij·z_j, i ≥ j): every row still accumulates
+// over j = 0, 1, … in ascending order, i.e. the oracle's row sums bit for bit,
+// and the D − j updates of a column are independent (ILP at 1 wave per SIMD).
+// Σ y_j² is accumulated as y_j leaves the sweep, in the canonical blocked order.
+//
+// Factor tables are packed column-major lower triangles (P = D(D+1)/2 doubles;
+// column j starts at chol_col(D, j) and holds rows j..D−1).  A "propose" table
+// keeps L_jj; a "solve" table stores 1/L_jj in its place, so a sweep is ONE flat
+// stream of scalar loads.  Constants (address space 4, in doubles):
+//   [0,P) L_rw propose | [P,2P) L_rw solve | [2P,3P) L_t solve | [3P,3P+D) x̄
+//   | [3P+D, 3P+D+nobs·D) observations, row-major
+typedef const __attribute__((address_space(4))) double cdouble;
+__host__ __device__ constexpr int chol_col(int D, int j) { return j * D - j * (j - 1) / 2; }
+__host__ __device__ constexpr int chol_col_of(int D, int e) {
+    int j = 0;
+    while (j + 1 < D && chol_col(D, j + 1) <= e) ++j;
+    return j;
+}
+
+// the opaque copy keeps the compiler from hoisting loop-invariant scalar loads
+// of the factors out of the step / observation loops (hundreds of SGPRs)
+__device__ __forceinline__ cdouble *opaque_cptr(const double *q) {
+    cdouble *p = (cdouble *)q;
+    asm volatile("" : "+s"(p));
+    return p;
+}
+__device__ __forceinline__ void sbar() { __builtin_amdgcn_sched_barrier(0); }
+// pins a value's computation between the surrounding volatile asm statements
+// (the IR moves pure arithmetic freely across sched_barrier)
+__device__ __forceinline__ void vpin(double &v) { asm volatile("" : "+v"(v)); }
+
+// compile-time loop (guaranteed full unrolling: the sweeps index register
+// arrays by the column, and a partially rolled loop would put them in scratch)
+template <int V>
+struct IntC {
+    static constexpr int value = V;
+};
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for(F &&f) {
+    if constexpr (I < N) {
+        f(IntC<I>{});
+        static_for<I + 1, N>(f);
+    }
+}
+
+// One flat stream of NA prefix doubles (X, e.g. an observation row) followed by
+// a packed factor table T, in chunks of CH doubles.  The next chunk's scalar
+// loads are issued right after the FIRST use of this chunk's values (SMEM
+// returns out of order, so every wait is lgkmcnt(0): loads issued earlier would
+// be waited for too) and stay in flight during the chunk's other CH − 1 fmas.
+// The chunk pointers go through an empty asm (loads from constant memory alias
+// nothing, so the IR would otherwise hoist and merge a whole sweep's loads into
+// SGPRs), and every result is pinned with vpin, so the stream keeps its order.
+// fpre(IntC<i>, x_i) for the prefix, ftab(IntC<j>, IntC<i>, T_ij) for the table.
+template <int D>
+constexpr int chol_chunk() { return D % 16 == 0 ? 16 : 8; }
+template <int D, int NA, typename FP, typename FT>
+__device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, FT &&ftab) {
+    constexpr int CH = chol_chunk<D>();
+    static_assert(NA % CH == 0, "prefix must be whole chunks");
+    constexpr int NT = NA + D * (D + 1) / 2, NCH = (NT + CH - 1) / CH;
+    auto load = [&](auto TC, double(&buf)[CH]) {
+        constexpr int e0 = decltype(TC)::value * CH;
+        cdouble *p = (e0 < NA) ? X + e0 : T + (e0 - NA);
+        asm volatile("" : "+s"(p));
+#pragma unroll
+        for (int r = 0; r < CH; ++r)
+            if (e0 + r < NT) buf[r] = p[r];
+    };
+    auto elem = [&](auto EC, double v) {
+        constexpr int e = decltype(EC)::value;
+        if constexpr (e < NA) {
+            fpre(IntC<e>{}, v);
+        } else {
+            constexpr int j = chol_col_of(D, e - NA);
+            ftab(IntC<j>{}, IntC<j + (e - NA) - chol_col(D, j)>{}, v);
+        }
+    };
+    double cur[CH], nxt[CH];
+    load(IntC<0>{}, cur);
+    static_for<0, NCH>([&](auto TC) {
+        constexpr int t = decltype(TC)::value, e0 = t * CH;
+        constexpr int n = (NT - e0) < CH ? (NT - e0) : CH;
+        elem(IntC<e0>{}, cur[0]);
+        sbar();
+        if constexpr (t + 1 < NCH) load(IntC<t + 1>{}, nxt);
+        sbar();
+        static_for<1, n>([&](auto RC) {
+            constexpr int r = decltype(RC)::value;
+            elem(IntC<e0 + r>{}, cur[r]);
+        });
+        sbar();
+#pragma unroll
+        for (int r = 0; r < CH; ++r) cur[r] = nxt[r];
+    });
+}
+
+// ‖L⁻¹ r‖² by forward substitution as column updates, r given by the prefix
+// (NA = D: acc_i = x_i − θ°_i) or already in acc (NA = 0); canonical order
+template <int D, int NA>
+__device__ __forceinline__ double chol_sqmahal(cdouble *X, cdouble *Ts, const double (&thp)[D], double (&acc)[D]) {
+    constexpr int BLK = SumShape<D>::BLK, NB = D / BLK;
+    double b[NB];
+    double s = 0.0, y = 0.0;
+    chol_stream<D, NA>(
+        X, Ts,
+        [&](auto IC, double x) {
+            constexpr int i = decltype(IC)::value;
+            acc[i] = x - thp[i];
+            vpin(acc[i]);
+        },
+        [&](auto JC, auto IC, double v) {
+            constexpr int j = decltype(JC)::value, i = decltype(IC)::value;
+            if constexpr (i == j) {  // v = 1/L_jj
+                y = acc[j] * v;
+                vpin(y);
+                s = (j % BLK == 0) ? y * y : fma(y, y, s);
+                if constexpr (j % BLK == BLK - 1) b[j / BLK] = s;
+            } else {
+                acc[i] = fma(-v, y, acc[i]);
+                vpin(acc[i]);
+            }
+        });
+    return tree_inplace<NB>(b);
+}
+
+// θ° = θ + L z with row sums over j ascending (rand(MvNormal(θ, Σ))): column
+// sweep acc_i += L_ij z_j for i ≥ j; row j is complete after column j
+template <int D>
+__device__ __forceinline__ void chol_propose(cdouble *Tp, const double (&z)[D], const double (&th)[D],
+                                             double (&thp)[D]) {
+    chol_stream<D, 0>(
+        Tp, Tp, [&](auto, double) {},
+        [&](auto JC, auto IC, double v) {
+            constexpr int j = decltype(JC)::value, i = decltype(IC)::value;
+            thp[i] = (j == 0) ? v * z[0] : fma(v, z[j], thp[i]);
+            if constexpr (i == j) thp[j] = th[j] + thp[j];
+            vpin(thp[i]);
+        });
+}
+
+// store_slot with the word stride made opaque at the store site: otherwise the
+// D/2 loop-invariant products j·stride are hoisted out of the step loop and
+// held in SGPRs across the sweeps
+template <int D, int N>
+__device__ __forceinline__ void store_slot_late(double *slot_base, const SlotOffset<D> &off, const double (&v)[N]) {
+    uint64_t stride = off.stride;
+    asm volatile("" : "+s"(stride));
+    char *b = reinterpret_cast<char *>(slot_base);
+    if constexpr (D % 2 == 0) {
+#pragma unroll
+        for (int j = 0; j < N / 2; ++j) {
+            d2v x = {v[2 * j], v[2 * j + 1]};
+            __builtin_nontemporal_store(x, reinterpret_cast<d2v *>(b + off.o));
+            b += stride;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+            __builtin_nontemporal_store(v[i], reinterpret_cast<double *>(b + off.o));
+            b += stride;
+        }
+    }
+}
+
+template <int D, bool FULL, int LLMODE>
+__global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
+    const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
+    constexpr int P = D * (D + 1) / 2;
+
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+    const uint64_t C = a.C;
+    const uint32_t c32 = (uint32_t)chain;
+    const SlotOffset<D> soff(C, chain, 0);
+    double th[D];
+    load_slot<D>(a.theta, soff, th);
+    double ll = chain_elem(a.ll, c32);
+    double ra = chain_elem(a.ra, c32);
+    uint64_t r0 = chain_elem(a.ring, 2 * c32), r1 = chain_elem(a.ring, 2 * c32 + 1);
+    uint32_t nacc = chain_elem(a.nacc, c32);
+    uint32_t faults = chain_elem(a.faults, c32);
+    AcceptStream accs;
+    const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
+    const uint32_t nobs = a.nobs;
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
+        const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
+        cdouble *cst = opaque_cptr(a.consts);
+        // ---- proposal!: θ° = θ + L z (random_walk.jl:145-151), row sums over j ascending
+        double thp[D];
+        {
+            double z[D];
+            normals<D, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, z, faults, vkeys);
+            chol_propose<D>(cst, z, th, thp);
+        }
+        // ---- log_transition_density both ways (random_walk.jl:161-171): one evaluation
+        double ltd;
+        {
+            double acc[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) acc[i] = thp[i] - th[i];
+            ltd = fma(-0.5, chol_sqmahal<D, 0>(cst, cst + P, thp, acc), a.rw_c0);
+        }
+        // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            llp = 0.0;
+            for (uint32_t k = 0; k < nobs; ++k) {
+                cdouble *c = opaque_cptr(a.consts);
+                double acc[D];
+                llp = llp + fma(-0.5, chol_sqmahal<D, D>(c + 3 * P + D + (size_t)k * D, c + 2 * P, thp, acc), a.t_c0);
+            }
+        } else {
+            cdouble *c = opaque_cptr(a.consts);
+            double acc[D];
+            const double qv = chol_sqmahal<D, D>(c + 3 * P, c + 2 * P, thp, acc);
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        // ---- accept_reject! (run.jl:271-278), left-associative as written
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double E = accs.next<true>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
+        const bool acc = E > -llr;
+        if constexpr (FULL) store_slot_late<D>(a.hist_prop + slot * D * C, soff, thp);
+#pragma unroll
+        for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        if (s + 1 == a.nsteps) chain_elem(a.ll_prop, c32) = llp;
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            store_slot_late<D>(a.hist_theta + slot * D * C, soff, th);
+            __builtin_nontemporal_store(ll, &chain_elem(a.hist_ll + slot * a.C, c32));
+        }
+        {
+            const uint64_t m = __ballot(acc);
+            if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
+        }
+        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
+    }
+    chain_elem(a.ll, c32) = ll;
+    chain_elem(a.ra, c32) = ra;
+    chain_elem(a.ring, 2 * c32) = r0;
+    chain_elem(a.ring, 2 * c32 + 1) = r1;
+    chain_elem(a.nacc, c32) = nacc;
+    chain_elem(a.faults, c32) = faults;
+    if (faults) *a.fault_flag = 1u;
+    store_slot_cached<D>(a.theta, soff, th);
 }
 
 // Host-unit kernels (diagnostics, gathers, probes): compiled once, in emcmc.hip.

@@ -71,6 +71,14 @@ def main():
     ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
     report("dense_d32_joint", eng, 1, ms, b)
     eng.close()
+    # (2b) the same with the sufficient-statistic likelihood (one solve per step)
+    eng = Engine(EngineConfig(dim=32, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed))
+    eng.add_gaussian_rw_update(np.arange(32), Sr)
+    eng.set_gsn_target(w.mu_true, St, w.obs, ll_mode=L.LL_SUFFSTAT)
+    eng.set_state(np.zeros((C, 32)))
+    ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
+    report("dense_d32_joint_suffstat", eng, 1, ms, b)
+    eng.close()
 
     # (3) user law: student-t regression, D = 4, 50 observations (run-time compiled)
     import user_target_cases as U

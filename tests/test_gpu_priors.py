@@ -88,6 +88,6 @@ def test_d32_correlated_joint_proposal_and_target(oracle):
     ups = [oracle.mwg_update(2, list(range(32)), sigma=R)]
     steps = full_steps(150, 1)
     eng, st, h = run_both(oracle, 32, 4096, 150, ups, mu, S, obs, steps, 77)
-    assert "mwg_wide_kernel<D=32" in eng.kernel_name()
+    assert "rwm_gsn_chol_kernel<D=32" in eng.kernel_name()  # the fused correlated-Σ kernel
     check(oracle, eng, st, h, steps, ups, 1)
     assert 0.1 < h["acc"][50:].mean() < 0.45

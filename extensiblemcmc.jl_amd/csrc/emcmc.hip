@@ -246,10 +246,11 @@ emcmc_status fail(emcmc_handle *h, emcmc_status st, const char *fmt, ...) {
     } while (0)
 
 KernelFn lookup(int D, int lpc, bool full, int ll, int dense, bool unit, int occ = 0) {
-    for (const auto &e : diag_table())
-        if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == dense &&
-            e.k.unit == (int)unit && e.k.occ == occ)
-            return e.fn;
+    for (const auto *tab : {&diag_table(), &chol_table()})
+        for (const auto &e : *tab)
+            if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == dense &&
+                e.k.unit == (int)unit && e.k.occ == occ)
+                return e.fn;
     return nullptr;
 }
 
@@ -631,7 +632,15 @@ emcmc_status select_variant(emcmc_handle *h) {
             v.fn = lookup(D, 1, full, ll, false, unit);
         }
         v.lpc = lpc;
-        v.dense = false;
+        v.dense = 0;
+        // one lane per chain with the observations through the scalar cache
+        if ((h->cfg.kernel_variant & EMCMC_VARIANT_SCALAR_OBS) && (!h->cfg.lanes_per_chain || lpc == 1))
+            if (KernelFn f = lookup(D, 1, full, ll, 3, unit)) {
+                v.fn = f;
+                v.lpc = 1;
+                v.dense = 3;
+                v.occ = 0;
+            }
     } else {
         v.dense = D > 8 ? 2 : 1;
         v.fn = lookup(D, 1, full, ll, v.dense, false);
@@ -644,14 +653,14 @@ emcmc_status select_variant(emcmc_handle *h) {
                     D, diag ? "diagonal" : "dense", h->cfg.lanes_per_chain);
     char nm[160];
     snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>",
-             v.dense == 2 ? "chol" : v.dense ? "dense" : "diag", D, v.lpc,
+             v.dense == 3 ? "diag_s" : v.dense == 2 ? "chol" : v.dense ? "dense" : "diag", D, v.lpc,
              full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
              v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : "");
     v.name = nm;
     // constants for this variant
     std::vector<double> c;
     const TargetHost &t = h->target;
-    if (!v.dense) {
+    if (v.dense == 0 || v.dense == 3) {
         c.resize(4 * (size_t)D);
         for (int i = 0; i < D; ++i) {
             c[i] = u.L[(size_t)i * D + i];
@@ -683,8 +692,9 @@ emcmc_status select_variant(emcmc_handle *h) {
         std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
         std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     }
-    const size_t obs_doubles = (ll == LL_PER_OBS && v.dense != 2) ? t.nobs * (size_t)D : 0;
-    // (the chol kernel reads its constants through the scalar cache: no dynamic LDS)
+    // (the chol kernel reads its constants, the diag_s kernel its observations,
+    // through the scalar cache)
+    const size_t obs_doubles = (ll == LL_PER_OBS && v.dense < 2) ? t.nobs * (size_t)D : 0;
     size_t lds = v.dense == 2 ? 0 : (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
     if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc, diag_block(v.occ) / 64);
     if (kZigLdsBytes + lds > kMaxLds)

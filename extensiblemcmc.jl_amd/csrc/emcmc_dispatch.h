@@ -30,6 +30,7 @@ struct Entry {
     KernelFn fn;
 };
 const std::vector<Entry> &diag_table();
+const std::vector<Entry> &chol_table();  // dense = 2 (chol) and 3 (diag_s): inst_chol.hip
 
 // general schedule kernel (mwg_gsn_kernel)
 struct MwgEntry {

@@ -1172,6 +1172,140 @@ __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
     store_slot_cached<D>(a.theta, soff, th);
 }
 
+// 16 doubles through the scalar cache (pointer opaque: see chol_stream)
+__device__ __forceinline__ void sload16(double (&buf)[16], cdouble *p) {
+    asm volatile("" : "+s"(p));
+#pragma unroll
+    for (int r = 0; r < 16; ++r) buf[r] = p[r];
+}
+// one 16-coordinate chunk of Σ_i ((x_i − θ°_i)/L_ii)² in the canonical blocked
+// order; the next chunk is requested right after the first use of this one
+template <int D, int BLK, bool UNIT_T, int c>
+__device__ __forceinline__ void sobs_chunk(const double (&cur)[16], double (&nxt)[16], cdouble *pn,
+                                           const double (&thp)[D], const double *iLt, double &sblk,
+                                           double (&b)[D / BLK]) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const int i = c * 16 + r;
+        double y = cur[r] - thp[i];
+        if constexpr (!UNIT_T) y = y * iLt[i];
+        sblk = (i % BLK == 0) ? y * y : fma(y, y, sblk);
+        vpin(sblk);
+        if (i % BLK == BLK - 1) b[i / BLK] = sblk;
+        if (r == 0) {
+            sbar();
+            sload16(nxt, pn);
+            sbar();
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// rwm_gsn_diag_kernel with one lane per chain and the OBSERVATIONS through the
+// scalar cache (EMCMC_VARIANT_SCALAR_OBS): with all D coordinates of a chain in
+// one lane, observation x_k,i is the same for every lane of the wave, so it
+// enters v_add_f64 as an SGPR operand instead of a ds_read (the LPC = 2 kernel
+// issues 80 ds_read_b128 per wave-step and waits on them for ≈ 30% of its
+// time).  The rows stream through two 16-double SGPR buffers: chunk t + 1 is
+// requested right after the first use of chunk t.  Same arithmetic, same order
+// and same bits as rwm_gsn_diag_kernel<D, 1, …>.
+template <int D, bool FULL, int LLMODE, bool UNIT_T>
+__global__ void __launch_bounds__(256) rwm_gsn_diag_s_kernel(const StepParams a) {
+    static_assert(D % 16 == 0, "rows stream in 16-double chunks");
+    constexpr int BLK = SumShape<D>::BLK, NB = D / BLK, NCK = D / 16;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const uint32_t nobs = a.nobs;
+    const ZigTabs zt = stage_lds(lds, a.zig, a.consts, 4 * D, nullptr, 0);
+    const double *cst0 = lds;
+
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+    const uint64_t C = a.C;
+    const SlotOffset<D> soff(C, chain, 0);
+    const uint32_t c32 = (uint32_t)chain;
+    double th[D];
+    load_slot<D>(a.theta, soff, th);
+    double ll = chain_elem(a.ll, c32);
+    double ra = chain_elem(a.ra, c32);
+    uint64_t r0 = chain_elem(a.ring, 2 * c32), r1 = chain_elem(a.ring, 2 * c32 + 1);
+    uint32_t nacc = chain_elem(a.nacc, c32);
+    uint32_t faults = chain_elem(a.faults, c32);
+    AcceptStream accs;
+    const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iter0 + s;
+        const uint64_t slot = (uint64_t)(iter - 1) * a.P + a.pidx0;
+        const double *cst = cst0;
+        const double *Lrw = cst, *iLrw = cst + D, *iLt = cst + 2 * D, *xbar = cst + 3 * D;
+        double thp[D];
+        propose_diag<D, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, 0u, th, Lrw, thp, faults, vkeys);
+        const double ltd =
+            fma(-0.5, canon_sumsq_f<D, 1, D>([&](int i) { return (thp[i] - th[i]) * iLrw[i]; }), a.rw_c0);
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            llp = 0.0;
+            cdouble *X = opaque_cptr(a.obs);
+            double bufA[16], bufB[16];
+            sload16(bufA, X);
+            for (uint32_t k = 0; k < nobs; ++k) {
+                // chunk c of row k is in bufA (c even) / bufB (c odd); NCK chunks per row
+                double b[NB];
+                double sblk = 0.0;
+                cdouble *xnext = X + (size_t)((k + 1 < nobs) ? k + 1 : 0u) * D;  // past the last row: row 0 again
+                static_for<0, NCK>([&](auto CC) {
+                    constexpr int c = decltype(CC)::value;
+                    cdouble *pn = (c + 1 < NCK) ? X + (size_t)k * D + (c + 1) * 16 : xnext;
+                    if constexpr (c % 2 == 0)
+                        sobs_chunk<D, BLK, UNIT_T, c>(bufA, bufB, pn, thp, iLt, sblk, b);
+                    else
+                        sobs_chunk<D, BLK, UNIT_T, c>(bufB, bufA, pn, thp, iLt, sblk, b);
+                });
+                if constexpr (NCK % 2 == 1) {  // keep row k+1's first chunk in bufA
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) bufA[r] = bufB[r];
+                }
+                const double q = tree_inplace<NB>(b);
+                llp = llp + fma(-0.5, q, a.t_c0);
+            }
+        } else {
+            const double qv = canon_sumsq_f<D, 1, D>([&](int i) {
+                const double y = xbar[i] - thp[i];
+                return UNIT_T ? y : y * iLt[i];
+            });
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double E = accs.next<true>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
+        const bool acc = E > -llr;
+        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
+#pragma unroll
+        for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        if (s + 1 == a.nsteps) chain_elem(a.ll_prop, c32) = llp;
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            store_slot<D>(a.hist_theta + slot * D * C, soff, th);
+            __builtin_nontemporal_store(ll, &chain_elem(a.hist_ll + slot * a.C, c32));
+        }
+        {
+            const uint64_t m = __ballot(acc);
+            if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
+        }
+        ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
+    }
+    chain_elem(a.ll, c32) = ll;
+    chain_elem(a.ra, c32) = ra;
+    chain_elem(a.ring, 2 * c32) = r0;
+    chain_elem(a.ring, 2 * c32 + 1) = r1;
+    chain_elem(a.nacc, c32) = nacc;
+    chain_elem(a.faults, c32) = faults;
+    if (faults) *a.fault_flag = 1u;
+    store_slot_cached<D>(a.theta, soff, th);
+}
+
 // Host-unit kernels (diagnostics, gathers, probes): compiled once, in emcmc.hip.
 #ifdef EMCMC_HOST_UNIT
 // ---------------------------------------------------------------------------

@@ -1,5 +1,5 @@
 // inst_diag.hip — gfx950 instantiations of the fused single-update step kernels
-// (rwm_gsn_diag_kernel, rwm_gsn_dense_kernel, rwm_gsn_chol_kernel); see emcmc_kernels.h.
+// (rwm_gsn_diag_kernel, rwm_gsn_dense_kernel); see emcmc_kernels.h.
 #include "emcmc_dispatch.h"
 
 namespace emcmc {
@@ -11,10 +11,6 @@ KernelFn diag_fn() {
 template <int D, bool FULL, int LL>
 KernelFn dense_fn() {
     return &rwm_gsn_dense_kernel<D, FULL, LL>;
-}
-template <int D, bool FULL, int LL>
-KernelFn chol_fn() {
-    return &rwm_gsn_chol_kernel<D, FULL, LL>;
 }
 
 #define DIAGU(D, LPC, U)                                                                          \
@@ -36,11 +32,6 @@ KernelFn chol_fn() {
 #define DENSE4(D)                                                                                    \
     {{D, 1, 1, 0, 1, 0, 0}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1, 0, 0}, dense_fn<D, true, 1>()},   \
         {{D, 1, 0, 0, 1, 0, 0}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1, 0, 0}, dense_fn<D, false, 1>()}
-// dense = 2: rwm_gsn_chol_kernel (factors through the scalar cache)
-#define CHOL4(D)                                                                                     \
-    {{D, 1, 1, 0, 2, 0, 0}, chol_fn<D, true, 0>()}, {{D, 1, 1, 1, 2, 0, 0}, chol_fn<D, true, 1>()},     \
-        {{D, 1, 0, 0, 2, 0, 0}, chol_fn<D, false, 0>()}, {{D, 1, 0, 1, 2, 0, 0}, chol_fn<D, false, 1>()}
-
 const std::vector<Entry> &diag_table() {
     static const std::vector<Entry> t = {
         DIAG4(1, 1),  DIAG4(2, 1),  DIAG4(3, 1),  DIAG4(4, 1),  DIAG4(8, 1),
@@ -48,7 +39,7 @@ const std::vector<Entry> &diag_table() {
         DIAG4(64, 2), DIAG4(64, 4), DIAGO(32, 4, true), DIAGO(32, 4, false), DIAGO(32, 2, true),
         DIAGO3(32, 2, true), DIAGO3(32, 4, true), DIAGO3(32, 1, true),
         DENSE4(1),    DENSE4(2),    DENSE4(3),
-        DENSE4(4),    DENSE4(8),    CHOL4(16),    CHOL4(24),    CHOL4(32),
+        DENSE4(4),    DENSE4(8),
     };
     return t;
 }

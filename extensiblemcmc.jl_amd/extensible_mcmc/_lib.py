@@ -51,6 +51,7 @@ FAULT_POSDEF = 4
 FAULT_PRIOR_RESAMPLES = 8
 VARIANT_HIGH_OCCUPANCY = 1
 VARIANT_OCCUPANCY3 = 2
+VARIANT_SCALAR_OBS = 4
 
 
 class EmcmcConfig(C.Structure):

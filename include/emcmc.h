@@ -146,6 +146,7 @@ typedef struct emcmc_config {
 /* kernel_variant flags: performance-only choices, bit-identical results */
 #define EMCMC_VARIANT_HIGH_OCCUPANCY 1u  /* cap registers for 4 waves/SIMD where instantiated */
 #define EMCMC_VARIANT_OCCUPANCY3 2u      /* cap registers for 3 waves/SIMD where instantiated */
+#define EMCMC_VARIANT_SCALAR_OBS 4u      /* diagonal Σ: one lane per chain, observations as SGPR operands */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,

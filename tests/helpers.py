@@ -12,10 +12,10 @@ def theta0_for(w, C):
 
 
 def run_engine(w, C, S, *, lpc=0, ll_mode=0, hist=L.HIST_FULL, spl=0, chain0=0, theta0=None, M=None,
-               iter_first=1, fetch=True):
+               iter_first=1, fetch=True, variant=0):
     eng = Engine(EngineConfig(dim=w.D, num_chains=C, num_mcmc_steps=M or (iter_first + S - 1), seed=w.seed,
                               first_chain_id=chain0, history_mode=hist, lanes_per_chain=lpc,
-                              steps_per_launch=spl))
+                              steps_per_launch=spl, kernel_variant=variant))
     eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
     eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
     eng.set_state(theta0_for(w, C) if theta0 is None else theta0)

@@ -185,3 +185,20 @@ def test_empty_schedule_is_a_no_op(oracle):
     assert np.array_equal(th, th0)
     assert np.all(ll == -np.inf)
     eng.close()
+
+
+@pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
+@pytest.mark.parametrize("unit", [True, False])
+def test_scalar_obs_variant_bitwise(oracle, ll_mode, unit):
+    """EMCMC_VARIANT_SCALAR_OBS (rwm_gsn_diag_s_kernel: one lane per chain, the
+    observation rows as SGPR operands streamed through the scalar cache): the
+    same bits as the oracle, with a unit and a non-unit diagonal target Σ,
+    1000 chains (a partial last wave) and launch splits."""
+    w = W.cfg2(1000)
+    if not unit:
+        w.t_sigma = np.diag(np.random.default_rng(9).uniform(0.5, 2.0, 32))
+    o = run_oracle(oracle, w, 1000, 110, ll_mode=ll_mode)
+    for spl in (0, 37):
+        e = run_engine(w, 1000, 110, ll_mode=ll_mode, spl=spl, variant=L.VARIANT_SCALAR_OBS)
+        assert e["kernel"].startswith("rwm_gsn_diag_s_kernel<D=32,LPC=1")
+        assert_bitwise(e, o)

@@ -697,10 +697,21 @@ emcmc_status select_variant(emcmc_handle *h) {
     const size_t obs_doubles = (ll == LL_PER_OBS && v.dense < 2) ? t.nobs * (size_t)D : 0;
     size_t lds = v.dense == 2 ? 0 : (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
     if (!v.dense) lds = lds_align16(lds) + diag_scratch_bytes(D, v.lpc, diag_block(v.occ) / 64);
-    if (kZigLdsBytes + lds > kMaxLds)
-        return fail(h, EMCMC_INVALID_ARG,
-                    "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu",
-                    lds, kMaxLds, (unsigned long long)t.nobs);
+    if (kZigLdsBytes + lds > kMaxLds) {
+        // more observations than the LDS holds (≈ 350 at D = 32): stream them
+        // through the scalar cache (rwm_gsn_diag_s_kernel, any n) where
+        // instantiated, else the general kernel (observations from global memory)
+        KernelFn f = (v.dense == 0 && ll == LL_PER_OBS) ? lookup(D, 1, full, ll, 3, v.unit) : nullptr;
+        if (!f) return select_mwg(h);
+        v.fn = f;
+        v.lpc = 1;
+        v.dense = 3;
+        v.occ = 0;
+        lds = c.size() * sizeof(double);
+        snprintf(nm, sizeof nm, "rwm_gsn_diag_s_kernel<D=%d,LPC=1,%s,PER_OBS%s>", D, full ? "FULL" : "ACCEPT_ONLY",
+                 v.unit ? ",UNIT_T" : "");
+        v.name = nm;
+    }
     if (h->d_consts) (void)hipFree(h->d_consts);
     HIPCHK(h, hipMalloc(&h->d_consts, c.size() * sizeof(double)));
     HIPCHK(h, hipMemcpy(h->d_consts, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));

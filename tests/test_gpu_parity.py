@@ -202,3 +202,29 @@ def test_scalar_obs_variant_bitwise(oracle, ll_mode, unit):
         e = run_engine(w, 1000, 110, ll_mode=ll_mode, spl=spl, variant=L.VARIANT_SCALAR_OBS)
         assert e["kernel"].startswith("rwm_gsn_diag_s_kernel<D=32,LPC=1")
         assert_bitwise(e, o)
+
+
+def test_many_observations_beyond_lds(oracle):
+    """Per-observation likelihood with more observations than the LDS holds
+    (600 × 32 doubles = 150 KiB next to the 70 KiB ziggurat): the fused path
+    streams them through the scalar cache (rwm_gsn_diag_s_kernel) instead of
+    refusing; bitwise against the oracle."""
+    w = W.cfg2(512, nobs=600)
+    e = run_engine(w, 512, 40)
+    assert e["kernel"].startswith("rwm_gsn_diag_s_kernel<D=32")
+    assert_bitwise(e, run_oracle(oracle, w, 512, 40))
+
+
+def test_many_observations_other_dims_use_the_general_kernel(oracle):
+    """The same at D = 4 with 6,000 observations (no scalar-cache instantiation):
+    the general kernel reads them from global memory; bitwise against its oracle."""
+    from test_gpu_mwg import check, full_steps, run_both
+
+    rng = np.random.default_rng(41)
+    mu = np.array([0.5, -1.0, 2.0, 0.0])
+    obs = mu + rng.standard_normal((6000, 4))
+    ups = [oracle.mwg_update(2, [0, 1, 2, 3], sigma=np.eye(4) * 2e-4)]
+    steps = full_steps(60, 1)
+    eng, st, h = run_both(oracle, 4, 300, 60, ups, mu, np.eye(4), obs, steps, 99)
+    assert "mwg_gsn_kernel<D=4" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 1)

@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
     ap.add_argument("--lpc", type=int, default=0)
     ap.add_argument("--steps-per-launch", type=int, default=100)
+    ap.add_argument("--variant", type=int, default=0,
+                    help="emcmc_config.kernel_variant (EMCMC_VARIANT_* flags; same results, for A/B timing)")
     ap.add_argument("--reps", type=int, default=0,
                     help="repeat the timed region, report the median (0: 5 when the histories fit in 96 GB, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -212,7 +214,8 @@ def main():
     M = a.warmup + a.steps * reps
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=first,
                               device=device, history_mode=hist, lanes_per_chain=a.lpc,
-                              steps_per_launch=a.steps_per_launch, history_ring=a.history_ring))
+                              steps_per_launch=a.steps_per_launch, history_ring=a.history_ring,
+                              kernel_variant=a.variant))
     stream_bufs = None
     if a.stream_thin:
         assert a.history_ring > 0 and a.history_ring % a.stream_thin == 0 and a.steps % a.history_ring == 0

@@ -141,6 +141,7 @@ struct Variant {
     int mo_tiles = 0;
     MalaFn afn = nullptr, ainit = nullptr;  // MALA step / ∇ℓ initialisation kernels
     bool mix = false;
+    bool xres = false;  // xfn is mix_res_kernel (16 lanes per chain, L_B in registers)
     int lpc = 1;
     int dense = 0;  // 0 rwm_gsn_diag_kernel, 1 rwm_gsn_dense_kernel, 2 rwm_gsn_chol_kernel
     bool unit = false;
@@ -512,12 +513,23 @@ emcmc_status select_mix(emcmc_handle *h) {
     std::tie(v.mofn, v.mo_tiles) = moments_lookup(D);
     if (!v.mofn) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no chain-moments kernel for D=%d", D);
     v.mix = true;
-    char nm[160];
-    snprintf(nm, sizeof nm, "mix_gsn_kernel<D=%d,%s,%s,%s,%s>+mix_moments_kernel%s", D, full ? "FULL" : "ACCEPT_ONLY",
-             ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", mix ? "MIX" : "GSN_MOMENTS", adiag ? "DIAG" : "DENSE",
-             v.rfn ? "+mix_readjust_kernel" : "");
-    v.name = nm;
     const TargetHost &t = h->target;
+    // L_B resident in registers across the launch (mix_res_kernel) where instantiated
+    bool unit = true;
+    for (int i = 0; i < D; ++i) unit = unit && t.invdiag[i] == 1.0;
+    if (mix && adiag && h->cfg.num_chains % kMixResChainsPerBlock == 0 &&
+        !(h->cfg.kernel_variant & EMCMC_VARIANT_MIX_STREAM)) {
+        for (const auto &e : mixres_table())
+            if (e.D == D && e.full == (int)full && e.ll == ll && e.unit == (int)unit) {
+                v.xfn = e.fn;
+                v.xres = true;
+            }
+    }
+    char nm[160];
+    snprintf(nm, sizeof nm, "%s<D=%d,%s,%s,%s,%s%s>+mix_moments_kernel%s", v.xres ? "mix_res_kernel" : "mix_gsn_kernel",
+             D, full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", mix ? "MIX" : "GSN_MOMENTS",
+             adiag ? "DIAG" : "DENSE", v.xres && unit ? ",UNIT_T" : "", v.rfn ? "+mix_readjust_kernel" : "");
+    v.name = nm;
     const size_t DD = (size_t)D * D;
     std::vector<double> c(2 * DD + 3 * (size_t)D);
     std::copy(u.L.begin(), u.L.end(), c.begin());
@@ -526,7 +538,8 @@ emcmc_status select_mix(emcmc_handle *h) {
     std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
     std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    const size_t lds = (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
+    const size_t lds = v.xres ? mixres_lds(D, t.nobs, h->cfg.steps_per_launch, ll == LL_PER_OBS)
+                              : (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
     if (kZigLdsBytes + lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu", lds,
@@ -741,8 +754,9 @@ double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps, bool readjust) {
         per_step += (h->cfg.history_mode == EMCMC_HIST_FULL) ? 8.0 * D : 16.0 * D;
         state += 16.0 * DP + 16.0 * D;
         if (h->updates[0].kernel == EMCMC_RW_GAUSSIAN_MIX) {
-            per_step += 8.0 * DP + 8.0 * D;  // L_B and 1/L_B,ii, read by every step
-            state += 8.0;                    // c0_B
+            if (h->var.xres) state += 8.0 * DP + 8.0 * D;  // L_B and 1/L_B,ii, read once per launch (registers)
+            else per_step += 8.0 * DP + 8.0 * D;            // L_B and 1/L_B,ii, read by every step
+            state += 8.0;                                   // c0_B
         }
         // readjust: cov read, L_B / 1/L_B,ii / c0_B written
         if (readjust) state += 8.0 * DP + 8.0 * DP + 8.0 * D + 8.0;
@@ -871,6 +885,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     r.C = C;
     r.sB = (2.38 * 2.38) / (double)h->cfg.dim;  // 2.38^2/length(rw), adaptation.jl:423
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
+    const dim3 rgrid_res((unsigned)(C / kMixResChainsPerBlock));  // mix_res_kernel: 16 chains per block (C % 16 == 0)
     const uint64_t K = h->cfg.steps_per_launch;
     uint64_t i = 0;
     while (i < num_steps) {
@@ -903,8 +918,8 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             HIPCHK(h, hipEventRecord(e0, h->stream));
         }
         void *args[] = {&p};
-        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.xfn), grid, block, args, h->lds_bytes,
-                                  h->stream));
+        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.xfn), h->var.xres ? rgrid_res : grid, block,
+                                  args, h->lds_bytes, h->stream));
         {  // the launch's mean/cov recurrence, from its θ history
             MixMomentsParams mp{};
             mp.theta = p.hist_theta ? p.hist_theta + (uint64_t)(p.iter0 - 1) * h->cfg.dim * C : h->d_mom_scratch;

@@ -46,6 +46,15 @@ struct MixEntry {
     MixFn fn;
 };
 const std::vector<MixEntry> &mix_table();
+// the same step with the chain's L_B resident in registers, 16 lanes per chain
+// (mix_res_kernel, emcmc_mixres.h; D = 32, MIX, diagonal Σ_A / Σ_t)
+struct MixResEntry {
+    int D, full, ll, unit;
+    MixFn fn;
+};
+const std::vector<MixResEntry> &mixres_table();
+constexpr int kMixResChainsPerBlock = 16;  // = kResChainsPerBlock (inst_mix.hip checks)
+size_t mixres_lds(int D, uint64_t nobs, uint64_t nsteps_max, bool perobs);
 std::pair<MomentsFn, int> moments_lookup(int D);
 ReadjustFn readjust_lookup(int D);
 

@@ -1,0 +1,324 @@
+// emcmc_mixres.h — GaussianRandomWalkMix step with each chain's Haario factor
+// L_B resident in registers for the whole K-step launch (BASELINE cfg 4, gfx950).
+//
+// Same semantics and the same bits as mix_gsn_kernel<D, FULL, LL, MIX=true,
+// DIAG=true> (emcmc_mix.h; oracle/emcmc_oracle.c orc_run_mix), another layout:
+// mix_gsn_kernel runs one lane per chain and streams the chain's 4.2 KB of
+// L_B from HBM on every step (random_walk.jl:229-232 needs L_B⁻¹(θ° − θ) on
+// every step whichever kernel was picked), which bounds it at the HBM roofline.
+// Here a chain owns one 16-lane DPP row; lane r holds rows 2r and 2r+1 of L_B
+// (zero-padded to D, 2·D doubles in VGPRs), loaded once per launch.
+//
+//   normals     lane r draws Philox block r: z_{2r}, z_{2r+1} (the pair layout of
+//               normals<D>); lane 0 the mixture pick, lanes ≥ 1 the accept Exp(1)
+//   θ° = θ + L z  column sweep: z_j broadcast from lane j/2 (row_newbcast), each
+//               lane fma's it into its two rows — every row still accumulates
+//               over j ascending from L_i0·z_0, the oracle's order; columns past
+//               a row's diagonal add 0·z_j, which changes nothing but the sign of
+//               an exact zero: a wave-uniform check redoes that (never seen) case
+//               with masks
+//   y_B = L_B⁻¹(θ° − θ)  column sweep: at column j lane j/2 forms y_j = acc_j /
+//               L_jj (as acc·(1/L_jj)), broadcasts it, every row i > j subtracts
+//               L_ij·y_j — the oracle's row order again; every lane sees every
+//               y_j, so Σ y_j² is accumulated redundantly in the canonical order
+//   Σ_A, Σ_t    diagonal: y_A,i and the target terms sit on the owner lane;
+//               canonical blocks of 8 coordinates are exactly the row's quads
+//               (serial quad scan, then the blocks' pairwise tree via row_shr)
+//   per-observation ll  θ° goes through a per-wave LDS row; lane r evaluates
+//               observation r (+16, +32, …) over all D coordinates, and the
+//               sum over observations is folded k = 0, 1, … through broadcasts
+// The accept bits of a block's 16 chains are two bytes per step: kept in LDS
+// for the launch and written once at its end.
+#pragma once
+
+#include "emcmc_mix.h"
+
+namespace emcmc {
+
+constexpr int kResLanes = 16;        // lanes per chain: one DPP row
+constexpr int kResChainsPerBlock = 16;  // 256-thread block
+constexpr int kResWaves = 4;
+
+// dynamic LDS of mix_res_kernel<D>: θ° rows [16 chains][D+2], observations
+// [nobs][D+2] (per-observation mode; rows padded by 16 B so that 16 lanes
+// reading 16 different rows hit 16 different bank groups), accept nibbles [nsteps][4]
+__host__ __device__ constexpr size_t mixres_lds_bytes(int D, uint64_t nobs, uint64_t nsteps_max, bool perobs) {
+    return (size_t)kResChainsPerBlock * (D + 2) * 8 + (perobs ? (size_t)nobs * (D + 2) * 8 : 0) +
+           (((size_t)nsteps_max * kResWaves + 15) & ~(size_t)15);
+}
+
+// lane L of the 16-lane row, to every lane of the row (one v_mov_b64_dpp)
+template <int L>
+__device__ __forceinline__ double rbcast(double v) {
+    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + L, 0xF, 0xF, false);
+}
+template <int L>
+__device__ __forceinline__ uint32_t rbcast_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + L, 0xF, 0xF, false);
+}
+
+// Σ y² over the chain's D = 32 coordinates in the canonical order (SumShape<32>:
+// blocks of 8 as s = y0·y0, s = fma(y, y, s), then ((b0 + b1) + (b2 + b3))),
+// lane r of the row holding coordinates 2r (y0) and 2r+1 (y1): block k is quad k
+// of the row.  The result is on every lane of the row.
+__device__ __forceinline__ double row_sumsq32(double y0, double y1, bool quad_lead) {
+    double a = fma(y1, y1, y0 * y0);  // block start (quad lane 0): y0·y0, then fma
+#pragma unroll
+    for (int step = 1; step < 4; ++step) {
+        // quad_perm [0,0,1,2]: lane q takes lane q−1's partial (lane 0 keeps its own)
+        const double p = dpp_perm<0x90>(a);
+        const double n = fma(y1, y1, fma(y0, y0, p));
+        a = quad_lead ? a : n;
+    }
+    // block sums in quad lanes 3: lane 7 = b0 + b1, lane 15 = b2 + b3 (operands in order)
+    const double s = dpp_perm<0x114>(a) + a;  // row_shr:4
+    const double t = dpp_perm<0x118>(s) + s;  // row_shr:8: lane 15 = (b0 + b1) + (b2 + b3)
+    return rbcast<15>(t);
+}
+
+template <int D, bool FULL, int LLMODE, bool UNIT_T>
+__global__ void __launch_bounds__(256, 2) mix_res_kernel(const MixParams a) {
+    static_assert(D == 2 * kResLanes, "two rows of L_B per lane");
+    constexpr int DP = packed_n(D), DD = D * D, XS = D + 2;
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const uint32_t nobs = a.nobs;
+    const ZigTabs zt = stage_lds(lds, a.zig, a.consts, 0, a.obs, 0);  // tables only (static LDS)
+    double *const ths = lds;                                           // [16 chains][XS]
+    double *const X = lds + kResChainsPerBlock * XS;                   // [nobs][XS]
+    uint8_t *const nib =
+        reinterpret_cast<uint8_t *>(X + ((LLMODE == LL_PER_OBS) ? (size_t)nobs * XS : 0));  // [nsteps][4]
+    if constexpr (LLMODE == LL_PER_OBS) {
+        for (uint32_t e = threadIdx.x; e < nobs * D; e += blockDim.x) X[(e / D) * XS + e % D] = a.obs[e];
+        __syncthreads();
+    }
+
+    const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+    const int g = lane >> 4, r = lane & 15;
+    const int i0 = 2 * r, i1 = 2 * r + 1;  // the lane's rows / coordinates
+    const bool qlead = (r & 3) == 0;
+    const uint64_t C = a.C;
+    const uint64_t chain = (uint64_t)blockIdx.x * kResChainsPerBlock + (uint64_t)(w * 4 + g);  // host: C % 16 == 0
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+    const uint32_t c32 = (uint32_t)chain;
+    double *const tprow = ths + (w * 4 + g) * XS;
+
+    // per-lane constants: Σ_A and Σ_t diagonal (consts = L_A | 1/L_A,ii | L_t | 1/L_t,ii | x̄)
+    const double *cs = a.consts;
+    const double LA0 = cs[i0 * D + i0], LA1 = cs[i1 * D + i1];
+    const double iLA0 = cs[DD + i0], iLA1 = cs[DD + i1];
+    const double iLt0 = cs[2 * DD + D + i0], iLt1 = cs[2 * DD + D + i1];
+    const double xb0 = cs[2 * DD + 2 * D + i0], xb1 = cs[2 * DD + 2 * D + i1];
+    const double *iLt = cs + 2 * DD + D;  // wave-uniform reads (per-observation, non-unit Σ_t)
+
+    // rows 2r and 2r+1 of L_B (packed lower, state_pos layout), zero past the diagonal
+    double L0[D], L1[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        // lo_idx(i, j) ≤ lo_idx(31, 31) = DP − 1 for every j: the loads stay in bounds
+        const double v0 = a.LB[state_pos((uint64_t)lo_idx(i0, j), chain, C, DP)];
+        const double v1 = a.LB[state_pos((uint64_t)lo_idx(i1, j), chain, C, DP)];
+        L0[j] = (j <= i0) ? v0 : 0.0;
+        L1[j] = (j <= i1) ? v1 : 0.0;
+    }
+    const double iLB0 = a.iLB[(uint64_t)i0 * C + chain], iLB1 = a.iLB[(uint64_t)i1 * C + chain];
+    const double c0B = a.c0B[chain];
+
+    const uint32_t po = (uint32_t)(((uint64_t)r * C + chain) * 16u);  // the lane's pair word in a slot
+    double th0, th1;
+    {
+        const d2v t = *reinterpret_cast<const d2v *>(reinterpret_cast<const char *>(a.theta) + po);
+        th0 = t.x;
+        th1 = t.y;
+    }
+    double ll = a.ll[chain];
+    double ra = a.ra[chain];
+    uint64_t rg0 = a.ring[2 * chain], rg1 = a.ring[2 * chain + 1];
+    uint32_t nacc = a.nacc[chain];
+    uint32_t faults = a.faults[chain];
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
+        const uint64_t N = a.N0 + s;
+        const uint64_t slot = (uint64_t)(iter - 1);
+        // ---- proposal!: normals (block r of normals<D>), the pick, the accept draw
+        double z0, z1;
+        {
+            const u32x4 q = draw(a.key0, a.key1, gid, iter, (uint32_t)r, 0, 0);
+            uint32_t pend = 0;
+            if (!zig_normal_fast(zig_split_n(q.x, q.y), zt.n, z0)) pend |= 1u;
+            if (!zig_normal_fast(zig_split_n(q.z, q.w), zt.n, z1)) pend |= 2u;
+            while (__ballot(pend != 0) != 0) {
+                const bool act = pend != 0;
+                const uint32_t k = act ? (uint32_t)__builtin_ctz(pend) : 0u;
+                pend &= pend - 1;
+                double v = 0.0;
+                if (act) v = normal_draw(zt, a.key0, a.key1, gid, iter, 0, (uint32_t)i0 + k, faults);
+                z0 = (act && k == 0) ? v : z0;
+                z1 = (act && k == 1) ? v : z1;
+            }
+        }
+        double ue;
+        {
+            const bool pick = r == 0;
+            const u32x4 q = draw(a.key0, a.key1, gid, pick ? iter : iter >> 1, pick ? kBlockMixPick : kBlockAccept, 0, 0);
+            const double u = u01_closed0(q.x, q.y);
+            const ZigDraw d = accept_split(q, iter);
+            double e;
+            const bool fast = zig_exp_fast(d, zt.e, e);
+            if (!pick && !fast) e = zig_exp_slow(d, zt.e, zt.ef, a.key0, a.key1, gid, iter, kBlockAccept, 0, faults);
+            ue = pick ? u : e;
+        }
+        const bool useB = rbcast<0>(ue) <= a.lam;
+        const double E = rbcast<1>(ue);
+
+        // ---- θ° = θ + L z (random_walk.jl:145-151), L = L_A (diagonal) or L_B
+        double lz0 = 0.0, lz1 = 0.0;
+        static_for<0, D>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const double zj = rbcast<j / 2>((j & 1) ? z1 : z0);
+            if constexpr (j == 0) {
+                lz0 = L0[0] * zj;
+                lz1 = L1[0] * zj;
+            } else {
+                lz0 = fma(L0[j], zj, lz0);
+                lz1 = fma(L1[j], zj, lz1);
+            }
+        });
+        if (__ballot(useB && (lz0 == 0.0 || lz1 == 0.0)) != 0) {
+            // an exact zero may carry the wrong sign after the padding columns: redo with masks
+            static_for<0, D>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const double zj = rbcast<j / 2>((j & 1) ? z1 : z0);
+                if constexpr (j == 0) {
+                    lz0 = L0[0] * zj;
+                    lz1 = L1[0] * zj;
+                } else {
+                    const double n0 = fma(L0[j], zj, lz0), n1 = fma(L1[j], zj, lz1);
+                    lz0 = (j <= i0) ? n0 : lz0;
+                    lz1 = (j <= i1) ? n1 : lz1;
+                }
+            });
+        }
+        const double thp0 = th0 + (useB ? lz0 : LA0 * z0);
+        const double thp1 = th1 + (useB ? lz1 : LA1 * z1);
+        const double rr0 = thp0 - th0, rr1 = thp1 - th1;
+
+        // ---- log_transition_density of the mixture (random_walk.jl:229-232)
+        const double qa = row_sumsq32(rr0 * iLA0, rr1 * iLA1, qlead);
+        double qbb[4];
+        {
+            double acc0 = rr0, acc1 = rr1;
+            static_for<0, D>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                const double t = (j & 1) ? acc1 * iLB1 : acc0 * iLB0;
+                const double y = rbcast<j / 2>(t);  // y_B,j
+                if constexpr (j % 8 == 0) qbb[j / 8] = y * y;
+                else qbb[j / 8] = fma(y, y, qbb[j / 8]);
+                if constexpr (j + 1 < D) {
+                    acc0 = fma(-L0[j], y, acc0);
+                    acc1 = fma(-L1[j], y, acc1);
+                }
+            });
+        }
+        const double qb = tree_inplace(qbb);
+        const double lpA = fma(-0.5, qa, a.c0A);
+        const double lpB = fma(-0.5, qb, c0B);
+        const double ltd = log_any(a.oml * exp_any(lpA) + a.lam * exp_any(lpB));
+
+        // ---- compute_ll! (gsn_target.jl:23-29)
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            *reinterpret_cast<d2v *>(tprow + i0) = d2v{thp0, thp1};
+            wave_lds_sync();
+            llp = 0.0;
+            for (uint32_t k0 = 0; k0 < nobs; k0 += kResLanes) {
+                const uint32_t k = k0 + (uint32_t)r;
+                const double *xr = X + (size_t)(k < nobs ? k : 0u) * XS;
+                double b[4];
+#pragma unroll
+                for (int blk = 0; blk < 4; ++blk) {
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int i = 0; i < 8; i += 2) {
+                        const d2v xv = *reinterpret_cast<const d2v *>(xr + 8 * blk + i);
+                        const d2v tv = *reinterpret_cast<const d2v *>(tprow + 8 * blk + i);
+                        double y0 = xv.x - tv.x, y1 = xv.y - tv.y;
+                        if constexpr (!UNIT_T) {
+                            y0 = y0 * iLt[8 * blk + i];
+                            y1 = y1 * iLt[8 * blk + i + 1];
+                        }
+                        b[blk] = (i == 0) ? y0 * y0 : fma(y0, y0, b[blk]);
+                        b[blk] = fma(y1, y1, b[blk]);
+                    }
+                }
+                const double f = fma(-0.5, tree_inplace(b), a.t_c0);
+                static_for<0, kResLanes>([&](auto rc) {
+                    constexpr int q = decltype(rc)::value;
+                    if (k0 + q < nobs) llp = llp + rbcast<q>(f);
+                });
+            }
+            wave_lds_sync();  // the next step's θ° write stays behind this step's reads
+        } else {
+            double y0 = xb0 - thp0, y1 = xb1 - thp1;
+            if constexpr (!UNIT_T) {
+                y0 = y0 * iLt0;
+                y1 = y1 * iLt1;
+            }
+            const double qv = row_sumsq32(y0, y1, qlead);
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        // ---- accept_reject! (run.jl:271-278)
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const bool acc = E > -llr;
+        if constexpr (FULL)
+            __builtin_nontemporal_store(d2v{thp0, thp1},
+                                        reinterpret_cast<d2v *>(reinterpret_cast<char *>(a.hist_prop + slot * D * C) + po));
+        th0 = acc ? thp0 : th0;
+        th1 = acc ? thp1 : th1;
+        if (s + 1 == a.nsteps && r == 0) a.ll_prop[chain] = llp;
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            __builtin_nontemporal_store(d2v{th0, th1},
+                                        reinterpret_cast<d2v *>(reinterpret_cast<char *>(a.hist_theta + slot * D * C) + po));
+            if (r == 0) __builtin_nontemporal_store(ll, &chain_elem(a.hist_ll + slot * C, c32));
+        } else {
+            // mix_moments_kernel reads θ after each step of the launch from here
+            *reinterpret_cast<d2v *>(reinterpret_cast<char *>(a.mom_theta + (uint64_t)s * D * C) + po) = d2v{th0, th1};
+        }
+        {
+            const uint64_t m = __ballot(acc);  // lanes 0, 16, 32, 48 carry the wave's 4 chains
+            if (lane == 0)
+                nib[s * kResWaves + w] = (uint8_t)((m & 1u) | ((m >> 15) & 2u) | ((m >> 30) & 4u) | ((m >> 45) & 8u));
+        }
+        ra = rolling_update(ra, rg0, rg1, iter, a.W, N, a.rcp_W, acc);
+    }
+
+    // accept bits: 16 chains = 2 bytes per slot row
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < a.nsteps; t += blockDim.x) {
+        const uint8_t *nb = nib + t * kResWaves;
+        const uint16_t v = (uint16_t)(nb[0] | (nb[1] << 4) | (nb[2] << 8) | (nb[3] << 12));
+        *reinterpret_cast<uint16_t *>(a.hist_acc + (uint64_t)(a.iter0 + t - 1) * a.row_bytes + blockIdx.x * 2u) = v;
+    }
+    // fault bits of any lane of the chain's row
+    uint32_t f = faults;
+    f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, 0x111, 0xF, 0xF, true);  // row_shr:1
+    f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, 0x112, 0xF, 0xF, true);  // row_shr:2
+    f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, 0x114, 0xF, 0xF, true);  // row_shr:4
+    f |= (uint32_t)__builtin_amdgcn_mov_dpp((int)f, 0x118, 0xF, 0xF, true);  // row_shr:8
+    faults = rbcast_u32<15>(f);
+    if (r == 0) {
+        a.ll[chain] = ll;
+        a.ra[chain] = ra;
+        a.ring[2 * chain] = rg0;
+        a.ring[2 * chain + 1] = rg1;
+        a.nacc[chain] = nacc;
+        a.faults[chain] = faults;
+        if (faults) *a.fault_flag = 1u;
+    }
+    *reinterpret_cast<d2v *>(reinterpret_cast<char *>(a.theta) + po) = d2v{th0, th1};
+}
+
+}  // namespace emcmc

@@ -1,8 +1,11 @@
 // inst_mix.hip — gfx950 instantiations of the GaussianRandomWalkMix / Haario / chain-moments
 // kernels (emcmc_mix.h).
 #include "emcmc_dispatch.h"
+#include "emcmc_mixres.h"
 
 namespace emcmc {
+
+static_assert(kMixResChainsPerBlock == kResChainsPerBlock, "chains per block of mix_res_kernel");
 
 template <int D, bool FULL, int LL, bool MIX, bool ADIAG>
 MixFn mix_fn() {
@@ -20,6 +23,22 @@ const std::vector<MixEntry> &mix_table() {
                                             MIX8(8, false), MIX8(16, true), MIX8(32, true)};
     return t;
 }
+template <int D, bool FULL, int LL, bool UNIT>
+MixFn mixres_fn() {
+    return &mix_res_kernel<D, FULL, LL, UNIT>;
+}
+#define MIXRES(D, F, L, U) {D, F, L, U, mixres_fn<D, F, L, U>()}
+const std::vector<MixResEntry> &mixres_table() {
+    static const std::vector<MixResEntry> t = {MIXRES(32, true, 0, false), MIXRES(32, true, 1, false),
+                                               MIXRES(32, false, 0, false), MIXRES(32, false, 1, false),
+                                               MIXRES(32, true, 0, true),  MIXRES(32, true, 1, true),
+                                               MIXRES(32, false, 0, true), MIXRES(32, false, 1, true)};
+    return t;
+}
+size_t mixres_lds(int D, uint64_t nobs, uint64_t nsteps_max, bool perobs) {
+    return mixres_lds_bytes(D, nobs, nsteps_max, perobs);
+}
+
 template <int D>
 ReadjustFn readjust_fn() {
     return &mix_readjust_kernel<D>;

@@ -52,6 +52,7 @@ FAULT_PRIOR_RESAMPLES = 8
 VARIANT_HIGH_OCCUPANCY = 1
 VARIANT_OCCUPANCY3 = 2
 VARIANT_SCALAR_OBS = 4
+VARIANT_MIX_STREAM = 8
 
 
 class EmcmcConfig(C.Structure):

@@ -147,6 +147,8 @@ typedef struct emcmc_config {
 #define EMCMC_VARIANT_HIGH_OCCUPANCY 1u  /* cap registers for 4 waves/SIMD where instantiated */
 #define EMCMC_VARIANT_OCCUPANCY3 2u      /* cap registers for 3 waves/SIMD where instantiated */
 #define EMCMC_VARIANT_SCALAR_OBS 4u      /* diagonal Σ: one lane per chain, observations as SGPR operands */
+#define EMCMC_VARIANT_MIX_STREAM 8u      /* GaussianRandomWalkMix: stream L_B from HBM every step (mix_gsn_kernel)
+                                            instead of keeping it in registers (mix_res_kernel) */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,

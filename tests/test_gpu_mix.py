@@ -1,4 +1,4 @@
-"""Row f1 on the GPU (BASELINE cfg 4): mix_gsn_kernel + mix_readjust_kernel
+"""Row f1 on the GPU (BASELINE cfg 4): mix_gsn_kernel / mix_res_kernel + mix_readjust_kernel
 against the oracle (orc_run_mix), bit for bit — accept stream, state, ll,
 rolling acceptance, GenericChainStats mean/cov, each chain's Σ_B factor after
 Haario readjusts, fault bits — through the C ABI."""
@@ -31,9 +31,9 @@ def _problem(D, dense=False):
     return w.seed, mu, ts, obs, sa
 
 
-def _engine(D, C, M, seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist, spl=0, moments_only=False):
+def _engine(D, C, M, seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist, spl=0, moments_only=False, variant=0):
     eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
-                              steps_per_launch=spl, chain_moments=moments_only))
+                              steps_per_launch=spl, chain_moments=moments_only, kernel_variant=variant))
     if moments_only:
         eng.add_gaussian_rw_update(range(D), sa)
     else:
@@ -86,13 +86,56 @@ def test_mix_haario_matches_oracle(oracle, D, lam, k, ll_mode, hist, dense):
     seed, mu, ts, obs, sa = _problem(D, dense)
     sb = 0.5 * sa
     C, M = (1024 if D >= 16 else 777), 300
-    eng = _engine(D, C, M, seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist)
+    eng = _engine(D, C, M, seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist, variant=L.VARIANT_MIX_STREAM)
     eng.run_iters(1, M)
     assert "mix_gsn_kernel<D=%d" % D in eng.kernel_name()
     st = oracle.MixState(np.zeros((C, D)), sigma_b=sb)
     h = oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=M, lam=lam, haario_k=k,
                        ll_mode=ll_mode, nthreads=8)
     _check(eng, st, [h], list(range(1, M + 1)), hist == L.HIST_FULL)
+
+
+RES_CASES = [  # lam, k, ll_mode, hist, unit Σ_t, nobs, C
+    (0.5, 100, L.LL_PER_OBS, L.HIST_FULL, True, 10, 1024),
+    (0.25, 60, L.LL_SUFFSTAT, L.HIST_ACCEPT_ONLY, True, 10, 1024),
+    (0.5, 50, L.LL_PER_OBS, L.HIST_ACCEPT_ONLY, False, 37, 528),
+    (0.7, 70, L.LL_SUFFSTAT, L.HIST_FULL, False, 10, 1040),
+    (1.0, 40, L.LL_PER_OBS, L.HIST_FULL, False, 16, 1024),
+]
+
+
+@pytest.mark.parametrize("lam,k,ll_mode,hist,unit,nobs,C", RES_CASES)
+def test_mix_res_kernel_matches_oracle(oracle, lam, k, ll_mode, hist, unit, nobs, C):
+    """mix_res_kernel (L_B resident in registers, 16 lanes per chain), the default
+    for D = 32 with diagonal Σ_A / Σ_t: the same bits as the oracle and as
+    mix_gsn_kernel — identity or general diagonal Σ_t, 10 / 16 / 37 observations
+    (one or three rounds of 16 observation lanes), FULL and ACCEPT_ONLY, Haario
+    readjusts in the run (random_walk.jl:193-232, adaptation.jl:399-426)."""
+    D, M = 32, 240
+    w = W.cfg2(8, D=D, nobs=nobs)
+    mu, obs, sa = np.asarray(w.mu_true), np.asarray(w.obs), np.asarray(w.rw_sigma)
+    ts = np.eye(D) if unit else np.diag(0.5 + np.random.default_rng(3).random(D))
+    sb = 0.5 * sa
+    eng = _engine(D, C, M, w.seed, mu, ts, obs, sa, sb, lam, k, ll_mode, hist)
+    eng.run_iters(1, M)
+    assert "mix_res_kernel<D=32" in eng.kernel_name() and ("UNIT_T" in eng.kernel_name()) == unit
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=sb)
+    h = oracle.run_mix(st, seed=w.seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=M, lam=lam, haario_k=k,
+                       ll_mode=ll_mode, nthreads=8)
+    _check(eng, st, [h], list(range(1, M + 1)), hist == L.HIST_FULL)
+
+
+def test_mix_res_kernel_falls_back_when_chains_do_not_fill_blocks(oracle):
+    """C % 16 != 0: the mixture runs on mix_gsn_kernel (one lane per chain), same bits."""
+    D, C, M = 32, 1000, 60
+    seed, mu, ts, obs, sa = _problem(D)
+    eng = _engine(D, C, M, seed, mu, ts, obs, sa, 0.5 * sa, 0.5, 30, L.LL_PER_OBS, L.HIST_FULL)
+    eng.run_iters(1, M)
+    assert "mix_gsn_kernel<D=32" in eng.kernel_name()
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=0.5 * sa)
+    h = oracle.run_mix(st, seed=seed, sigma_a=sa, t_sigma=ts, obs=obs, iter0=1, nsteps=M, lam=0.5, haario_k=30,
+                       nthreads=8)
+    _check(eng, st, [h], list(range(1, M + 1)), True)
 
 
 def test_split_calls_launch_cuts_and_gap(oracle):

@@ -76,8 +76,11 @@ __device__ __forceinline__ double row_sumsq32(double y0, double y1, bool quad_le
     return rbcast<15>(t);
 }
 
+#ifndef EMCMC_MIXRES_MINB
+#define EMCMC_MIXRES_MINB 2  // blocks per CU the register budget is sized for (2: 256 VGPRs, 2 waves/SIMD)
+#endif
 template <int D, bool FULL, int LLMODE, bool UNIT_T>
-__global__ void __launch_bounds__(256, 2) mix_res_kernel(const MixParams a) {
+__global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const MixParams a) {
     static_assert(D == 2 * kResLanes, "two rows of L_B per lane");
     constexpr int DP = packed_n(D), DD = D * D, XS = D + 2;
     extern __shared__ __attribute__((aligned(16))) double lds[];

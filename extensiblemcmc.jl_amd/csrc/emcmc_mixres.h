@@ -48,13 +48,16 @@ __host__ __device__ constexpr size_t mixres_lds_bytes(int D, uint64_t nobs, uint
 }
 
 // lane L of the 16-lane row, to every lane of the row (one v_mov_b64_dpp)
+// (mov_dpp: every lane of the row has a source, so no "old" operand — update_dpp(0, …)
+// materialised one with a v_mov_b64 + s_nop per broadcast, ≈ 100 per chain-step)
 template <int L>
 __device__ __forceinline__ double rbcast(double v) {
-    return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + L, 0xF, 0xF, false);
+    const long b = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(long, v), 0x150 + L, 0xF, 0xF, true);
+    return __builtin_bit_cast(double, b);
 }
 template <int L>
 __device__ __forceinline__ uint32_t rbcast_u32(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + L, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + L, 0xF, 0xF, true);
 }
 
 // Σ y² over the chain's D = 32 coordinates in the canonical order (SumShape<32>:

@@ -417,9 +417,12 @@ struct MomentUnitState {
             for (int v = DIAG ? u : 0; v < NJ; ++v) c[UT::slot(u, v)] = *soa_ptr<DP>(a.cov, lc, up_idx(D, I0 + u, J0 + v));
     }
     // one step of chain_statistics.jl:46-49 with θ from the staged rows
+    // ROWS_NEW: the new row means of another unit of the same wave with the same
+    // row block, already advanced this step (the same formula, so the same bits):
+    // taken instead of recomputed; nullptr: advance them here
     template <typename TH>
     __device__ __forceinline__ void step(TH theta_at, double Nd, double N1d, double ca, double cb, double cc, double rN,
-                                         double rN1) {
+                                         double rN1, const double *rows_new = nullptr) {
         double ti[TB], tj[NJ];
 #pragma unroll
         for (int u = 0; u < TB; ++u) ti[u] = theta_at(I0 + u);
@@ -436,8 +439,13 @@ struct MomentUnitState {
                 c[UT::slot(u, v)] = old_sq + div_markstein(ti[u] * tj[v], Nd, rN);
             }
         }
+        if (rows_new) {
 #pragma unroll
-        for (int u = 0; u < TB; ++u) mi[u] = mi[u] * cb + div_markstein(ti[u], N1d, rN1);
+            for (int u = 0; u < TB; ++u) mi[u] = rows_new[u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < TB; ++u) mi[u] = mi[u] * cb + div_markstein(ti[u], N1d, rN1);
+        }
         if constexpr (!DIAG) {
 #pragma unroll
             for (int v = 0; v < NJ; ++v) mj[v] = mj[v] * cb + div_markstein(tj[v], N1d, rN1);
@@ -464,12 +472,29 @@ struct MomentUnitState {
     }
 };
 
-// The whole launch sweep of wave W (units W and W + WPB); every wave runs the
+// Units of wave W: W and W + WPB, except at D = 32 (16 units, 2 per wave), where
+// the pairs are chosen so that 6 of the 8 waves hold two units of one row block
+// and advance its 8 row means once: (0,4) (5,6) (7,8) (9,13) (1,10) (11,12)
+// (2,14) (15,3) — the diagonal unit of each row block first, so it stores them.
+template <int D>
+struct MomentPairs {
+    static constexpr int WPB = MomentTiles<D>::WPB;
+    static constexpr int a(int W) {
+        constexpr int t[8] = {0, 5, 7, 9, 1, 11, 2, 15};
+        return (MomentTiles<D>::NU == 16 && WPB == 8) ? t[W] : W;
+    }
+    static constexpr int b(int W) {
+        constexpr int t[8] = {4, 6, 8, 13, 10, 12, 14, 3};
+        return (MomentTiles<D>::NU == 16 && WPB == 8) ? t[W] : W + WPB;
+    }
+};
+
+// The whole launch sweep of wave W (units a(W) and b(W)); every wave runs the
 // same number of block barriers.
 template <int D, int W>
 __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *stage0, double *stage1) {
     using MT = MomentTiles<D>;
-    constexpr int PR = MT::PR, EW = MT::EW, NPF = MT::NPF, WPB = MT::WPB;
+    constexpr int PR = MT::PR, EW = MT::EW, NPF = MT::NPF;
     constexpr bool TWO = MT::UPW == 2;
     typedef double rowv __attribute__((ext_vector_type(EW)));
     const int lane = threadIdx.x & 63;
@@ -496,8 +521,10 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
             if (e < PR * 64) dst[e] = pf[q];
         }
     };
-    MomentUnitState<D, W> ua;
-    MomentUnitState<D, TWO ? W + WPB : W> ub;
+    constexpr int UA = MomentPairs<D>::a(W), UB = TWO ? MomentPairs<D>::b(W) : UA;
+    constexpr bool SHARE_ROWS = TWO && MomentUnit<D, UA>::I0 == MomentUnit<D, UB>::I0;
+    MomentUnitState<D, UA> ua;
+    MomentUnitState<D, UB> ub;
     ua.load(a, cl);
     if constexpr (TWO) ub.load(a, cl);
     {
@@ -518,7 +545,7 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
         const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
         const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
         ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
-        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
+        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr);
         if (s + 1 < a.nsteps) put((s & 1u) ? stage0 : stage1, pf);
         __syncthreads();
     }

@@ -110,10 +110,12 @@ struct UpdateHost {
     emcmc_haario_adaptation haario{};
     emcmc_lambda_fn flam = nullptr;  // HaarioTypeAdaptation fλ (host callback; nullptr = identity)
     void *flam_ctx = nullptr;
-    // prior (priors.jl) per local coordinate: family, parameters, host constant; factor starts
-    std::vector<uint32_t> pfam;
-    std::vector<double> pa, pb, pc;
-    uint64_t pstart = 0;
+    // prior (priors.jl) as MwgUpdate term slots (emcmc_mwg.h): per slot a family,
+    // its parameters and host constant; MvNormal rows; factor boundaries
+    uint32_t nslot = 0;
+    uint64_t psrc0 = 0, pstart = 0, pend = 0, pmvn = 0;
+    std::vector<uint32_t> pfam, pmvs;
+    std::vector<double> pa, pb, pc, pmu, piL, pL;
 };
 
 struct TargetHost {
@@ -438,13 +440,23 @@ emcmc_status select_mwg(emcmc_handle *h) {
             for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1ull << j) : 0ull;
         }
         m.prior = u.prior;
+        m.nslot = u.nslot;
+        m.psrc0 = u.psrc0;
         m.pstart = u.pstart;
-        for (size_t j = 0; j < u.pfam.size(); ++j) {
+        m.pend = u.pend;
+        m.pmvn = u.pmvn;
+        for (uint32_t j = 0; j < u.nslot; ++j) {
             m.pfam[j] = u.pfam[j];
+            m.pmvs[j] = u.pmvs[j];
             m.pa[j] = u.pa[j];
             m.pb[j] = u.pb[j];
             m.pc[j] = u.pc[j];
+            m.pmu[j] = u.pmu[j];
+            m.piL[j] = u.piL[j];
         }
+        if (u.pmvn)
+            for (uint32_t j = 0; j < u.nslot; ++j)
+                for (uint32_t q = 0; q <= j; ++q) m.pL[j * kMwgMaxD + q] = u.pL[(size_t)j * kMwgMaxD + q];
     }
     if (h->d_mwg) (void)hipFree(h->d_mwg);
     HIPCHK(h, hipMalloc(&h->d_mwg, tab.size() * sizeof(MwgUpdate)));
@@ -498,6 +510,16 @@ emcmc_status select_mix(emcmc_handle *h) {
     const int ll = (int)h->target.ll_mode;
     const bool mix = u.kernel == EMCMC_RW_GAUSSIAN_MIX;
     const bool adiag = (u.diag && h->target.diag) || D == 1;
+    // the mix / chain-moments kernels have no prior term and no proposal! redraw
+    // loop: a prior or positivity flags there would be dropped silently
+    if (u.prior != EMCMC_PRIOR_IMPROPER)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "chain moments / GaussianRandomWalkMix run on device with ImproperPrior only");
+    for (uint8_t f : u.pos)
+        if (f)
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                        "chain moments / GaussianRandomWalkMix: positivity-restricted coordinates have no device "
+                        "plugin on the mix kernels");
     Variant v;
     for (const auto &e : mix_table())
         if (e.D == D && e.full == (int)full && e.ll == ll && e.mix == (int)mix && e.adiag == (int)adiag) v.xfn = e.fn;
@@ -1208,6 +1230,143 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
     return EMCMC_OK;
 }
 
+namespace {
+// (family, a, b) of a univariate prior factor → the device's (a, b, c)
+// (emcmc_mwg.h univariate_logpdf; restated in oracle/emcmc_oracle.c)
+emcmc_status univariate_consts(emcmc_handle *h, uint32_t fam, double a, double b, double &pa, double &pb,
+                               double &pc) {
+    pa = a, pb = b;
+    switch (fam) {
+    case EMCMC_DIST_NORMAL:
+    case EMCMC_DIST_LOGNORMAL:
+        if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Normal/LogNormal prior: σ must be > 0");
+        pc = log_pos(b);
+        return EMCMC_OK;
+    case EMCMC_DIST_UNIFORM:
+        if (!(a < b)) return fail(h, EMCMC_INVALID_ARG, "Uniform prior: a < b");
+        pc = -log_pos(b - a);
+        return EMCMC_OK;
+    case EMCMC_DIST_EXPONENTIAL:
+        if (!(a > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Exponential prior: θ must be > 0");
+        pb = 1.0 / a;
+        pc = log_pos(pb);
+        return EMCMC_OK;
+    case EMCMC_DIST_GAMMA:
+        if (!(a > 0.0 && b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Gamma prior: α, θ must be > 0");
+        pc = (-std::lgamma(a)) - a * log_pos(b);
+        return EMCMC_OK;
+    case EMCMC_DIST_BETA:
+        if (!(a > 0.0 && b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Beta prior: α, β must be > 0");
+        pc = (std::lgamma(a) + std::lgamma(b)) - std::lgamma(a + b);
+        return EMCMC_OK;
+    case EMCMC_DIST_INVERSE_GAMMA:
+        if (!(a > 0.0 && b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "InverseGamma prior: α, θ must be > 0");
+        pc = a * log_pos(b) - std::lgamma(a);
+        return EMCMC_OK;
+    case EMCMC_DIST_CAUCHY:
+        if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Cauchy prior: σ must be > 0");
+        pc = 1.1447298858494002 + log_pos(b);  // log π + log σ
+        return EMCMC_OK;
+    case EMCMC_DIST_LAPLACE:
+        if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Laplace prior: θ must be > 0");
+        pc = log_pos(2.0 * b);
+        return EMCMC_OK;
+    case EMCMC_DIST_TDIST:
+        if (!(a > 0.0)) return fail(h, EMCMC_INVALID_ARG, "TDist prior: ν must be > 0");
+        pb = (a + 1.0) / 2.0;
+        pc = (std::lgamma((a + 1.0) / 2.0) - std::lgamma(a / 2.0)) - log_pos(a * 3.141592653589793) / 2.0;
+        return EMCMC_OK;
+    }
+    return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior family %u has no device plugin", fam);
+}
+
+// ProductPrior / StandardPrior → term slots (emcmc_mwg.h MwgUpdate).  The index
+// list is the constructor's (priors.jl:64-79): a dims-1 factor reads θ_local[1]
+// and takes one slot; a dims-k factor reads θ_local[last:last+k−1] and takes k
+// slots; `last` advances by dims either way, so slot j reads θ_local[j] unless it
+// belongs to a dims-1 factor.
+emcmc_status build_prior_slots(emcmc_handle *h, const emcmc_update_desc *u, UpdateHost &uh) {
+    const emcmc_prior_desc *pd = u->prior_params;
+    const uint32_t n = u->num_coords;
+    if (!pd || !pd->factors || pd->num_factors == 0)
+        return fail(h, EMCMC_INVALID_ARG, "ProductPrior/StandardPrior needs prior_params factors");
+    if (u->prior == EMCMC_PRIOR_STANDARD && pd->num_factors != 1)
+        return fail(h, EMCMC_INVALID_ARG, "StandardPrior has exactly one distribution");
+    uh.pfam.assign(kMwgMaxD, 0u);
+    uh.pmvs.assign(kMwgMaxD, 0u);
+    uh.pa.assign(kMwgMaxD, 0.0);
+    uh.pb.assign(kMwgMaxD, 0.0);
+    uh.pc.assign(kMwgMaxD, 0.0);
+    uh.pmu.assign(kMwgMaxD, 0.0);
+    uh.piL.assign(kMwgMaxD, 0.0);
+    uh.pL.assign((size_t)kMwgMaxD * kMwgMaxD, 0.0);
+    uint32_t last = 0;
+    for (uint32_t f = 0; f < pd->num_factors; ++f) {
+        const emcmc_prior_factor &fa = pd->factors[f];
+        const uint32_t k = fa.count;
+        const bool multi = fa.family == EMCMC_DIST_PRODUCT || fa.family == EMCMC_DIST_MVNORMAL;
+        if (k == 0) return fail(h, EMCMC_INVALID_ARG, "prior factor %u: dims must be ≥ 1", f);
+        if (u->prior == EMCMC_PRIOR_STANDARD) {
+            if (!multi)
+                return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                            "StandardPrior(univariate) on a coordinate vector: logpdf(dist, θ::Vector) has no "
+                            "scalar value in the reference (priors.jl:39); use Product([dist]) or ProductPrior");
+            if (k != n) return fail(h, EMCMC_INVALID_ARG, "StandardPrior: length(dist) must equal length(coords)");
+        } else if (multi != (k > 1)) {
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                        multi ? "ProductPrior factor %u: a multivariate dist with dims 1 reads the scalar θ[1] "
+                                "(priors.jl:68-70), a MethodError in the reference"
+                              : "ProductPrior factor %u: a univariate dist over dims > 1 reads the vector "
+                                "θ[last:last+dims-1] (priors.jl:72), a MethodError in the reference",
+                        f);
+        }
+        const uint32_t st = (k == 1) ? 0u : last;
+        const uint32_t s0 = last;  // first slot of this factor
+        if (last + k > n)
+            return fail(h, EMCMC_INVALID_ARG,
+                        "ProductPrior dims sum to more than the update's %u coordinates (the reference raises a "
+                        "BoundsError for a dims > 1 factor past the end; more dims-1 factors than coordinates are "
+                        "not supported on device)",
+                        n);
+        last += k;
+        uh.pstart |= 1ull << s0;
+        uh.pend |= 1ull << (s0 + k - 1);
+        if (k == 1) uh.psrc0 |= 1ull << s0;
+        if (fa.family == EMCMC_DIST_PRODUCT) {
+            if (!fa.components) return fail(h, EMCMC_INVALID_ARG, "Product prior factor needs its components");
+            for (uint32_t i = 0; i < k; ++i) {
+                const emcmc_prior_factor &cp = fa.components[i];
+                if (cp.family == EMCMC_DIST_PRODUCT || cp.family == EMCMC_DIST_MVNORMAL || cp.count != 1)
+                    return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "Product components must be univariate");
+                uh.pfam[s0 + i] = cp.family;
+                if (emcmc_status e = univariate_consts(h, cp.family, cp.a, cp.b, uh.pa[s0 + i], uh.pb[s0 + i],
+                                                       uh.pc[s0 + i]))
+                    return e;
+            }
+        } else if (fa.family == EMCMC_DIST_MVNORMAL) {
+            if (!fa.mu || !fa.sigma) return fail(h, EMCMC_INVALID_ARG, "MvNormal prior factor needs μ and Σ");
+            std::vector<double> Lk;
+            if (!cholesky_upper_colmajor(fa.sigma, (int)k, Lk))
+                return fail(h, EMCMC_INVALID_ARG, "MvNormal prior factor %u: Σ is not positive definite", f);
+            for (uint32_t i = 0; i < k; ++i) {
+                const uint32_t j = st + i;
+                uh.pmvn |= 1ull << j;
+                uh.pmvs[j] = st;
+                uh.pmu[j] = fa.mu[i];
+                uh.piL[j] = 1.0 / Lk[(size_t)i * k + i];
+                for (uint32_t q = 0; q <= i; ++q) uh.pL[(size_t)j * kMwgMaxD + st + q] = Lk[(size_t)i * k + q];
+            }
+            uh.pc[st + k - 1] = mvnormal_c0((int)k, logdet_chol(Lk, (int)k));
+        } else {
+            uh.pfam[s0] = fa.family;
+            if (emcmc_status e = univariate_consts(h, fa.family, fa.a, fa.b, uh.pa[s0], uh.pb[s0], uh.pc[s0])) return e;
+        }
+    }
+    uh.nslot = last;
+    return EMCMC_OK;
+}
+}  // namespace
+
 emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     if (!h || !u) return EMCMC_INVALID_ARG;
     if (h->allocated) return fail(h, EMCMC_STATE_ERROR, "updates must be added before set_state/run");
@@ -1249,49 +1408,8 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     uh.adaptation = u->adaptation;
     uh.coords.assign(u->coords, u->coords + u->num_coords);
     uh.pos = pos;
-    if (u->prior == EMCMC_PRIOR_PRODUCT || u->prior == EMCMC_PRIOR_STANDARD) {
-        // priors.jl:35-88 over the update's local coordinates; constants as the
-        // Distributions/StatsFuns forms need them (see emcmc_mwg.h univariate_logpdf)
-        const emcmc_prior_desc *pd = u->prior_params;
-        if (!pd || !pd->factors || pd->num_factors == 0)
-            return fail(h, EMCMC_INVALID_ARG, "ProductPrior/StandardPrior needs prior_params factors");
-        uint32_t j = 0;
-        for (uint32_t f = 0; f < pd->num_factors; ++f) {
-            const emcmc_prior_factor &fa = pd->factors[f];
-            if (fa.count == 0 || j + fa.count > u->num_coords)
-                return fail(h, EMCMC_INVALID_ARG, "prior factor counts must sum to num_coords");
-            double a = fa.a, b = fa.b, c = 0.0;
-            switch (fa.family) {
-            case EMCMC_DIST_NORMAL:
-                if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Normal prior: σ must be > 0");
-                c = log_pos(b);
-                break;
-            case EMCMC_DIST_UNIFORM:
-                if (!(a < b)) return fail(h, EMCMC_INVALID_ARG, "Uniform prior: a < b");
-                c = -log_pos(b - a);
-                break;
-            case EMCMC_DIST_EXPONENTIAL:
-                if (!(a > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Exponential prior: θ must be > 0");
-                b = 1.0 / a;
-                c = log_pos(b);
-                break;
-            case EMCMC_DIST_GAMMA:
-                if (!(a > 0.0 && b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Gamma prior: α, θ must be > 0");
-                c = (-std::lgamma(a)) - a * log_pos(b);
-                break;
-            default:
-                return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior family %u has no device plugin", fa.family);
-            }
-            if (u->prior == EMCMC_PRIOR_PRODUCT && j > 0) uh.pstart |= 1ull << j;
-            for (uint32_t k = 0; k < fa.count; ++k, ++j) {
-                uh.pfam.push_back(fa.family);
-                uh.pa.push_back(a);
-                uh.pb.push_back(b);
-                uh.pc.push_back(c);
-            }
-        }
-        if (j != u->num_coords) return fail(h, EMCMC_INVALID_ARG, "prior factor counts must sum to num_coords");
-    }
+    if (u->prior == EMCMC_PRIOR_PRODUCT || u->prior == EMCMC_PRIOR_STANDARD)
+        if (emcmc_status st = build_prior_slots(h, u, uh)) return st;
     const int n = (int)u->num_coords;
     if (u->kernel == EMCMC_RW_GAUSSIAN || u->kernel == EMCMC_RW_GAUSSIAN_MIX) {
         if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");

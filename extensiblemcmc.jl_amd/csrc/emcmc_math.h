@@ -302,6 +302,18 @@ EMCMC_HD double log_any(double x) {
     return log_pos(x);
 }
 
+// ---- log(1 + y) (prior densities: Beta, Cauchy, TDist) -------------------------
+// u = 1 + y rounded, then log u corrected by that rounding: log(1 + y) =
+// log u + log((1 + y)/u) ≈ log u − ((u − 1) − y)/u.  −Inf at y = −1, NaN below
+// (and for NaN), +Inf at +Inf.  Restated as orc_log1p_any in oracle/oracle_math.h.
+EMCMC_HD double log1p_any(double y) {
+    const double u = 1.0 + y;
+    if (!(u >= 0.0)) return __builtin_nan("");
+    if (u == 0.0) return -__builtin_inf();
+    if (u == __builtin_inf()) return u;
+    return log_any(u) - ((u - 1.0) - y) / u;
+}
+
 // ---- table-driven exp (x ≤ 0) and log (1 ≤ u ≤ 2): the MALA logistic terms --
 // e^{−|η|} and log(1 + e^{−|η|}) run once per observation and chain (4·10⁹ times
 // per cfg 3 step), so they get shorter forms than exp_any / log_pos; the

@@ -29,12 +29,14 @@
 //   AdaptationUnifRW    register on own turn, readjust at k proposals
 //                                                   run.jl:136-178, adaptation.jl:273-329
 //   proposal! resample  θ° is drawn again while logpdf(prior, θ°) === −Inf
-//                       (resample r uses counter blocks (r << 16) | j/2; capped at
-//                       kMaxResample with fault bit 8)                  updates.jl:191-196
+//                       (resample r uses counter blocks (r << 16) | j/2, Gaussian normal
+//                       indices (r << 17) | j; capped at kMaxResample / kMaxResampleGsn
+//                       with fault bit 8)                               updates.jl:191-196
 //   log_prior           logpdf(prior, θ_local) of ImproperPrior, ImproperPosPrior,
-//                       StandardPrior / ProductPrior of univariate Normal, Uniform,
-//                       Exponential, Gamma factors; llr adds lp(θ°) − lp(θ)
-//                                                   priors.jl:18-88, run.jl:374-385
+//                       ProductPrior (the constructor's index list: a dims-1 factor
+//                       reads θ[1], a dims-k factor θ[last:last+k−1]) and StandardPrior
+//                       of univariate, Product and MvNormal factors; llr adds
+//                       lp(θ°) − lp(θ)                 priors.jl:18-88, run.jl:374-385
 //   loglikelihood       a target policy: GsnTargetLaw (gsn_target.jl:23-29) or a
 //                       user device function compiled at run time (emcmc_rtc.h)
 #pragma once
@@ -44,12 +46,16 @@
 namespace emcmc {
 
 constexpr int kMwgMaxD = 64;  // largest D of the general kernel (D ≤ 32 instantiated ahead of time, the rest at run time)
-constexpr uint32_t kMaxResample = 0xFFFEu;          // proposal! resamples before fault bit 8
+constexpr uint32_t kMaxResample = 0xFFFEu;          // proposal! resamples before fault bit 8 (UniformRandomWalk:
+                                                    // counter block (r << 16) | j/2)
+constexpr uint32_t kMaxResampleGsn = 0x7FFEu;       // GaussianRandomWalk: normal index (r << 17) | j stays below
+                                                    // 2^32, so no redraw repeats an earlier one's variates
 constexpr uint32_t kFaultPriorResample = 8u;       // EMCMC_FAULT_PRIOR_RESAMPLES
 
 // prior kinds / univariate families (include/emcmc.h EMCMC_PRIOR_*, EMCMC_DIST_*)
 constexpr uint32_t kPriorImproper = 0u, kPriorImproperPos = 1u, kPriorProduct = 2u, kPriorStandard = 3u;
-constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, kDistGamma = 4u;
+constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, kDistGamma = 4u, kDistLogNormal = 5u,
+                   kDistBeta = 6u, kDistInverseGamma = 7u, kDistCauchy = 8u, kDistLaplace = 9u, kDistTDist = 10u;
 
 // One RandomWalkUpdate, host-built; read with scalar (uniform) loads.
 struct MwgUpdate {
@@ -67,13 +73,23 @@ struct MwgUpdate {
     double target;                  // AdaptationUnifRW target_accpt_rate
     double ascale[kMwgMaxD], amin[kMwgMaxD], amax[kMwgMaxD], aoff[kMwgMaxD];  // per coordinate (the scalar
                                     // form repeats its values)
-    // prior over the update's local coordinates (priors.jl): kind, and for
-    // Product/Standard priors one univariate family per coordinate, with
-    // bit j of pstart set where coordinate j starts a new ProductPrior factor
-    uint32_t prior, reserved1;
-    uint64_t pstart;
+    // prior over the update's local coordinates (priors.jl), host-built from the
+    // factors as a list of nslot term slots.  The constructor's index list makes
+    // every factor take as many slots as its dims advance `last` (priors.jl:64-79),
+    // so slot j reads θ_local[j] — or θ_local[1] (bit j of psrc0) for a dims-1
+    // factor — and the slots of one factor are contiguous: bit j of pstart / pend
+    // marks a factor's first / last slot.  Univariate and Product-component slots
+    // hold a family and its parameters; MvNormal slots (bit j of pmvn) a row of the
+    // forward substitution: μ_j, L_j· (lower factor, block-diagonal over the
+    // factors, row-major by slot), 1/L_jj, the factor's first slot pmvs[j]; the
+    // factor's c0 sits in pc of its last slot.
+    uint32_t prior, nslot;
+    uint64_t psrc0, pstart, pend, pmvn;
     uint32_t pfam[kMwgMaxD];
+    uint32_t pmvs[kMwgMaxD];
     double pa[kMwgMaxD], pb[kMwgMaxD], pc[kMwgMaxD];  // family parameters + host-computed constants
+    double pmu[kMwgMaxD], piL[kMwgMaxD];
+    double pL[kMwgMaxD * kMwgMaxD];
 };
 
 struct MwgParams {
@@ -110,27 +126,60 @@ struct MwgParams {
 __device__ __forceinline__ double log_real(double x) { return (x < 0.0) ? __builtin_nan("") : log_any(x); }
 
 // logpdf of one univariate prior factor at x (Distributions.jl / StatsFuns
-// forms; a, b the parameters, c a constant computed once on the host):
+// forms; a, b the parameters, c a constant computed once on the
+// host; restated in oracle/emcmc_oracle.c orc_univariate_logpdf):
 //   Normal(μ=a, σ=b), c = log σ:      −(z² + log2π)/2 − c, z = (x − μ)/σ
 //   Uniform(a, b), c = −log(b − a):   c on [a, b], else −Inf
 //   Exponential(θ), b = 1/θ, c = log(1/θ):   x < 0 ? −Inf : c − b·x
 //   Gamma(α=a, θ=b), c = −lgamma(α) − α·log θ:  x < 0 ? −Inf : (c + (α − 1)·log x) − x/θ
+//   LogNormal(μ=a, σ=b), c = log σ:   x ≤ 0 ? −Inf : (−(z² + log2π)/2 − c) − log x, z = (log x − μ)/σ
+//   Beta(α=a, β=b), c = logbeta(α, β): x ∉ [0, 1] ? −Inf : (xlogy(α−1, x) + xlog1py(β−1, −x)) − c
+//   InverseGamma(α=a, θ=b), c = α·log θ − lgamma(α): x ≤ 0 ? −Inf : (c − (α + 1)·log x) − θ/x
+//   Cauchy(μ=a, σ=b), c = log π + log σ:  −(c + log1p(z²)), z = (x − μ)/σ
+//   Laplace(μ=a, θ=b), c = log(2θ):   −(|x − μ|/θ + c)
+//   TDist(ν=a), b = (ν + 1)/2, c = (lgamma((ν+1)/2) − lgamma(ν/2)) − log(νπ)/2:  c − b·log1p(x²/ν)
 __device__ __forceinline__ double univariate_logpdf(uint32_t fam, double a, double b, double c, double x) {
-    if (fam == kDistNormal) {
+    const double ninf = -__builtin_inf();
+    switch (fam) {
+    case kDistNormal: {
         const double z = (x - a) / b;
         return -(z * z + kLog2Pi) / 2.0 - c;
     }
-    if (fam == kDistUniform) return (x >= a && x <= b) ? c : -__builtin_inf();
-    if (fam == kDistExponential) return (x < 0.0) ? -__builtin_inf() : c - b * x;
-    // Gamma
-    return (x < 0.0) ? -__builtin_inf() : (c + (a - 1.0) * log_real(x)) - x / b;
+    case kDistUniform: return (x >= a && x <= b) ? c : ninf;
+    case kDistExponential: return (x < 0.0) ? ninf : c - b * x;
+    case kDistGamma: return (x < 0.0) ? ninf : (c + (a - 1.0) * log_real(x)) - x / b;
+    case kDistLogNormal: {
+        if (!(x > 0.0)) return (x != x) ? x : ninf;
+        const double lx = log_any(x);
+        const double z = (lx - a) / b;
+        return (-(z * z + kLog2Pi) / 2.0 - c) - lx;
+    }
+    case kDistBeta: {
+        if (x < 0.0 || x > 1.0) return ninf;
+        const double t1 = (a - 1.0 == 0.0) ? 0.0 : (a - 1.0) * log_real(x);
+        const double t2 = (b - 1.0 == 0.0) ? 0.0 : (b - 1.0) * log1p_any(-x);
+        return (t1 + t2) - c;
+    }
+    case kDistInverseGamma:
+        if (!(x > 0.0)) return (x != x) ? x : ninf;
+        return (c - (a + 1.0) * log_any(x)) - b / x;
+    case kDistCauchy: {
+        const double z = (x - a) / b;
+        return -(c + log1p_any(z * z));
+    }
+    case kDistLaplace: return -(fabs(x - a) / b + c);
+    default:  // kDistTDist
+        return c - b * log1p_any((x * x) / a);
+    }
 }
 
 // logpdf(prior, θ_local) (priors.jl:18-88) over the first n of D local entries.
 //   ImproperPrior: 0.0.  ImproperPosPrior: −sum(log.(θ)), the sum folded left
-//   from θ_1.  ProductPrior: lp = 0.0; lp += logpdf(factor) in order, each
-//   factor's own coordinates folded left.  StandardPrior of a product of
-//   univariates: the left fold alone.
+//   from θ_1.  ProductPrior: lp = 0.0; lp += logpdf(dist_k, θ[idx_k]) in factor
+//   order over the constructor's index list (MwgUpdate slots).  StandardPrior:
+//   logpdf(dist, θ) of its one multivariate factor.  A factor's value: a
+//   univariate's logpdf; a Product's component logpdfs folded left; an MvNormal's
+//   c0 − ‖L⁻¹(θ − μ)‖²/2 with the squares folded left (s = y₁², s = fma(y_j, y_j, s)).
 template <int D, bool ROLL = false>
 __device__ __forceinline__ double mwg_log_prior(const MwgUpdate &u, uint32_t n, const double (&x)[D]) {
     constexpr int UJ = ROLL ? 1 : D;
@@ -146,22 +195,35 @@ __device__ __forceinline__ double mwg_log_prior(const MwgUpdate &u, uint32_t n, 
         }
         return -s;
     }
+    const bool mvn = u.pmvn != 0ull;  // wave-uniform: the MvNormal rows only when a factor needs them
     double lp = 0.0, s = 0.0;
+    double y[D];  // MvNormal factors: L⁻¹(θ − μ) by slot
 #pragma unroll UJ
     for (int j = 0; j < D; ++j) {
-        if ((uint32_t)j < n) {
-            const double v = univariate_logpdf(u.pfam[j], u.pa[j], u.pb[j], u.pc[j], x[j]);
-            if (j == 0) {
-                s = v;
-            } else if ((u.pstart >> j) & 1ull) {
-                lp = lp + s;
-                s = v;
+        y[j] = 0.0;
+        if ((uint32_t)j < u.nslot) {
+            const double xv = ((u.psrc0 >> j) & 1ull) ? x[0] : x[j];
+            const bool first = ((u.pstart >> j) & 1ull) != 0ull;
+            const bool mj = ((u.pmvn >> j) & 1ull) != 0ull;
+            if (mvn && mj) {
+                double acc = xv - u.pmu[j];
+                const uint32_t m0 = u.pmvs[j];
+#pragma unroll UJ
+                for (int m = 0; m < j; ++m)
+                    if ((uint32_t)m >= m0) acc = fma(-u.pL[j * kMwgMaxD + m], y[m], acc);
+                y[j] = acc * u.piL[j];
+                s = first ? y[j] * y[j] : fma(y[j], y[j], s);
             } else {
-                s = s + v;
+                const double v = univariate_logpdf(u.pfam[j], u.pa[j], u.pb[j], u.pc[j], xv);
+                s = first ? v : s + v;
+            }
+            if ((u.pend >> j) & 1ull) {
+                const double fv = mj ? u.pc[j] - s / 2.0 : s;
+                lp = (u.prior == kPriorProduct) ? lp + fv : fv;
             }
         }
     }
-    return (u.prior == kPriorProduct) ? lp + s : s;
+    return lp;
 }
 
 // ‖L⁻¹ r‖² for a D-vector (target Σ; dense forward substitution unless
@@ -336,7 +398,7 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
         }
         if (u.prior == kPriorImproper) break;
         if (!(mwg_log_prior<NU, ROLL>(u, n, tp) == -__builtin_inf())) break;
-        if (rs >= kMaxResample) {
+        if (rs >= (u.kind == 1 ? kMaxResample : kMaxResampleGsn)) {
             faults |= kFaultPriorResample;
             break;
         }

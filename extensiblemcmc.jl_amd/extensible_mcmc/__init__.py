@@ -12,7 +12,8 @@ from .kernels import (AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMi
                       HamiltonianMCUpdate, ImproperPosPrior, ImproperPrior, MALAUpdate, MCMCBackend,
                       MCMCParamUpdate, MCMCUpdate, NoAdaptation, ProductPrior, RandomWalkUpdate, StandardPrior,
                       UniformRandomWalk, UnsupportedPlugin, isdecorator, isequal_except, Normal, Uniform,
-                      Exponential, Gamma, Product)
+                      Exponential, Gamma, Product, LogNormal, Beta, InverseGamma, Cauchy, Laplace, TDist,
+                      MvNormal)
 from .mcmc import (MCMC, GenericMCMCBackend, MI355XBackend, MI355XGlobalWorkspace, MI355XLocalWorkspace,
                    create_workspaces, get_decorators, init, run, run_)
 from .schedule import JRange, MCMCSchedule, Step, reschedule, reschedule_
@@ -25,5 +26,6 @@ __all__ = [
     "GsnTargetLaw", "run", "run_", "get_decorators", "isdecorator", "ImproperPosPrior", "ImproperPrior",
     "SavingCallback", "REPLCallback", "MCMCSchedule", "JRange", "reschedule", "Engine", "EngineConfig",
     "EMCMCError", "device_count", "rhat_from_moments", "allgather_moments", "merge_moments", "MALAUpdate", "LogisticRegressionLaw",
-    "StandardPrior", "ProductPrior", "Normal", "Uniform", "Exponential", "Gamma", "Product", "UserTargetLaw",
+    "StandardPrior", "ProductPrior", "Normal", "Uniform", "Exponential", "Gamma", "Product",
+    "LogNormal", "Beta", "InverseGamma", "Cauchy", "Laplace", "TDist", "MvNormal", "UserTargetLaw",
 ]

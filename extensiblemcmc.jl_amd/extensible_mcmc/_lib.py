@@ -13,7 +13,7 @@ from pathlib import Path
 
 import numpy as np
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 OK = 0
 INVALID_ARG = 1
@@ -40,6 +40,8 @@ STATUS_NAMES = {
 RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA = 1, 2, 3, 4
 PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
 DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
+DIST_LOGNORMAL, DIST_BETA, DIST_INVERSE_GAMMA, DIST_CAUCHY, DIST_LAPLACE, DIST_TDIST = 5, 6, 7, 8, 9, 10
+DIST_PRODUCT, DIST_MVNORMAL = 32, 33
 ADPT_NONE, ADPT_UNIF_RW, ADPT_HAARIO, ADPT_UNIF_RW_VEC = 0, 1, 2, 3
 TARGET_GSN, TARGET_LOGISTIC, TARGET_USER = 1, 2, 3
 LL_PER_OBS, LL_SUFFSTAT = 0, 1
@@ -96,7 +98,11 @@ class EmcmcUpdateDesc(C.Structure):
 
 class EmcmcPriorFactor(C.Structure):
     """One ProductPrior / StandardPrior factor (include/emcmc.h emcmc_prior_factor)."""
-    _fields_ = [("family", C.c_uint32), ("count", C.c_uint32), ("a", C.c_double), ("b", C.c_double)]
+
+
+EmcmcPriorFactor._fields_ = [("family", C.c_uint32), ("count", C.c_uint32), ("a", C.c_double), ("b", C.c_double),
+                             ("components", C.POINTER(EmcmcPriorFactor)), ("mu", C.POINTER(C.c_double)),
+                             ("sigma", C.POINTER(C.c_double))]
 
 
 class EmcmcPriorDesc(C.Structure):

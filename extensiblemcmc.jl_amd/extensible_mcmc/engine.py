@@ -107,12 +107,34 @@ class Engine:
 
     # -- setup ------------------------------------------------------------------
     @staticmethod
-    def _prior_desc(u, prior, factors, keep):
-        """emcmc_update_desc.prior/prior_params; factors: [(EMCMC_DIST_*, count, a, b), ...]."""
+    def _prior_factor(f, keep):
+        """One emcmc_prior_factor from (family, 1, a, b), (DIST_PRODUCT, k, [(family, a, b), ...])
+        or (DIST_MVNORMAL, k, mu, Sigma) — count is the factor's dims entry."""
+        fam, cnt = int(f[0]), int(f[1])
+        pf = L.EmcmcPriorFactor()
+        pf.family, pf.count = fam, cnt
+        if fam == L.DIST_PRODUCT:
+            comps = (L.EmcmcPriorFactor * len(f[2]))()
+            for i, (cf, a, b) in enumerate(f[2]):
+                comps[i].family, comps[i].count, comps[i].a, comps[i].b = int(cf), 1, float(a), float(b)
+            keep.append(comps)
+            pf.components = C.cast(comps, C.POINTER(L.EmcmcPriorFactor))
+        elif fam == L.DIST_MVNORMAL:
+            mu = np.ascontiguousarray(np.asarray(f[2], dtype=np.float64).reshape(cnt))
+            S = np.ascontiguousarray(np.asarray(f[3], dtype=np.float64).reshape(cnt, cnt).ravel(order="F"))
+            keep += [mu, S]
+            pf.mu = mu.ctypes.data_as(C.POINTER(C.c_double))
+            pf.sigma = S.ctypes.data_as(C.POINTER(C.c_double))
+        else:
+            pf.a, pf.b = float(f[2]), float(f[3])
+        return pf
+
+    @classmethod
+    def _prior_desc(cls, u, prior, factors, keep):
+        """emcmc_update_desc.prior/prior_params; factors in constructor order (_prior_factor)."""
         u.prior = prior
         if factors:
-            arr = (L.EmcmcPriorFactor * len(factors))(*[L.EmcmcPriorFactor(int(f), int(c), float(a), float(b))
-                                                       for f, c, a, b in factors])
+            arr = (L.EmcmcPriorFactor * len(factors))(*[cls._prior_factor(f, keep) for f in factors])
             pd = L.EmcmcPriorDesc(len(factors), 0, C.cast(arr, C.POINTER(L.EmcmcPriorFactor)))
             keep += [arr, pd]
             u.prior_params = C.cast(C.pointer(pd), C.c_void_p)

@@ -14,6 +14,7 @@ from dataclasses import dataclass, field
 from typing import Callable, Optional, Sequence
 
 import numpy as np
+from math import lgamma  # noqa: E402
 
 from . import _lib as L
 
@@ -114,9 +115,18 @@ class ImproperPosPrior(Prior):
         return -float(np.sum(np.log(theta)))
 
 
-# univariate prior families with a device plugin (Distributions.jl parameterisations);
-# logpdf here is the host restatement (StatsFuns forms), the device computes the same
-class Normal:
+# prior distributions with a device plugin (Distributions.jl parameterisations);
+# logpdf here is a host restatement in numpy (libm), the device and the oracle
+# compute the StatsFuns forms of DESIGN.md §2 (within ~1e-15 of these)
+class UnivariateDistribution:
+    family = 0
+    a = b = 0.0
+
+    def to_factor(self):
+        return (self.family, 1, self.a, self.b)
+
+
+class Normal(UnivariateDistribution):
     family = L.DIST_NORMAL
 
     def __init__(self, mu=0.0, sigma=1.0):
@@ -128,7 +138,7 @@ class Normal:
         return -(z * z + np.log(2 * np.pi)) / 2.0 - np.log(self.b)
 
 
-class Uniform:
+class Uniform(UnivariateDistribution):
     family = L.DIST_UNIFORM
 
     def __init__(self, a=0.0, b=1.0):
@@ -140,7 +150,7 @@ class Uniform:
         return np.where((x >= self.a) & (x <= self.b), -np.log(self.b - self.a), -np.inf)
 
 
-class Exponential:
+class Exponential(UnivariateDistribution):
     family = L.DIST_EXPONENTIAL
 
     def __init__(self, theta=1.0):
@@ -153,7 +163,7 @@ class Exponential:
         return np.where(x < 0, -np.inf, np.log(lam) - lam * x)
 
 
-class Gamma:
+class Gamma(UnivariateDistribution):
     family = L.DIST_GAMMA
 
     def __init__(self, alpha=1.0, theta=1.0):
@@ -161,52 +171,193 @@ class Gamma:
         self.a, self.b = float(alpha), float(theta)
 
     def logpdf(self, x):
-        from math import lgamma
-
         x = np.asarray(x, dtype=float)
         with np.errstate(divide="ignore", invalid="ignore"):
             v = -lgamma(self.a) - self.a * np.log(self.b) + (self.a - 1) * np.log(x) - x / self.b
         return np.where(x < 0, -np.inf, v)
 
 
-class Product:
-    """Distributions.Product of univariates (a StandardPrior argument)."""
+class LogNormal(UnivariateDistribution):
+    family = L.DIST_LOGNORMAL
+
+    def __init__(self, mu=0.0, sigma=1.0):
+        assert sigma > 0
+        self.a, self.b = float(mu), float(sigma)
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            lx = np.log(x)
+            z = (lx - self.a) / self.b
+            v = -(z * z + np.log(2 * np.pi)) / 2.0 - np.log(self.b) - lx
+        return np.where(x <= 0, -np.inf, v)
+
+
+class Beta(UnivariateDistribution):
+    family = L.DIST_BETA
+
+    def __init__(self, alpha=1.0, beta=1.0):
+        assert alpha > 0 and beta > 0
+        self.a, self.b = float(alpha), float(beta)
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t1 = 0.0 if self.a == 1 else (self.a - 1) * np.log(x)
+            t2 = 0.0 if self.b == 1 else (self.b - 1) * np.log1p(-x)
+            v = t1 + t2 - (lgamma(self.a) + lgamma(self.b) - lgamma(self.a + self.b))
+        return np.where((x < 0) | (x > 1), -np.inf, v)
+
+
+class InverseGamma(UnivariateDistribution):
+    family = L.DIST_INVERSE_GAMMA
+
+    def __init__(self, alpha=1.0, theta=1.0):
+        assert alpha > 0 and theta > 0
+        self.a, self.b = float(alpha), float(theta)
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            v = self.a * np.log(self.b) - lgamma(self.a) - (self.a + 1) * np.log(x) - self.b / x
+        return np.where(x <= 0, -np.inf, v)
+
+
+class Cauchy(UnivariateDistribution):
+    family = L.DIST_CAUCHY
+
+    def __init__(self, mu=0.0, sigma=1.0):
+        assert sigma > 0
+        self.a, self.b = float(mu), float(sigma)
+
+    def logpdf(self, x):
+        z = (np.asarray(x, dtype=float) - self.a) / self.b
+        return -(np.log(np.pi) + np.log(self.b) + np.log1p(z * z))
+
+
+class Laplace(UnivariateDistribution):
+    family = L.DIST_LAPLACE
+
+    def __init__(self, mu=0.0, theta=1.0):
+        assert theta > 0
+        self.a, self.b = float(mu), float(theta)
+
+    def logpdf(self, x):
+        return -(np.abs(np.asarray(x, dtype=float) - self.a) / self.b + np.log(2 * self.b))
+
+
+class TDist(UnivariateDistribution):
+    family = L.DIST_TDIST
+
+    def __init__(self, nu=1.0):
+        assert nu > 0
+        self.a, self.b = float(nu), 0.0
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        nu = self.a
+        return (lgamma((nu + 1) / 2) - lgamma(nu / 2) - np.log(nu * np.pi) / 2
+                - (nu + 1) / 2 * np.log1p(x * x / nu))
+
+
+class MultivariateDistribution:
+    pass
+
+
+class Product(MultivariateDistribution):
+    """Distributions.Product of univariates: logpdf = Σ_i logpdf(v_i, x_i), folded left."""
 
     def __init__(self, dists):
         self.v = list(dists)
+        assert all(isinstance(d, UnivariateDistribution) for d in self.v)
+
+    def __len__(self):
+        return len(self.v)
 
     def logpdf(self, x):
-        return sum(float(d.logpdf(xi)) for d, xi in zip(self.v, np.atleast_1d(x)))
+        x = np.asarray(x, dtype=float)
+        if x.ndim != 1 or x.size != len(self.v):
+            raise ValueError("DimensionMismatch: length(d) != length(x)")
+        return sum(float(d.logpdf(xi)) for d, xi in zip(self.v, x))
+
+    def to_factor(self):
+        return (L.DIST_PRODUCT, len(self.v), [(d.family, d.a, d.b) for d in self.v])
 
 
-_UNIVARIATE = (Normal, Uniform, Exponential, Gamma)
+class MvNormal(MultivariateDistribution):
+    """MvNormal(μ, Σ): logpdf = −(k·log2π + logdet Σ + (x − μ)ᵀΣ⁻¹(x − μ))/2."""
+
+    def __init__(self, mu, Sigma):
+        self.mu = np.asarray(mu, dtype=float).reshape(-1)
+        self.Sigma = np.asarray(Sigma, dtype=float).reshape(self.mu.size, self.mu.size)
+        self.chol = np.linalg.cholesky(np.triu(self.Sigma) + np.triu(self.Sigma, 1).T)
+
+    def __len__(self):
+        return self.mu.size
+
+    def logpdf(self, x):
+        x = np.asarray(x, dtype=float)
+        if x.ndim != 1 or x.size != self.mu.size:
+            raise ValueError("DimensionMismatch")
+        y = np.linalg.solve(self.chol, x - self.mu)
+        k = self.mu.size
+        return -(k * np.log(2 * np.pi) + 2 * np.sum(np.log(np.diag(self.chol))) + float(y @ y)) / 2.0
+
+    def to_factor(self):
+        return (L.DIST_MVNORMAL, self.mu.size, self.mu, self.Sigma)
+
+
+_UNIVARIATE = (UnivariateDistribution,)
+
+
+def _logpdf(dist, x):
+    """Distributions.logpdf(dist, x) with Julia's dispatch: a univariate needs a
+    scalar, a multivariate a vector (anything else is a MethodError there)."""
+    if isinstance(dist, UnivariateDistribution):
+        if np.ndim(x) != 0:
+            raise TypeError(f"MethodError: no method matching logpdf(::{type(dist).__name__}, ::Vector{{Float64}})")
+        return float(dist.logpdf(float(x)))
+    if np.ndim(x) == 0:
+        raise TypeError(f"MethodError: no method matching logpdf(::{type(dist).__name__}, ::Float64)")
+    return float(dist.logpdf(x))
 
 
 class StandardPrior(Prior):
-    """StandardPrior(dist) with a scipy-like ``logpdf`` (priors.jl:35-39)."""
+    """StandardPrior(dist) (priors.jl:35-39): logpdf(dist, θ).  On a coordinate
+    vector only a multivariate dist has a scalar value."""
 
     def __init__(self, dist):
         self.dist = dist
 
     def logpdf(self, theta):
-        return float(np.sum(self.dist.logpdf(theta)))
+        return _logpdf(self.dist, np.asarray(theta, dtype=float))
 
 
 class ProductPrior(Prior):
-    """ProductPrior(dists, dims) (priors.jl:60-88)."""
+    """ProductPrior(dists, dims) (priors.jl:60-88).  The constructor's index
+    list, restated (priors.jl:64-79): a factor with dims 1 gets the index 1 — it
+    reads θ[1], not the next coordinate — and a factor with dims k > 1 the range
+    last:last+k−1; `last` advances by dims either way.  ``idx`` holds 0-based
+    ints / slices."""
 
     def __init__(self, dists, dims):
         idx, last = [], 0
         for d in dims:
-            idx.append(slice(last, last + d))
-            last += d
-        self.dists, self.idx = tuple(dists), tuple(idx)
+            if d == 1:
+                idx.append(0)
+                last += 1
+            else:
+                idx.append(slice(last, last + d))
+                last += d
+        self.dists, self.dims, self.idx = tuple(dists), tuple(int(d) for d in dims), tuple(idx)
 
     def logpdf(self, theta):
         theta = np.asarray(theta, dtype=float)
         lp = 0.0
         for dist, ix in zip(self.dists, self.idx):
-            lp += float(np.sum(dist.logpdf(theta[ix])))
+            if isinstance(ix, slice) and ix.stop > theta.size:
+                raise IndexError("BoundsError")
+            lp += _logpdf(dist, theta[ix])
         return lp
 
 
@@ -378,28 +529,32 @@ class HaarioTypeAdaptation(Adaptation):
 
 def prior_to_device(prior, n):
     """(EMCMC_PRIOR_*, factors) of a prior over an update's n coordinates (priors.jl).
-    ProductPrior(dists, dims): one factor per dist, dims[i] iid coordinates each;
-    StandardPrior(univariate) on n = 1, or StandardPrior(Product([...]))."""
+    ProductPrior(dists, dims): one factor per dist with its dims entry as count
+    (the engine rebuilds the constructor's index list); StandardPrior(dist): the
+    one multivariate dist.  The pairings the reference cannot evaluate (a
+    univariate over dims > 1 or on the whole vector, a multivariate over dims 1)
+    raise UnsupportedPlugin, as the engine does."""
     if isinstance(prior, ImproperPrior):
         return L.PRIOR_IMPROPER, None
     if isinstance(prior, ImproperPosPrior):
         return L.PRIOR_IMPROPER_POS, None
     if isinstance(prior, ProductPrior):
         fs = []
-        for dist, ix in zip(prior.dists, prior.idx):
-            if not isinstance(dist, _UNIVARIATE):
+        for dist, d in zip(prior.dists, prior.dims):
+            if not isinstance(dist, (UnivariateDistribution, Product, MvNormal)):
                 raise UnsupportedPlugin(f"ProductPrior factor {type(dist).__name__} has no device plugin")
-            fs.append((dist.family, ix.stop - ix.start, dist.a, dist.b))
-        if sum(f[1] for f in fs) != n:
-            raise ValueError("ProductPrior dims must cover the update's coordinates")
+            if isinstance(dist, UnivariateDistribution) != (d == 1):
+                raise UnsupportedPlugin(f"ProductPrior factor {type(dist).__name__} over dims {d}: a MethodError "
+                                        "in the reference (priors.jl:68-72, 85)")
+            f = dist.to_factor()
+            fs.append((f[0], d) + tuple(f[2:]))
         return L.PRIOR_PRODUCT, fs
     if isinstance(prior, StandardPrior):
         d = prior.dist
-        if isinstance(d, _UNIVARIATE) and n == 1:
-            return L.PRIOR_STANDARD, [(d.family, 1, d.a, d.b)]
-        if isinstance(d, Product) and len(d.v) == n and all(isinstance(x, _UNIVARIATE) for x in d.v):
-            return L.PRIOR_STANDARD, [(x.family, 1, x.a, x.b) for x in d.v]
-        raise UnsupportedPlugin(f"StandardPrior({type(d).__name__}) has no device plugin")
+        if isinstance(d, (Product, MvNormal)) and len(d) == n:
+            return L.PRIOR_STANDARD, [d.to_factor()]
+        raise UnsupportedPlugin(f"StandardPrior({type(d).__name__}) on {n} coordinates has no scalar logpdf in the "
+                                "reference (priors.jl:39) and no device plugin")
     raise UnsupportedPlugin(f"prior {type(prior).__name__} has no device plugin")
 
 

@@ -19,7 +19,7 @@ import Distributions
 const eMCMC = ExtensibleMCMC
 
 const LIB = get(ENV, "EMCMC_LIB", joinpath(@__DIR__, "..", "lib", "libemcmc.so"))
-const ABI_VERSION = UInt32(1)
+const ABI_VERSION = UInt32(2)
 
 # ---- C structs (include/emcmc.h) ---------------------------------------------
 struct EmcmcConfig
@@ -93,6 +93,9 @@ struct EmcmcPriorFactor
     count::UInt32
     a::Float64
     b::Float64
+    components::Ptr{EmcmcPriorFactor}   # EMCMC_DIST_PRODUCT: count univariate components
+    mu::Ptr{Float64}                    # EMCMC_DIST_MVNORMAL: μ
+    sigma::Ptr{Float64}                 # EMCMC_DIST_MVNORMAL: Σ, column-major
 end
 
 struct EmcmcPriorDesc
@@ -111,6 +114,9 @@ const RW_GAUSSIAN_MIX = UInt32(3)
 const ADPT_HAARIO = UInt32(2)
 const PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
 const DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = UInt32(1), UInt32(2), UInt32(3), UInt32(4)
+const DIST_LOGNORMAL, DIST_BETA, DIST_INVERSE_GAMMA = UInt32(5), UInt32(6), UInt32(7)
+const DIST_CAUCHY, DIST_LAPLACE, DIST_TDIST = UInt32(8), UInt32(9), UInt32(10)
+const DIST_PRODUCT, DIST_MVNORMAL = UInt32(32), UInt32(33)
 const ADPT_NONE = UInt32(0)
 const TARGET_GSN = UInt32(1)
 const H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
@@ -220,27 +226,45 @@ const RW_UNIFORM = UInt32(1)
 const ADPT_UNIF_RW = UInt32(1)
 const ADPT_UNIF_RW_VEC = UInt32(3)
 
-# priors.jl:18-88 → (EMCMC_PRIOR_*, emcmc_prior_desc pointer or C_NULL)
-_dist_factor(d::Distributions.Normal, k) = EmcmcPriorFactor(DIST_NORMAL, UInt32(k), d.μ, d.σ)
-_dist_factor(d::Distributions.Uniform, k) = EmcmcPriorFactor(DIST_UNIFORM, UInt32(k), d.a, d.b)
-_dist_factor(d::Distributions.Exponential, k) = EmcmcPriorFactor(DIST_EXPONENTIAL, UInt32(k), d.θ, 0.0)
-_dist_factor(d::Distributions.Gamma, k) = EmcmcPriorFactor(DIST_GAMMA, UInt32(k), d.α, d.θ)
-_dist_factor(d, k) = error("no device plugin for prior distribution $(typeof(d))")
+# priors.jl:18-88 → (EMCMC_PRIOR_*, emcmc_prior_desc pointer or C_NULL).
+# Every factor goes with its `dims` entry as count; the engine rebuilds the
+# constructor's index list (priors.jl:64-79: dims 1 → θ[1], dims k → a range).
+_uf(fam, a, b) = EmcmcPriorFactor(fam, UInt32(1), Float64(a), Float64(b), C_NULL, C_NULL, C_NULL)
+_dist_factor(d::Distributions.Normal, k, keep) = _uf(DIST_NORMAL, d.μ, d.σ)
+_dist_factor(d::Distributions.Uniform, k, keep) = _uf(DIST_UNIFORM, d.a, d.b)
+_dist_factor(d::Distributions.Exponential, k, keep) = _uf(DIST_EXPONENTIAL, d.θ, 0.0)
+_dist_factor(d::Distributions.Gamma, k, keep) = _uf(DIST_GAMMA, d.α, d.θ)
+_dist_factor(d::Distributions.LogNormal, k, keep) = _uf(DIST_LOGNORMAL, d.μ, d.σ)
+_dist_factor(d::Distributions.Beta, k, keep) = _uf(DIST_BETA, d.α, d.β)
+_dist_factor(d::Distributions.InverseGamma, k, keep) = _uf(DIST_INVERSE_GAMMA, Distributions.shape(d), Distributions.scale(d))
+_dist_factor(d::Distributions.Cauchy, k, keep) = _uf(DIST_CAUCHY, d.μ, d.σ)
+_dist_factor(d::Distributions.Laplace, k, keep) = _uf(DIST_LAPLACE, d.μ, d.θ)
+_dist_factor(d::Distributions.TDist, k, keep) = _uf(DIST_TDIST, d.ν, 0.0)
+function _dist_factor(d::Distributions.Product, k, keep)
+    comps = EmcmcPriorFactor[_dist_factor(c, 1, keep) for c in d.v]
+    push!(keep, comps)
+    EmcmcPriorFactor(DIST_PRODUCT, UInt32(k), 0.0, 0.0, pointer(comps), C_NULL, C_NULL)
+end
+function _dist_factor(d::Distributions.MvNormal, k, keep)
+    μ, Σ = Vector{Float64}(Distributions.mean(d)), Matrix{Float64}(Distributions.cov(d))
+    push!(keep, μ, Σ)
+    EmcmcPriorFactor(DIST_MVNORMAL, UInt32(k), 0.0, 0.0, C_NULL, pointer(μ), pointer(Σ))
+end
+_dist_factor(d, k, keep) = error("no device plugin for prior distribution $(typeof(d))")
 
 function _prior_desc(prior, n, keep)
     prior isa eMCMC.ImproperPrior && return PRIOR_IMPROPER, C_NULL
     prior isa eMCMC.ImproperPosPrior && return PRIOR_IMPROPER_POS, C_NULL
     if prior isa eMCMC.ProductPrior
-        fs = EmcmcPriorFactor[_dist_factor(d, length(ix)) for (d, ix) in zip(prior.dists, prior.idx)]
+        # prior.idx holds 1 for a dims-1 factor and a range otherwise (priors.jl:68-73)
+        fs = EmcmcPriorFactor[_dist_factor(d, ix isa Integer ? 1 : length(ix), keep)
+                              for (d, ix) in zip(prior.dists, prior.idx)]
         kind = PRIOR_PRODUCT
-    elseif prior isa eMCMC.StandardPrior && prior.dist isa Distributions.UnivariateDistribution && n == 1
-        fs = EmcmcPriorFactor[_dist_factor(prior.dist, 1)]
-        kind = PRIOR_STANDARD
-    elseif prior isa eMCMC.StandardPrior && prior.dist isa Distributions.Product
-        fs = EmcmcPriorFactor[_dist_factor(d, 1) for d in prior.dist.v]
+    elseif prior isa eMCMC.StandardPrior && prior.dist isa Distributions.MultivariateDistribution
+        fs = EmcmcPriorFactor[_dist_factor(prior.dist, length(prior.dist), keep)]
         kind = PRIOR_STANDARD
     else
-        error("no device plugin for $(typeof(prior))")
+        error("no device plugin for $(typeof(prior)) on $n coordinates")
     end
     pd = Ref(EmcmcPriorDesc(UInt32(length(fs)), UInt32(0), pointer(fs)))
     push!(keep, fs, pd)

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define EMCMC_ABI_VERSION 1u
+#define EMCMC_ABI_VERSION 2u  /* 2: emcmc_prior_factor gained components / mu / sigma (round 3) */
 
 typedef enum emcmc_status {
     EMCMC_OK = 0,
@@ -67,16 +67,30 @@ typedef enum emcmc_status {
  * the general schedule kernel (D ≤ 64). */
 #define EMCMC_PRIOR_IMPROPER 0u     /* ImproperPrior     priors.jl:18-19: 0.0 */
 #define EMCMC_PRIOR_IMPROPER_POS 1u /* ImproperPosPrior  priors.jl:25-26: −sum(log.(θ)) */
-#define EMCMC_PRIOR_PRODUCT 2u      /* ProductPrior(dists, dims) priors.jl:60-88: lp = 0.0; lp += logpdf(dist, θ[idx])
-                                       per factor; a factor over k > 1 coordinates is k iid copies
-                                       (Product(fill(dist, k))) */
-#define EMCMC_PRIOR_STANDARD 3u     /* StandardPrior(dist) priors.jl:35-39 with dist a univariate on a 1-coordinate
-                                       update or a Product of univariates: one left fold, no leading 0.0 */
-/* Univariate families of a prior factor (Distributions.jl parameterisations) */
+#define EMCMC_PRIOR_PRODUCT 2u      /* ProductPrior(dists, dims) priors.jl:60-88.  The factors are `dists` with
+                                       count = dims[k]; the engine builds the index list as the constructor does
+                                       (priors.jl:64-79): a factor with dims 1 reads local θ[1] (index 1, not
+                                       the next coordinate), a factor with dims k > 1 reads θ[last:last+k−1],
+                                       last advancing by dims either way; then lp = 0.0; lp += logpdf(dist, θ[idx])
+                                       in factor order.  dims 1 needs a univariate family, dims > 1 a multivariate
+                                       one (EMCMC_DIST_PRODUCT / EMCMC_DIST_MVNORMAL): the other pairings raise a
+                                       MethodError in the reference and EMCMC_UNSUPPORTED_PLUGIN here */
+#define EMCMC_PRIOR_STANDARD 3u     /* StandardPrior(dist) priors.jl:35-39: logpdf(dist, θ_local), one factor, dist
+                                       multivariate with count = num_coords (a univariate dist on the local vector
+                                       raises in the reference: EMCMC_UNSUPPORTED_PLUGIN) */
+/* Families of a prior factor (Distributions.jl parameterisations, StatsFuns forms) */
 #define EMCMC_DIST_NORMAL 1u        /* Normal(μ = a, σ = b) */
 #define EMCMC_DIST_UNIFORM 2u       /* Uniform(a, b) */
 #define EMCMC_DIST_EXPONENTIAL 3u   /* Exponential(θ = a), the scale */
 #define EMCMC_DIST_GAMMA 4u         /* Gamma(α = a, θ = b), shape and scale */
+#define EMCMC_DIST_LOGNORMAL 5u     /* LogNormal(μ = a, σ = b) */
+#define EMCMC_DIST_BETA 6u          /* Beta(α = a, β = b) */
+#define EMCMC_DIST_INVERSE_GAMMA 7u /* InverseGamma(α = a, θ = b), shape and scale */
+#define EMCMC_DIST_CAUCHY 8u        /* Cauchy(μ = a, σ = b) */
+#define EMCMC_DIST_LAPLACE 9u       /* Laplace(μ = a, θ = b) */
+#define EMCMC_DIST_TDIST 10u        /* TDist(ν = a) */
+#define EMCMC_DIST_PRODUCT 32u      /* Product([d_1, …, d_k]) of univariates: `components`, k = count */
+#define EMCMC_DIST_MVNORMAL 33u     /* MvNormal(μ, Σ) over count coordinates: `mu`, `sigma` */
 
 /* Adaptation — src/transition_kernels/adaptation.jl */
 #define EMCMC_ADPT_NONE 0u      /* NoAdaptation          adaptation.jl:26 */
@@ -196,16 +210,19 @@ typedef struct emcmc_haario_adaptation {
     double scale;
 } emcmc_haario_adaptation;
 
-/* One factor of a ProductPrior / StandardPrior: `count` consecutive local
- * coordinates with the same univariate family EMCMC_DIST_* and parameters (a, b). */
+/* One factor of a ProductPrior (one of its `dists`, with its `dims` entry as
+ * count) or the `dist` of a StandardPrior (count = its length). */
 typedef struct emcmc_prior_factor {
-    uint32_t family;
-    uint32_t count;
-    double a, b;
+    uint32_t family;      /* EMCMC_DIST_* */
+    uint32_t count;       /* dims[k] (ProductPrior) / length(dist) (StandardPrior); 1 for a univariate */
+    double a, b;          /* univariate parameters (EMCMC_DIST_* above) */
+    const struct emcmc_prior_factor *components; /* EMCMC_DIST_PRODUCT: count univariate factors, else NULL */
+    const double *mu;     /* EMCMC_DIST_MVNORMAL: μ, count doubles, else NULL */
+    const double *sigma;  /* EMCMC_DIST_MVNORMAL: Σ, count² column-major (upper triangle read), else NULL */
 } emcmc_prior_factor;
 
 /* emcmc_update_desc.prior_params for EMCMC_PRIOR_PRODUCT / EMCMC_PRIOR_STANDARD:
- * the factors in coordinate order, their counts summing to num_coords. */
+ * the factors in the order given to the reference constructor. */
 typedef struct emcmc_prior_desc {
     uint32_t num_factors;
     uint32_t reserved;

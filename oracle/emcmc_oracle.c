@@ -568,53 +568,116 @@ ORC_EXPORT uint64_t orc_markstein_mismatches(double b, const double *x, uint64_t
  * ========================================================================== */
 
 #define ORC_MWG_MAXD 64
-#define ORC_MAX_RESAMPLE 0xFFFEu
+#define ORC_MAX_RESAMPLE 0xFFFEu     /* UniformRandomWalk: counter blocks (r << 16) | j/2 */
+#define ORC_MAX_RESAMPLE_GSN 0x7FFEu /* GaussianRandomWalk: normal index (r << 17) | j < 2^32, never repeated */
 #define ORC_FAULT_PRIOR_RESAMPLES 8u
 
 /* priors.jl, restated: EMCMC_PRIOR_* kinds, EMCMC_DIST_* families */
 enum { ORC_PRIOR_IMPROPER = 0, ORC_PRIOR_IMPROPER_POS = 1, ORC_PRIOR_PRODUCT = 2, ORC_PRIOR_STANDARD = 3 };
-enum { ORC_DIST_NORMAL = 1, ORC_DIST_UNIFORM = 2, ORC_DIST_EXPONENTIAL = 3, ORC_DIST_GAMMA = 4 };
+enum {
+    ORC_DIST_NORMAL = 1, ORC_DIST_UNIFORM = 2, ORC_DIST_EXPONENTIAL = 3, ORC_DIST_GAMMA = 4, ORC_DIST_LOGNORMAL = 5,
+    ORC_DIST_BETA = 6, ORC_DIST_INVERSE_GAMMA = 7, ORC_DIST_CAUCHY = 8, ORC_DIST_LAPLACE = 9, ORC_DIST_TDIST = 10,
+    ORC_DIST_PRODUCT = 32, ORC_DIST_MVNORMAL = 33
+};
+#define ORC_LOGPI 1.1447298858494002 /* log π */
 
 static double orc_log_real(double x) { return (x < 0.0) ? NAN : orc_log_any(x); }
 
-/* logpdf of one univariate factor (Distributions.jl / StatsFuns forms):
+/* logpdf of one univariate factor (Distributions.jl / StatsFuns forms; the
+ * Distributions version is unpinned):
  *   Normal(μ, σ): normlogpdf(z) − log σ = −(z² + log2π)/2 − log σ, z = (x − μ)/σ
  *   Uniform(a, b): −log(b − a) on [a, b], else −Inf
  *   Exponential(θ): x < 0 ? −Inf : log λ − λx, λ = 1/θ
  *   Gamma(α, θ): x < 0 ? −Inf : −loggamma(α) − α log θ + (α − 1) log x − x/θ (left to right)
- * (a, b) are the parameters as the device holds them (Exponential: b = 1/θ),
- * c the constant the host computes once. */
+ *   LogNormal(μ, σ): x ≤ 0 ? −Inf : normlogpdf(μ, σ, log x) − log x
+ *   Beta(α, β): x ∉ [0, 1] ? −Inf : xlogy(α − 1, x) + xlog1py(β − 1, −x) − logbeta(α, β)
+ *   InverseGamma(α, θ): x ≤ 0 ? −Inf : α log θ − loggamma(α) − (α + 1) log x − θ/x
+ *   Cauchy(μ, σ): −(log π + log σ + log1p(z²))
+ *   Laplace(μ, θ): −(|x − μ|/θ + log(2θ))
+ *   TDist(ν): loggamma((ν+1)/2) − loggamma(ν/2) − log(νπ)/2 − (ν+1)/2 · log1p(x²/ν)
+ * (a, b) are the parameters as the device holds them (Exponential: b = 1/θ,
+ * TDist: b = (ν+1)/2), c the constant the host computes once. */
 static double orc_univariate_logpdf(uint32_t fam, double a, double b, double c, double x) {
-    if (fam == ORC_DIST_NORMAL) {
+    switch (fam) {
+    case ORC_DIST_NORMAL: {
         const double z = (x - a) / b;
         return -(z * z + ORC_LOG2PI) / 2.0 - c;
     }
-    if (fam == ORC_DIST_UNIFORM) return (x >= a && x <= b) ? c : -INFINITY;
-    if (fam == ORC_DIST_EXPONENTIAL) return (x < 0.0) ? -INFINITY : c - b * x;
-    return (x < 0.0) ? -INFINITY : (c + (a - 1.0) * orc_log_real(x)) - x / b;
+    case ORC_DIST_UNIFORM: return (x >= a && x <= b) ? c : -INFINITY;
+    case ORC_DIST_EXPONENTIAL: return (x < 0.0) ? -INFINITY : c - b * x;
+    case ORC_DIST_GAMMA: return (x < 0.0) ? -INFINITY : (c + (a - 1.0) * orc_log_real(x)) - x / b;
+    case ORC_DIST_LOGNORMAL: {
+        if (x != x) return x;
+        if (x <= 0.0) return -INFINITY;
+        const double lx = orc_log_any(x);
+        const double z = (lx - a) / b;
+        return (-(z * z + ORC_LOG2PI) / 2.0 - c) - lx;
+    }
+    case ORC_DIST_BETA: {
+        if (x < 0.0 || x > 1.0) return -INFINITY;
+        const double t1 = (a - 1.0 == 0.0) ? 0.0 : (a - 1.0) * orc_log_real(x); /* xlogy */
+        const double t2 = (b - 1.0 == 0.0) ? 0.0 : (b - 1.0) * orc_log1p_any(-x); /* xlog1py */
+        return (t1 + t2) - c;
+    }
+    case ORC_DIST_INVERSE_GAMMA:
+        if (x != x) return x;
+        if (x <= 0.0) return -INFINITY;
+        return (c - (a + 1.0) * orc_log_any(x)) - b / x;
+    case ORC_DIST_CAUCHY: {
+        const double z = (x - a) / b;
+        return -(c + orc_log1p_any(z * z));
+    }
+    case ORC_DIST_LAPLACE: return -(fabs(x - a) / b + c);
+    default: /* TDist */
+        return c - b * orc_log1p_any((x * x) / a);
+    }
 }
 
-/* (family, a, b) of a factor → device parameters and constant (engine host code) */
+/* (family, a, b) of a univariate factor → device parameters and constant
+ * (engine host code); −1 on invalid parameters, −4 for a family with no plugin */
 static int orc_prior_factor_consts(uint32_t fam, double a, double b, double *pa, double *pb, double *pc) {
+    *pa = a, *pb = b;
     switch (fam) {
     case ORC_DIST_NORMAL:
+    case ORC_DIST_LOGNORMAL:
         if (!(b > 0.0)) return -1;
-        *pa = a, *pb = b, *pc = orc_log(b);
+        *pc = orc_log(b);
         return 0;
     case ORC_DIST_UNIFORM:
         if (!(a < b)) return -1;
-        *pa = a, *pb = b, *pc = -orc_log(b - a);
+        *pc = -orc_log(b - a);
         return 0;
     case ORC_DIST_EXPONENTIAL:
         if (!(a > 0.0)) return -1;
-        *pa = a, *pb = 1.0 / a, *pc = orc_log(1.0 / a);
+        *pb = 1.0 / a, *pc = orc_log(1.0 / a);
         return 0;
     case ORC_DIST_GAMMA:
         if (!(a > 0.0 && b > 0.0)) return -1;
-        *pa = a, *pb = b, *pc = (-lgamma(a)) - a * orc_log(b);
+        *pc = (-lgamma(a)) - a * orc_log(b);
+        return 0;
+    case ORC_DIST_BETA:
+        if (!(a > 0.0 && b > 0.0)) return -1;
+        *pc = (lgamma(a) + lgamma(b)) - lgamma(a + b);
+        return 0;
+    case ORC_DIST_INVERSE_GAMMA:
+        if (!(a > 0.0 && b > 0.0)) return -1;
+        *pc = a * orc_log(b) - lgamma(a);
+        return 0;
+    case ORC_DIST_CAUCHY:
+        if (!(b > 0.0)) return -1;
+        *pc = ORC_LOGPI + orc_log(b);
+        return 0;
+    case ORC_DIST_LAPLACE:
+        if (!(b > 0.0)) return -1;
+        *pc = orc_log(2.0 * b);
+        return 0;
+    case ORC_DIST_TDIST:
+        if (!(a > 0.0)) return -1;
+        *pb = (a + 1.0) / 2.0;
+        *pc = (lgamma((a + 1.0) / 2.0) - lgamma(a / 2.0)) - orc_log(a * 3.141592653589793) / 2.0;
         return 0;
     }
-    return -2;
+    return -4;
 }
 typedef struct {
     uint32_t kind; /* 1 uniform, 2 gaussian */
@@ -626,13 +689,46 @@ typedef struct {
     int diag;
     uint32_t adapt, k;
     double target, scale[ORC_MWG_MAXD], amin[ORC_MWG_MAXD], amax[ORC_MWG_MAXD], offset[ORC_MWG_MAXD];
-    uint32_t prior, pstart, pfam[ORC_MWG_MAXD];
-    double pa[ORC_MWG_MAXD], pb[ORC_MWG_MAXD], pc[ORC_MWG_MAXD];
+    /* prior: the factors with the local index each reads (priors.jl:64-79) */
+    uint32_t prior, nfac;
+    uint32_t ffam[ORC_MWG_MAXD], fcnt[ORC_MWG_MAXD], fstart[ORC_MWG_MAXD], fcomp[ORC_MWG_MAXD];
+    double fa[ORC_MWG_MAXD], fb[ORC_MWG_MAXD], fc[ORC_MWG_MAXD];
+    uint32_t cfam[ORC_MWG_MAXD]; /* Product components, in factor order */
+    double ca[ORC_MWG_MAXD], cb[ORC_MWG_MAXD], cc[ORC_MWG_MAXD];
+    double mmu[ORC_MWG_MAXD], mL[ORC_MWG_MAXD * ORC_MWG_MAXD], miL[ORC_MWG_MAXD]; /* MvNormal factors, by local index */
 } orc_mwg_update;
 
+/* logpdf(dist_f, θ[idx_f]) of factor f: a univariate at its one index; a
+ * Product (Distributions' sum over its components, folded left); an MvNormal
+ * c0 − ‖L⁻¹(θ − μ)‖²/2 (forward substitution, squares folded left). */
+static double orc_factor_logpdf(const orc_mwg_update *u, uint32_t f, const double *x) {
+    const uint32_t st = u->fstart[f], k = u->fcnt[f];
+    if (u->ffam[f] == ORC_DIST_PRODUCT) {
+        double s = 0.0;
+        for (uint32_t i = 0; i < k; ++i) {
+            const uint32_t q = u->fcomp[f] + i;
+            const double v = orc_univariate_logpdf(u->cfam[q], u->ca[q], u->cb[q], u->cc[q], x[st + i]);
+            s = (i == 0) ? v : s + v;
+        }
+        return s;
+    }
+    if (u->ffam[f] == ORC_DIST_MVNORMAL) {
+        double y[ORC_MWG_MAXD], s = 0.0;
+        for (uint32_t i = 0; i < k; ++i) {
+            double acc = x[st + i] - u->mmu[st + i];
+            for (uint32_t m = 0; m < i; ++m) acc = fma(-u->mL[(size_t)(st + i) * ORC_MWG_MAXD + st + m], y[m], acc);
+            y[i] = acc * u->miL[st + i];
+            s = (i == 0) ? y[i] * y[i] : fma(y[i], y[i], s);
+        }
+        return u->fc[f] - s / 2.0;
+    }
+    return orc_univariate_logpdf(u->ffam[f], u->fa[f], u->fb[f], u->fc[f], x[st]);
+}
+
 /* logpdf(prior, x) over the update's n local coordinates (priors.jl:18-88):
- * ImproperPosPrior −(x₁ + x₂ + …) of the logs; ProductPrior lp = 0.0; lp += factor
- * (each factor folded left); StandardPrior of univariates: the left fold alone. */
+ * ImproperPosPrior −(x₁ + x₂ + …) of the logs; ProductPrior lp = 0.0;
+ * lp += logpdf(dist, θ[idx]) per factor (priors.jl:82-88); StandardPrior
+ * logpdf(dist, θ) (priors.jl:39). */
 static double orc_mwg_log_prior(const orc_mwg_update *u, uint32_t n, const double *x) {
     if (u->prior == ORC_PRIOR_IMPROPER) return 0.0;
     if (u->prior == ORC_PRIOR_IMPROPER_POS) {
@@ -643,19 +739,91 @@ static double orc_mwg_log_prior(const orc_mwg_update *u, uint32_t n, const doubl
         }
         return -s;
     }
-    double lp = 0.0, s = 0.0;
-    for (uint32_t j = 0; j < n; ++j) {
-        const double v = orc_univariate_logpdf(u->pfam[j], u->pa[j], u->pb[j], u->pc[j], x[j]);
-        if (j == 0) {
-            s = v;
-        } else if ((u->pstart >> j) & 1u) {
-            lp = lp + s;
-            s = v;
+    if (u->prior == ORC_PRIOR_STANDARD) return orc_factor_logpdf(u, 0, x);
+    double lp = 0.0;
+    for (uint32_t f = 0; f < u->nfac; ++f) lp += orc_factor_logpdf(u, f, x);
+    return lp;
+}
+
+/* The prior of update u from the caller's tables: factor f = (ffam, fcnt, fa, fb);
+ * Product components in cfam/ca/cb, consecutively in factor order; MvNormal
+ * μ / Σ in mvmu / mvS placed at the factor's local index range (Σ column-major
+ * in a 64 × 64 block).  The index each factor reads is the constructor's
+ * (priors.jl:64-79): dims 1 → θ[1], dims k > 1 → θ[last:last+k−1], `last`
+ * advancing by dims either way.  Returns 0, −2 (invalid) or −4 (a pairing the
+ * reference raises a MethodError on: univariate over dims > 1, multivariate
+ * over dims 1, a univariate StandardPrior). */
+static int orc_build_prior(orc_mwg_update *u, uint32_t nfac, const uint32_t *ffam, const uint32_t *fcnt,
+                           const double *fa, const double *fb, const uint32_t *cfam, const double *ca,
+                           const double *cb, const double *mvmu, const double *mvS) {
+    const uint32_t n = u->nc;
+    if (nfac == 0 || nfac > ORC_MWG_MAXD) return -2;
+    if (u->prior == ORC_PRIOR_STANDARD && nfac != 1) return -2;
+    u->nfac = nfac;
+    uint32_t last = 0, ncomp = 0;
+    for (uint32_t f = 0; f < nfac; ++f) {
+        const uint32_t fam = ffam[f], k = fcnt[f];
+        const int multi = (fam == ORC_DIST_PRODUCT || fam == ORC_DIST_MVNORMAL);
+        if (k == 0) return -2;
+        if (u->prior == ORC_PRIOR_STANDARD) {
+            if (!multi) return -4; /* logpdf(univariate, θ::Vector): no scalar in the reference */
+            if (k != n) return -2;
+        } else if (multi != (k > 1)) {
+            return -4;
+        }
+        u->ffam[f] = fam;
+        u->fcnt[f] = k;
+        u->fstart[f] = (k == 1) ? 0u : last;
+        last += k;
+        if (last > n) return -2;
+        if (fam == ORC_DIST_PRODUCT) {
+            if (ncomp + k > ORC_MWG_MAXD) return -2;
+            u->fcomp[f] = ncomp;
+            for (uint32_t i = 0; i < k; ++i, ++ncomp) {
+                u->cfam[ncomp] = cfam[ncomp];
+                const int rc = orc_prior_factor_consts(cfam[ncomp], ca[ncomp], cb[ncomp], &u->ca[ncomp], &u->cb[ncomp],
+                                                       &u->cc[ncomp]);
+                if (rc) return rc == -4 ? -4 : -2;
+            }
+        } else if (fam == ORC_DIST_MVNORMAL) {
+            const uint32_t st = u->fstart[f];
+            double S[ORC_MWG_MAXD * ORC_MWG_MAXD], Lk[ORC_MWG_MAXD * ORC_MWG_MAXD];
+            for (uint32_t j = 0; j < k; ++j)
+                for (uint32_t i = 0; i < k; ++i) S[i + (size_t)j * k] = mvS[(st + i) + (size_t)(st + j) * ORC_MWG_MAXD];
+            if (orc_cholesky(S, (int)k, Lk)) return -2;
+            for (uint32_t i = 0; i < k; ++i) {
+                u->mmu[st + i] = mvmu[st + i];
+                u->miL[st + i] = 1.0 / Lk[(size_t)i * k + i];
+                for (uint32_t m = 0; m <= i; ++m) u->mL[(size_t)(st + i) * ORC_MWG_MAXD + st + m] = Lk[(size_t)i * k + m];
+            }
+            u->fc[f] = mvnormal_c0((int)k, logdet_chol(Lk, (int)k));
         } else {
-            s = s + v;
+            const int rc = orc_prior_factor_consts(fam, fa[f], fb[f], &u->fa[f], &u->fb[f], &u->fc[f]);
+            if (rc) return rc == -4 ? -4 : -2;
         }
     }
-    return (u->prior == ORC_PRIOR_PRODUCT) ? lp + s : s;
+    return 0;
+}
+
+/* Test entry: logpdf(prior, x) for each of nx local vectors x (n entries each),
+ * from the same factor tables as orc_run_mwg (one update).  Returns the
+ * orc_build_prior status (0, −2 invalid, −4 a pairing the reference raises on). */
+ORC_EXPORT int orc_eval_prior(uint32_t prior, uint32_t n, uint32_t nfac, const uint32_t *ffam, const uint32_t *fcnt,
+                              const double *fa, const double *fb, const uint32_t *cfam, const double *ca,
+                              const double *cb, const double *mvmu, const double *mvS, uint64_t nx, const double *x,
+                              double *out) {
+    if (n < 1 || n > ORC_MWG_MAXD) return -2;
+    orc_mwg_update *u = (orc_mwg_update *)calloc(1, sizeof(orc_mwg_update));
+    if (!u) return -3;
+    u->nc = n;
+    u->prior = prior;
+    int rc = 0;
+    if (prior == ORC_PRIOR_PRODUCT || prior == ORC_PRIOR_STANDARD)
+        rc = orc_build_prior(u, nfac, ffam, fcnt, fa, fb, cfam, ca, cb, mvmu, mvS);
+    if (rc == 0)
+        for (uint64_t i = 0; i < nx; ++i) out[i] = orc_mwg_log_prior(u, n, x + i * n);
+    free(u);
+    return rc;
 }
 
 /* user target (EMCMC_TARGET_USER): loglikelihood(P°, obs) of a user function,
@@ -681,7 +849,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                            double *hist_ll, uint8_t *hist_acc, int nthreads, const uint32_t *prior_kind,
                            const uint32_t *nfac, const uint32_t *ffam, const uint32_t *fcnt, const double *fa,
                            const double *fb, double *ll_prop, orc_user_loglik_fn user_ll,
-                           const double *user_params) {
+                           const double *user_params, const uint32_t *pcfam, const double *pca, const double *pcb,
+                           const double *pmvmu, const double *pmvS) {
     if (D < 1 || D > ORC_MWG_MAXD || P < 1 || P > 64) return -2;
     (void)zig();
     orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
@@ -741,28 +910,14 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         }
         u->prior = prior_kind ? prior_kind[p] : ORC_PRIOR_IMPROPER;
         if (u->prior == ORC_PRIOR_PRODUCT || u->prior == ORC_PRIOR_STANDARD) {
-            uint32_t j = 0;
-            for (uint32_t f = 0; f < nfac[p]; ++f) {
-                const uint32_t fam = ffam[p * ORC_MWG_MAXD + f], cnt = fcnt[p * ORC_MWG_MAXD + f];
-                double a, b, cc;
-                if (cnt == 0 || j + cnt > u->nc ||
-                    orc_prior_factor_consts(fam, fa[p * ORC_MWG_MAXD + f], fb[p * ORC_MWG_MAXD + f], &a, &b, &cc)) {
-                    free(g);
-                    free(U);
-                    return -2;
-                }
-                if (u->prior == ORC_PRIOR_PRODUCT && j > 0) u->pstart |= 1u << j;
-                for (uint32_t k = 0; k < cnt; ++k, ++j) {
-                    u->pfam[j] = fam;
-                    u->pa[j] = a;
-                    u->pb[j] = b;
-                    u->pc[j] = cc;
-                }
-            }
-            if (j != u->nc) {
+            const size_t o = (size_t)p * ORC_MWG_MAXD;
+            const int prc = orc_build_prior(u, nfac[p], ffam + o, fcnt + o, fa + o, fb + o, pcfam ? pcfam + o : NULL,
+                                            pca ? pca + o : NULL, pcb ? pcb + o : NULL, pmvmu ? pmvmu + o : NULL,
+                                            pmvS ? pmvS + o * ORC_MWG_MAXD : NULL);
+            if (prc) {
                 free(g);
                 free(U);
-                return -2;
+                return prc;
             }
         }
     }
@@ -827,7 +982,7 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 }
                 if (u->prior == ORC_PRIOR_IMPROPER) break;
                 if (!(orc_mwg_log_prior(u, n, tp) == -INFINITY)) break;
-                if (rs >= ORC_MAX_RESAMPLE) {
+                if (rs >= (u->kind == 1 ? ORC_MAX_RESAMPLE : ORC_MAX_RESAMPLE_GSN)) {
                     f |= ORC_FAULT_PRIOR_RESAMPLES;
                     break;
                 }

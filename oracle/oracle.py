@@ -261,13 +261,18 @@ KIND_UNIFORM, KIND_GAUSSIAN = 1, 2
 
 PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
 DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
+DIST_LOGNORMAL, DIST_BETA, DIST_INVERSE_GAMMA, DIST_CAUCHY, DIST_LAPLACE, DIST_TDIST = 5, 6, 7, 8, 9, 10
+DIST_PRODUCT, DIST_MVNORMAL = 32, 33
 
 
 def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=PRIOR_IMPROPER, factors=None):
     """One RandomWalkUpdate for run_mwg.  coords0: 0-based coordinates.
     adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW).
     pos: None or per-coordinate positivity flags (UniformRandomWalk).
-    prior: PRIOR_*; factors: [(family, count, a, b), ...] for PRIOR_PRODUCT / PRIOR_STANDARD."""
+    prior: PRIOR_*; factors for PRIOR_PRODUCT / PRIOR_STANDARD, in constructor order, each
+    (family, 1, a, b) for a univariate, (DIST_PRODUCT, k, [(family, a, b), ...]) for a
+    Product of k univariates, (DIST_MVNORMAL, k, mu, Sigma) for an MvNormal; the count is
+    the factor's `dims` entry (ProductPrior(dists, dims), priors.jl:64-79)."""
     return {"kind": kind, "coords": [int(c) for c in coords0], "eps": None if eps is None else list(eps),
             "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt,
             "pos": None if pos is None else [bool(x) for x in pos], "prior": int(prior),
@@ -330,6 +335,9 @@ def _mwg_tables(updates):
 
 
 def _prior_tables(updates):
+    """Flat prior tables of orc_run_mwg: factors (ffam, fcnt, fa, fb), Product
+    components (cfam, ca, cb, consecutively in factor order) and MvNormal μ / Σ
+    placed at the local range the factor reads (the constructor's `last`)."""
     P = len(updates)
     pk = np.zeros(P, dtype=np.uint32)
     nf = np.zeros(P, dtype=np.uint32)
@@ -337,13 +345,55 @@ def _prior_tables(updates):
     fcnt = np.zeros((P, MWG_MAXD), dtype=np.uint32)
     fa = np.zeros((P, MWG_MAXD))
     fb = np.zeros((P, MWG_MAXD))
+    cfam = np.zeros((P, MWG_MAXD), dtype=np.uint32)
+    ca = np.zeros((P, MWG_MAXD))
+    cb = np.zeros((P, MWG_MAXD))
+    mvmu = np.zeros((P, MWG_MAXD))
+    mvS = np.zeros((P, MWG_MAXD, MWG_MAXD))  # [p][col][row]: column-major 64 × 64 blocks
     for p, u in enumerate(updates):
         pk[p] = u.get("prior", PRIOR_IMPROPER)
         fs = u.get("factors", [])
         nf[p] = len(fs)
-        for k, (fam, cnt, a, b) in enumerate(fs):
-            ffam[p, k], fcnt[p, k], fa[p, k], fb[p, k] = fam, cnt, a, b
-    return pk, nf, ffam, fcnt, fa, fb
+        last, nc = 0, 0
+        for k, f in enumerate(fs):
+            fam, cnt = int(f[0]), int(f[1])
+            ffam[p, k], fcnt[p, k] = fam, cnt
+            st = 0 if cnt == 1 else last
+            last += cnt
+            if fam == DIST_PRODUCT:
+                for (cf, a, b) in f[2]:
+                    cfam[p, nc], ca[p, nc], cb[p, nc] = cf, a, b
+                    nc += 1
+            elif fam == DIST_MVNORMAL:
+                mu = np.asarray(f[2], dtype=np.float64).reshape(cnt)
+                S = np.asarray(f[3], dtype=np.float64).reshape(cnt, cnt)
+                mvmu[p, st:st + cnt] = mu
+                mvS[p, st:st + cnt, st:st + cnt] = S.T  # [col][row]
+            else:
+                fa[p, k], fb[p, k] = f[2], f[3]
+    return pk, nf, ffam, fcnt, fa, fb, cfam, ca, cb, mvmu, mvS
+
+
+def eval_prior(prior, n, factors, x):
+    """logpdf(prior, x) of one update's prior (orc_eval_prior) at each row of x
+    ([m][n]); factors as in mwg_update.  Raises ValueError with the oracle's
+    status (−2 invalid, −4 a pairing the reference raises a MethodError on)."""
+    L = lib()
+    if not hasattr(L, "_evp_ready"):
+        dp, u32p = C.POINTER(C.c_double), C.POINTER(C.c_uint32)
+        L.orc_eval_prior.restype = C.c_int
+        L.orc_eval_prior.argtypes = [C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p, dp, dp, u32p, dp, dp, dp, dp,
+                                     C.c_uint64, dp, dp]
+        L._evp_ready = True
+    pk, nf, ffam, fcnt, fa, fb, cfam, ca, cb, mvmu, mvS = _prior_tables([{"prior": prior, "factors": factors or []}])
+    x = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1, n))
+    out = np.empty(x.shape[0])
+    u32 = lambda a: a.ctypes.data_as(C.POINTER(C.c_uint32))  # noqa: E731
+    rc = L.orc_eval_prior(int(prior), n, int(nf[0]), u32(ffam), u32(fcnt), _d(fa), _d(fb), u32(cfam), _d(ca),
+                          _d(cb), _d(mvmu), _d(mvS), x.shape[0], _d(x), _d(out))
+    if rc != 0:
+        raise ValueError(f"orc_eval_prior: {rc}")
+    return out
 
 
 USER_LL_FN = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_uint64,
@@ -363,11 +413,11 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         L.orc_run_mwg.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, u32p, u32p, u32p, dp, dp,
                                   u8p, u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
                                   u64p, u32p, dp, dp, dp, dp, u64p, u32p, u32p, u32p, dp, u32p, dp, dp, dp, u8p,
-                                  C.c_int, u32p, u32p, u32p, u32p, dp, dp, dp, C.c_void_p, dp]
+                                  C.c_int, u32p, u32p, u32p, u32p, dp, dp, dp, C.c_void_p, dp, u32p, dp, dp, dp, dp]
         L._mwg_ready = True
     Cn, D = state.C, state.D
     kind, nc, coords, eps, sigma, adapt, ak, ap, pos = _mwg_tables(updates)
-    pk, nf, ffam, fcnt, fa, fb = _prior_tables(updates)
+    pk, nf, ffam, fcnt, fa, fb, cfam, ca, cb, mvmu, mvS = _prior_tables(updates)
     if getattr(state, "ll_prop", None) is None:
         state.ll_prop = np.full((len(updates), state.C), np.nan)
     up = None if user_params is None else np.ascontiguousarray(user_params, dtype=np.float64)
@@ -394,7 +444,8 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         _d(hist.get("theta")), _d(hist.get("prop")), _d(hist.get("ll")),
         None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads,
         u32(pk), u32(nf), u32(ffam), u32(fcnt), _d(fa), _d(fb), _d(state.ll_prop),
-        None if user_ll is None else C.cast(user_ll, C.c_void_p), None if up is None else _d(up))
+        None if user_ll is None else C.cast(user_ll, C.c_void_p), None if up is None else _d(up),
+        u32(cfam), _d(ca), _d(cb), _d(mvmu), _d(mvS))
     if rc != 0:
         raise ValueError(f"orc_run_mwg failed: {rc}")
     if history:

@@ -167,6 +167,16 @@ static inline double orc_log_any(double x) {
     return orc_log(x);
 }
 
+/* log(1 + y) — emcmc_math.h log1p_any: log u − ((u − 1) − y)/u with u = 1 + y;
+ * −Inf at y = −1, NaN below */
+static inline double orc_log1p_any(double y) {
+    const double u = 1.0 + y;
+    if (!(u >= 0.0)) return NAN;
+    if (u == 0.0) return -INFINITY;
+    if (u == INFINITY) return u;
+    return orc_log_any(u) - ((u - 1.0) - y) / u;
+}
+
 /* ---- table-driven exp (x <= 0) and log (1 <= u <= 2) of the MALA logistic
  * terms.  exp: x = k·ln2/64 + r (Cody–Waite), e^x = 2^floor(k/64) ·
  * 2^((k mod 64)/64) · (1 + (e^r − 1)), e^r − 1 to degree 6, scaled by ldexp.

@@ -26,9 +26,11 @@ adapt = {"k": 5, "target": 0.234, "scale": [0.1, 0.2], "min": [1e-12, 1e-3], "ma
          "offset": [1.0, 2.0]}
 ups = [O.mwg_update(1, [0, 1], eps=[0.3, 0.2], adapt=adapt, pos=[True, False]),
        O.mwg_update(2, [2, 3], sigma=[[0.1, 0.02], [0.02, 0.1]], pos=[False, True], prior=O.PRIOR_PRODUCT,
-                    factors=[(1, 1, 0.0, 2.0), (4, 1, 2.0, 1.0)])]
-st = O.MWGState(np.full((5, 4), 0.5), np.zeros(4), ups)
-O.run_mwg(st, ups, seed=4, t_sigma=np.eye(4), obs=rng.normal(size=(6, 4)), steps=[(i, p) for i in range(1, 31) for p in (1, 2)])
+                    factors=[(32, 2, [(1, 0.0, 2.0), (4, 2.0, 1.0)])]),
+       O.mwg_update(2, [4, 5, 6], sigma=0.1 * np.eye(3), prior=O.PRIOR_PRODUCT,
+                    factors=[(1, 1, 0.0, 2.0), (33, 2, [0.0, 0.0], [[1.0, 0.3], [0.3, 1.0]])])]
+st = O.MWGState(np.full((5, 7), 0.5), np.zeros(7), ups)
+O.run_mwg(st, ups, seed=4, t_sigma=np.eye(7), obs=rng.normal(size=(6, 7)), steps=[(i, p) for i in range(1, 31) for p in (1, 2, 3)])
 ups64 = [O.mwg_update(2, range(0, 40), sigma=0.01 * np.eye(40)), O.mwg_update(2, range(40, 64), sigma=0.01 * np.eye(24))]
 st = O.MWGState(np.zeros((3, 64)), np.zeros(64), ups64)
 O.run_mwg(st, ups64, seed=5, t_sigma=np.eye(64), obs=rng.normal(size=(4, 64)), steps=[(i, p) for i in range(1, 11) for p in (1, 2)])

@@ -239,7 +239,7 @@ def test_d64_general_kernel_blocks_and_dense(oracle):
     """D = 64 on the general kernel (compiled at run time): a diagonal Gaussian
     block of 16, a correlated Gaussian block of 40 (five canonical 8-blocks: the
     run-time tree 5 → 3 → 2 → 1) and a UniformRandomWalk block of 8 with a
-    Normal ProductPrior, against a dense D = 64 target."""
+    ProductPrior([Product(fill(Normal, 8))], [8]), against a dense D = 64 target."""
     rng = np.random.default_rng(9)
     D, C, M = 64, 700, 120
     A = rng.standard_normal((D, D))
@@ -251,7 +251,7 @@ def test_d64_general_kernel_blocks_and_dense(oracle):
     ups = [oracle.mwg_update(2, range(0, 16), sigma=0.01 * np.eye(16)),
            oracle.mwg_update(2, range(16, 56), sigma=S40),
            oracle.mwg_update(1, range(56, 64), eps=[0.05] * 8, prior=L.PRIOR_PRODUCT,
-                             factors=[(L.DIST_NORMAL, 8, 0.0, 3.0)])]
+                             factors=[(L.DIST_PRODUCT, 8, [(L.DIST_NORMAL, 0.0, 3.0)] * 8)])]
     steps = full_steps(M, 3)
     eng, st, h = run_both(oracle, D, C, M, ups, mu, ts, obs, steps, 31)
     assert "D=64" in eng.kernel_name()
@@ -267,7 +267,7 @@ def test_d48_block_of_48(oracle):
     mu = rng.normal(size=D)
     obs = mu + rng.normal(size=(5, D))
     ups = [oracle.mwg_update(2, range(D), sigma=0.004 * np.eye(D), pos=[False] * D, prior=L.PRIOR_PRODUCT,
-                             factors=[(L.DIST_NORMAL, D, 0.0, 10.0)])]
+                             factors=[(L.DIST_PRODUCT, D, [(L.DIST_NORMAL, 0.0, 10.0)] * D)])]
     steps = full_steps(M, 1)
     eng, st, h = run_both(oracle, D, C, M, ups, mu, np.eye(D), obs, steps, 32)
     check(oracle, eng, st, h, steps, ups, 1)

@@ -54,7 +54,7 @@ def test_student_t_joint_gaussian_walk(oracle):
 def test_poisson_dense_sigma_with_normal_prior(oracle):
     case = U.poisson()
     S = np.array([[0.010, 0.002, 0.0], [0.002, 0.008, -0.001], [0.0, -0.001, 0.012]])
-    fac = [(L.DIST_NORMAL, case.D, 0.0, 10.0)]
+    fac = [(L.DIST_PRODUCT, case.D, [(L.DIST_NORMAL, 0.0, 10.0)] * case.D)]
     ups = [oracle.mwg_update(2, range(case.D), sigma=S, prior=L.PRIOR_PRODUCT, factors=fac)]
     steps = full_steps(250, 1)
     eng, st, h = run_user(oracle, case, ups, steps, 1537, 250, spl=37)

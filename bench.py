@@ -299,11 +299,13 @@ def main():
     traffic = None
     pmc = ROOT / "profiles" / "pmc_traffic.json"
     kname = eng.kernel_name()
-    if pmc.exists():
+    traffic_src = None
+    if pmc.exists():  # measured HBM bytes per launch of this kernel at this launch length and chain count
         try:
-            tb = json.loads(pmc.read_text()).get(kname)
-            if tb:
-                traffic = tb["bytes_per_chain_step"] * Cg * (a.steps / launches)
+            tb = json.loads(pmc.read_text()).get(kname, {}).get("by_steps_per_launch", {})
+            e = tb.get(str(int(round(a.steps / launches))))
+            if e and e.get("chains") == Cg:
+                traffic, traffic_src = e["traffic_per_launch"], e["source"]
         except Exception:
             traffic = None
 
@@ -358,6 +360,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": kname,
             "algorithmic_bytes_per_launch": bytes_per_launch,
             "avg_launch_ms": avg_launch_s * 1e3,

@@ -110,6 +110,9 @@ struct UpdateHost {
     emcmc_haario_adaptation haario{};
     emcmc_lambda_fn flam = nullptr;  // HaarioTypeAdaptation fλ (host callback; nullptr = identity)
     void *flam_ctx = nullptr;
+    // EMCMC_USER_UPDATE: the source (shared by the handle's user updates) and parameters
+    std::string usrc, uopts;
+    std::vector<double> uparams;
     // prior (priors.jl) as MwgUpdate term slots (emcmc_mwg.h): per slot a family,
     // its parameters and host constant; MvNormal rows; factor boundaries
     uint32_t nslot = 0;
@@ -372,8 +375,11 @@ emcmc_status select_mwg(emcmc_handle *h) {
     for (const auto &u : h->updates) nmax = std::max(nmax, u.coords.size());
     int best_nu = 1 << 30;
     const bool user = h->target.kind == EMCMC_TARGET_USER;
+    std::string usrc, uopts;  // a user update's source: compiled into the same kernel
+    for (const auto &u : h->updates)
+        if (u.kernel == EMCMC_USER_UPDATE) usrc = u.usrc, uopts = u.uopts;
     for (const auto &e : mwg_table()) {
-        if (user) break;
+        if (user || !usrc.empty()) break;
         if (e.D != D) continue;
         if (e.nu != 0 && ((size_t)e.nu < nmax || e.nu >= best_nu)) continue;  // smallest NU that fits
         if (e.nu != 0) best_nu = e.nu;
@@ -382,14 +388,16 @@ emcmc_status select_mwg(emcmc_handle *h) {
     }
     // a user law, or a dimension without an ahead-of-time instantiation: the
     // same kernel compiled at run time (emcmc_rtc.hip, cached per process)
-    if (user || (!v.mfn && D <= kMwgMaxD)) {
+    if (user || !usrc.empty() || (!v.mfn && D <= kMwgMaxD)) {
         RtcKernel k;
         const int nu = rtc_wide_nu(D, (int)nmax);
-        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k)
-                                     : rtc_compile_gsn(D, full, ll, nu, k);
+        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k, usrc, uopts)
+                                     : rtc_compile_gsn(D, full, ll, nu, k, usrc, uopts);
         if (!log.empty()) {
-            h->err = std::string(user ? "user target does not compile:\n" : "run-time kernel build failed:\n") + log;
-            return user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
+            h->err = std::string(user || !usrc.empty() ? "user target / update does not compile:\n"
+                                                        : "run-time kernel build failed:\n") +
+                     log;
+            return (user || !usrc.empty()) ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
         }
         const std::string key = k.name + '|' + k.lowered + '|' + std::to_string(std::hash<std::string>{}(
                                     std::string(k.code.begin(), k.code.end())));
@@ -417,7 +425,9 @@ emcmc_status select_mwg(emcmc_handle *h) {
         m.nc = (uint32_t)u.coords.size();
         m.adapt = u.adaptation;
         for (uint32_t j = 0; j < m.nc; ++j) m.coords[j] = u.coords[j];
-        if (u.kernel == EMCMC_RW_UNIFORM) {
+        if (u.kernel == EMCMC_USER_UPDATE) {
+            for (size_t q = 0; q < u.uparams.size(); ++q) m.L[q] = u.uparams[q];
+        } else if (u.kernel == EMCMC_RW_UNIFORM) {
             for (uint32_t j = 0; j < m.nc; ++j) m.eps0[j] = u.eps[j];
             for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1ull << j) : 0ull;
             if (u.adaptation == EMCMC_ADPT_UNIF_RW) {
@@ -1379,8 +1389,24 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
             if (u->coords[j] == u->coords[i]) return fail(h, EMCMC_INVALID_ARG, "repeated coord %u", u->coords[i]);
     }
     if (u->kernel != EMCMC_RW_GAUSSIAN && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN_MIX &&
-        u->kernel != EMCMC_MALA)
+        u->kernel != EMCMC_MALA && u->kernel != EMCMC_USER_UPDATE)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "transition kernel %u has no device plugin yet", u->kernel);
+    if (u->kernel == EMCMC_USER_UPDATE) {
+        const emcmc_user_update_desc *ud = u->user_update;
+        if (!ud || !ud->source) return fail(h, EMCMC_INVALID_ARG, "user update: needs user_update->source");
+        if (ud->num_params > (uint64_t)kMwgMaxD * kMwgMaxD || (ud->num_params && !ud->params))
+            return fail(h, EMCMC_INVALID_ARG, "user update: params (≤ %d doubles)", kMwgMaxD * kMwgMaxD);
+        if (u->adaptation != EMCMC_ADPT_NONE)
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "user update: adaptation has no device plugin");
+        if (h->cfg.dim > (uint32_t)kMwgMaxD)
+            return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "user update: D=%u > %d (general schedule kernel)", h->cfg.dim,
+                        kMwgMaxD);
+        for (const auto &o : h->updates)
+            if (o.kernel == EMCMC_USER_UPDATE &&
+                (o.usrc != ud->source || o.uopts != (ud->options ? ud->options : "")))
+                return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                            "user updates of one handle share one source (dispatch on params to combine several)");
+    }
     if (u->prior > EMCMC_PRIOR_STANDARD)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin", u->prior);
     if (u->prior != EMCMC_PRIOR_IMPROPER && (u->kernel == EMCMC_RW_GAUSSIAN_MIX || u->kernel == EMCMC_MALA))
@@ -1411,7 +1437,12 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     if (u->prior == EMCMC_PRIOR_PRODUCT || u->prior == EMCMC_PRIOR_STANDARD)
         if (emcmc_status st = build_prior_slots(h, u, uh)) return st;
     const int n = (int)u->num_coords;
-    if (u->kernel == EMCMC_RW_GAUSSIAN || u->kernel == EMCMC_RW_GAUSSIAN_MIX) {
+    if (u->kernel == EMCMC_USER_UPDATE) {
+        const emcmc_user_update_desc *ud = u->user_update;
+        uh.usrc = ud->source;
+        uh.uopts = ud->options ? ud->options : "";
+        if (ud->num_params) uh.uparams.assign(ud->params, ud->params + ud->num_params);
+    } else if (u->kernel == EMCMC_RW_GAUSSIAN || u->kernel == EMCMC_RW_GAUSSIAN_MIX) {
         if (!u->sigma) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalk needs Σ");
         uh.sigma.assign(u->sigma, u->sigma + (size_t)n * n);
         if (!cholesky_upper_colmajor(uh.sigma.data(), n, uh.L))
@@ -1619,6 +1650,19 @@ emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const cha
     return log.empty() ? EMCMC_OK : EMCMC_INVALID_ARG;
 }
 
+emcmc_status emcmc_check_user_update(const char *source, uint32_t dim, const char *options, char *log_out,
+                                     size_t log_len) {
+    if (!source) return EMCMC_INVALID_ARG;
+    RtcKernel k;
+    const std::string log = rtc_compile_gsn((int)dim, true, 0, (int)dim, k, source, options ? options : "");
+    if (log_out && log_len) {
+        const size_t n = std::min(log.size(), log_len - 1);
+        std::memcpy(log_out, log.data(), n);
+        log_out[n] = '\0';
+    }
+    return log.empty() ? EMCMC_OK : EMCMC_INVALID_ARG;
+}
+
 emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {
     if (!h || !theta) return EMCMC_INVALID_ARG;
     emcmc_status st = ensure_alloc(h);
@@ -1733,6 +1777,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     p.S_c = t.S_c;
     p.nobs_d = (double)t.nobs;
     p.rcp_W = 1.0 / (double)h->cfg.roll_window;
+    p.xcd = (h->cfg.kernel_variant & EMCMC_VARIANT_NO_XCD_ORDER) ? 0u : 1u;
     const uint64_t K = h->cfg.steps_per_launch;
     uint64_t i = 0;
     while (i < num_steps) {

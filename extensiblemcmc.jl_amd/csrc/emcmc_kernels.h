@@ -65,7 +65,7 @@ struct StepParams {
     uint32_t P;           // number of updates
     uint32_t W;           // roll window (≤ 128)
     uint32_t nobs;
-    uint32_t _pad;
+    uint32_t xcd;         // 1: XCD-aware block order (xcd_block), 0: blockIdx order
     uint64_t N0;          // GenericChainStats.N before the first step of this launch
     double rw_c0;         // −(D·log2π + logdet Σ_rw)/2
     double t_c0;          // −(D·log2π + logdet Σ_t)/2
@@ -628,6 +628,19 @@ __device__ __forceinline__ T &chain_elem(T *base, uint32_t c) {
     return *reinterpret_cast<T *>(reinterpret_cast<char *>(base) + c * (uint32_t)sizeof(T));
 }
 
+// XCD-aware block order (cdna_hip_programming.md §5 T1).  Blocks are dealt
+// round-robin over the 8 XCDs (block b on the XCD of b mod 8); block b runs the
+// work of block x·q + min(x, r) + b/8 (x = b mod 8, q = nwg/8, r = nwg mod 8),
+// so each XCD sweeps one contiguous eighth of the chains.  A step's history
+// stores then touch each slot's pages from one XCD instead of all eight: each
+// XCD's L2 TLB translates 1/8 of the ≈34 MB a step writes.  Bijective for any
+// nwg; speed only (every chain's results are keyed by its id).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nwg, uint32_t enable) {
+    if (!enable) return b;
+    const uint32_t q = nwg >> 3, r = nwg & 7u, x = b & 7u;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 // MINW = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
 template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1>
@@ -643,7 +656,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
     const double *cst0 = lds;
 
-    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t tid = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x;
     const uint64_t chain = tid / LPC;
     const int sub = (int)(tid % LPC);
     if (chain >= a.C) return;
@@ -815,7 +828,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_dense_kernel(const StepParams a) 
     const double *xbar = cst + 2 * D * D + 2 * D;
     const double *X = cst + 2 * D * D + 3 * D;
 
-    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t chain = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
 
@@ -1090,7 +1103,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     constexpr int P = D * (D + 1) / 2;
 
-    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t chain = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
     const uint64_t C = a.C;
@@ -1218,7 +1231,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_diag_s_kernel(const StepParams a)
     const ZigTabs zt = stage_lds(lds, a.zig, a.consts, 4 * D, nullptr, 0);
     const double *cst0 = lds;
 
-    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t chain = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x;
     if (chain >= a.C) return;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
     const uint64_t C = a.C;

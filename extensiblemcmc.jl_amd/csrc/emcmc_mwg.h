@@ -39,6 +39,9 @@
 //                       lp(θ°) − lp(θ)                 priors.jl:18-88, run.jl:374-385
 //   loglikelihood       a target policy: GsnTargetLaw (gsn_target.jl:23-29) or a
 //                       user device function compiled at run time (emcmc_rtc.h)
+//   user updates        an update policy: a user's proposal! and log_transition_density
+//                       (updates.jl:42-93) compiled at run time; draws come from the
+//                       engine's stream by index (UserRng)
 #pragma once
 
 #include "emcmc_kernels.h"
@@ -57,7 +60,10 @@ constexpr uint32_t kPriorImproper = 0u, kPriorImproperPos = 1u, kPriorProduct = 
 constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, kDistGamma = 4u, kDistLogNormal = 5u,
                    kDistBeta = 6u, kDistInverseGamma = 7u, kDistCauchy = 8u, kDistLaplace = 9u, kDistTDist = 10u;
 
-// One RandomWalkUpdate, host-built; read with scalar (uniform) loads.
+// update kinds (include/emcmc.h): EMCMC_RW_UNIFORM 1, EMCMC_RW_GAUSSIAN 2, a user update 5
+constexpr uint32_t kKindUser = 5u;
+
+// One RandomWalkUpdate (or user update), host-built; read with scalar (uniform) loads.
 struct MwgUpdate {
     uint32_t kind;    // EMCMC_RW_UNIFORM (1) / EMCMC_RW_GAUSSIAN (2)
     uint32_t nc;      // number of coordinates
@@ -65,7 +71,8 @@ struct MwgUpdate {
     uint32_t k;       // adapt_every_k_steps
     uint32_t coords[kMwgMaxD];
     double eps0[kMwgMaxD];          // UniformRandomWalk ϵ (initial for adaptive updates)
-    double L[kMwgMaxD * kMwgMaxD];  // GaussianRandomWalk: lower Cholesky factor, row-major, local indices
+    double L[kMwgMaxD * kMwgMaxD];  // GaussianRandomWalk: lower Cholesky factor, row-major, local indices;
+                                    // a user update: its parameters (≤ 4096 doubles)
     double iL[kMwgMaxD];            // 1 / L_ii
     double c0;                      // −(nc·log2π + logdet Σ)/2
     uint32_t diag, reserved0;
@@ -325,18 +332,66 @@ struct GsnTarget {
     }
 };
 
+// ---- user updates (EMCMC_USER_UPDATE; emcmc_rtc.hip compiles the source) -----
+// The draws a user proposal! makes come from the engine's counter-based stream,
+// indexed, so the oracle (oracle/user_prelude.h) reproduces them: em_randn(j) is
+// normal j of (chain, mcmciter, update) — the index space of the random walks'
+// normals, blocks j/2 — and em_rand(j) the uniform [0, 1) from words (x, y) or
+// (z, w) of block 2^31 + j/2, a range no other draw of the update uses.
+struct UserRng {
+    ZigTabs zt;
+    uint32_t key0, key1, gid, iter, p;
+    uint32_t faults;
+};
+__device__ __forceinline__ double user_randn(UserRng &r, uint32_t j) {
+    return normal_draw(r.zt, r.key0, r.key1, r.gid, r.iter, r.p, j & 0x3FFFFFFFu, r.faults);
+}
+__device__ __forceinline__ double user_rand(const UserRng &r, uint32_t j) {
+    const u32x4 w = draw(r.key0, r.key1, r.gid, r.iter, 0x80000000u | ((j & 0x3FFFFFFFu) >> 1), r.p, 0);
+    return (j & 1u) ? u01_closed0(w.z, w.w) : u01_closed0(w.x, w.y);
+}
+// no user update in this kernel: the branch compiles away
+struct NoUserUpdate {
+    static constexpr bool kEnabled = false;
+    __device__ __forceinline__ static void propose(UserRng &, const double *, double *, int, const double *) {}
+    __device__ __forceinline__ static double ltd(const double *, const double *, int, const double *) { return 0.0; }
+};
+
 // ---- one update step on the update's local coordinates (shared by both kernels)
 // proposal! with resampling, log_transition_density both ways, and the two
 // log-priors of the MH ratio.  tl: θ_local in (pos Gaussian: left as the
 // reference's in-place round trips leave it); tp: θ° (proposal history, P°);
 // ta: θ° as set_chain_param! copies it on accept.
-template <int NU, bool ROLL = false>
+template <int NU, bool ROLL = false, class UPD = NoUserUpdate>
 __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs &zt, const MwgUpdate &u, uint32_t n,
                                                uint64_t chain, uint32_t gid, uint32_t iter, uint32_t p,
                                                double (&tl)[NU], double (&tp)[NU], double (&ta)[NU], double &ltd_fwd,
                                                double &ltd_rev, double &lpp, double &lpc, uint32_t &faults) {
     constexpr int UJ = ROLL ? 1 : NU;
     const uint64_t C = a.C;
+    if constexpr (UPD::kEnabled) {
+        if (u.kind == kKindUser) {  // wave-uniform: the update's kind
+            // proposal!(updt, …) and log_transition_density(updt, θ, θ°) of the user's
+            // update (updates.jl:42-93); the prior enters the ratio as for any update
+            // (run.jl:374-385), proposal! has no redraw loop unless the user writes one
+            UserRng rng{zt, a.key0, a.key1, gid, iter, p, 0u};
+#pragma unroll UJ
+            for (int j = 0; j < NU; ++j) tp[j] = 0.0;
+            UPD::propose(rng, tl, tp, (int)n, u.L);
+            faults |= rng.faults;
+            ltd_fwd = UPD::ltd(tl, tp, (int)n, u.L);  // log_transition_density(__PREVIOUS): (θ, θ°)
+            ltd_rev = UPD::ltd(tp, tl, (int)n, u.L);  // log_transition_density(__PROPOSAL): (θ°, θ)
+#pragma unroll UJ
+            for (int j = 0; j < NU; ++j) ta[j] = tp[j];
+            lpp = 0.0;
+            lpc = 0.0;
+            if (u.prior != kPriorImproper) {
+                lpp = mwg_log_prior<NU, ROLL>(u, n, tp);
+                lpc = mwg_log_prior<NU, ROLL>(u, n, tl);
+            }
+            return;
+        }
+    }
     double t3[NU];  // θ as log_prior(::Previous) sees it (pos GaussianRandomWalk: after the round trips)
     // ---- proposal!: draw θ°; draw again while logpdf(prior, θ°) === −Inf
     // (updates.jl:191-196).  Resample r reads counter blocks (r << 16) | j/2.
@@ -547,7 +602,7 @@ __device__ __forceinline__ void mwg_register_step(const MwgParams &a, const MwgU
 
 // One lane per chain; θ and P°.θ in registers, coordinates moved between global
 // and update-local order by selects over the compile-time D (D ≤ 16).
-template <int D, bool FULL, int LLMODE, class TGT = GsnTarget>
+template <int D, bool FULL, int LLMODE, class TGT = GsnTarget, class UPD = NoUserUpdate>
 __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
     static_assert(D <= 16, "register-state MWG kernel: D ≤ 16 (mwg_wide_kernel below for larger D)");
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
@@ -584,7 +639,8 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
             tl[j] = v;
         }
         double ltd_fwd, ltd_rev, lpp, lpc;
-        mwg_local_step<D>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
+        mwg_local_step<D, false, UPD>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
+                                      faults);
         // ---- set_proposal!: proposal history and P°.θ[coords] ← θ°
         double prop[D], nst[D];
 #pragma unroll
@@ -642,7 +698,7 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 // wave-uniform indices, so no select network over D is needed; only the
 // update's NU-sized local vectors and, for the likelihood, P°.θ live in
 // registers.  The arithmetic is mwg_gsn_kernel's.
-template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget>
+template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget, class UPD = NoUserUpdate>
 __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
     static_assert(NU <= D && D <= kMwgMaxD, "NU ≤ D ≤ 64");
     // loops over the update's NU coordinates and over the target's D stay rolled
@@ -667,7 +723,7 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
         double tl[NU], tp[NU], ta[NU];
         for (int j = 0; j < NU; ++j) tl[j] = ((uint32_t)j < n) ? a.theta[state_pos(u.coords[j], chain, C, D)] : 0.0;
         double ltd_fwd, ltd_rev, lpp, lpc;
-        mwg_local_step<NU, RU>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
+        mwg_local_step<NU, RU, UPD>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
         // ---- set_proposal!: P°.θ[coords] ← θ°, then all of P°.θ for the likelihood
         for (int j = 0; j < NU; ++j)
             if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tp[j];

@@ -37,8 +37,10 @@ struct RtcKernel {
 // has ≤ 16 coordinates — unrolled, in registers — else NU = D).  Returns "" on
 // success, else the compiler's log.
 int rtc_wide_nu(int D, int nmax);
+// usrc / uopts: a user update's EMCMC_USER_PROPOSAL + EMCMC_USER_LTD source (empty: none)
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
-                             RtcKernel &out);
+                             RtcKernel &out, const std::string &usrc = std::string(),
+                             const std::string &uopts = std::string());
 
 // The text of a law the library ships as an EMCMC_USER_LOGLIK source
 // (csrc/laws/<name>), or nullptr.
@@ -46,6 +48,7 @@ const char *rtc_builtin_law(const char *name);
 
 // The same kernel with the built-in GsnTargetLaw (emcmc_mwg.h GsnTarget) for a
 // dimension the library has no ahead-of-time instantiation of (inst_mwg.hip).
-std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out);
+std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out,
+                            const std::string &usrc = std::string(), const std::string &uopts = std::string());
 
 }  // namespace emcmc

@@ -27,9 +27,17 @@ const char *const kPrelude = R"EMCMC_RTC(#include "emcmc_mwg.h"
     extern "C" __device__ __attribute__((always_inline)) inline double emcmc_user_loglik(                 \
         const double *__restrict__ theta, int D, const double *__restrict__ obs, uint64_t nobs,            \
         const double *__restrict__ params)
+#define EMCMC_USER_PROPOSAL                                                                                \
+    extern "C" __device__ __attribute__((always_inline)) inline void emcmc_user_proposal(                 \
+        const double *__restrict__ theta, double *__restrict__ theta_prop, int n,                          \
+        const double *__restrict__ params, emcmc::UserRng *__restrict__ rng)
+#define EMCMC_USER_LTD                                                                                     \
+    extern "C" __device__ __attribute__((always_inline)) inline double emcmc_user_ltd(                    \
+        const double *__restrict__ x, const double *__restrict__ y, int n, const double *__restrict__ params)
 #define em_exp(x) emcmc::exp_any(x)
 #define em_log(x) emcmc::log_real(x)
-#line 1 "user_target"
+#define em_randn(j) emcmc::user_randn(*rng, (uint32_t)(j))
+#define em_rand(j) emcmc::user_rand(*rng, (uint32_t)(j))
 )EMCMC_RTC";
 
 const char *const kEpilogue = R"EMCMC_RTC(
@@ -39,6 +47,22 @@ struct UserTarget {
     template <int D, int LLMODE, bool ROLL = false>
     __device__ __forceinline__ static double loglik(const MwgParams &a, const double (&mp)[D]) {
         return emcmc_user_loglik(mp, D, a.obs, (uint64_t)a.nobs, a.user_params);
+    }
+};
+}  // namespace emcmc
+)EMCMC_RTC";
+
+const char *const kUpdEpilogue = R"EMCMC_RTC(
+namespace emcmc {
+// proposal! / log_transition_density of the user's update (updates.jl:42-93)
+struct UserUpdate {
+    static constexpr bool kEnabled = true;
+    __device__ __forceinline__ static void propose(UserRng &rng, const double *th, double *tp, int n,
+                                                   const double *params) {
+        emcmc_user_proposal(th, tp, n, params, &rng);
+    }
+    __device__ __forceinline__ static double ltd(const double *x, const double *y, int n, const double *params) {
+        return emcmc_user_ltd(x, y, n, params);
     }
 };
 }  // namespace emcmc
@@ -62,12 +86,12 @@ std::string program_log(hiprtcProgram p) {
 int rtc_wide_nu(int D, int nmax) { return (D > 16 && nmax <= 16) ? 16 : D; }
 
 std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
-                        RtcKernel &out) {
+                        RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string()) {
     if (D < 1 || D > 64) return "the general schedule kernel runs 1 ≤ D ≤ 64";
     if (nu < 1 || nu > D) nu = D;
-    const bool user = !src.empty();
+    const bool user = !src.empty(), upd = !usrc.empty();
     std::ostringstream key;
-    key << D << '|' << nu << '|' << full << '|' << ll << '|' << opts << '|' << src;
+    key << D << '|' << nu << '|' << full << '|' << ll << '|' << opts << '|' << src << '|' << uopts << '|' << usrc;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_cache.find(key.str());
@@ -79,27 +103,30 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     std::ostringstream expr, name;
     const char *fl = full ? "true" : "false";
     const char *tgt = user ? "emcmc::UserTarget" : "emcmc::GsnTarget";
+    const char *ut = upd ? "emcmc::UserUpdate" : "emcmc::NoUserUpdate";
     if (D <= 16) {
-        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ">";
+        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ", " << ut << ">";
         name << "mwg_gsn_kernel<D=" << D;
     } else {
-        expr << "emcmc::mwg_wide_kernel<" << D << ", " << nu << ", " << fl << ", " << ll << ", " << tgt << ">";
+        expr << "emcmc::mwg_wide_kernel<" << D << ", " << nu << ", " << fl << ", " << ll << ", " << tgt << ", " << ut
+             << ">";
         name << "mwg_wide_kernel<D=" << D << ",NU=" << nu;
     }
     name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
-         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << "[hiprtc]>";
-    const std::string prog_src =
-        user ? std::string(kPrelude) + src + "\n" + kEpilogue : std::string("#include \"emcmc_mwg.h\"\n");
+         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << (upd ? ",UserUpdate" : "") << "[hiprtc]>";
+    std::string prog_src = std::string(kPrelude);
+    if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
+    if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, prog_src.c_str(), user ? "user_target.hip" : "gsn_target.hip", kRtcHeaderCount,
-                            kRtcHeaderSrc, kRtcHeaderNames) != HIPRTC_SUCCESS)
+    if (hiprtcCreateProgram(&prog, prog_src.c_str(), user ? "user_target.hip" : upd ? "user_update.hip" : "gsn_target.hip",
+                            kRtcHeaderCount, kRtcHeaderSrc, kRtcHeaderNames) != HIPRTC_SUCCESS)
         return "hiprtcCreateProgram failed";
     const std::string ex = expr.str();
     hiprtcAddNameExpression(prog, ex.c_str());
     // -ffp-contract=off: the parity contract with oracle/ (no implicit fma)
     std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
-    {
-        std::istringstream is(opts);
+    for (const std::string *op : {&opts, &uopts}) {
+        std::istringstream is(*op);
         for (std::string w; is >> w;) o.push_back(w);
     }
     std::vector<const char *> ov;
@@ -135,9 +162,9 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
 }
 
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
-                             RtcKernel &out) {
+                             RtcKernel &out, const std::string &usrc, const std::string &uopts) {
     if (src.empty()) return "empty user source";
-    return rtc_compile(src, opts, D, full, 0, nu, out);
+    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts);
 }
 
 const char *rtc_builtin_law(const char *name) {
@@ -146,8 +173,9 @@ const char *rtc_builtin_law(const char *name) {
     return nullptr;
 }
 
-std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out) {
-    return rtc_compile("", "", D, full, ll_mode, nu, out);
+std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out, const std::string &usrc,
+                            const std::string &uopts) {
+    return rtc_compile("", "", D, full, ll_mode, nu, out, usrc, uopts);
 }
 
 }  // namespace emcmc

@@ -13,7 +13,7 @@ from .kernels import (AdaptationUnifRW, GaussianRandomWalk, GaussianRandomWalkMi
                       MCMCParamUpdate, MCMCUpdate, NoAdaptation, ProductPrior, RandomWalkUpdate, StandardPrior,
                       UniformRandomWalk, UnsupportedPlugin, isdecorator, isequal_except, Normal, Uniform,
                       Exponential, Gamma, Product, LogNormal, Beta, InverseGamma, Cauchy, Laplace, TDist,
-                      MvNormal)
+                      MvNormal, UserUpdate)
 from .mcmc import (MCMC, GenericMCMCBackend, MI355XBackend, MI355XGlobalWorkspace, MI355XLocalWorkspace,
                    create_workspaces, get_decorators, init, run, run_)
 from .schedule import JRange, MCMCSchedule, Step, reschedule, reschedule_
@@ -27,5 +27,5 @@ __all__ = [
     "SavingCallback", "REPLCallback", "MCMCSchedule", "JRange", "reschedule", "Engine", "EngineConfig",
     "EMCMCError", "device_count", "rhat_from_moments", "allgather_moments", "merge_moments", "MALAUpdate", "LogisticRegressionLaw",
     "StandardPrior", "ProductPrior", "Normal", "Uniform", "Exponential", "Gamma", "Product",
-    "LogNormal", "Beta", "InverseGamma", "Cauchy", "Laplace", "TDist", "MvNormal", "UserTargetLaw",
+    "LogNormal", "Beta", "InverseGamma", "Cauchy", "Laplace", "TDist", "MvNormal", "UserUpdate", "UserTargetLaw",
 ]

@@ -37,7 +37,7 @@ STATUS_NAMES = {
     8: "EMCMC_STATE_ERROR",
 }
 
-RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA = 1, 2, 3, 4
+RW_UNIFORM, RW_GAUSSIAN, RW_GAUSSIAN_MIX, MALA, USER_UPDATE = 1, 2, 3, 4, 5
 PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = 0, 1, 2, 3
 DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = 1, 2, 3, 4
 DIST_LOGNORMAL, DIST_BETA, DIST_INVERSE_GAMMA, DIST_CAUCHY, DIST_LAPLACE, DIST_TDIST = 5, 6, 7, 8, 9, 10
@@ -55,6 +55,7 @@ VARIANT_HIGH_OCCUPANCY = 1
 VARIANT_OCCUPANCY3 = 2
 VARIANT_SCALAR_OBS = 4
 VARIANT_MIX_STREAM = 8
+VARIANT_NO_XCD_ORDER = 16
 
 
 class EmcmcConfig(C.Structure):
@@ -90,7 +91,7 @@ class EmcmcUpdateDesc(C.Structure):
         ("adaptation_params", C.c_void_p),
         ("sigma_b", C.POINTER(C.c_double)),
         ("prior_params", C.c_void_p),
-        ("reserved_ptr", C.c_void_p),
+        ("user_update", C.c_void_p),
         ("mix_lambda", C.c_double),
         ("reserved_f64", C.c_double * 3),
     ]
@@ -160,6 +161,12 @@ class EmcmcTargetDesc(C.Structure):
     ]
 
 
+class EmcmcUserUpdateDesc(C.Structure):
+    """A user update compiled at run time (include/emcmc.h emcmc_user_update_desc)."""
+    _fields_ = [("source", C.c_char_p), ("options", C.c_char_p), ("num_params", C.c_uint64),
+                ("params", C.POINTER(C.c_double))]
+
+
 class EmcmcUserTargetDesc(C.Structure):
     """A user law compiled at run time (include/emcmc.h emcmc_user_target_desc)."""
     _fields_ = [
@@ -200,6 +207,7 @@ SIGNATURES = {
     "emcmc_set_target": (_ST, [_H, C.POINTER(EmcmcTargetDesc)]),
     "emcmc_set_user_target": (_ST, [_H, C.POINTER(EmcmcUserTargetDesc)]),
     "emcmc_check_user_target": (_ST, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_size_t]),
+    "emcmc_check_user_update": (_ST, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_size_t]),
     "emcmc_set_state": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_run": (_ST, [_H, C.POINTER(EmcmcStep), C.c_uint64]),
     "emcmc_synchronize": (_ST, [_H]),
@@ -315,6 +323,14 @@ def check_user_target(source: str, dim: int, options: str = "") -> None:
     st = lib().emcmc_check_user_target(source.encode(), dim, options.encode(), buf, len(buf))
     if st != OK:
         raise EMCMCError(st, "emcmc_check_user_target", buf.value.decode(errors="replace"))
+
+
+def check_user_update(source: str, dim: int, options: str = "") -> None:
+    """Compile-only check of a user update's proposal! / log_transition_density source."""
+    buf = C.create_string_buffer(1 << 16)
+    st = lib().emcmc_check_user_update(source.encode(), dim, options.encode(), buf, len(buf))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_check_user_update", buf.value.decode(errors="replace"))
 
 
 def device_count() -> int:

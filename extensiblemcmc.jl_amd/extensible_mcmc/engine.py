@@ -218,6 +218,25 @@ class Engine:
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
 
+    def add_user_update(self, coords0, source, params=(), options="", prior=L.PRIOR_IMPROPER, prior_factors=None):
+        """A user-defined update on coords0 (0-based): its proposal! and
+        log_transition_density as an EMCMC_USER_PROPOSAL / EMCMC_USER_LTD source
+        (include/emcmc.h emcmc_user_update_desc; updates.jl:42-93), compiled at run time."""
+        keep = []
+        coords = np.ascontiguousarray(coords0, dtype=np.uint32)
+        prm = np.ascontiguousarray(np.ravel(np.asarray(params, dtype=np.float64)))
+        ud = L.EmcmcUserUpdateDesc(source.encode(), options.encode() if options else None, prm.size,
+                                   L.dptr(prm) if prm.size else None)
+        keep += [prm, ud]
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.USER_UPDATE
+        self._prior_desc(u, prior, prior_factors, keep)
+        u.num_coords = len(coords)
+        u.coords = L.u32ptr(coords)
+        u.user_update = C.cast(C.pointer(ud), C.c_void_p)
+        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
+        self.num_updates += 1
+
     def add_mala_update(self, coords0, eps, prior=L.PRIOR_IMPROPER):
         """MALA with step size ϵ on coords0 (0-based; the engine's definition of
         the reference's stub MALAUpdate, updates.jl:216-218)."""

@@ -634,6 +634,36 @@ class RandomWalkUpdate(MCMCParamUpdate):
 
 
 @dataclass
+class UserUpdate(MCMCParamUpdate):
+    """A user-defined ``MCMCParamUpdate`` (the reference's update plugin surface,
+    updates.jl:42-93: ``proposal!``, ``log_transition_density``; docs
+    manual/updates_and_decorators.md:58-87).  Its two methods are written once as
+    an ``EMCMC_USER_PROPOSAL { … } EMCMC_USER_LTD { … }`` source in the C subset the
+    device compiler (hiprtc) and a C compiler both accept (include/emcmc.h
+    emcmc_user_update_desc); ``params`` are its constants.  ``set_parameters!`` is
+    the generic ``P°.θ[coords] ← θ°`` (updates.jl:198-205) and the prior enters the
+    ratio like any update's (run.jl:374-385).  ``coords`` are 1-based."""
+
+    source: str
+    coords: Sequence[int]
+    params: Sequence[float] = ()
+    prior: Prior = field(default_factory=ImproperPrior)
+    adpt: Adaptation = field(default_factory=NoAdaptation)
+    options: str = ""
+
+    def __post_init__(self):
+        self.coords = [int(c) for c in np.atleast_1d(self.coords)]
+        self.invcoords = {c: i + 1 for i, c in enumerate(self.coords)}
+
+    def to_device(self, engine):
+        if not isinstance(self.adpt, NoAdaptation):
+            raise UnsupportedPlugin("adaptation of a user update has no device plugin")
+        prior, factors = prior_to_device(self.prior, len(self.coords))
+        engine.add_user_update(np.asarray(self.coords, dtype=np.int64) - 1, self.source, self.params,
+                               options=self.options, prior=prior, prior_factors=factors)
+
+
+@dataclass
 class MALAUpdate(MCMCGradientBasedUpdate):
     """``MALAUpdate`` — a stub in the reference (updates.jl:216-218, "✗" at
     updates.jl:7) whose hook is ``compute_gradients_and_momenta!`` (run.jl:110,

@@ -52,7 +52,7 @@ struct EmcmcUpdateDesc
     adaptation_params::Ptr{Cvoid}
     sigma_b::Ptr{Float64}
     prior_params::Ptr{Cvoid}          # const emcmc_prior_desc* (ProductPrior / StandardPrior)
-    reserved_ptr::Ptr{Cvoid}
+    user_update::Ptr{Cvoid}           # const emcmc_user_update_desc* (EMCMC_USER_UPDATE)
     mix_lambda::Float64
     reserved_f64::NTuple{3,Float64}
 end
@@ -109,8 +109,16 @@ struct EmcmcStep
     pidx::UInt32
 end
 
+struct EmcmcUserUpdateDesc
+    source::Cstring
+    options::Cstring
+    num_params::UInt64
+    params::Ptr{Float64}
+end
+
 const RW_GAUSSIAN = UInt32(2)
 const RW_GAUSSIAN_MIX = UInt32(3)
+const USER_UPDATE = UInt32(5)
 const ADPT_HAARIO = UInt32(2)
 const PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
 const DIST_NORMAL, DIST_UNIFORM, DIST_EXPONENTIAL, DIST_GAMMA = UInt32(1), UInt32(2), UInt32(3), UInt32(4)
@@ -155,6 +163,42 @@ function _set_user_target(h, P::HipTargetLaw, obs)
         check(ccall((:emcmc_set_user_target, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcUserTargetDesc}), h, t),
               h, "emcmc_set_user_target")
     end
+end
+
+"""
+    HipUpdate(source, coords; params = Float64[], prior = ImproperPrior(), options = "")
+
+A user-defined `MCMCParamUpdate` for `MI355XBackend`.  The reference's update
+plugin surface — `proposal!(updt, global_ws, ws, step)` and
+`log_transition_density(updt, θ, θ°)` (src/updates.jl:42-93) — written once as an
+`EMCMC_USER_PROPOSAL { … } EMCMC_USER_LTD { … }` source (include/emcmc.h
+emcmc_user_update_desc) that the engine compiles for the device, with `params`
+as its constants and draws from the engine's stream (`em_randn(j)`,
+`em_rand(j)`).  `set_parameters!` is the generic `P°.θ[coords] ← θ°`
+(updates.jl:198-205); the prior enters the ratio as for any update.
+"""
+struct HipUpdate{K,P} <: eMCMC.MCMCParamUpdate
+    source::String
+    coords::K
+    invcoords::Dict{Int,Int}
+    params::Vector{Float64}
+    prior::P
+    adpt::eMCMC.NoAdaptation
+    options::String
+end
+HipUpdate(source::String, coords; params = Float64[], prior = eMCMC.ImproperPrior(), options = "") =
+    HipUpdate(source, coords, Dict(c => i for (i, c) in enumerate(coords)), Float64.(params), prior,
+              eMCMC.NoAdaptation(), options)
+
+function _update_desc(updt::HipUpdate, keep)
+    coords = UInt32.(collect(updt.coords) .- 1)
+    pk, pp = _prior_desc(updt.prior, length(coords), keep)
+    ud = Ref(EmcmcUserUpdateDesc(Base.unsafe_convert(Cstring, updt.source), Base.unsafe_convert(Cstring, updt.options),
+                                 UInt64(length(updt.params)),
+                                 isempty(updt.params) ? Ptr{Float64}(C_NULL) : pointer(updt.params)))
+    push!(keep, coords, ud, updt)
+    EmcmcUpdateDesc(USER_UPDATE, pk, ADPT_NONE, UInt32(length(coords)), pointer(coords), C_NULL, C_NULL, C_NULL,
+                    C_NULL, C_NULL, pp, Base.unsafe_convert(Ptr{Cvoid}, ud), 0.0, (0.0, 0.0, 0.0))
 end
 
 function check(st, h, where)
@@ -762,6 +806,7 @@ eMCMC.state°(lws::MI355XLocalWorkspace) = lws.sub_ws°.state
 eMCMC.name_of_update(lws::MI355XLocalWorkspace) = lws.updt_name
 
 export MI355XBackend, state_history, proposal_history, ll_history, acceptance_history, rolling_acceptance,
-       adaptation_state, chain_moments, mix_state, faults, moments_window, kernel_name, device_count
+       adaptation_state, chain_moments, mix_state, faults, moments_window, kernel_name, device_count,
+       HipTargetLaw, HipUpdate
 
 end # module

@@ -60,6 +60,9 @@ typedef enum emcmc_status {
 #define EMCMC_RW_GAUSSIAN_MIX 3u  /* GaussianRandomWalkMix    random_walk.jl:193-232 */
 #define EMCMC_MALA 4u             /* MALAUpdate: a stub in the reference (updates.jl:216-218); the engine's
                                      definition is in DESIGN.md §2.  epsilon[0] = step size ϵ. */
+#define EMCMC_USER_UPDATE 5u      /* a user-defined MCMCParamUpdate: its proposal! and log_transition_density
+                                     (updates.jl:42-93, the methods an update MUST implement) as device source
+                                     compiled at run time; emcmc_update_desc.user_update */
 
 /* Priors — src/priors.jl.  Evaluated on the update's local coordinates
  * (log_prior, updates.jl:104; run.jl:374-385); proposal! draws θ° again while
@@ -163,6 +166,7 @@ typedef struct emcmc_config {
 #define EMCMC_VARIANT_SCALAR_OBS 4u      /* diagonal Σ: one lane per chain, observations as SGPR operands */
 #define EMCMC_VARIANT_MIX_STREAM 8u      /* GaussianRandomWalkMix: stream L_B from HBM every step (mix_gsn_kernel)
                                             instead of keeping it in registers (mix_res_kernel) */
+#define EMCMC_VARIANT_NO_XCD_ORDER 16u   /* blocks in blockIdx order instead of one contiguous chain range per XCD */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,
@@ -229,6 +233,31 @@ typedef struct emcmc_prior_desc {
     const emcmc_prior_factor *factors;
 } emcmc_prior_desc;
 
+/* A user-defined update (EMCMC_USER_UPDATE): the reference's update plugin
+ * surface (updates.jl:42-93) — `proposal!(updt, gws, ws, step)` writing
+ * state°(ws) from state(ws), and `log_transition_density(updt, θ, θ°)` — as
+ *
+ *     EMCMC_USER_PROPOSAL {   // in scope: const double *theta (state(ws), n entries),
+ *         …                   //   double *theta_prop (state°(ws), out), int n,
+ *     }                       //   const double *params (num_params); em_randn(j), em_rand(j)
+ *     EMCMC_USER_LTD {        // in scope: const double *x, const double *y, int n, params:
+ *         return …;           //   log_transition_density(updt, x, y)
+ *     }
+ *
+ * in the C subset both hiprtc and a C compiler accept (emcmc_user_target_desc's
+ * rules; em_randn(j) = normal j, em_rand(j) = uniform [0, 1) j of the engine's
+ * stream for (chain, mcmciter, update), j < 2^30).  The MH ratio adds
+ * ltd(θ°, θ) − ltd(θ, θ°) and the prior as run.jl:268-281 does; set_parameters!
+ * is P°.θ[coords] ← θ° (updates.jl:198-205).  Every user update of a handle
+ * shares one source (updates differ by coords, params and prior); it runs on
+ * the general schedule kernel, beside the built-in updates, with any target. */
+typedef struct emcmc_user_update_desc {
+    const char *source;   /* EMCMC_USER_PROPOSAL { … } EMCMC_USER_LTD { … } */
+    const char *options;  /* extra hiprtc options, or NULL */
+    uint64_t num_params;  /* ≤ 4096 */
+    const double *params;
+} emcmc_user_update_desc;
+
 /* One `RandomWalkUpdate(rw, coords; prior, adpt)` (src/updates.jl:163-183).
  * Any number of updates, each on any coordinate subset (Metropolis-within-Gibbs,
  * BASELINE cfg 1 and the reference's own test, test/runtests.jl:87-114).  A single
@@ -254,7 +283,7 @@ typedef struct emcmc_update_desc {
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
     const double *sigma_b;    /* GaussianRandomWalkMix Σ_B: num_coords² column-major */
     const emcmc_prior_desc *prior_params; /* EMCMC_PRIOR_PRODUCT / EMCMC_PRIOR_STANDARD factors, else NULL */
-    const void *reserved_ptr;
+    const struct emcmc_user_update_desc *user_update; /* EMCMC_USER_UPDATE: its source and parameters, else NULL */
     double mix_lambda;        /* GaussianRandomWalkMix λ ∈ [0, 1] (B is picked iff rand() ≤ λ) */
     double reserved_f64[3];
 } emcmc_update_desc;
@@ -348,6 +377,9 @@ emcmc_status emcmc_set_user_target(emcmc_handle *h, const emcmc_user_target_desc
  * needed): EMCMC_OK, or EMCMC_INVALID_ARG with the compiler log in log_out
  * (truncated to log_len bytes, NUL-terminated; log_out may be NULL). */
 emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const char *options, char *log_out,
+                                     size_t log_len);
+/* The same for a user update's source (emcmc_user_update_desc) at dimension dim. */
+emcmc_status emcmc_check_user_update(const char *source, uint32_t dim, const char *options, char *log_out,
                                      size_t log_len);
 
 /* θinit for every chain (row-major [C][D]); ll = NULL means the reference's

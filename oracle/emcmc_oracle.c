@@ -830,6 +830,11 @@ ORC_EXPORT int orc_eval_prior(uint32_t prior, uint32_t n, uint32_t nfac, const u
  * the same source the engine compiles for the device (tests/user_targets/) */
 typedef double (*orc_user_loglik_fn)(const double *theta, int D, const double *obs, uint64_t nobs,
                                      const double *params);
+/* user update (EMCMC_USER_UPDATE): proposal! and log_transition_density of the
+ * same source the engine compiles (tests/user_updates/, oracle/user_prelude.h) */
+typedef void (*orc_user_prop_fn)(const double *theta, double *theta_prop, int n, const double *params,
+                                 emcmc_rng *rng);
+typedef double (*orc_user_ltd_fn)(const double *x, const double *y, int n, const double *params);
 
 /* table layout from Python (ORC_MWG_MAXD = 64 slots per update):
  *   kind[P], nc[P], coords[P*64], eps[P*64], sigma[P*4096] (nc×nc column-major),
@@ -850,7 +855,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                            const uint32_t *nfac, const uint32_t *ffam, const uint32_t *fcnt, const double *fa,
                            const double *fb, double *ll_prop, orc_user_loglik_fn user_ll,
                            const double *user_params, const uint32_t *pcfam, const double *pca, const double *pcb,
-                           const double *pmvmu, const double *pmvS) {
+                           const double *pmvmu, const double *pmvS, orc_user_prop_fn user_prop,
+                           orc_user_ltd_fn user_ltd, const double *user_uparams) {
     if (D < 1 || D > ORC_MWG_MAXD || P < 1 || P > 64) return -2;
     (void)zig();
     orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
@@ -949,8 +955,18 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             int anypos = 0;
             for (uint32_t j = 0; j < n; ++j) anypos |= u->pos[j];
             /* proposal! (updates.jl:191-196): rand!, again while logpdf(prior, θ°) === −Inf;
-             * resample r reads counter blocks (r << 16) | j/2 */
-            for (uint32_t rs = 0;; ++rs) {
+             * resample r reads counter blocks (r << 16) | j/2.  A user update
+             * (kind 5): its own proposal! and log_transition_density
+             * (updates.jl:42-93), compiled from the engine's source */
+            if (u->kind == 5) {
+                emcmc_rng rng = {zt, k0, k1, chain_id, iter, p, 0u};
+                for (uint32_t j = 0; j < ORC_MWG_MAXD; ++j) tp[j] = 0.0;
+                user_prop(tl, tp, (int)n, user_uparams + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD, &rng);
+                f |= rng.faults;
+                ltd_fwd = user_ltd(tl, tp, (int)n, user_uparams + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD);
+                ltd_rev = user_ltd(tp, tl, (int)n, user_uparams + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD);
+            }
+            for (uint32_t rs = 0; u->kind != 5; ++rs) {
                 if (u->kind == 1) { /* UniformRandomWalk */
                     for (uint32_t j = 0; j < n; ++j) {
                         const orc_u32x4 r = orc_draw(k0, k1, chain_id, iter, (rs << 16) | (j >> 1), p, 0);
@@ -988,7 +1004,9 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 }
             }
             double t3[ORC_MWG_MAXD]; /* θ as log_prior(::Previous) reads it */
-            if (u->kind == 1) {
+            if (u->kind == 5) {
+                /* transition densities done above */
+            } else if (u->kind == 1) {
                 /* logpdf(rw, θ, θ°) (subtracted) and logpdf(rw, θ°, θ) (added), left folds */
                 for (uint32_t j = 0; j < n; ++j) {
                     const double c = u->pos[j] ? -orc_log_any(2.0 * ep[j]) : 0.0;

@@ -265,7 +265,11 @@ DIST_LOGNORMAL, DIST_BETA, DIST_INVERSE_GAMMA, DIST_CAUCHY, DIST_LAPLACE, DIST_T
 DIST_PRODUCT, DIST_MVNORMAL = 32, 33
 
 
-def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=PRIOR_IMPROPER, factors=None):
+KIND_USER = 5
+
+
+def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=PRIOR_IMPROPER, factors=None,
+               params=None):
     """One RandomWalkUpdate for run_mwg.  coords0: 0-based coordinates.
     adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW).
     pos: None or per-coordinate positivity flags (UniformRandomWalk).
@@ -276,7 +280,8 @@ def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=
     return {"kind": kind, "coords": [int(c) for c in coords0], "eps": None if eps is None else list(eps),
             "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt,
             "pos": None if pos is None else [bool(x) for x in pos], "prior": int(prior),
-            "factors": [] if factors is None else [tuple(f) for f in factors]}
+            "factors": [] if factors is None else [tuple(f) for f in factors],
+            "params": None if params is None else [float(x) for x in np.ravel(params)]}
 
 
 class MWGState:
@@ -401,7 +406,7 @@ USER_LL_FN = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int, C.POINTER(C
 
 
 def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll_mode=0, W=100, history=True,
-            nthreads=1, user_ll=None, user_params=None):
+            nthreads=1, user_ll=None, user_params=None, user_upd=None):
     """Advance `state` over `steps` [(mcmciter, pidx 1-based), …]; histories per step.
     user_ll: a C function pointer (ctypes) of the user target's loglikelihood, or None
     for GsnTargetLaw; state.ll_prop receives sub_ws°.ll of every update."""
@@ -413,11 +418,17 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         L.orc_run_mwg.argtypes = [C.c_int, C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint32, u32p, u32p, u32p, dp, dp,
                                   u8p, u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
                                   u64p, u32p, dp, dp, dp, dp, u64p, u32p, u32p, u32p, dp, u32p, dp, dp, dp, u8p,
-                                  C.c_int, u32p, u32p, u32p, u32p, dp, dp, dp, C.c_void_p, dp, u32p, dp, dp, dp, dp]
+                                  C.c_int, u32p, u32p, u32p, u32p, dp, dp, dp, C.c_void_p, dp, u32p, dp, dp, dp, dp,
+                                  C.c_void_p, C.c_void_p, dp]
         L._mwg_ready = True
     Cn, D = state.C, state.D
     kind, nc, coords, eps, sigma, adapt, ak, ap, pos = _mwg_tables(updates)
     pk, nf, ffam, fcnt, fa, fb, cfam, ca, cb, mvmu, mvS = _prior_tables(updates)
+    uparams = np.zeros((len(updates), MWG_MAXD * MWG_MAXD))  # user updates: their parameters
+    for p, u in enumerate(updates):
+        if u.get("params") is not None:
+            v = np.asarray(u["params"], dtype=np.float64).ravel()
+            uparams[p, :v.size] = v
     if getattr(state, "ll_prop", None) is None:
         state.ll_prop = np.full((len(updates), state.C), np.nan)
     up = None if user_params is None else np.ascontiguousarray(user_params, dtype=np.float64)
@@ -445,7 +456,9 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         None if not history else hist["acc"].ctypes.data_as(C.POINTER(C.c_uint8)), nthreads,
         u32(pk), u32(nf), u32(ffam), u32(fcnt), _d(fa), _d(fb), _d(state.ll_prop),
         None if user_ll is None else C.cast(user_ll, C.c_void_p), None if up is None else _d(up),
-        u32(cfam), _d(ca), _d(cb), _d(mvmu), _d(mvS))
+        u32(cfam), _d(ca), _d(cb), _d(mvmu), _d(mvS),
+        None if user_upd is None else C.cast(user_upd[0], C.c_void_p),
+        None if user_upd is None else C.cast(user_upd[1], C.c_void_p), _d(uparams))
     if rc != 0:
         raise ValueError(f"orc_run_mwg failed: {rc}")
     if history:
@@ -469,6 +482,26 @@ def user_loglik(name):
     fn = USER_LL_FN(("emcmc_user_loglik", dll))
     fn._dll = dll  # keep the library loaded
     return fn, src.read_text()
+
+
+USER_PROP_FN = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double),
+                           C.c_void_p)
+USER_LTD_FN = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double))
+
+
+def user_update(name):
+    """The oracle build of user update tests/user_updates/<name>.c (oracle/Makefile:
+    lib/userupd_<name>.so, compiled with oracle/user_prelude.h): ((proposal, ltd)
+    ctypes functions, source text).  The engine compiles the same source for the device."""
+    so = Path(__file__).resolve().parent / "lib" / f"userupd_{name}.so"
+    src = Path(__file__).resolve().parent.parent / "tests" / "user_updates" / f"{name}.c"
+    if not so.exists():
+        raise ImportError(f"{so} not built (make -C oracle)")
+    dll = C.CDLL(str(so))
+    prop = USER_PROP_FN(("emcmc_user_proposal", dll))
+    ltd = USER_LTD_FN(("emcmc_user_ltd", dll))
+    prop._dll = ltd._dll = dll
+    return (prop, ltd), src.read_text()
 
 
 def uniform01(seed, chain, it, pidx0, j):

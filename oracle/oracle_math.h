@@ -363,4 +363,21 @@ static inline double orc_exponential(const orc_zig_tables *t, uint32_t k0, uint3
 
 #define ORC_LOG2PI 1.8378770664093454835606594728112
 
+/* ---- user updates (EMCMC_USER_UPDATE): the draws a user proposal! makes, by
+ * index (emcmc_mwg.h UserRng): normal j of (chain, iter, update) as the random
+ * walks index theirs, and the uniform [0, 1) j from words (x, y) / (z, w) of
+ * block 2^31 + j/2 (attempt 0, a range no other draw of the update uses). */
+typedef struct emcmc_rng {
+    const orc_zig_tables *zt;
+    uint32_t k0, k1, chain, iter, p;
+    uint32_t faults;
+} emcmc_rng;
+static inline double orc_user_randn(emcmc_rng *r, uint32_t j) {
+    return orc_normal(r->zt, r->k0, r->k1, r->chain, r->iter, r->p, j & 0x3FFFFFFFu, &r->faults);
+}
+static inline double orc_user_rand(const emcmc_rng *r, uint32_t j) {
+    const orc_u32x4 w = orc_draw(r->k0, r->k1, r->chain, r->iter, 0x80000000u | ((j & 0x3FFFFFFFu) >> 1), r->p, 0);
+    return (j & 1u) ? orc_u01_closed0(w.v[2], w.v[3]) : orc_u01_closed0(w.v[0], w.v[1]);
+}
+
 #endif

@@ -22,7 +22,7 @@ C_NAME = {"EmcmcConfig": "emcmc_config", "EmcmcUpdateDesc": "emcmc_update_desc",
           "EmcmcUnifRWAdaptationVec": "emcmc_unifrw_adaptation_vec",
           "EmcmcTargetDesc": "emcmc_target_desc", "EmcmcStep": "emcmc_step", "EmcmcMoments": "emcmc_moments",
           "EmcmcPriorFactor": "emcmc_prior_factor", "EmcmcPriorDesc": "emcmc_prior_desc",
-          "EmcmcUserTargetDesc": "emcmc_user_target_desc"}
+          "EmcmcUserTargetDesc": "emcmc_user_target_desc", "EmcmcUserUpdateDesc": "emcmc_user_update_desc"}
 
 JL_SCALAR = {"UInt8": 1, "Int8": 1, "UInt16": 2, "Int16": 2, "UInt32": 4, "Int32": 4, "Cint": 4, "Float32": 4,
              "UInt64": 8, "Int64": 8, "Float64": 8, "Csize_t": 8, "Cstring": 8}

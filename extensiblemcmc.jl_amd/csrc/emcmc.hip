@@ -106,7 +106,9 @@ struct UpdateHost {
     double c0 = 0.0;
     // GaussianRandomWalkMix: Σ_B, its factor, λ; HaarioTypeAdaptation
     std::vector<double> sigma_b, LB, invdiagB;
-    double c0B = 0.0, lam = 0.0;
+    double c0B = 0.0, lam = 0.0, lam0 = 0.0;  // λ now / as constructed (emcmc_set_state restores it)
+    // general-kernel per-chain state offsets in emcmc_handle::d_mixpool (MwgUpdate)
+    uint64_t lb_off = 0, lbi_off = 0, lbc_off = 0, lbs_off = 0, hm_off = 0, hc_off = 0;
     emcmc_haario_adaptation haario{};
     emcmc_lambda_fn flam = nullptr;  // HaarioTypeAdaptation fλ (host callback; nullptr = identity)
     void *flam_ctx = nullptr;
@@ -201,6 +203,14 @@ struct emcmc_handle {
     double *d_mom_consts = nullptr;  // [steps_per_launch][8] per-step scalars of the moments recurrence
     double *d_mom_scratch = nullptr;  // ACCEPT_ONLY: θ of each step of a launch, for the moments kernel
     uint32_t mix_M = 0;
+    // general schedule path: GaussianRandomWalkMix / Haario per-chain pool,
+    // GenericChainStats mean [D][C] / cov packed [D(D+1)/2][C], Haario M per update
+    double *d_mixpool = nullptr;
+    uint64_t mixpool_elems = 0;
+    double *d_smean = nullptr, *d_scov = nullptr;
+    std::vector<uint32_t> mwg_M;
+    uint32_t nhaario = 0;
+    bool mwg_pool_ready = false;
     // MALA path: carried ∇ℓ(θ) (state_pos layout), padded X and y
     double *d_grad = nullptr, *d_X = nullptr, *d_y = nullptr;
     uint32_t mala_tiles = 0;
@@ -280,11 +290,80 @@ bool joint_all_coords(const emcmc_handle *h) {
 
 // GaussianRandomWalkMix (± Haario), or GaussianRandomWalk with chain moments:
 // the mix kernels
+// the fused mix / chain-moments kernels (cfg 4): one joint update on coords 1:D,
+// ImproperPrior, no positivity flags, the built-in target; everything else with
+// GaussianRandomWalkMix or chain moments runs on the general kernel
 bool mix_path(const emcmc_handle *h) {
     if (!joint_all_coords(h)) return false;
+    if (h->target_set && h->target.kind != EMCMC_TARGET_GSN) return false;
     const UpdateHost &u = h->updates[0];
+    if (u.prior != EMCMC_PRIOR_IMPROPER) return false;
+    for (uint8_t f : u.pos)
+        if (f) return false;
     return u.kernel == EMCMC_RW_GAUSSIAN_MIX ||
            (u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE && h->cfg.chain_moments);
+}
+
+// general kernel: layout of the per-chain mix / Haario pool (MwgUpdate offsets)
+uint64_t mwg_pool_layout(emcmc_handle *h) {
+    const uint64_t C = h->cfg.num_chains;
+    uint64_t off = 0;
+    h->nhaario = 0;
+    for (auto &u : h->updates) {
+        const uint64_t n = u.coords.size(), tn = n * (n + 1) / 2;
+        u.lb_off = u.lbi_off = u.lbc_off = u.lbs_off = u.hm_off = u.hc_off = 0;
+        if (u.kernel != EMCMC_RW_GAUSSIAN_MIX) continue;
+        u.lb_off = off, off += tn * C;
+        u.lbi_off = off, off += n * C;
+        u.lbc_off = off, off += C;
+        u.lbs_off = off, off += tn * C;
+        if (u.adaptation == EMCMC_ADPT_HAARIO) {
+            u.hm_off = off, off += n * C;
+            u.hc_off = off, off += tn * C;
+            ++h->nhaario;
+        }
+    }
+    return off;
+}
+
+// (Re)start the general kernel's mix / Haario / chain-moment state: every chain's
+// L_B from the user's Σ_B, Haario mean/cov and GenericChainStats mean/cov zero
+// (N = 1, the phantom zero sample: chain_statistics.jl:30-35, adaptation.jl:387-395).
+emcmc_status reset_mwg_pool(emcmc_handle *h) {
+    const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    const uint64_t elems = mwg_pool_layout(h);
+    if (elems != h->mixpool_elems) {
+        if (h->d_mixpool) (void)hipFree(h->d_mixpool);
+        h->d_mixpool = nullptr;
+        h->mixpool_elems = elems;
+        if (elems) HIPCHK(h, hipMalloc(&h->d_mixpool, elems * sizeof(double)));
+    }
+    if (elems) {
+        std::vector<double> pool(elems, 0.0);
+        for (const auto &u : h->updates) {
+            if (u.kernel != EMCMC_RW_GAUSSIAN_MIX) continue;
+            const uint64_t n = u.coords.size();
+            for (uint64_t i = 0; i < n; ++i) {
+                for (uint64_t j = 0; j <= i; ++j)
+                    std::fill_n(pool.begin() + u.lb_off + (i * (i + 1) / 2 + j) * C, C, u.LB[i * n + j]);
+                std::fill_n(pool.begin() + u.lbi_off + i * C, C, u.invdiagB[i]);
+            }
+            std::fill_n(pool.begin() + u.lbc_off, C, u.c0B);
+        }
+        HIPCHK(h, hipMemcpy(h->d_mixpool, pool.data(), elems * sizeof(double), hipMemcpyHostToDevice));
+    }
+    if (h->cfg.chain_moments) {
+        const uint64_t DP = D * (D + 1) / 2;
+        if (!h->d_smean) {
+            HIPCHK(h, hipMalloc(&h->d_smean, D * C * sizeof(double)));
+            HIPCHK(h, hipMalloc(&h->d_scov, DP * C * sizeof(double)));
+        }
+        HIPCHK(h, hipMemset(h->d_smean, 0, D * C * sizeof(double)));
+        HIPCHK(h, hipMemset(h->d_scov, 0, DP * C * sizeof(double)));
+    }
+    h->mwg_M.assign(h->updates.size(), 0u);
+    h->mwg_pool_ready = true;
+    return EMCMC_OK;
 }
 
 // P°.θ[1:d] ← μ for every chain (workspaces.jl:225-233: P° = deepcopy(data.P))
@@ -376,10 +455,13 @@ emcmc_status select_mwg(emcmc_handle *h) {
     int best_nu = 1 << 30;
     const bool user = h->target.kind == EMCMC_TARGET_USER;
     std::string usrc, uopts;  // a user update's source: compiled into the same kernel
-    for (const auto &u : h->updates)
+    bool xt = h->cfg.chain_moments != 0;  // GaussianRandomWalkMix / Haario / chain moments: compiled at run time
+    for (const auto &u : h->updates) {
         if (u.kernel == EMCMC_USER_UPDATE) usrc = u.usrc, uopts = u.uopts;
+        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) xt = true;
+    }
     for (const auto &e : mwg_table()) {
-        if (user || !usrc.empty()) break;
+        if (user || !usrc.empty() || xt) break;
         if (e.D != D) continue;
         if (e.nu != 0 && ((size_t)e.nu < nmax || e.nu >= best_nu)) continue;  // smallest NU that fits
         if (e.nu != 0) best_nu = e.nu;
@@ -388,11 +470,11 @@ emcmc_status select_mwg(emcmc_handle *h) {
     }
     // a user law, or a dimension without an ahead-of-time instantiation: the
     // same kernel compiled at run time (emcmc_rtc.hip, cached per process)
-    if (user || !usrc.empty() || (!v.mfn && D <= kMwgMaxD)) {
+    if (user || !usrc.empty() || xt || (!v.mfn && D <= kMwgMaxD)) {
         RtcKernel k;
         const int nu = rtc_wide_nu(D, (int)nmax);
-        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k, usrc, uopts)
-                                     : rtc_compile_gsn(D, full, ll, nu, k, usrc, uopts);
+        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k, usrc, uopts, xt)
+                                     : rtc_compile_gsn(D, full, ll, nu, k, usrc, uopts, xt);
         if (!log.empty()) {
             h->err = std::string(user || !usrc.empty() ? "user target / update does not compile:\n"
                                                         : "run-time kernel build failed:\n") +
@@ -416,6 +498,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
     if (!v.mfn && !v.ufn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "no general-schedule device kernel for D=%d (D ≤ 64)", D);
+    (void)mwg_pool_layout(h);  // the mix / Haario offsets the table records
     std::vector<MwgUpdate> tab(h->updates.size());
     for (size_t p = 0; p < h->updates.size(); ++p) {
         const UpdateHost &u = h->updates[p];
@@ -425,6 +508,13 @@ emcmc_status select_mwg(emcmc_handle *h) {
         m.nc = (uint32_t)u.coords.size();
         m.adapt = u.adaptation;
         for (uint32_t j = 0; j < m.nc; ++j) m.coords[j] = u.coords[j];
+        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) {
+            m.lam = u.lam;
+            m.hk = (u.adaptation == EMCMC_ADPT_HAARIO) ? u.haario.adapt_every_k_steps : 0u;
+            m.adapt = 0;  // Haario runs in mwg_post_step, not as AdaptationUnifRW
+            m.lb_off = u.lb_off, m.lbi_off = u.lbi_off, m.lbc_off = u.lbc_off, m.lbs_off = u.lbs_off;
+            m.hm_off = u.hm_off, m.hc_off = u.hc_off;
+        }
         if (u.kernel == EMCMC_USER_UPDATE) {
             for (size_t q = 0; q < u.uparams.size(); ++q) m.L[q] = u.uparams[q];
         } else if (u.kernel == EMCMC_RW_UNIFORM) {
@@ -495,6 +585,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
     v.name = nm;
     h->lds_bytes = 0;  // tables only, in static LDS
     h->var = v;
+    if (h->allocated) return reset_mwg_pool(h);
     return EMCMC_OK;
 }
 
@@ -631,22 +722,18 @@ emcmc_status select_variant(emcmc_handle *h) {
         if (u.kernel == EMCMC_MALA) return select_mala(h);
     if (h->target.kind == EMCMC_TARGET_LOGISTIC)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "the logistic-regression target runs on device with MALA only");
-    if (h->target.kind == EMCMC_TARGET_USER) {
-        for (const auto &u : h->updates)
-            if (u.kernel == EMCMC_RW_GAUSSIAN_MIX)
-                return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "GaussianRandomWalkMix runs on device with GsnTargetLaw only");
-        if (h->cfg.chain_moments)
-            return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "chain moments on device need GsnTargetLaw");
+    if (h->target.kind == EMCMC_TARGET_USER) return select_mwg(h);  // mix, Haario, chain moments included
+    if (mix_path(h)) {
+        // the fused mix kernels where instantiated (cfg 4 shapes), else the general kernel
+        const std::string keep = h->err;
+        const emcmc_status st = select_mix(h);
+        if (st != EMCMC_UNSUPPORTED_PLUGIN) return st;
+        h->err = keep;
         return select_mwg(h);
     }
-    if (mix_path(h)) return select_mix(h);
     for (const auto &u : h->updates)
-        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX)
-            return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                        "GaussianRandomWalkMix runs on device as the single joint update on coords 1:D");
-    if (h->cfg.chain_moments)
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                    "chain moments on device need a single joint GaussianRandomWalk(Mix) update on coords 1:D");
+        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) return select_mwg(h);
+    if (h->cfg.chain_moments) return select_mwg(h);
     if (!fused_eligible(h)) return select_mwg(h);
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
@@ -1092,7 +1179,16 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     const uint64_t cap = h->cfg.num_mcmc_steps * P;
     if (num_steps == 0) return EMCMC_OK;
     if (num_steps > cap) return fail(h, EMCMC_INVALID_ARG, "more steps than M·P in one call");
+    if (!h->mwg_pool_ready) {
+        emcmc_status ps = reset_mwg_pool(h);
+        if (ps) return ps;
+    }
     std::vector<uint32_t> st(4 * num_steps);
+    // HaarioTypeAdaptation: M += 1 on its own turn, readjust! at M ≥ k (flags bit 1,
+    // adaptation.jl:399-426); with a user fλ the launch ends after a readjust and
+    // the next one reads the new λ (cut[i]: λ of the following steps)
+    std::vector<std::pair<uint64_t, std::pair<uint32_t, double>>> cuts;
+    uint64_t Nh = h->stats_N;
     for (uint64_t i = 0; i < num_steps; ++i) {
         const uint32_t it = steps[i].mcmciter, q = steps[i].pidx - 1;
         st[4 * i] = it;
@@ -1100,6 +1196,17 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
         st[4 * i + 2] = (it > 1 && h->last_iter[q] == it - 1) ? 1u : 0u;  // rolling_ar[it−1][q] was written
         st[4 * i + 3] = 0;
         h->last_iter[q] = it;
+        UpdateHost &u = h->updates[q];
+        ++Nh;  // adpt.N after this step's register! (= GenericChainStats.N)
+        if (u.kernel == EMCMC_RW_GAUSSIAN_MIX && u.adaptation == EMCMC_ADPT_HAARIO &&
+            ++h->mwg_M[q] >= u.haario.adapt_every_k_steps) {
+            h->mwg_M[q] = 0;
+            st[4 * i + 2] |= 2u;
+            if (u.flam) {  // rw.λ = adpt.fλ(rw.λ, adpt.N, mcmc_iter) (adaptation.jl:425)
+                u.lam = u.flam(u.lam, (int64_t)Nh, (int64_t)it, u.flam_ctx);
+                cuts.push_back({i + 1, {q, u.lam}});
+            }
+        }
     }
     if (h->steps_used + num_steps > cap) h->steps_used = 0;  // earlier lists were consumed in stream order
     uint32_t *dst = h->d_steps + 4 * h->steps_used;
@@ -1144,11 +1251,26 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.n_tc0 = (double)t.nobs * t.c0;
     a.S_c = t.S_c;
     a.nobs_d = (double)t.nobs;
+    a.mixpool = h->d_mixpool;
+    a.smean = h->d_smean;
+    a.scov = h->d_scov;
+    a.chain_moments = h->cfg.chain_moments ? 1u : 0u;
+    a.nhaario = h->nhaario;
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
     const uint64_t K = h->cfg.steps_per_launch;
+    size_t ci = 0;  // next λ cut
     for (uint64_t i = 0, n = 0; i < num_steps; i += n) {
+        while (ci < cuts.size() && cuts[ci].first <= i) {  // λ after an fλ readjust, in stream order
+            const uint32_t q = cuts[ci].second.first;
+            const double lam = cuts[ci].second.second;
+            HIPCHK(h, hipMemcpyAsync(reinterpret_cast<char *>(h->d_mwg + q) + offsetof(MwgUpdate, lam), &lam,
+                                     sizeof(double), hipMemcpyHostToDevice, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));  // the host value is a loop temporary
+            ++ci;
+        }
+        const uint64_t lim = (ci < cuts.size()) ? cuts[ci].first : num_steps;  // end the launch at the next cut
         n = 1;  // ≤ K steps, all in one ring epoch
-        while (i + n < num_steps && n < K && ring_epoch(h, steps[i + n].mcmciter) == ring_epoch(h, steps[i].mcmciter))
+        while (i + n < lim && n < K && ring_epoch(h, steps[i + n].mcmciter) == ring_epoch(h, steps[i].mcmciter))
             ++n;
         a.steps = dst + 4 * i;
         a.nsteps = (uint32_t)n;
@@ -1409,9 +1531,8 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     }
     if (u->prior > EMCMC_PRIOR_STANDARD)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin", u->prior);
-    if (u->prior != EMCMC_PRIOR_IMPROPER && (u->kernel == EMCMC_RW_GAUSSIAN_MIX || u->kernel == EMCMC_MALA))
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                    "priors other than ImproperPrior run on device with Gaussian/Uniform random walks only");
+    if (u->prior != EMCMC_PRIOR_IMPROPER && u->kernel == EMCMC_MALA)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA runs on device with ImproperPrior only");
     if (u->adaptation != EMCMC_ADPT_NONE &&
         !((u->adaptation == EMCMC_ADPT_UNIF_RW || u->adaptation == EMCMC_ADPT_UNIF_RW_VEC) &&
           u->kernel == EMCMC_RW_UNIFORM) &&
@@ -1422,10 +1543,10 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     if (u->pos)
         for (uint32_t i = 0; i < u->num_coords; ++i) {
             pos[i] = u->pos[i] ? 1 : 0;
-            if (pos[i] && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN)
+            if (pos[i] && u->kernel != EMCMC_RW_UNIFORM && u->kernel != EMCMC_RW_GAUSSIAN &&
+                u->kernel != EMCMC_RW_GAUSSIAN_MIX)
                 return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
-                            "positivity-restricted coordinates are on device for UniformRandomWalk and "
-                            "GaussianRandomWalk only");
+                            "positivity-restricted coordinates are on device for the random walks only");
         }
     if (h->updates.size() >= 64) return fail(h, EMCMC_INVALID_ARG, "at most 64 updates");
     UpdateHost uh;
@@ -1455,7 +1576,7 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
             if (!u->sigma_b) return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalkMix needs Σ_B (sigma_b)");
             if (!(u->mix_lambda >= 0.0 && u->mix_lambda <= 1.0))
                 return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalkMix: @assert 0.0 <= λ <= 1.0");
-            uh.lam = u->mix_lambda;
+            uh.lam = uh.lam0 = u->mix_lambda;
             uh.sigma_b.assign(u->sigma_b, u->sigma_b + (size_t)n * n);
             if (!cholesky_upper_colmajor(uh.sigma_b.data(), n, uh.LB))
                 return fail(h, EMCMC_INVALID_ARG, "GaussianRandomWalkMix Σ_B is not positive definite");
@@ -1721,6 +1842,16 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
     h->hi_iter = 0;
     h->stats_N = 1;
     h->last_iter.assign(P, 0u);
+    for (auto &u : h->updates) u.lam = u.lam0;  // rw.λ as constructed (fλ adapts it during a run)
+    if (h->var.mfn || h->var.ufn) {
+        if ((st = reset_mwg_pool(h))) return st;
+        if (h->nhaario) {  // the table's λ back to its constructed value
+            for (size_t q = 0; q < h->updates.size(); ++q)
+                if (h->updates[q].kernel == EMCMC_RW_GAUSSIAN_MIX)
+                    HIPCHK(h, hipMemcpy(reinterpret_cast<char *>(h->d_mwg + q) + offsetof(MwgUpdate, lam),
+                                        &h->updates[q].lam, sizeof(double), hipMemcpyHostToDevice));
+        }
+    }
     return EMCMC_OK;
 }
 
@@ -1917,9 +2048,55 @@ emcmc_status emcmc_get_update_state(emcmc_handle *h, uint32_t pidx, double *epsi
     return EMCMC_OK;
 }
 
+namespace {
+// [n][C] mean and packed lower [n(n+1)/2][C] cov (general kernel) → [C][n], [C][n][n]
+emcmc_status copy_soa_moments(emcmc_handle *h, const double *dmean, const double *dcov, uint64_t n, double *mean,
+                              double *cov) {
+    const uint64_t C = h->cfg.num_chains, tn = n * (n + 1) / 2;
+    if (mean) {
+        std::vector<double> m(n * C);
+        HIPCHK(h, hipMemcpy(m.data(), dmean, m.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (uint64_t i = 0; i < n; ++i) mean[c * n + i] = m[i * C + c];
+    }
+    if (cov) {
+        std::vector<double> v(tn * C);
+        HIPCHK(h, hipMemcpy(v.data(), dcov, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+        for (uint64_t c = 0; c < C; ++c)
+            for (uint64_t i = 0; i < n; ++i)
+                for (uint64_t j = 0; j <= i; ++j) {
+                    const double x = v[(i * (i + 1) / 2 + j) * C + c];
+                    cov[(c * n + i) * n + j] = x;
+                    cov[(c * n + j) * n + i] = x;
+                }
+    }
+    return EMCMC_OK;
+}
+bool general_path(const emcmc_handle *h) { return h->var.mfn || h->var.ufn; }
+}  // namespace
+
+emcmc_status emcmc_get_adaptation_moments(emcmc_handle *h, uint32_t pidx, double *mean, double *cov) {
+    if (!h) return EMCMC_INVALID_ARG;
+    if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (pidx < 1 || pidx > h->updates.size()) return fail(h, EMCMC_INVALID_ARG, "pidx %u", pidx);
+    const UpdateHost &u = h->updates[pidx - 1];
+    if (u.kernel != EMCMC_RW_GAUSSIAN_MIX || u.adaptation != EMCMC_ADPT_HAARIO)
+        return fail(h, EMCMC_INVALID_ARG, "update %u has no HaarioTypeAdaptation", pidx);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (general_path(h))
+        return copy_soa_moments(h, h->d_mixpool + u.hm_off, h->d_mixpool + u.hc_off, u.coords.size(), mean, cov);
+    return emcmc_get_chain_moments(h, mean, cov);  // the fused path (P = 1): the same recurrence on the same θ
+}
+
 emcmc_status emcmc_get_chain_moments(emcmc_handle *h, double *mean, double *cov) {
     if (!h) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (general_path(h)) {
+        if (!h->cfg.chain_moments || !h->d_smean)
+            return fail(h, EMCMC_STATE_ERROR, "chain moments are kept on device with emcmc_config.chain_moments");
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        return copy_soa_moments(h, h->d_smean, h->d_scov, h->cfg.dim, mean, cov);
+    }
     if (!h->d_mean)
         return fail(h, EMCMC_STATE_ERROR,
                     "chain moments are kept on device only with GaussianRandomWalkMix or emcmc_config.chain_moments");
@@ -1949,9 +2126,24 @@ emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_si
     if (!h) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
     if (pidx < 1 || pidx > h->updates.size()) return fail(h, EMCMC_INVALID_ARG, "pidx %u", pidx);
-    if (h->updates[pidx - 1].kernel != EMCMC_RW_GAUSSIAN_MIX || !h->d_LB)
+    if (h->updates[pidx - 1].kernel != EMCMC_RW_GAUSSIAN_MIX)
         return fail(h, EMCMC_INVALID_ARG, "update %u is not a GaussianRandomWalkMix", pidx);
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (general_path(h)) {  // the chain's L_B in the pool, packed lower [n(n+1)/2][C]
+        const UpdateHost &u = h->updates[pidx - 1];
+        const uint64_t C = h->cfg.num_chains, n = u.coords.size(), tn = n * (n + 1) / 2;
+        if (chol_sigma_b) {
+            std::vector<double> v(tn * C);
+            HIPCHK(h, hipMemcpy(v.data(), h->d_mixpool + u.lb_off, v.size() * sizeof(double), hipMemcpyDeviceToHost));
+            for (uint64_t c = 0; c < C; ++c)
+                for (uint64_t i = 0; i < n; ++i)
+                    for (uint64_t j = 0; j < n; ++j)
+                        chol_sigma_b[(c * n + i) * n + j] = (j <= i) ? v[(i * (i + 1) / 2 + j) * C + c] : 0.0;
+        }
+        if (steps_since_adapt) *steps_since_adapt = h->mwg_M.empty() ? 0u : h->mwg_M[pidx - 1];
+        return EMCMC_OK;
+    }
+    if (!h->d_LB) return fail(h, EMCMC_STATE_ERROR, "no mix state");
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim, DP = (uint64_t)packed_n((int)D);
     if (chol_sigma_b) {
         std::vector<double> v(C * DP);

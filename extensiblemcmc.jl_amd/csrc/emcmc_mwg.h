@@ -61,7 +61,8 @@ constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, k
                    kDistBeta = 6u, kDistInverseGamma = 7u, kDistCauchy = 8u, kDistLaplace = 9u, kDistTDist = 10u;
 
 // update kinds (include/emcmc.h): EMCMC_RW_UNIFORM 1, EMCMC_RW_GAUSSIAN 2, a user update 5
-constexpr uint32_t kKindUser = 5u;
+constexpr uint32_t kKindUser = 5u, kKindMix = 3u;
+constexpr uint32_t kFaultPosdefMwg = 4u;  // EMCMC_FAULT_POSDEF
 
 // One RandomWalkUpdate (or user update), host-built; read with scalar (uniform) loads.
 struct MwgUpdate {
@@ -97,6 +98,15 @@ struct MwgUpdate {
     double pa[kMwgMaxD], pb[kMwgMaxD], pc[kMwgMaxD];  // family parameters + host-computed constants
     double pmu[kMwgMaxD], piL[kMwgMaxD];
     double pL[kMwgMaxD * kMwgMaxD];
+    // GaussianRandomWalkMix (kind 3): Σ_A in L / iL / c0 / diag, λ, and per-chain
+    // state in MwgParams::mixpool, SoA over chains: L_B packed lower row-major
+    // [n(n+1)/2][C] at lb_off, 1/L_B,ii [n][C] at lbi_off, c0_B [C] at lbc_off,
+    // a readjust scratch factor [n(n+1)/2][C] at lbs_off.  HaarioTypeAdaptation
+    // (hk = adapt_every_k_steps > 0): mean [n][C] at hm_off, cov packed lower
+    // [n(n+1)/2][C] at hc_off.
+    double lam;
+    uint32_t hk, reserved2;
+    uint64_t lb_off, lbi_off, lbc_off, lbs_off, hm_off, hc_off;
 };
 
 struct MwgParams {
@@ -122,10 +132,13 @@ struct MwgParams {
     const double *iLt;         // 1 / Lt_ii
     const double *xbar;        // [D]
     const double *obs;         // [nobs][D]
+    double *mixpool;           // GaussianRandomWalkMix / Haario per-chain state (MwgUpdate offsets)
+    double *smean, *scov;      // GenericChainStats mean [D][C] and cov packed lower [D(D+1)/2][C]
     uint64_t C;
     uint64_t row_bytes;
     uint64_t N0;
     uint32_t chain0, key0, key1, nsteps, P, W, nobs, tdiag;
+    uint32_t chain_moments, nhaario;  // update_stats! mean/cov on; number of Haario updates
     double t_c0, n_tc0, S_c, nobs_d;
 };
 
@@ -251,6 +264,9 @@ __device__ __forceinline__ double mwg_sqmahal_t(const MwgParams &a, const double
     return canon_sumsq<D, 1>(y);
 }
 
+template <int D, bool ROLL>
+__device__ __forceinline__ double mwg_sumsq_n(const double (&y)[D], uint32_t n);
+
 // ‖L⁻¹ r‖² over the first n of D local entries (the update's Σ), canonical
 // order of an n-vector: blocks of 8 when n % 8 == 0 and n ≥ 16, else one block.
 template <int D, bool ROLL = false>
@@ -270,6 +286,14 @@ __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, 
             y[i] = 0.0;
         }
     }
+    return mwg_sumsq_n<D, ROLL>(y, n);
+}
+
+// Σ y_i² over the first n of D entries in the canonical order of an n-vector:
+// blocks of 8 when n % 8 == 0 and n ≥ 16, else one block (s = y₀², s = fma(y_i, y_i, s)).
+template <int D, bool ROLL>
+__device__ __forceinline__ double mwg_sumsq_n(const double (&y)[D], uint32_t n) {
+    constexpr int UJ = ROLL ? 1 : D;
     const bool blocks = (n % 8 == 0 && n >= 16);
     if (!blocks) {
         double s = y[0] * y[0];
@@ -305,6 +329,73 @@ __device__ __forceinline__ double mwg_sqmahal_u(const MwgUpdate &u, uint32_t n, 
         nb = (nb + 1) / 2;
     }
     return b[0];
+}
+
+// ---- GaussianRandomWalkMix on the general kernel -----------------------------
+__device__ __forceinline__ uint32_t tri_idx(uint32_t i, uint32_t j) { return i * (i + 1) / 2 + j; }
+
+// The chain's own L_B (packed lower, SoA over chains in MwgParams::mixpool).
+struct MixB {
+    const double *lb, *lbi;
+    uint64_t C, chain;
+    __device__ __forceinline__ double L(uint32_t i, uint32_t j) const { return lb[(uint64_t)tri_idx(i, j) * C + chain]; }
+    __device__ __forceinline__ double iL(uint32_t i) const { return lbi[(uint64_t)i * C + chain]; }
+};
+
+// ‖L_B⁻¹ r‖², the same substitution and canonical sum as mwg_sqmahal_u
+template <int D, bool ROLL>
+__device__ __forceinline__ double mwg_sqmahal_b(const MixB &B, uint32_t n, const double (&r)[D]) {
+    constexpr int UJ = ROLL ? 1 : D;
+    double y[D];
+#pragma unroll UJ
+    for (int i = 0; i < D; ++i) {
+        if ((uint32_t)i < n) {
+            double acc = r[i];
+#pragma unroll UJ
+            for (int j = 0; j < i; ++j) acc = fma(-B.L((uint32_t)i, (uint32_t)j), y[j], acc);
+            y[i] = acc * B.iL((uint32_t)i);
+        } else {
+            y[i] = 0.0;
+        }
+    }
+    return mwg_sumsq_n<D, ROLL>(y, n);
+}
+
+// logpdf(rw::GaussianRandomWalk, a, b) (random_walk.jl:161-171) with its in-place
+// round trips (oracle orc_gsn_rw_lp): logJ = −sum(log b[pos]) folded left,
+// logpdf(MvNormal(log a, Σ), log b) + logJ, then a, b ← exp(log ·) where pos.
+// B: nullptr for the update's Σ_A, else the chain's Σ_B.
+template <int NU, bool ROLL>
+__device__ __forceinline__ double mwg_gsn_rw_lp(const MwgUpdate &u, const MixB *B, double c0, uint32_t n,
+                                                double (&a)[NU], double (&b)[NU]) {
+    constexpr int UJ = ROLL ? 1 : NU;
+    const uint64_t pm = u.posmask;
+    double x[NU], y[NU], r[NU];
+    double lj = 0.0;
+    bool first = true;
+#pragma unroll UJ
+    for (int i = 0; i < NU; ++i)
+        if ((uint32_t)i < n && ((pm >> i) & 1ull)) {
+            const double v = log_any(b[i]);
+            lj = first ? v : lj + v;
+            first = false;
+        }
+#pragma unroll UJ
+    for (int i = 0; i < NU; ++i) {
+        const bool pi = (uint32_t)i < n && ((pm >> i) & 1ull);
+        x[i] = pi ? log_any(a[i]) : a[i];
+        y[i] = pi ? log_any(b[i]) : b[i];
+        r[i] = ((uint32_t)i < n) ? y[i] - x[i] : 0.0;
+    }
+    double lp = c0 - (B ? mwg_sqmahal_b<NU, ROLL>(*B, n, r) : mwg_sqmahal_u<NU, ROLL>(u, n, r)) / 2.0;
+    if (pm) lp = lp + (-lj);
+#pragma unroll UJ
+    for (int i = 0; i < NU; ++i)
+        if ((uint32_t)i < n && ((pm >> i) & 1ull)) {
+            a[i] = exp_any(x[i]);
+            b[i] = exp_any(y[i]);
+        }
+    return lp;
 }
 
 // The built-in target: loglikelihood(P°::GsnTargetLaw, obs) (gsn_target.jl:23-29),
@@ -362,7 +453,7 @@ struct NoUserUpdate {
 // log-priors of the MH ratio.  tl: θ_local in (pos Gaussian: left as the
 // reference's in-place round trips leave it); tp: θ° (proposal history, P°);
 // ta: θ° as set_chain_param! copies it on accept.
-template <int NU, bool ROLL = false, class UPD = NoUserUpdate>
+template <int NU, bool ROLL = false, class UPD = NoUserUpdate, bool XT = false>
 __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs &zt, const MwgUpdate &u, uint32_t n,
                                                uint64_t chain, uint32_t gid, uint32_t iter, uint32_t p,
                                                double (&tl)[NU], double (&tp)[NU], double (&ta)[NU], double &ltd_fwd,
@@ -400,6 +491,8 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
     double ev[NU];  // UniformRandomWalk ϵ of each local coordinate
     const uint64_t pm = u.posmask;  // positivity-restricted coordinates
     auto isp = [&](int i) { return ((pm >> i) & 1ull) != 0ull; };
+    bool useB = false;  // GaussianRandomWalkMix: the last rand! picked gsn_B
+    const MixB mb{a.mixpool + u.lb_off, a.mixpool + u.lbi_off, C, chain};
     for (uint32_t rs = 0;; ++rs) {
         if (u.kind == 1) {  // UniformRandomWalk: θ° = θ·1 + U, or θ·e^U where pos
 #pragma unroll UJ
@@ -419,7 +512,15 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
                     }
                 }
             }
-        } else {  // GaussianRandomWalk over the update's coordinates
+        } else {  // GaussianRandomWalk over the update's coordinates; GaussianRandomWalkMix:
+                  // pick_kernel at every rand! (B iff rand() ≤ λ, random_walk.jl:225-227),
+                  // block 0xFFFFFFFE, attempt = the redraw
+            if constexpr (XT) {
+                if (u.kind == kKindMix) {
+                    const u32x4 pr = draw(a.key0, a.key1, gid, iter, 0xFFFFFFFEu, p, rs);
+                    useB = u01_closed0(pr.x, pr.y) <= u.lam;
+                }
+            }
             if (rs > 0 && pm != 0ull) {  // the previous rand! left θ ← exp(log θ) where pos
 #pragma unroll UJ
                 for (int i = 0; i < NU; ++i)
@@ -435,7 +536,11 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
             for (int i = 0; i < NU; ++i) {
                 if ((uint32_t)i < n) {
                     double lz;
-                    if (u.diag) {
+                    if (XT && useB) {
+                        lz = mb.L((uint32_t)i, 0) * z[0];
+#pragma unroll UJ
+                        for (int j = 1; j <= i; ++j) lz = fma(mb.L((uint32_t)i, (uint32_t)j), z[j], lz);
+                    } else if (u.diag) {
                         lz = u.L[i * kMwgMaxD + i] * z[i];
                     } else {
                         lz = u.L[i * kMwgMaxD] * z[0];
@@ -471,6 +576,38 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
                     ltd_fwd = (j == 0) ? f : ltd_fwd + f;
                     ltd_rev = (j == 0) ? g : ltd_rev + g;
                 }
+            }
+        }
+    } else if (XT && u.kind == kKindMix) {
+        // logpdf(rw::GaussianRandomWalkMix, a, b) = log((1−λ)·exp(logpdf(gsn_A, a, b)) +
+        // λ·exp(logpdf(gsn_B, a, b))) (random_walk.jl:229-232), each component with its
+        // round trips; ltd(__PROPOSAL) = logpdf(rw, θ°, θ) first (run.jl:271-277)
+        const double c0B = a.mixpool[u.lbc_off + chain];
+        double xa[NU], xb[NU];
+#pragma unroll UJ
+        for (int i = 0; i < NU; ++i) {
+            xa[i] = tp[i];                                                        // θ°₁
+            xb[i] = ((uint32_t)i < n && isp(i)) ? exp_any(log_any(tl[i])) : tl[i];  // θ₁
+        }
+#pragma unroll
+        for (int dir = 0; dir < 2; ++dir) {
+            const double lpA = mwg_gsn_rw_lp<NU, ROLL>(u, nullptr, u.c0, n, xa, xb);
+            const double lpB = mwg_gsn_rw_lp<NU, ROLL>(u, &mb, c0B, n, xa, xb);
+            const double t = log_any((1.0 - u.lam) * exp_any(lpA) + u.lam * exp_any(lpB));
+            if (dir == 0) ltd_rev = t;
+            else ltd_fwd = t;
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) {  // the second call is logpdf(rw, θ, θ°)
+                const double tmp = xa[i];
+                xa[i] = xb[i];
+                xb[i] = tmp;
+            }
+        }
+        if (pm) {  // two swaps: xa is θ°₅ (set_chain_param!), xb θ₅ (log_prior(::Previous))
+#pragma unroll UJ
+            for (int i = 0; i < NU; ++i) {
+                ta[i] = xa[i];
+                t3[i] = xb[i];
             }
         }
     } else {
@@ -535,14 +672,14 @@ __device__ __forceinline__ void mwg_local_step(const MwgParams &a, const ZigTabs
             ltd_fwd = (u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0) + (-lj);
         }
     }
-    if (!(u.kind == 2 && pm != 0ull)) {
+    const bool rt = ((u.kind == 2 || (XT && u.kind == kKindMix)) && pm != 0ull);  // after the pos round trips
+    if (!rt) {
 #pragma unroll UJ
         for (int j = 0; j < NU; ++j) ta[j] = tp[j];
     }
     lpp = 0.0;
     lpc = 0.0;
     if (u.prior != kPriorImproper) {
-        const bool rt = (u.kind == 2 && pm != 0ull);  // after the pos round trips: θ°₃, θ₃
         lpp = mwg_log_prior<NU, ROLL>(u, n, rt ? ta : tp);
         lpc = mwg_log_prior<NU, ROLL>(u, n, rt ? t3 : tl);
     }
@@ -600,9 +737,132 @@ __device__ __forceinline__ void mwg_register_step(const MwgParams &a, const MwgU
     }
 }
 
+// ---- GenericChainStats mean/cov and HaarioTypeAdaptation on the general kernel
+// The rank-one recurrence (chain_statistics.jl:46-49, adaptation.jl:406-414) on
+// n values, elementwise with each product rounded, over the packed lower
+// triangle (the full matrix is symmetric bit for bit: each element's operands
+// commute): old = (N−1)/N·cov + m m', m ← m·(N/(N+1)) + x/(N+1),
+// new = old + (x x')/N, cov = new − (N+1)/N·(m m').  SoA [·][C].
+template <int D, bool ROLL>
+__device__ __forceinline__ void mwg_rank1(double *mean, double *cov, const double (&x)[D], uint32_t n, uint64_t C,
+                                          uint64_t chain, uint64_t N) {
+    constexpr int UJ = ROLL ? 1 : D;
+    const double ka = (double)(N - 1) / (double)N, kb = (double)N / (double)(N + 1);
+    const double kc = (double)(N + 1) / (double)N, Np1 = (double)(N + 1), Nd = (double)N;
+    double mo[D], mn[D];
+#pragma unroll UJ
+    for (int i = 0; i < D; ++i) {
+        if ((uint32_t)i < n) {
+            mo[i] = mean[(uint64_t)i * C + chain];
+            mn[i] = mo[i] * kb + x[i] / Np1;
+            mean[(uint64_t)i * C + chain] = mn[i];
+        }
+    }
+#pragma unroll UJ
+    for (int i = 0; i < D; ++i) {
+        if ((uint32_t)i < n) {
+#pragma unroll UJ
+            for (int j = 0; j <= i; ++j) {
+                double &cv = cov[(uint64_t)tri_idx((uint32_t)i, (uint32_t)j) * C + chain];
+                const double old = ka * cv + mo[i] * mo[j];
+                const double nw = old + (x[i] * x[j]) / Nd;
+                cv = nw - kc * (mn[i] * mn[j]);
+            }
+        }
+    }
+}
+
+// readjust!(rw::GaussianRandomWalkMix, adpt, iter) (adaptation.jl:422-426): Σ_B =
+// 2.38²/n·cov, its Cholesky factor in orc_cholesky's order into the scratch,
+// then L_B, 1/L_B,ii and c0_B — or, if a pivot is not positive (the reference's
+// PosDefException at the next MvNormal), fault bit 4 and the old factor kept.
+__device__ __forceinline__ void mwg_readjust(const MwgParams &a, const MwgUpdate &v, uint64_t chain,
+                                             uint32_t &faults) {
+    const uint64_t C = a.C;
+    const uint32_t n = v.nc;
+    const double sB = (2.38 * 2.38) / (double)n;  // 2.38^2/length(rw)
+    const double *cov = a.mixpool + v.hc_off;
+    double *Ls = a.mixpool + v.lbs_off;
+    auto S = [&](uint32_t i, uint32_t j) { return sB * cov[(uint64_t)tri_idx(i > j ? i : j, i > j ? j : i) * C + chain]; };
+    auto LS = [&](uint32_t i, uint32_t j) -> double & { return Ls[(uint64_t)tri_idx(i, j) * C + chain]; };
+    for (uint32_t col = 0; col < n; ++col) {
+        double diag = S(col, col);
+        for (uint32_t k = 0; k < col; ++k) {
+            const double l = LS(col, k);
+            diag = diag - l * l;
+        }
+        if (!(diag > 0.0)) {
+            faults |= kFaultPosdefMwg;
+            return;
+        }
+        const double ljj = sqrt(diag);
+        LS(col, col) = ljj;
+        for (uint32_t row = col + 1; row < n; ++row) {
+            double t = S(col, row);
+            for (uint32_t k = 0; k < col; ++k) t = t - LS(row, k) * LS(col, k);
+            LS(row, col) = t / ljj;
+        }
+    }
+    double *lb = a.mixpool + v.lb_off, *lbi = a.mixpool + v.lbi_off;
+    double dd = 0.0;
+    for (uint32_t i = 0; i < n; ++i) {
+        for (uint32_t j = 0; j <= i; ++j) lb[(uint64_t)tri_idx(i, j) * C + chain] = LS(i, j);
+        const double dg = LS(i, i);
+        lbi[(uint64_t)i * C + chain] = 1.0 / dg;
+        dd = dd + log_pos(dg);
+    }
+    a.mixpool[v.lbc_off + chain] = -((double)n * kLog2Pi + (dd + dd)) / 2.0;
+}
+
+// After step s of update p: update_stats!' mean/cov of the whole θ (when kept),
+// then update_adaptation! of every HaarioTypeAdaptation — register! on every
+// step (register_only_on_my_turn is false both ways), the global θ at the
+// update's coordinates, log-transformed where pos and transformed back in place
+// (remove/reimpose_constraints! on the view), and readjust! on its own turn
+// when the host marks the step (flags bit 1: M reached k).  get(d) / set(d, v):
+// the chain's global θ_d.
+template <int D, bool ROLL, class GET, class SET>
+__device__ __forceinline__ void mwg_post_step(const MwgParams &a, uint64_t chain, uint32_t p, uint32_t s,
+                                              uint32_t flags, uint32_t &faults, GET get, SET set) {
+    constexpr int UJ = ROLL ? 1 : D;
+    const uint64_t N = a.N0 + s;
+    if (a.chain_moments) {
+        double x[D];
+#pragma unroll UJ
+        for (int d = 0; d < D; ++d) x[d] = get((uint32_t)d);
+        mwg_rank1<D, ROLL>(a.smean, a.scov, x, (uint32_t)D, a.C, chain, N);
+    }
+    if (a.nhaario == 0) return;
+    for (uint32_t q = 0; q < a.P; ++q) {
+        const MwgUpdate &v = a.updates[q];
+        if (!v.hk) continue;
+        const uint32_t n = v.nc;
+        const uint64_t pm = v.posmask;
+        double x[D];
+#pragma unroll UJ
+        for (int j = 0; j < D; ++j) {
+            x[j] = 0.0;
+            if ((uint32_t)j < n) {
+                const double t = get(v.coords[j]);
+                x[j] = ((pm >> j) & 1ull) ? log_any(t) : t;
+            }
+        }
+        mwg_rank1<D, ROLL>(a.mixpool + v.hm_off, a.mixpool + v.hc_off, x, n, a.C, chain, N);
+        if (pm) {
+#pragma unroll UJ
+            for (int j = 0; j < D; ++j)
+                if ((uint32_t)j < n && ((pm >> j) & 1ull)) set(v.coords[j], exp_any(x[j]));
+        }
+        if (q == p && (flags & 2u)) mwg_readjust(a, v, chain, faults);
+    }
+}
+
 // One lane per chain; θ and P°.θ in registers, coordinates moved between global
 // and update-local order by selects over the compile-time D (D ≤ 16).
-template <int D, bool FULL, int LLMODE, class TGT = GsnTarget, class UPD = NoUserUpdate>
+// XT: GaussianRandomWalkMix updates, HaarioTypeAdaptation and GenericChainStats
+// mean/cov compiled in (the ahead-of-time instantiations leave them out; the
+// library compiles XT kernels at run time when a schedule needs them).
+template <int D, bool FULL, int LLMODE, class TGT = GsnTarget, class UPD = NoUserUpdate, bool XT = false>
 __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
     static_assert(D <= 16, "register-state MWG kernel: D ≤ 16 (mwg_wide_kernel below for larger D)");
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
@@ -639,8 +899,10 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
             tl[j] = v;
         }
         double ltd_fwd, ltd_rev, lpp, lpc;
-        mwg_local_step<D, false, UPD>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
-                                      faults);
+        // XT kernels keep the update-local loops rolled: the mixture densities would
+        // otherwise unroll four triangular solves per direction (minutes of hiprtc time)
+        mwg_local_step<D, XT, UPD, XT>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
+                                       faults);
         // ---- set_proposal!: proposal history and P°.θ[coords] ← θ°
         double prop[D], nst[D];
 #pragma unroll
@@ -682,6 +944,19 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
             __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
         }
         mwg_register_step(a, u, n, chain, iter, p, s, flags, slot, acc);
+        if (XT && (a.chain_moments | a.nhaario))
+            mwg_post_step<D, true>(
+                a, chain, p, s, flags, faults,
+                [&](uint32_t c) {
+                    double v = 0.0;
+#pragma unroll
+                    for (int d = 0; d < D; ++d) v = (c == (uint32_t)d) ? th[d] : v;
+                    return v;
+                },
+                [&](uint32_t c, double v) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) th[d] = (c == (uint32_t)d) ? v : th[d];
+                });
     }
 #pragma unroll
     for (int d = 0; d < D; ++d) {
@@ -698,12 +973,12 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 // wave-uniform indices, so no select network over D is needed; only the
 // update's NU-sized local vectors and, for the likelihood, P°.θ live in
 // registers.  The arithmetic is mwg_gsn_kernel's.
-template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget, class UPD = NoUserUpdate>
+template <int D, int NU, bool FULL, int LLMODE, class TGT = GsnTarget, class UPD = NoUserUpdate, bool XT = false>
 __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
     static_assert(NU <= D && D <= kMwgMaxD, "NU ≤ D ≤ 64");
     // loops over the update's NU coordinates and over the target's D stay rolled
     // only for the largest updates: unrolled, the local vectors live in registers
-    constexpr bool RU = NU > 16;
+    constexpr bool RU = NU > 16 || XT;  // XT: rolled, as in mwg_gsn_kernel
     constexpr bool RT = NU > 16;
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -723,7 +998,8 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
         double tl[NU], tp[NU], ta[NU];
         for (int j = 0; j < NU; ++j) tl[j] = ((uint32_t)j < n) ? a.theta[state_pos(u.coords[j], chain, C, D)] : 0.0;
         double ltd_fwd, ltd_rev, lpp, lpc;
-        mwg_local_step<NU, RU, UPD>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc, faults);
+        mwg_local_step<NU, RU, UPD, XT>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
+                                        faults);
         // ---- set_proposal!: P°.θ[coords] ← θ°, then all of P°.θ for the likelihood
         for (int j = 0; j < NU; ++j)
             if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tp[j];
@@ -758,6 +1034,10 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
             __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
         }
         mwg_register_step(a, u, n, chain, iter, p, s, flags, slot, acc);
+        if (XT && (a.chain_moments | a.nhaario))
+            mwg_post_step<D, true>(
+                a, chain, p, s, flags, faults, [&](uint32_t c) { return a.theta[state_pos(c, chain, C, D)]; },
+                [&](uint32_t c, double v) { a.theta[state_pos(c, chain, C, D)] = v; });
     }
     a.ll[chain] = ll;
     a.faults[chain] = faults;

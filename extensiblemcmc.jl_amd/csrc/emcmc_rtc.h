@@ -38,9 +38,10 @@ struct RtcKernel {
 // success, else the compiler's log.
 int rtc_wide_nu(int D, int nmax);
 // usrc / uopts: a user update's EMCMC_USER_PROPOSAL + EMCMC_USER_LTD source (empty: none)
+// xt: compile GaussianRandomWalkMix / Haario / chain moments in (emcmc_mwg.h XT)
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
                              RtcKernel &out, const std::string &usrc = std::string(),
-                             const std::string &uopts = std::string());
+                             const std::string &uopts = std::string(), bool xt = false);
 
 // The text of a law the library ships as an EMCMC_USER_LOGLIK source
 // (csrc/laws/<name>), or nullptr.
@@ -49,6 +50,7 @@ const char *rtc_builtin_law(const char *name);
 // The same kernel with the built-in GsnTargetLaw (emcmc_mwg.h GsnTarget) for a
 // dimension the library has no ahead-of-time instantiation of (inst_mwg.hip).
 std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out,
-                            const std::string &usrc = std::string(), const std::string &uopts = std::string());
+                            const std::string &usrc = std::string(), const std::string &uopts = std::string(),
+                            bool xt = false);
 
 }  // namespace emcmc

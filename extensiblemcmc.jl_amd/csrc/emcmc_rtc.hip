@@ -86,12 +86,14 @@ std::string program_log(hiprtcProgram p) {
 int rtc_wide_nu(int D, int nmax) { return (D > 16 && nmax <= 16) ? 16 : D; }
 
 std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
-                        RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string()) {
+                        RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string(),
+                        bool xt = false) {
     if (D < 1 || D > 64) return "the general schedule kernel runs 1 ≤ D ≤ 64";
     if (nu < 1 || nu > D) nu = D;
     const bool user = !src.empty(), upd = !usrc.empty();
     std::ostringstream key;
-    key << D << '|' << nu << '|' << full << '|' << ll << '|' << opts << '|' << src << '|' << uopts << '|' << usrc;
+    key << D << '|' << nu << '|' << full << '|' << ll << '|' << xt << '|' << opts << '|' << src << '|' << uopts << '|'
+        << usrc;
     {
         std::lock_guard<std::mutex> lk(g_mu);
         auto it = g_cache.find(key.str());
@@ -104,16 +106,19 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     const char *fl = full ? "true" : "false";
     const char *tgt = user ? "emcmc::UserTarget" : "emcmc::GsnTarget";
     const char *ut = upd ? "emcmc::UserUpdate" : "emcmc::NoUserUpdate";
+    const char *xs = xt ? "true" : "false";
     if (D <= 16) {
-        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ", " << ut << ">";
+        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ", " << ut << ", " << xs
+             << ">";
         name << "mwg_gsn_kernel<D=" << D;
     } else {
         expr << "emcmc::mwg_wide_kernel<" << D << ", " << nu << ", " << fl << ", " << ll << ", " << tgt << ", " << ut
-             << ">";
+             << ", " << xs << ">";
         name << "mwg_wide_kernel<D=" << D << ",NU=" << nu;
     }
     name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
-         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << (upd ? ",UserUpdate" : "") << "[hiprtc]>";
+         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << (upd ? ",UserUpdate" : "")
+         << (xt ? ",MIX_MOMENTS" : "") << "[hiprtc]>";
     std::string prog_src = std::string(kPrelude);
     if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
     if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
@@ -162,9 +167,9 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
 }
 
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
-                             RtcKernel &out, const std::string &usrc, const std::string &uopts) {
+                             RtcKernel &out, const std::string &usrc, const std::string &uopts, bool xt) {
     if (src.empty()) return "empty user source";
-    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts);
+    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts, xt);
 }
 
 const char *rtc_builtin_law(const char *name) {
@@ -174,8 +179,8 @@ const char *rtc_builtin_law(const char *name) {
 }
 
 std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out, const std::string &usrc,
-                            const std::string &uopts) {
-    return rtc_compile("", "", D, full, ll_mode, nu, out, usrc, uopts);
+                            const std::string &uopts, bool xt) {
+    return rtc_compile("", "", D, full, ll_mode, nu, out, usrc, uopts, xt);
 }
 
 }  // namespace emcmc

@@ -224,6 +224,7 @@ SIGNATURES = {
     "emcmc_get_proposal_ll": (_ST, [_H, C.POINTER(C.c_double)]),
     "emcmc_get_chain_moments": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_get_mix_state": (_ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_uint32)]),
+    "emcmc_get_adaptation_moments": (_ST, [_H, C.c_uint32, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "emcmc_get_history": (_ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]),
     "emcmc_get_history_chains": (
         _ST, [_H, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]

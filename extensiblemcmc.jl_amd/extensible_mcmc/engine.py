@@ -87,6 +87,8 @@ class Engine:
             raise L.EMCMCError(st, "emcmc_create", "" if st != L.NO_DEVICE else "no HIP device visible")
         self._h = h
         self.num_updates = 0
+        self._update_n = []  # coordinates per update (shapes of per-update read-backs)
+        self._cb_error = None  # an exception raised inside a host callback (fλ), re-raised after emcmc_run
 
     # -- plumbing -------------------------------------------------------------
     def _check(self, st: int, where: str):
@@ -157,6 +159,7 @@ class Engine:
             u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
+        self._update_n.append(int(len(coords)))
 
     def add_uniform_rw_update(self, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):
         """UniformRandomWalk(ϵ) on coords0 (0-based); adapt: None or a dict with
@@ -190,18 +193,20 @@ class Engine:
             u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
+        self._update_n.append(int(len(coords)))
 
     def add_gaussian_rw_mix_update(self, coords0, sigma_a, sigma_b, lam=0.5, haario_k=None, haario_scale=2.38 ** 2,
-                                   prior=L.PRIOR_IMPROPER, pos=None):
+                                   prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):
         """GaussianRandomWalkMix(Σ_A, Σ_B, λ) on coords0 (0-based); haario_k: None
         or HaarioTypeAdaptation's adapt_every_k_steps."""
         coords = np.ascontiguousarray(coords0, dtype=np.uint32)
         n = len(coords)
         SA = np.ascontiguousarray(np.asarray(sigma_a, dtype=np.float64).reshape(n, n).ravel(order="F"))
         SB = np.ascontiguousarray(np.asarray(sigma_b, dtype=np.float64).reshape(n, n).ravel(order="F"))
+        keep = []
         u = L.EmcmcUpdateDesc()
         u.kernel = L.RW_GAUSSIAN_MIX
-        u.prior = prior
+        self._prior_desc(u, prior, prior_factors, keep)
         u.num_coords = n
         u.coords = L.u32ptr(coords)
         u.sigma = L.dptr(SA)
@@ -217,6 +222,7 @@ class Engine:
             u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
+        self._update_n.append(int(len(coords)))
 
     def add_user_update(self, coords0, source, params=(), options="", prior=L.PRIOR_IMPROPER, prior_factors=None):
         """A user-defined update on coords0 (0-based): its proposal! and
@@ -236,6 +242,7 @@ class Engine:
         u.user_update = C.cast(C.pointer(ud), C.c_void_p)
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
+        self._update_n.append(int(len(coords)))
 
     def add_mala_update(self, coords0, eps, prior=L.PRIOR_IMPROPER):
         """MALA with step size ϵ on coords0 (0-based; the engine's definition of
@@ -250,6 +257,7 @@ class Engine:
         u.epsilon = L.dptr(e)
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
+        self._update_n.append(int(len(coords)))
 
     def set_logistic_target(self, X, y):
         """Logistic regression: ℓ(θ) = Σ_n y_n x_nᵀθ − log(1 + exp(x_nᵀθ))."""
@@ -266,6 +274,7 @@ class Engine:
     def add_update_desc(self, u: L.EmcmcUpdateDesc, keepalive=()):
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
+        self._update_n.append(int(len(coords)))
 
     def set_gsn_target(self, mu, sigma, obs, ll_mode=L.LL_PER_OBS):
         mu = np.ascontiguousarray(mu, dtype=np.float64)
@@ -318,7 +327,11 @@ class Engine:
         if n == 0:
             return
         ptr = arr.ctypes.data_as(C.POINTER(L.EmcmcStep))
-        self._check(self._lib.emcmc_run(self._h, ptr, n), "emcmc_run")
+        st = self._lib.emcmc_run(self._h, ptr, n)
+        if self._cb_error is not None:  # fλ raised on the host while emcmc_run enqueued a readjust
+            e, self._cb_error = self._cb_error, None
+            raise e
+        self._check(st, "emcmc_run")
 
     def run_iters(self, iter_first: int, n: int, pidx: int = 1):
         it = np.arange(iter_first, iter_first + n, dtype=np.uint32)
@@ -374,9 +387,18 @@ class Engine:
         self._check(self._lib.emcmc_get_chain_moments(self._h, L.dptr(m), L.dptr(v)), "emcmc_get_chain_moments")
         return m, v
 
+    def get_adaptation_moments(self, pidx: int = 1):
+        """HaarioTypeAdaptation (mean [C][n], cov [C][n][n]) of update pidx."""
+        Cn, n = self.cfg.num_chains, self._update_n[pidx - 1]
+        m = np.empty((Cn, n), dtype=np.float64)
+        v = np.empty((Cn, n, n), dtype=np.float64)
+        self._check(self._lib.emcmc_get_adaptation_moments(self._h, pidx, L.dptr(m), L.dptr(v)),
+                    "emcmc_get_adaptation_moments")
+        return m, v
+
     def get_mix_state(self, pidx: int = 1):
-        """(lower Cholesky factor of each chain's Σ_B [C][D][D], Haario M)."""
-        Cn, D = self.cfg.num_chains, self.cfg.dim
+        """(lower Cholesky factor of each chain's Σ_B [C][n][n], Haario M)."""
+        Cn, D = self.cfg.num_chains, self._update_n[pidx - 1]
         Lb = np.empty((Cn, D, D), dtype=np.float64)
         M = C.c_uint32()
         self._check(self._lib.emcmc_get_mix_state(self._h, pidx, L.dptr(Lb), C.byref(M)), "emcmc_get_mix_state")
@@ -385,7 +407,14 @@ class Engine:
     def set_mix_lambda_fn(self, pidx: int, f):
         """HaarioTypeAdaptation's fλ(λ, N, mcmc_iter) (adaptation.jl:425), called on the
         host at each readjust; None restores the identity."""
-        cb = L.LAMBDA_FN(lambda lam, N, it, ctx: float(f(lam, int(N), int(it)))) if f is not None else L.LAMBDA_FN()
+        def tramp(lam, N, it, ctx):  # an exception cannot cross the C ABI: keep it for run() to raise
+            try:
+                return float(f(lam, int(N), int(it)))
+            except BaseException as e:  # noqa: BLE001
+                self._cb_error = e
+                return lam
+
+        cb = L.LAMBDA_FN(tramp) if f is not None else L.LAMBDA_FN()
         self._flam = cb  # keep the trampoline alive while the handle may call it
         self._check(self._lib.emcmc_set_mix_lambda_fn(self._h, pidx, cb, None), "emcmc_set_mix_lambda_fn")
 

@@ -590,17 +590,14 @@ class RandomWalkUpdate(MCMCParamUpdate):
         else:
             raise UnsupportedPlugin(f"adaptation {type(self.adpt).__name__} has no device plugin for "
                                     f"{type(self.rw).__name__} yet")
-        pos = getattr(self.rw, "pos", None)
         if isinstance(self.rw, GaussianRandomWalkMix):
-            pos = np.concatenate([self.rw.gsn_A.pos, self.rw.gsn_B.pos])
-        if np.any(pos if pos is not None else False) and isinstance(self.rw, GaussianRandomWalkMix):
-            raise UnsupportedPlugin("positivity-restricted coordinates have no device plugin for "
-                                    "GaussianRandomWalkMix yet")
-        if isinstance(self.rw, GaussianRandomWalkMix):
+            # the same pos for both components (random_walk.jl:198-205)
+            pos = self.rw.gsn_A.pos
             engine.add_gaussian_rw_mix_update(coords0, self.rw.gsn_A.Sigma, self.rw.gsn_B.Sigma, lam=self.rw.lam,
                                               haario_k=None if adapt is None else adapt["k"],
                                               haario_scale=2.38 ** 2 if adapt is None else adapt["scale"],
-                                              prior=prior)
+                                              prior=prior, prior_factors=factors,
+                                              pos=pos if np.any(pos) else None)
             if isinstance(self.adpt, HaarioTypeAdaptation) and not self.adpt.identity_f:
                 # fλ(λ, N, mcmc_iter): one λ for all chains, called on the host at each readjust
                 engine.set_mix_lambda_fn(engine.num_updates, self.adpt.f)
@@ -623,7 +620,7 @@ class RandomWalkUpdate(MCMCParamUpdate):
             Lb, M = engine.get_mix_state(pidx)
             self.rw.gsn_B.chol_chains = Lb
             if isinstance(self.adpt, HaarioTypeAdaptation):
-                self.adpt.mean_chains, self.adpt.cov_chains = engine.get_chain_moments()
+                self.adpt.mean_chains, self.adpt.cov_chains = engine.get_adaptation_moments(pidx)
                 self.adpt.M = M
             self.rw.lam = engine.get_mix_lambda(pidx)  # rw.λ after fλ (adaptation.jl:425)
         if isinstance(self.rw, UniformRandomWalk):

@@ -329,11 +329,10 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
                                pointer(Σ), C_NULL, pointer(pos), C_NULL, C_NULL, pp, C_NULL, 0.0,
                                (0.0, 0.0, 0.0))
     elseif updt.rw isa eMCMC.GaussianRandomWalkMix                # random_walk.jl:193-232
-        (any(updt.rw.gsn_A.pos) || any(updt.rw.gsn_B.pos)) &&
-            error("positivity-restricted coordinates are not on device yet")
         ΣA = Matrix{Float64}(updt.rw.gsn_A.Σ)
         ΣB = Matrix{Float64}(updt.rw.gsn_B.Σ)
-        push!(keep, ΣA, ΣB)
+        pos = UInt8.(updt.rw.gsn_A.pos)                           # both components share pos (:198-205)
+        push!(keep, ΣA, ΣB, pos)
         if updt.adpt isa eMCMC.HaarioTypeAdaptation              # adaptation.jl:372-426 (fλ must be identity)
             p = Ref(EmcmcHaarioAdaptation(UInt32(updt.adpt.adapt_every_k_steps), UInt32(0), updt.adpt.scale))
             push!(keep, p)
@@ -342,7 +341,7 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
             error("no device plugin for $(typeof(updt.adpt)) with GaussianRandomWalkMix")
         end
         return EmcmcUpdateDesc(RW_GAUSSIAN_MIX, pk, adpt, UInt32(length(coords)), pointer(coords),
-                               pointer(ΣA), C_NULL, C_NULL, adptp, pointer(ΣB), pp, C_NULL, updt.rw.λ,
+                               pointer(ΣA), C_NULL, pointer(pos), adptp, pointer(ΣB), pp, C_NULL, updt.rw.λ,
                                (0.0, 0.0, 0.0))
     elseif updt.rw isa eMCMC.UniformRandomWalk                      # random_walk.jl:45-94, pos included
         ϵ = Float64.(collect(updt.rw.ϵ))
@@ -594,12 +593,27 @@ GaussianRandomWalkMix: lower Cholesky factor of every chain's Σ_B and
 HaarioTypeAdaptation's own-turn count since the last readjust (adaptation.jl:399-426).
 """
 function mix_state(gws::MI355XGlobalWorkspace, pidx::Integer)
-    C, D = gws.backend.num_chains, gws.dim
+    C, D = gws.backend.num_chains, gws.num_coords[pidx]
     L = Array{Float64}(undef, D, D, C)     # [C][D][D] row-major, transposed below
     M = Ref{UInt32}(0)                     # the same for every chain
     check(ccall((:emcmc_get_mix_state, LIB), Cint, (Ptr{Cvoid}, UInt32, Ptr{Float64}, Ref{UInt32}),
                 gws.handle, UInt32(pidx), L, M), gws.handle, "emcmc_get_mix_state")
     permutedims(L, (2, 1, 3)), Int(M[])
+end
+
+"""
+    adaptation_moments(gws, pidx) -> (mean::Matrix{Float64} (C, n), cov::Array{Float64,3} (n, n, C))
+
+HaarioTypeAdaptation's own running mean/cov of update `pidx` (adaptation.jl:406-414):
+the update's coordinates, log scale where pos, registered after every update step.
+"""
+function adaptation_moments(gws::MI355XGlobalWorkspace, pidx::Integer)
+    C, n = gws.backend.num_chains, gws.num_coords[pidx]
+    m = Matrix{Float64}(undef, n, C)
+    cov = Array{Float64}(undef, n, n, C)
+    check(ccall((:emcmc_get_adaptation_moments, LIB), Cint, (Ptr{Cvoid}, UInt32, Ptr{Float64}, Ptr{Float64}),
+                gws.handle, UInt32(pidx), m, cov), gws.handle, "emcmc_get_adaptation_moments")
+    permutedims(m), cov
 end
 
 """
@@ -806,7 +820,7 @@ eMCMC.state°(lws::MI355XLocalWorkspace) = lws.sub_ws°.state
 eMCMC.name_of_update(lws::MI355XLocalWorkspace) = lws.updt_name
 
 export MI355XBackend, state_history, proposal_history, ll_history, acceptance_history, rolling_acceptance,
-       adaptation_state, chain_moments, mix_state, faults, moments_window, kernel_name, device_count,
+       adaptation_state, chain_moments, adaptation_moments, mix_state, faults, moments_window, kernel_name, device_count,
        HipTargetLaw, HipUpdate
 
 end # module

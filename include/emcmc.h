@@ -153,8 +153,8 @@ typedef struct emcmc_config {
     uint32_t steps_per_launch; /* 0 = auto (64) */
     uint32_t kernel_variant;   /* 0 = auto; EMCMC_VARIANT_* tuning flags (results are identical) */
     uint32_t chain_moments;    /* 1 = keep GenericChainStats mean/cov (chain_statistics.jl:46-49) on
-                                  device for a single joint GaussianRandomWalk update (always on with
-                                  GaussianRandomWalkMix); read with emcmc_get_chain_moments */
+                                  device, after every update step of any schedule (always on with a
+                                  single joint GaussianRandomWalkMix); read with emcmc_get_chain_moments */
     uint32_t history_ring;     /* iterations of history kept on device as a ring (0 = all num_mcmc_steps);
                                   older iterations are streamed out with emcmc_stream_history */
     uint32_t reserved[4];
@@ -275,9 +275,9 @@ typedef struct emcmc_update_desc {
     const uint32_t *coords;   /* 0-based indices into θ (reference coords are 1-based), any order */
     const double *sigma;      /* GaussianRandomWalk Σ, GaussianRandomWalkMix Σ_A: num_coords² column-major */
     const double *epsilon;    /* UniformRandomWalk ϵ: num_coords */
-    const uint8_t *pos;       /* positivity flags or NULL (all false); true on device for UniformRandomWalk
-                                 (θ° = θ·e^U, random_walk.jl:63-94) and GaussianRandomWalk (log scale,
-                                 random_walk.jl:136-171; D ≤ 64), not for GaussianRandomWalkMix */
+    const uint8_t *pos;       /* positivity flags or NULL (all false): UniformRandomWalk (θ° = θ·e^U,
+                                 random_walk.jl:63-94), GaussianRandomWalk and GaussianRandomWalkMix (log
+                                 scale with the in-place round trips, random_walk.jl:136-232; D ≤ 64) */
     const void *adaptation_params; /* const emcmc_unifrw_adaptation* (EMCMC_ADPT_UNIF_RW),
                                       const emcmc_unifrw_adaptation_vec* (EMCMC_ADPT_UNIF_RW_VEC) or
                                       const emcmc_haario_adaptation* (EMCMC_ADPT_HAARIO) */
@@ -416,15 +416,23 @@ emcmc_status emcmc_get_update_state(emcmc_handle *h, uint32_t pidx, double *epsi
                                     uint32_t *accepted);
 
 /* GenericChainStats running mean and covariance of θ (chain_statistics.jl:46-49,
- * phantom zero sample included), per chain: mean [C][D], cov [C][D][D]
- * (symmetric).  Kept on device by the mix kernels (and with
- * emcmc_config.chain_moments); EMCMC_STATE_ERROR otherwise.  Either may be NULL.
+ * phantom zero sample included), updated after every update step, per chain:
+ * mean [C][D], cov [C][D][D] (symmetric).  Kept on device with
+ * emcmc_config.chain_moments (any schedule) and with a single joint
+ * GaussianRandomWalkMix update; EMCMC_STATE_ERROR otherwise.  Either may be NULL.
  * With HaarioTypeAdaptation and P = 1 these equal the adaptation's mean/cov
  * (same recurrence on the same θ, adaptation.jl:406-414). */
 emcmc_status emcmc_get_chain_moments(emcmc_handle *h, double *mean, double *cov);
 
+/* HaarioTypeAdaptation mean and cov of update `pidx` (adaptation.jl:372-414):
+ * its own running moments of the update's coordinates (log scale where pos), per
+ * chain: mean [C][n], cov [C][n][n].  They register after every update step of
+ * the schedule (register_only_on_my_turn is false both ways); for a single joint
+ * update they equal emcmc_get_chain_moments.  Either may be NULL. */
+emcmc_status emcmc_get_adaptation_moments(emcmc_handle *h, uint32_t pidx, double *mean, double *cov);
+
 /* GaussianRandomWalkMix state of update `pidx`: the lower Cholesky factor of
- * each chain's current Σ_B ([C][D][D], row-major, zeros above the diagonal),
+ * each chain's current Σ_B ([C][n][n], row-major, zeros above the diagonal),
  * and HaarioTypeAdaptation's M (own-turn steps since the last readjust).
  * Either may be NULL. */
 emcmc_status emcmc_get_mix_state(emcmc_handle *h, uint32_t pidx, double *chol_sigma_b, uint32_t *steps_since_adapt);

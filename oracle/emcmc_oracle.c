@@ -836,6 +836,77 @@ typedef void (*orc_user_prop_fn)(const double *theta, double *theta_prop, int n,
                                  emcmc_rng *rng);
 typedef double (*orc_user_ltd_fn)(const double *x, const double *y, int n, const double *params);
 
+#define ORC_FAULT_POSDEF 4u
+
+static void mix_factor_consts(const double *L, int D, double *iL, double *c0) {
+    for (int i = 0; i < D; ++i) iL[i] = 1.0 / L[(size_t)i * D + i];
+    *c0 = mvnormal_c0(D, logdet_chol(L, D));
+}
+
+/* GaussianRandomWalkMix / HaarioTypeAdaptation / GenericChainStats mean-cov
+ * state of the general schedule (kind 3 updates; chain moments for any P).
+ * Per update p, per chain c: L_B (lower, row-major n_p × n_p) at
+ * LB + off_sq[p] + c·n_p², the Haario mean at hmean + off_v[p] + c·n_p and cov
+ * at hcov + off_sq[p] + c·n_p²; M_io[p] Haario's M (uniform over chains);
+ * smean [C][D], scov [C][D][D] the chain's running mean/cov of θ. */
+typedef struct orc_mwg_ext {
+    const double *mix_lam;    /* [P] λ of each GaussianRandomWalkMix update */
+    const uint32_t *haario_k; /* [P] adapt_every_k_steps, 0: no HaarioTypeAdaptation */
+    uint32_t *M_io;           /* [P] */
+    double *LB, *hmean, *hcov;
+    const uint64_t *off_sq, *off_v;
+    int chain_moments;
+    int reserved;
+    double *smean, *scov;
+} orc_mwg_ext;
+
+/* logpdf(rw::GaussianRandomWalk, a, b) (random_walk.jl:161-171) with its
+ * in-place round trips: logJ = −sum(log b[pos]) (left fold; only where a
+ * coordinate is restricted), logpdf(MvNormal(log a, Σ), log b) + logJ, then
+ * a ← exp(log a), b ← exp(log b) at the restricted coordinates. */
+static double orc_gsn_rw_lp(const double *L, const double *iL, double c0, int diag, const uint8_t *pos, uint32_t n,
+                            int anypos, double *a, double *b) {
+    double x[ORC_MWG_MAXD], y[ORC_MWG_MAXD], r[ORC_MWG_MAXD], lj = 0.0;
+    int first = 1;
+    for (uint32_t i = 0; i < n; ++i)
+        if (pos[i]) {
+            const double v = orc_log_any(b[i]);
+            lj = first ? v : lj + v;
+            first = 0;
+        }
+    for (uint32_t i = 0; i < n; ++i) {
+        x[i] = pos[i] ? orc_log_any(a[i]) : a[i];
+        y[i] = pos[i] ? orc_log_any(b[i]) : b[i];
+        r[i] = y[i] - x[i];
+    }
+    double lp = c0 - sqmahal(L, iL, r, (int)n, diag) / 2.0;
+    if (anypos) lp = lp + (-lj);
+    for (uint32_t i = 0; i < n; ++i)
+        if (pos[i]) {
+            a[i] = orc_exp_any(x[i]);
+            b[i] = orc_exp_any(y[i]);
+        }
+    return lp;
+}
+
+/* GenericChainStats / Haario register! recurrence on n values (chain_statistics.jl:46-49,
+ * adaptation.jl:406-414): old = (N−1)/N·cov + m m', m ← m·(N/(N+1)) + θ/(N+1),
+ * new = old + (θθ')/N, cov = new − (N+1)/N·(m m'), elementwise, products rounded */
+static void orc_rank1_register(double *m, double *cv, const double *x, uint32_t n, uint64_t N) {
+    const double a = (double)(N - 1) / (double)N;
+    const double b = (double)N / (double)(N + 1);
+    const double cN = (double)(N + 1) / (double)N;
+    double mo[ORC_MWG_MAXD];
+    memcpy(mo, m, sizeof(double) * n);
+    for (uint32_t i = 0; i < n; ++i) m[i] = m[i] * b + x[i] / (double)(N + 1);
+    for (uint32_t i = 0; i < n; ++i)
+        for (uint32_t j = 0; j < n; ++j) {
+            const double old_sq = a * cv[(size_t)i * n + j] + mo[i] * mo[j];
+            const double new_sq = old_sq + (x[i] * x[j]) / (double)N;
+            cv[(size_t)i * n + j] = new_sq - cN * (m[i] * m[j]);
+        }
+}
+
 /* table layout from Python (ORC_MWG_MAXD = 64 slots per update):
  *   kind[P], nc[P], coords[P*64], eps[P*64], sigma[P*4096] (nc×nc column-major),
  *   pos[P*64] (uint8), adapt[P], k[P], aparams[P*257] = (target, scale[64], min[64], max[64], offset[64])
@@ -856,7 +927,7 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                            const double *fb, double *ll_prop, orc_user_loglik_fn user_ll,
                            const double *user_params, const uint32_t *pcfam, const double *pca, const double *pcb,
                            const double *pmvmu, const double *pmvS, orc_user_prop_fn user_prop,
-                           orc_user_ltd_fn user_ltd, const double *user_uparams) {
+                           orc_user_ltd_fn user_ltd, const double *user_uparams, const orc_mwg_ext *ext) {
     if (D < 1 || D > ORC_MWG_MAXD || P < 1 || P > 64) return -2;
     (void)zig();
     orc_gsn *g = (orc_gsn *)malloc(sizeof(orc_gsn));
@@ -891,7 +962,12 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 return -2;
             }
         }
-        if (u->kind == 2) {
+        if ((u->kind == 3 || (ext && ext->haario_k && ext->haario_k[p])) && !ext) {
+            free(g);
+            free(U);
+            return -2;
+        }
+        if (u->kind == 2 || u->kind == 3) {
             const int n = (int)u->nc;
             if (orc_cholesky(sigma + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD, n, u->L)) {
                 free(g);
@@ -941,8 +1017,9 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
         memcpy(mp, mu_p + c * D, sizeof(double) * D);
         double cll = ll[c];
         uint32_t f = faults[c];
-        uint32_t last[64];
+        uint32_t last[64], Mloc[64];
         memcpy(last, last0, sizeof(uint32_t) * P);
+        for (uint32_t q = 0; q < P; ++q) Mloc[q] = (ext && ext->M_io) ? ext->M_io[q] : 0u;
         for (uint32_t s = 0; s < nsteps; ++s) {
             const uint32_t iter = step_iter[s], p = step_pidx[s] - 1;
             const orc_mwg_update *u = &U[p];
@@ -950,6 +1027,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             double *ep = eps_state + ((size_t)p * C + c) * ORC_MWG_MAXD;
             double tl[ORC_MWG_MAXD], tp[ORC_MWG_MAXD], ta[ORC_MWG_MAXD];
             int accept_ta = 0; /* accepted values differ from the proposal (Gaussian with pos) */
+            int useB = 0;      /* GaussianRandomWalkMix: the last rand! picked gsn_B */
+            (void)useB;
             for (uint32_t j = 0; j < n; ++j) tl[j] = th[u->coords[j]];
             double ltd_fwd = 0.0, ltd_rev = 0.0;
             int anypos = 0;
@@ -976,7 +1055,16 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                         const double Uv = a + (b - a) * uu;
                         tp[j] = u->pos[j] ? tl[j] * orc_exp_any(Uv) + copysign(0.0, Uv) : tl[j] * 1.0 + Uv;
                     }
-                } else { /* GaussianRandomWalk over the update's coordinates */
+                } else { /* GaussianRandomWalk over the update's coordinates; GaussianRandomWalkMix:
+                          * pick_kernel (B iff rand() ≤ λ, random_walk.jl:225-227) at every rand!,
+                          * from block 0xFFFFFFFE, attempt = the redraw */
+                    const double *Lx = u->L;
+                    int dg = u->diag;
+                    if (u->kind == 3) {
+                        const orc_u32x4 pr = orc_draw(k0, k1, chain_id, iter, 0xFFFFFFFEu, p, rs);
+                        useB = orc_u01_closed0(pr.v[0], pr.v[1]) <= ext->mix_lam[p];
+                        if (useB) Lx = ext->LB + ext->off_sq[p] + c * (uint64_t)n * n, dg = 0;
+                    }
                     if (rs > 0) /* the previous rand! left θ ← exp(log θ) where pos */
                         for (uint32_t i = 0; i < n; ++i)
                             if (u->pos[i]) tl[i] = orc_exp_any(orc_log_any(tl[i]));
@@ -984,11 +1072,11 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                     for (uint32_t j = 0; j < n; ++j) z[j] = orc_normal(zt, k0, k1, chain_id, iter, p, (rs << 17) | j, &f);
                     for (uint32_t i = 0; i < n; ++i) {
                         double lz;
-                        if (u->diag) {
-                            lz = u->L[(size_t)i * n + i] * z[i];
+                        if (dg) {
+                            lz = Lx[(size_t)i * n + i] * z[i];
                         } else {
-                            lz = u->L[(size_t)i * n] * z[0];
-                            for (uint32_t j = 1; j <= i; ++j) lz = fma(u->L[(size_t)i * n + j], z[j], lz);
+                            lz = Lx[(size_t)i * n] * z[0];
+                            for (uint32_t j = 1; j <= i; ++j) lz = fma(Lx[(size_t)i * n + j], z[j], lz);
                         }
                         /* remove_constraints!: θ_i ← log θ_i where pos (random_walk.jl:136);
                          * reimpose_constraints!: θ°_i ← exp θ°_i (θ°₁) */
@@ -1006,6 +1094,39 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             double t3[ORC_MWG_MAXD]; /* θ as log_prior(::Previous) reads it */
             if (u->kind == 5) {
                 /* transition densities done above */
+            } else if (u->kind == 3) {
+                /* logpdf(rw::GaussianRandomWalkMix, a, b) = log((1−λ)·exp(logpdf(gsn_A, a, b)) +
+                 * λ·exp(logpdf(gsn_B, a, b))) (random_walk.jl:229-232), each component's logpdf
+                 * with its own round trips on a and b; ltd(__PROPOSAL) = logpdf(rw, θ°, θ) is
+                 * evaluated first (run.jl:271-277) */
+                const double lam = ext->mix_lam[p];
+                const double *Lb = ext->LB + ext->off_sq[p] + c * (uint64_t)n * n;
+                double iLb[ORC_MWG_MAXD], c0b;
+                mix_factor_consts(Lb, (int)n, iLb, &c0b);
+                double a[ORC_MWG_MAXD], b[ORC_MWG_MAXD];
+                for (uint32_t i = 0; i < n; ++i) {
+                    a[i] = tp[i];                                                 /* θ°₁ */
+                    b[i] = u->pos[i] ? orc_exp_any(orc_log_any(tl[i])) : tl[i];  /* θ₁ */
+                }
+                for (int dir = 0; dir < 2; ++dir) {
+                    const double lpA = orc_gsn_rw_lp(u->L, u->iL, u->c0, u->diag, u->pos, n, anypos, a, b);
+                    const double lpB = orc_gsn_rw_lp(Lb, iLb, c0b, 0, u->pos, n, anypos, a, b);
+                    const double t = orc_log_any((1.0 - lam) * orc_exp_any(lpA) + lam * orc_exp_any(lpB));
+                    if (dir == 0) ltd_rev = t;
+                    else ltd_fwd = t;
+                    for (uint32_t i = 0; i < n; ++i) { /* the second call is logpdf(rw, θ, θ°) */
+                        const double tmp = a[i];
+                        a[i] = b[i];
+                        b[i] = tmp;
+                    }
+                }
+                if (anypos) { /* two swaps: a is θ° again, b is θ */
+                    for (uint32_t i = 0; i < n; ++i) {
+                        ta[i] = a[i]; /* θ°₅, what set_chain_param! copies */
+                        t3[i] = b[i]; /* θ₅, what log_prior(::Previous) reads */
+                    }
+                    accept_ta = 1;
+                }
             } else if (u->kind == 1) {
                 /* logpdf(rw, θ, θ°) (subtracted) and logpdf(rw, θ°, θ) (added), left folds */
                 for (uint32_t j = 0; j < n; ++j) {
@@ -1145,6 +1266,44 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                     }
                 }
             }
+            if (ext) {
+                const uint64_t N = N_start + s;
+                /* update_stats!: GenericChainStats mean/cov of the whole θ after every
+                 * update (chain_statistics.jl:46-49), before update_adaptation! */
+                if (ext->chain_moments) orc_rank1_register(ext->smean + c * D, ext->scov + c * D * D, th, D, N);
+                /* update_adaptation! (run.jl:136-178): every HaarioTypeAdaptation registers on
+                 * every step — register_only_on_my_turn is false both ways (adaptation.jl:399-404)
+                 * — the global θ at its coordinates, log-transformed where pos and transformed
+                 * back in place (remove/reimpose_constraints! on the view, :407,412); M += 1
+                 * and the readjust only on its own turn */
+                for (uint32_t q = 0; q < P; ++q) {
+                    const uint32_t hk = ext->haario_k ? ext->haario_k[q] : 0u;
+                    if (!hk) continue;
+                    const orc_mwg_update *v = &U[q];
+                    const uint32_t nq = v->nc;
+                    double x[ORC_MWG_MAXD];
+                    for (uint32_t j = 0; j < nq; ++j) {
+                        const double t = th[v->coords[j]];
+                        x[j] = v->pos[j] ? orc_log_any(t) : t;
+                    }
+                    double *hm = ext->hmean + ext->off_v[q] + c * (uint64_t)nq;
+                    double *hc = ext->hcov + ext->off_sq[q] + c * (uint64_t)nq * nq;
+                    orc_rank1_register(hm, hc, x, nq, N);
+                    for (uint32_t j = 0; j < nq; ++j)
+                        if (v->pos[j]) th[v->coords[j]] = orc_exp_any(x[j]);
+                    if (q == p && ++Mloc[q] >= hk) { /* time_to_update: readjust!(rw, adpt, iter) */
+                        Mloc[q] = 0;
+                        const double sB = (2.38 * 2.38) / (double)nq; /* 2.38^2/length(rw) */
+                        double S[ORC_MWG_MAXD * ORC_MWG_MAXD], Ln[ORC_MWG_MAXD * ORC_MWG_MAXD];
+                        for (uint32_t i = 0; i < nq; ++i)
+                            for (uint32_t j = 0; j < nq; ++j) S[(size_t)j * nq + i] = sB * hc[(size_t)i * nq + j];
+                        if (orc_cholesky(S, (int)nq, Ln))
+                            f |= ORC_FAULT_POSDEF;
+                        else
+                            memcpy(ext->LB + ext->off_sq[q] + c * (uint64_t)nq * nq, Ln, sizeof(double) * nq * nq);
+                    }
+                }
+            }
         }
         memcpy(theta + c * D, th, sizeof(double) * D);
         memcpy(mu_p + c * D, mp, sizeof(double) * D);
@@ -1153,6 +1312,11 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
     }
     *N_io = N_start + nsteps;
     for (uint32_t s = 0; s < nsteps; ++s) last_iter_io[step_pidx[s] - 1] = step_iter[s];
+    if (ext && ext->M_io && ext->haario_k) /* M advances by the own-turn steps, uniform over chains */
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            const uint32_t q = step_pidx[s] - 1;
+            if (ext->haario_k[q] && ++ext->M_io[q] >= ext->haario_k[q]) ext->M_io[q] = 0;
+        }
     free(g);
     free(U);
     return 0;
@@ -1183,12 +1347,6 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
  * (lower, row-major) in/out; *N_io = GenericChainStats.N (= Haario N),
  * *M_io = Haario M (uniform over chains).
  */
-#define ORC_FAULT_POSDEF 4u
-
-static void mix_factor_consts(const double *L, int D, double *iL, double *c0) {
-    for (int i = 0; i < D; ++i) iL[i] = 1.0 / L[(size_t)i * D + i];
-    *c0 = mvnormal_c0(D, logdet_chol(L, D));
-}
 
 ORC_EXPORT int orc_run_mix(int D, uint64_t C, uint32_t chain0, uint64_t seed, const double *sigma_a, int mix,
                            double lam, int haario, uint32_t k, const double *t_sigma, uint64_t nobs,

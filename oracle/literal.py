@@ -75,10 +75,13 @@ def run_chain(seed, chain, theta0, rw_sigma, t_sigma, obs, nsteps, iter0=1, W=10
     return {k: np.array(v) for k, v in out.items()}
 
 
-def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100):
+def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100, chain_moments=False):
     """Literal single-chain restatement of the P-update loop (see
     oracle/emcmc_oracle.c orc_run_mwg for the reference lines): plain Python
-    floats and numpy/LAPACK for the MvNormal logpdf."""
+    floats and numpy/LAPACK for the MvNormal logpdf.  GaussianRandomWalkMix
+    updates (kind 3) with HaarioTypeAdaptation register the global θ view of
+    their coordinates after every step, in place through remove/reimpose
+    (adaptation.jl:406-414), and readjust Σ_B = 2.38²/n·cov on their own turn."""
     Lt = np.linalg.cholesky(np.asarray(t_sigma, dtype=float))
     obs = np.asarray(obs, dtype=float)
     th = np.array(theta0, dtype=float)
@@ -91,6 +94,11 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
     ra = {}                                    # (iter, p) → rolling_ar value
     acc_hist = {}
     out = {"theta": [], "prop": [], "ll": [], "acc": [], "ra": [], "eps": []}
+    SB = [np.asarray(u["sigma_b"], dtype=float) if u["kind"] == 3 else None for u in updates]
+    hmean = [np.zeros(len(u["coords"])) for u in updates]
+    hcov = [np.zeros((len(u["coords"]),) * 2) for u in updates]
+    M = [0] * P
+    smean, scov = np.zeros(th.size), np.zeros((th.size, th.size))
     for it, pidx in steps:
         p = pidx - 1
         u = updates[p]
@@ -110,6 +118,38 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
             ltd_fwd, ltd_rev = fwd[0], rev[0]
             for j in range(1, len(cs)):
                 ltd_fwd, ltd_rev = ltd_fwd + fwd[j], ltd_rev + rev[j]
+        elif u["kind"] == 3:                   # GaussianRandomWalkMix (random_walk.jl:193-232)
+            n = len(cs)
+            pos = np.array(u["pos"], dtype=bool) if u.get("pos") is not None else np.zeros(n, dtype=bool)
+            LA = np.linalg.cholesky(np.asarray(u["sigma"], dtype=float))
+            LB = np.linalg.cholesky(SB[p])        # raises LinAlgError ≙ PosDefException
+            lam = u["lam"]
+            useB = _oracle.pick_uniform(seed, chain, it, p) <= lam   # pick_kernel: rand(Bernoulli(λ))
+            Lr = LB if useB else LA
+            z, _, _ = _oracle.step_variates(seed, chain, it, n, pidx0=p)
+            th_l = tl.copy()                   # state(ws)
+            th_l[pos] = np.log(th_l[pos])      # rand(gsn_X, θ): remove_constraints!
+            th_o = th_l + Lr @ z
+            th_o[pos] = np.exp(th_o[pos])
+            th_l[pos] = np.exp(th_l[pos])
+            tp = th_o.copy()
+
+            def gsn_logpdf(a, b, Lx):          # logpdf(gsn_X, a, b), mutating a and b (:166-171)
+                logJ = -sum(np.log(b[pos]))    # −sum(empty) = −0.0 without positivity flags
+                a[pos] = np.log(a[pos])
+                b[pos] = np.log(b[pos])
+                lp = mvnormal_logpdf(b, a, Lx) + logJ
+                a[pos] = np.exp(a[pos])
+                b[pos] = np.exp(b[pos])
+                return lp
+
+            def mix_logpdf(a, b):              # log((1−λ)e^{lp_A} + λe^{lp_B}) (:229-232)
+                lpa = gsn_logpdf(a, b, LA)
+                lpb = gsn_logpdf(a, b, LB)
+                return np.log((1 - lam) * np.exp(lpa) + lam * np.exp(lpb))
+            ltd_rev = mix_logpdf(th_o, th_l)   # __PROPOSAL first (run.jl:271-277)
+            ltd_fwd = mix_logpdf(th_l, th_o)
+            ta = th_o.copy()
         else:                                  # GaussianRandomWalk
             Lr = np.linalg.cholesky(np.asarray(u["sigma"], dtype=float))
             z, _, _ = _oracle.step_variates(seed, chain, it, len(cs), pidx0=p)
@@ -172,11 +212,44 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100)
                                   (sc[j] / np.sqrt(max(1.0, it / ad["k"] - off[j]))), mx[j]), mn[j])
                           for j, e in enumerate(eps[p])]
         out["theta"].append(th.copy())
+        if chain_moments:                      # update_stats! (chain_statistics.jl:46-49), N before += 1
+            Nc = N - 1
+            old_sum_sq = (Nc - 1) / Nc * scov + np.outer(smean, smean)
+            smean = smean * (Nc / (Nc + 1)) + th / (Nc + 1)
+            new_sum_sq = old_sum_sq + np.outer(th, th) / Nc
+            scov = new_sum_sq - (Nc + 1) / Nc * np.outer(smean, smean)
+        for q, v in enumerate(updates):        # update_adaptation! (run.jl:136-178)
+            if not v.get("haario_k"):
+                continue
+            Nh = N - 1
+            if q == p:
+                M[q] += 1                      # register_only_on_my_turn(Val(true)) (adaptation.jl:401-404)
+            cq = v["coords"]
+            posq = np.array(v["pos"], dtype=bool) if v.get("pos") is not None else np.zeros(len(cq), dtype=bool)
+            x = th[cq]                         # state(global_ws, updt): a view; remove_constraints! on it
+            x[posq] = np.log(x[posq])
+            old_sum_sq = (Nh - 1) / Nh * hcov[q] + np.outer(hmean[q], hmean[q])
+            hmean[q] = hmean[q] * (Nh / (Nh + 1)) + x / (Nh + 1)
+            new_sum_sq = old_sum_sq + np.outer(x, x) / Nh
+            hcov[q] = new_sum_sq - (Nh + 1) / Nh * np.outer(hmean[q], hmean[q])
+            x[posq] = np.exp(x[posq])          # reimpose_constraints!
+            th[cq] = x
+            if q == p and M[q] >= v["haario_k"]:   # time_to_update → readjust!
+                M[q] = 0
+                S_new = 2.38 ** 2 / len(cq) * hcov[q]
+                try:                           # the reference throws PosDefException at the next
+                    np.linalg.cholesky(S_new)  # MvNormal; the engine keeps the factor (fault bit 4)
+                    SB[q] = S_new
+                except np.linalg.LinAlgError:
+                    out.setdefault("posdef_faults", []).append((it, q))
         out["prop"].append(prop)
         out["ll"].append(ll)
         out["acc"].append(acc)
         out["ra"].append(ra[(it, p)])
         out["eps"].append([list(e) if e is not None else None for e in eps])
+    out["state"] = th.copy()
+    out["smean"], out["scov"] = smean, scov
+    out["hmean"], out["hcov"], out["sigma_b"] = hmean, hcov, SB
     return out
 
 

@@ -268,8 +268,11 @@ DIST_PRODUCT, DIST_MVNORMAL = 32, 33
 KIND_USER = 5
 
 
+KIND_MIX = 3
+
+
 def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=PRIOR_IMPROPER, factors=None,
-               params=None):
+               params=None, sigma_b=None, lam=0.5, haario_k=None):
     """One RandomWalkUpdate for run_mwg.  coords0: 0-based coordinates.
     adapt: None or dict(k, target, scale, min, max, offset) (AdaptationUnifRW).
     pos: None or per-coordinate positivity flags (UniformRandomWalk).
@@ -281,11 +284,17 @@ def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=
             "sigma": None if sigma is None else np.asarray(sigma, dtype=np.float64), "adapt": adapt,
             "pos": None if pos is None else [bool(x) for x in pos], "prior": int(prior),
             "factors": [] if factors is None else [tuple(f) for f in factors],
-            "params": None if params is None else [float(x) for x in np.ravel(params)]}
+            "params": None if params is None else [float(x) for x in np.ravel(params)],
+            "sigma_b": None if sigma_b is None else np.asarray(sigma_b, dtype=np.float64), "lam": float(lam),
+            "haario_k": haario_k}
 
 
 class MWGState:
-    def __init__(self, theta, mu0, updates, ll=None):
+    """State of orc_run_mwg: the carried chain state and, for GaussianRandomWalkMix /
+    HaarioTypeAdaptation updates and chain_moments, the per-chain L_B (from Σ_B),
+    Haario mean/cov (zeros, N = 1 phantom sample) and GenericChainStats mean/cov."""
+
+    def __init__(self, theta, mu0, updates, ll=None, chain_moments=False):
         theta = np.ascontiguousarray(theta, dtype=np.float64)
         self.C, self.D = theta.shape
         P = len(updates)
@@ -304,6 +313,45 @@ class MWGState:
         self.faults = np.zeros(self.C, dtype=np.uint32)
         self.N = np.array([1], dtype=np.uint64)
         self.last_iter = np.zeros(P, dtype=np.uint32)
+        # mix / Haario / chain moments (the ext block of orc_run_mwg)
+        ns = [len(u["coords"]) for u in updates]
+        self.off_sq = np.array(np.cumsum([0] + [self.C * n * n for n in ns])[:P], dtype=np.uint64)
+        self.off_v = np.array(np.cumsum([0] + [self.C * n for n in ns])[:P], dtype=np.uint64)
+        tot_sq, tot_v = sum(self.C * n * n for n in ns), sum(self.C * n for n in ns)
+        self.LB = np.zeros(tot_sq)
+        self.hmean = np.zeros(tot_v)
+        self.hcov = np.zeros(tot_sq)
+        self.M = np.zeros(P, dtype=np.uint32)
+        self.lam = np.array([float(u.get("lam", 0.0)) for u in updates])
+        self.haario_k = np.array([int(u.get("haario_k") or 0) for u in updates], dtype=np.uint32)
+        for p, u in enumerate(updates):
+            if u["kind"] == 3:
+                Lb = cholesky(np.asarray(u["sigma_b"], dtype=np.float64).reshape(ns[p], ns[p]))
+                o = int(self.off_sq[p])
+                self.LB[o:o + self.C * ns[p] ** 2] = np.tile(Lb.ravel(), self.C)
+        self.chain_moments = bool(chain_moments)
+        self.smean = np.zeros((self.C, self.D))
+        self.scov = np.zeros((self.C, self.D, self.D))
+
+    def lb(self, p, n):
+        """The chains' L_B of update p: [C][n][n]."""
+        o = int(self.off_sq[p])
+        return self.LB[o:o + self.C * n * n].reshape(self.C, n, n)
+
+    def haario(self, p, n):
+        """The chains' Haario mean [C][n] and cov [C][n][n] of update p."""
+        o, v = int(self.off_sq[p]), int(self.off_v[p])
+        return (self.hmean[v:v + self.C * n].reshape(self.C, n),
+                self.hcov[o:o + self.C * n * n].reshape(self.C, n, n))
+
+
+class _MwgExt(C.Structure):
+    """orc_mwg_ext (oracle/emcmc_oracle.c)."""
+    _fields_ = [("mix_lam", C.POINTER(C.c_double)), ("haario_k", C.POINTER(C.c_uint32)),
+                ("M_io", C.POINTER(C.c_uint32)), ("LB", C.POINTER(C.c_double)), ("hmean", C.POINTER(C.c_double)),
+                ("hcov", C.POINTER(C.c_double)), ("off_sq", C.POINTER(C.c_uint64)),
+                ("off_v", C.POINTER(C.c_uint64)), ("chain_moments", C.c_int), ("reserved", C.c_int),
+                ("smean", C.POINTER(C.c_double)), ("scov", C.POINTER(C.c_double))]
 
 
 def _mwg_tables(updates):
@@ -419,7 +467,7 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
                                   u8p, u32p, u32p, dp, dp, C.c_uint64, dp, C.c_int, C.c_uint32, C.c_uint32, u32p, u32p,
                                   u64p, u32p, dp, dp, dp, dp, u64p, u32p, u32p, u32p, dp, u32p, dp, dp, dp, u8p,
                                   C.c_int, u32p, u32p, u32p, u32p, dp, dp, dp, C.c_void_p, dp, u32p, dp, dp, dp, dp,
-                                  C.c_void_p, C.c_void_p, dp]
+                                  C.c_void_p, C.c_void_p, dp, C.POINTER(_MwgExt)]
         L._mwg_ready = True
     Cn, D = state.C, state.D
     kind, nc, coords, eps, sigma, adapt, ak, ap, pos = _mwg_tables(updates)
@@ -431,6 +479,12 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
             uparams[p, :v.size] = v
     if getattr(state, "ll_prop", None) is None:
         state.ll_prop = np.full((len(updates), state.C), np.nan)
+    state.lam = np.ascontiguousarray(state.lam, dtype=np.float64)
+    ext = _MwgExt(_d(state.lam), state.haario_k.ctypes.data_as(C.POINTER(C.c_uint32)),
+                  state.M.ctypes.data_as(C.POINTER(C.c_uint32)), _d(state.LB), _d(state.hmean), _d(state.hcov),
+                  state.off_sq.ctypes.data_as(C.POINTER(C.c_uint64)),
+                  state.off_v.ctypes.data_as(C.POINTER(C.c_uint64)), int(state.chain_moments), 0, _d(state.smean),
+                  _d(state.scov))
     up = None if user_params is None else np.ascontiguousarray(user_params, dtype=np.float64)
     steps = np.asarray(steps, dtype=np.uint32).reshape(-1, 2)
     si = np.ascontiguousarray(steps[:, 0])
@@ -458,7 +512,7 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
         None if user_ll is None else C.cast(user_ll, C.c_void_p), None if up is None else _d(up),
         u32(cfam), _d(ca), _d(cb), _d(mvmu), _d(mvS),
         None if user_upd is None else C.cast(user_upd[0], C.c_void_p),
-        None if user_upd is None else C.cast(user_upd[1], C.c_void_p), _d(uparams))
+        None if user_upd is None else C.cast(user_upd[1], C.c_void_p), _d(uparams), C.byref(ext))
     if rc != 0:
         raise ValueError(f"orc_run_mwg failed: {rc}")
     if history:
@@ -564,9 +618,10 @@ def run_mix(state: MixState, *, seed, sigma_a, t_sigma, obs, iter0, nsteps, mix=
     return hist
 
 
-def pick_uniform(seed, chain, it):
-    """The [0,1) uniform that picks GaussianRandomWalkMix's kernel (B iff u ≤ λ)."""
-    r = philox([chain, it, 0xFFFFFFFE, 0], [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
+def pick_uniform(seed, chain, it, pidx0=0, attempt=0):
+    """The [0,1) uniform that picks GaussianRandomWalkMix's kernel (B iff u ≤ λ):
+    block 0xFFFFFFFE of (chain, iter), update pidx0, redraw `attempt`."""
+    r = philox([chain, it, 0xFFFFFFFE, (pidx0 << 16) | attempt], [seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF])
     return float((int(r[0]) << 21) | (int(r[1]) >> 11)) * 2.0 ** -53
 
 

@@ -48,16 +48,35 @@ def test_run_bivariate_joint_gaussian_rw(oracle, tmp_path):
 
 
 def test_unsupported_plugins_raise_not_fallback():
+    """A plugin without a device implementation raises UnsupportedPlugin — no CPU fallback."""
+    from extensible_mcmc import MALAUpdate, Normal, ProductPrior, StandardPrior
+
     w = W.ref_test()
-    # GaussianRandomWalkMix runs on device only as the single joint update on 1:D
-    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(np.eye(1), 2 * np.eye(1)), [1]),
+    # a univariate StandardPrior on a coordinate vector has no scalar logpdf in the reference
+    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalk(np.eye(1)), [1], prior=StandardPrior(Normal())),
                  RandomWalkUpdate(GaussianRandomWalk(np.eye(1)), [2])], backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
-    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(np.eye(2), 2 * np.eye(2), pos=[True, False]), [1, 2])],
-                backend=MI355XBackend(num_chains=8))
-    with pytest.raises(UnsupportedPlugin):  # positivity-restricted mixture walk
+    # MALA's device plugin takes ImproperPrior only
+    mcmc = MCMC([MALAUpdate(0.1, [1, 2], prior=ProductPrior([Normal()], [1]))], backend=MI355XBackend(num_chains=8))
+    with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [1.0, 0.0])
+
+
+def test_positive_mixture_walk_beside_a_gaussian_walk_through_the_api(oracle):
+    """GaussianRandomWalkMix with positivity flags on coordinate 1 and a GaussianRandomWalk on
+    coordinate 2 through MCMC / run (general kernel): the device run equals the oracle's."""
+    w = W.ref_test()
+    mcmc = MCMC([RandomWalkUpdate(GaussianRandomWalkMix(0.3 * np.eye(1), 0.9 * np.eye(1), 0.3, [True]), [1]),
+                 RandomWalkUpdate(GaussianRandomWalk(0.5 * np.eye(1)), [2])],
+                backend=MI355XBackend(num_chains=64, seed=w.seed))
+    gws, _ = run(mcmc, 150, dict(P=GsnTargetLaw([1.0, 2.0], w.t_sigma), obs=w.obs), [1.0, 2.0])
+    ups = [oracle.mwg_update(oracle.KIND_MIX, [0], sigma=[[0.3]], sigma_b=[[0.9]], lam=0.3, pos=[True]),
+           oracle.mwg_update(2, [1], sigma=[[0.5]])]
+    st = oracle.MWGState(np.tile([1.0, 2.0], (64, 1)), [1.0, 2.0], ups)
+    oracle.run_mwg(st, ups, seed=w.seed, t_sigma=w.t_sigma, obs=w.obs,
+                   steps=[(i, p) for i in range(1, 151) for p in (1, 2)], history=False)
+    assert np.array_equal(gws.state, st.theta) and np.all(gws.state[:, 0] > 0)
 
 
 def test_positive_uniform_walk_through_the_api(oracle):

@@ -109,3 +109,25 @@ def test_mala_rejects_other_shapes():
     with pytest.raises(L.EMCMCError) as e:
         eng.set_logistic_target(X, y)
     assert e.value.status == L.UNSUPPORTED_PLUGIN
+
+
+def test_cfg3_grid_on_sampled_chains(oracle):
+    """The real cfg 3 grid (32,768 chains, N = 1e5, D = 64: 512 workgroups re-reading X
+    from L2/MALL) for 3 steps; 8 chains across the grid — first and last workgroups,
+    different XCDs — replayed on the oracle, bit for bit: accept stream, θ / θ° / ll
+    histories and the final state."""
+    w = W.cfg3()
+    C, M = w.num_chains, 3
+    eng = _engine(w.X, w.y, C, M, w.eps, w.seed)
+    eng.run_iters(1, M)
+    eng.synchronize()
+    th, ll = eng.get_state()
+    acc = eng.get_history(L.H_ACCEPT, 1, M)[:, 0]
+    hth = eng.get_history_chains(L.H_STATE, 1, M, 0, C)
+    picks = [0, 1, 63, 64, 4097, 16383, 20000, C - 1]
+    for c in picks:
+        st = oracle.MALAState(np.zeros((1, w.D)), w.X, w.y, nthreads=16)
+        h = oracle.run_mala(st, seed=w.seed, eps=w.eps, X=w.X, y=w.y, iter0=1, nsteps=M, chain0=c, nthreads=16)
+        assert np.array_equal(acc[:, c], h["acc"][:, 0]), c
+        assert np.array_equal(th[c], st.theta[0]) and ll[c] == st.ll[0], c
+        assert np.array_equal(hth[:, 0, c], h["theta"][:, 0]), c

@@ -190,21 +190,23 @@ def test_chain_moments_flag_on_plain_gaussian_rw(oracle, D):
     _check(eng, st, [h], list(range(1, M + 1)), True, mix=False)
 
 
-def test_mix_rejects_unsupported_shapes():
-    """GaussianRandomWalkMix only as the single joint update on 1:D; dense Σ at D = 32."""
+def test_shapes_outside_the_fused_kernels_run_on_the_general_kernel():
+    """GaussianRandomWalkMix beside another update, and a dense Σ at D = 32, leave the
+    fused cfg 4 kernels for the general schedule kernel (tests/test_gpu_mix_general.py
+    checks their results); the fused kernels keep the shapes they instantiate."""
     seed, mu, ts, obs, sa = _problem(4)
     eng = Engine(EngineConfig(dim=4, num_chains=64, num_mcmc_steps=10, seed=seed))
     eng.add_gaussian_rw_mix_update([0, 1], sa[:2, :2], sa[:2, :2])
-    with pytest.raises(L.EMCMCError) as e:
-        eng.add_gaussian_rw_update([2, 3], sa[:2, :2])
-        eng.set_gsn_target(mu, ts, obs)
-    assert e.value.status == L.UNSUPPORTED_PLUGIN
+    eng.add_gaussian_rw_update([2, 3], sa[:2, :2])
+    eng.set_gsn_target(mu, ts, obs)
+    assert eng.kernel_name().startswith("mwg_gsn_kernel<D=4")
+    eng.close()
     seed, mu, ts, obs, sa = _problem(32, dense=True)
     eng = Engine(EngineConfig(dim=32, num_chains=64, num_mcmc_steps=10, seed=seed))
     eng.add_gaussian_rw_mix_update(range(32), sa, sa)
-    with pytest.raises(L.EMCMCError) as e:
-        eng.set_gsn_target(mu, ts, obs)
-    assert e.value.status == L.UNSUPPORTED_PLUGIN
+    eng.set_gsn_target(mu, ts, obs)
+    assert eng.kernel_name().startswith("mwg_wide_kernel<D=32")
+    eng.close()
 
 
 @pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])

@@ -140,15 +140,13 @@ def test_product_prior_with_mvnormal_and_all_families(oracle):
     assert 0.05 < h["acc"].mean() < 0.95
 
 
-@pytest.mark.parametrize("case", ["univariate_dims3", "mvnormal_dims1", "standard_univariate", "past_the_end",
-                                  "mix_with_prior"])
+@pytest.mark.parametrize("case", ["univariate_dims3", "mvnormal_dims1", "standard_univariate", "past_the_end"])
 def test_prior_pairings_without_a_reference_value_are_refused(case):
     """The pairings the reference raises on (MethodError / BoundsError) are refused by the
-    engine, as is a prior on the mix / chain-moments path (no prior term there)."""
+    engine."""
     from extensible_mcmc.engine import Engine, EngineConfig
 
-    eng = Engine(EngineConfig(dim=3, num_chains=64, num_mcmc_steps=4, seed=1, device=0,
-                              chain_moments=1 if case == "mix_with_prior" else 0))
+    eng = Engine(EngineConfig(dim=3, num_chains=64, num_mcmc_steps=4, seed=1, device=0))
     want = L.UNSUPPORTED_PLUGIN
     try:
         if case == "univariate_dims3":
@@ -157,10 +155,8 @@ def test_prior_pairings_without_a_reference_value_are_refused(case):
             fs, kind = [(MV_, 1, [0.0], [[1.0]]), (P_, 2, [(N_, 0.0, 1.0)] * 2)], L.PRIOR_PRODUCT
         elif case == "standard_univariate":
             fs, kind = [(N_, 1, 0.0, 1.0)], L.PRIOR_STANDARD
-        elif case == "past_the_end":
-            fs, kind, want = [(N_, 1, 0.0, 1.0), (P_, 3, [(N_, 0.0, 1.0)] * 3)], L.PRIOR_PRODUCT, L.INVALID_ARG
         else:
-            fs, kind = [(P_, 3, [(N_, 0.0, 1.0)] * 3)], L.PRIOR_PRODUCT
+            fs, kind, want = [(N_, 1, 0.0, 1.0), (P_, 3, [(N_, 0.0, 1.0)] * 3)], L.PRIOR_PRODUCT, L.INVALID_ARG
         with pytest.raises(L.EMCMCError) as e:
             eng.add_gaussian_rw_update(np.arange(3), 0.1 * np.eye(3), prior=kind, prior_factors=fs)
             eng.set_gsn_target(np.zeros(3), np.eye(3), np.zeros((2, 3)))
@@ -169,3 +165,29 @@ def test_prior_pairings_without_a_reference_value_are_refused(case):
         assert e.value.status == want
     finally:
         eng.close()
+
+
+def test_chain_moments_with_a_prior_run_on_the_general_kernel(oracle):
+    """emcmc_config.chain_moments with a prior on the joint update (no prior term in the
+    fused cfg 4 kernels): the general kernel keeps GenericChainStats mean/cov, bitwise."""
+    from extensible_mcmc.engine import Engine, EngineConfig
+
+    rng = np.random.default_rng(8)
+    D, C, M = 3, 512, 80
+    mu = rng.normal(size=D)
+    obs = mu + rng.normal(size=(6, D))
+    fs = [(P_, 3, [(N_, 0.0, 3.0)] * 3)]
+    ups = [oracle.mwg_update(2, range(D), sigma=0.1 * np.eye(D), prior=L.PRIOR_PRODUCT, factors=fs)]
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=3, chain_moments=True))
+    eng.add_gaussian_rw_update(np.arange(D), 0.1 * np.eye(D), prior=L.PRIOR_PRODUCT, prior_factors=fs)
+    eng.set_gsn_target(mu, np.eye(D), obs)
+    eng.set_state(np.tile(mu, (C, 1)))
+    eng.run_iters(1, M)
+    assert eng.kernel_name().startswith("mwg_gsn_kernel")
+    st = oracle.MWGState(np.tile(mu, (C, 1)), mu, ups, chain_moments=True)
+    oracle.run_mwg(st, ups, seed=3, t_sigma=np.eye(D), obs=obs, steps=full_steps(M, 1), nthreads=8, history=False)
+    eng.synchronize()
+    th, _ = eng.get_state()
+    m, v = eng.get_chain_moments()
+    assert np.array_equal(th, st.theta)
+    assert np.array_equal(m, st.smean) and np.array_equal(v, st.scov)

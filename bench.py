@@ -64,6 +64,10 @@ def parse():
                     help="repeat the timed region, report the median (0: 5 when the histories fit in 96 GB, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="run the same step kernel on a throwaway handle for this long before the warm-up steps, "
+                         "so the timed steps see the steady-state clock (DESIGN.md §6: the clock bursts, dips, "
+                         "then settles over ~40 ms of load); 0 disables")
     return ap.parse_args()
 
 
@@ -176,6 +180,46 @@ def cpu_baseline(w, seconds, ll_mode):
     return out
 
 
+def settle_clock(w, Cg, device, a, first, cfg3, cfg4, ll_mode):
+    """Bring the GPU to its steady-state clock right before the timed steps: the same step
+    kernel (same workload shape, full histories into a ring of one launch) on a throwaway
+    handle for a.settle_ms of wall time.  Under this load the clock bursts for ~1 ms, dips
+    for ~10 ms, then settles; the measured handle's chains are untouched.
+    Returns (handle, info); the caller closes the handle after the timed region."""
+    from extensible_mcmc import _lib as L
+    from extensible_mcmc.engine import Engine, EngineConfig
+
+    spl = 1 if cfg3 else a.steps_per_launch
+    eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=1 << 20,
+                              seed=w.seed ^ 0x5E77, first_chain_id=first, device=device,
+                              history_mode=L.HIST_FULL, lanes_per_chain=a.lpc, steps_per_launch=spl,
+                              history_ring=spl, kernel_variant=a.variant))
+    if cfg3:
+        eng.add_mala_update(np.arange(w.D), w.eps)
+        eng.set_logistic_target(w.X, w.y)
+    elif cfg4:
+        eng.add_gaussian_rw_mix_update(np.arange(w.D), w.rw_sigma, w.sigma_b, lam=w.lam, haario_k=w.haario_k)
+    else:
+        eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    if not cfg3:
+        eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs, ll_mode=ll_mode)
+    eng.set_state(np.ascontiguousarray(np.broadcast_to(np.asarray(w.theta_init, dtype=np.float64), (Cg, w.D))))
+    eng.synchronize(allow_faults=True)  # setup done before the clock starts to settle
+    times, it, t0 = [], 1, time.perf_counter()
+    while time.perf_counter() - t0 < a.settle_ms / 1e3:
+        t1 = time.perf_counter()
+        eng.run_iters(it, spl)
+        eng.synchronize(allow_faults=True)
+        times.append(time.perf_counter() - t1)
+        it += spl
+    # the handle is closed after the timed region: freeing it now would idle the GPU
+    return eng, {"ms": (time.perf_counter() - t0) * 1e3, "launches": len(times), "steps_per_launch": spl,
+                 "first_launch_ms": times[0] * 1e3 if times else None,
+                 "last_launch_ms": times[-1] * 1e3 if times else None,
+                 "note": "throwaway handle, same kernel and shape, between the warm-up steps and the timed "
+                         "steps; not in the timed region"}
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -249,6 +293,9 @@ def main():
     if a.warmup:
         eng.run_iters(1, a.warmup)
     eng.synchronize(allow_faults=cfg4)  # cfg 4: PosDef faults are counted and reported
+    # the clock settles under load right before the timed steps (no idle gap in between)
+    settle_eng, settle = settle_clock(w, Cg, device, a, first, cfg3, cfg4, ll_mode) if a.settle_ms > 0 \
+        else (None, None)
 
     def barrier():
         if dist is not None:
@@ -290,6 +337,8 @@ def main():
             dt = float(t.item())
         times.append(dt)
         it += a.steps
+    if settle_eng is not None:
+        settle_eng.close()
     order = np.argsort(times)
     mid = int(order[len(order) // 2])
     dt = times[mid]
@@ -365,6 +414,7 @@ def main():
                             "rolling acceptance + running mean/cov (chain_statistics.jl:41-66)" if cfg4
                             else "rolling acceptance (chain_statistics.jl:51-65)"),
             "steps_per_launch": a.steps_per_launch,
+            "clock_settle": settle,
             "kernel": kname,
             "parallelism": f"chain-sharded x{world}",
         },

@@ -429,6 +429,12 @@ emcmc_status ensure_alloc(emcmc_handle *h) {
         HIPCHK(h, hipMalloc(&h->d_hist_theta, R * P * C * D * sizeof(double)));
         HIPCHK(h, hipMalloc(&h->d_hist_prop, R * P * C * D * sizeof(double)));
         HIPCHK(h, hipMalloc(&h->d_hist_ll, R * P * C * sizeof(double)));
+        // The reference preallocates its histories zero-filled in init! (workspaces.jl:413-476,
+        // `zero(θ)` per slot): a slot read before its iteration ran reads 0, as there.  (The
+        // zero-fill does not change the step kernels' time: DESIGN.md §6, r3 zero-fill A/B.)
+        HIPCHK(h, hipMemsetAsync(h->d_hist_theta, 0, R * P * C * D * sizeof(double), h->stream));
+        HIPCHK(h, hipMemsetAsync(h->d_hist_prop, 0, R * P * C * D * sizeof(double), h->stream));
+        HIPCHK(h, hipMemsetAsync(h->d_hist_ll, 0, R * P * C * sizeof(double), h->stream));
     }
     h->allocated = true;
     return EMCMC_OK;
@@ -1334,9 +1340,9 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
     if (cfg->num_mcmc_steps >= (1ull << 32)) return EMCMC_INVALID_ARG;
     if (cfg->history_mode > EMCMC_HIST_ACCEPT_ONLY) return EMCMC_INVALID_ARG;
     if (cfg->roll_window > 128) return EMCMC_INVALID_ARG;
-    // history stores address a slot with a 32-bit byte offset (SlotOffsets)
-    if (cfg->history_mode == EMCMC_HIST_FULL && cfg->num_chains * cfg->dim * sizeof(double) > 0xFFFFFFFFull)
-        return EMCMC_INVALID_ARG;
+    // history slots and the state array are addressed with a 32-bit per-lane byte offset
+    // (SlotOffset, LaneSoA) from a wave-uniform base, whatever the history mode
+    if (cfg->num_chains * cfg->dim * sizeof(double) > 0xFFFFFFFFull) return EMCMC_INVALID_ARG;
     if (cfg->lanes_per_chain != 0 && cfg->lanes_per_chain != 1 && cfg->lanes_per_chain != 2 &&
         cfg->lanes_per_chain != 4)
         return EMCMC_INVALID_ARG;

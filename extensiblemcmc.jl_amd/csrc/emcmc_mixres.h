@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
     const double iLB0 = a.iLB[(uint64_t)i0 * C + chain], iLB1 = a.iLB[(uint64_t)i1 * C + chain];
     const double c0B = a.c0B[chain];
 
-    const uint32_t po = (uint32_t)(((uint64_t)r * C + chain) * 16u);  // the lane's pair word in a slot
+    const uint64_t po = ((uint64_t)r * C + chain) * 16u;  // the lane's pair word in a slot (64-bit: any C)
     double th0, th1;
     {
         const d2v t = *reinterpret_cast<const d2v *>(reinterpret_cast<const char *>(a.theta) + po);

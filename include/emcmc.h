@@ -142,7 +142,8 @@ typedef struct emcmc_handle emcmc_handle;
 typedef struct emcmc_config {
     uint32_t abi_version;      /* must be EMCMC_ABI_VERSION */
     uint32_t dim;              /* D = length(θinit) */
-    uint64_t num_chains;       /* C: chains held by this handle (one shard) */
+    uint64_t num_chains;       /* C: chains held by this handle (one shard); C·dim·8 bytes ≤ 4 GiB − 1
+                                  (the state and one history slot are addressed with 32-bit offsets) */
     uint64_t first_chain_id;   /* global id of local chain 0 (sharding; RNG key) */
     uint64_t num_mcmc_steps;   /* M: history length, run.jl:34 `num_mcmc_steps` */
     uint64_t seed;             /* master seed of the counter-based stream */

@@ -10,7 +10,7 @@
 # Every GPU step has its own limit; a fault/abort/timeout ends the script.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r3roof
+OUT=gpurun_out/${RTAG:-r3roof}
 mkdir -p $OUT
 step() {
   local name=$1; shift
@@ -34,11 +34,13 @@ for cfg in s20 s1000; do
   step ${cfg}_clock rocprofv3 --pmc $CLK --output-format csv -d $OUT/$cfg/clock -o run -- \
     python3 bench.py $B --no-cpu > $OUT/$cfg/clock.json 2> $OUT/$cfg/clock.err
 done
-# the gap experiments (un-profiled; HIP-event kernel times in each line)
+# the gap experiments (un-profiled; HIP-event kernel times in each line); GAP=0 skips them
+if [ "${GAP:-1}" = 1 ]; then
 step gap_spl20 python3 bench.py --no-cpu --steps 1000 --steps-per-launch 20 > $OUT/gap_spl20.json 2> $OUT/gap.err
 step gap_ring100 python3 bench.py --no-cpu --steps 1000 --history-ring 100 > $OUT/gap_ring100.json 2>> $OUT/gap.err
 step gap_warm1000 python3 bench.py --no-cpu --steps 20 --warmup 1000 > $OUT/gap_warm1000.json 2>> $OUT/gap.err
 step gap_s20_spl20 python3 bench.py --no-cpu --steps 20 --warmup 5 --steps-per-launch 20 > $OUT/gap_s20_spl20.json 2>> $OUT/gap.err
 step gap_s20_again python3 bench.py --no-cpu --steps 20 --warmup 5 > $OUT/gap_s20_again.json 2>> $OUT/gap.err
 step gap_s1000_again python3 bench.py --no-cpu > $OUT/gap_s1000_again.json 2>> $OUT/gap.err
+fi
 python3 scripts/r3_roofline_summary.py $OUT > $OUT/summary.json; cat $OUT/summary.json

@@ -100,3 +100,16 @@ def test_invalid_config_rejected_without_device():
     assert L.lib().emcmc_create(C.byref(h), C.byref(cfg)) == L.INVALID_ARG
     n = C.c_int(-1)
     assert L.lib().emcmc_device_count(C.byref(n)) == L.OK and n.value >= 0
+
+
+@pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
+def test_state_beyond_32bit_offsets_rejected(hist):
+    """C·D·8 bytes above 4 GiB − 1 is refused in every history mode: the state and a
+    history slot are addressed with 32-bit per-lane offsets."""
+    cfg = L.EmcmcConfig()
+    cfg.abi_version = L.ABI_VERSION
+    cfg.dim, cfg.num_mcmc_steps, cfg.history_mode = 32, 10, hist
+    cfg.num_chains = (1 << 32) // (32 * 8)  # exactly 4 GiB of state
+    cfg.roll_window = 10
+    h = C.c_void_p()
+    assert L.lib().emcmc_create(C.byref(h), C.byref(cfg)) == L.INVALID_ARG

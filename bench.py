@@ -173,6 +173,17 @@ def cpu_baseline(w, seconds, ll_mode):
                            "sample": f"{Cf} chains x {stepsf} iterations, {dtf:.1f} s: a Cholesky of Σ at every "
                                      "MvNormal construction (rand, both logpdfs, P° and P set_parameters!) and a "
                                      "logdet per logpdf, as the reference; same bits as the factor-once oracle"}
+    ac = hi["affinity_cores"] or 1
+    if ac > threads:  # every core of the affinity mask, measured (the cgroup quota still caps their CPU time)
+        va, Ca, stepsa, dta = rate(ac, 0.2 * seconds)
+        out["all_affinity_cores_measured"] = {
+            "value": va, "cores": ac, "sample": f"{Ca} chains x {stepsa} iterations, {dta:.1f} s",
+            "note": "one OpenMP thread per core of the affinity mask; the box's cgroup CPU quota "
+                    "(cgroup_cpu_quota_cores) caps the CPU time they get, so this is not the whole host's rate"}
+        if not mix:
+            vfa, Cfa, stepsfa, dtfa = rate(ac, 0.2 * seconds, faithful=True)
+            out["all_affinity_cores_measured"]["faithful"] = {
+                "value": vfa, "sample": f"{Cfa} chains x {stepsfa} iterations, {dtfa:.1f} s"}
     what = ("GaussianRandomWalkMix + HaarioTypeAdaptation(k=%d) + chain mean/cov" % w.haario_k) if mix else "RWM"
     out["sample"] = (f"{C} chains x {steps} iterations of the same D=32 {what} workload ({w.nobs} obs, "
                      f"{'per-observation' if ll_mode == 0 else 'sufficient-statistic'} log-likelihood, "
@@ -228,10 +239,13 @@ def main():
     # EMCMC_BENCH_SHARED_DEVICE=1: every rank on device 0 with gloo (a rehearsal of
     # the torchrun path on a one-GPU box; RCCL needs one GPU per rank)
     shared = os.environ.get("EMCMC_BENCH_SHARED_DEVICE") == "1"
+    # EMCMC_BENCH_FORCE_NCCL=1: the RCCL process group even at world size 1 (RCCL init, the
+    # device all-gather of the diagnostics and libemcmc beside torch's HIP context in one process)
+    force_nccl = os.environ.get("EMCMC_BENCH_FORCE_NCCL") == "1" and not shared
     device = 0 if shared else local
     dist = None
     dev = None  # where the diagnostics all-gather runs
-    if world > 1:
+    if world > 1 or force_nccl:
         import torch
         import torch.distributed as dist
 
@@ -417,6 +431,7 @@ def main():
             "clock_settle": settle,
             "kernel": kname,
             "parallelism": f"chain-sharded x{world}",
+            "process_group": None if dist is None else ("gloo" if shared else "nccl"),
         },
         "roofline": {
             "bound": "hbm",

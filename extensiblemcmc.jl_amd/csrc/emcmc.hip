@@ -8,6 +8,7 @@
 // at every MvNormal construction, random_walk.jl:147,167 and
 // gsn_target.jl:20 — same matrices, so the same factor), and turns a schedule
 // of (mcmciter, pidx) steps into fused multi-step launches.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -900,6 +901,22 @@ hipEvent_t get_event(emcmc_handle *h) {
     return e;
 }
 
+// One step-kernel launch on the handle's stream.  With timing on, the launch
+// carries its own start/stop events (hipExtLaunchKernel: the timestamps of the
+// dispatch packet itself, as rocprofv3's kernel trace reports them, without the
+// few µs of a separate event marker on either side).
+hipError_t launch_step(emcmc_handle *h, const void *fn, dim3 grid, dim3 block, void **args, size_t lds,
+                       uint64_t bytes) {
+    if (!h->timing) return hipLaunchKernel(fn, grid, block, args, lds, h->stream);
+    hipEvent_t e0 = get_event(h), e1 = get_event(h);
+    const hipError_t e = hipExtLaunchKernel(fn, grid, block, args, lds, h->stream, e0, e1, 0);
+    if (e == hipSuccess) {
+        h->ev.emplace_back(e0, e1);
+        h->pending_bytes += bytes;
+    }
+    return e;
+}
+
 emcmc_status drain_timing(emcmc_handle *h) {
     for (auto &p : h->ev) {
         float ms = 0.f;
@@ -1160,19 +1177,9 @@ emcmc_status run_mala(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
         if (p.iter > 1 && h->last_iter[0] != p.iter - 1)  // rolling_ar[iter−1] never written → 0.0
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[0] = p.iter;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (h->timing) {
-            e0 = get_event(h);
-            e1 = get_event(h);
-            HIPCHK(h, hipEventRecord(e0, h->stream));
-        }
         void *args[] = {&p};
-        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.afn), grid, block, args, 0, h->stream));
-        if (h->timing) {
-            HIPCHK(h, hipEventRecord(e1, h->stream));
-            h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, 1, false);
-        }
+        HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.afn), grid, block, args, 0,
+                              bytes_per_launch(h, 1, false)));
         h->stats_N += 1;
     }
     return EMCMC_OK;
@@ -1295,23 +1302,24 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             emcmc_status gs = guard_ring(h, lo, hi);
             if (gs) return gs;
         }
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (h->timing) {
-            e0 = get_event(h);
-            e1 = get_event(h);
-            HIPCHK(h, hipEventRecord(e0, h->stream));
-        }
         void *args[] = {&a};
-        if (h->var.ufn)
+        if (h->var.ufn) {  // a run-time compiled module: event markers around the launch
+            hipEvent_t e0 = nullptr, e1 = nullptr;
+            if (h->timing) {
+                e0 = get_event(h);
+                e1 = get_event(h);
+                HIPCHK(h, hipEventRecord(e0, h->stream));
+            }
             HIPCHK(h, hipModuleLaunchKernel(h->var.ufn, grid.x, 1, 1, block.x, 1, 1, (unsigned)h->lds_bytes, h->stream,
                                             args, nullptr));
-        else
-            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mfn), grid, block, args, h->lds_bytes,
-                                      h->stream));
-        if (h->timing) {
-            HIPCHK(h, hipEventRecord(e1, h->stream));
-            h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, n, false);
+            if (h->timing) {
+                HIPCHK(h, hipEventRecord(e1, h->stream));
+                h->ev.emplace_back(e0, e1);
+                h->pending_bytes += bytes_per_launch(h, n, false);
+            }
+        } else {
+            HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.mfn), grid, block, args, h->lds_bytes,
+                                  bytes_per_launch(h, n, false)));
         }
         h->stats_N += n;
     }
@@ -1943,20 +1951,9 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
         if (p.iter0 > 1 && h->last_iter[p.pidx0] != p.iter0 - 1)
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[p.pidx0] = steps[j - 1].mcmciter;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (h->timing) {
-            e0 = get_event(h);
-            e1 = get_event(h);
-            HIPCHK(h, hipEventRecord(e0, h->stream));
-        }
         void *args[] = {&p};
-        HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.fn), grid, block, args, h->lds_bytes,
-                                  h->stream));
-        if (h->timing) {
-            HIPCHK(h, hipEventRecord(e1, h->stream));
-            h->ev.emplace_back(e0, e1);
-            h->pending_bytes += bytes_per_launch(h, n, false);
-        }
+        HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.fn), grid, block, args, h->lds_bytes,
+                              bytes_per_launch(h, n, false)));
         h->stats_N += n;
         i = j;
     }

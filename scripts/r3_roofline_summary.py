@@ -35,9 +35,11 @@ def rows(pattern):
 
 
 def timed_slice(b, n_dispatch):
-    """Indices of the timed launches: warm-up launches first, then reps × launches per rep."""
+    """Indices of the timed launches: warm-up launches first, then the clock-settle
+    launches of the throwaway handle (bench.py settle_clock), then reps × launches per rep."""
     spl = b["config"]["steps_per_launch"]
     nw = math.ceil(b["warmup"] / spl) if b["warmup"] else 0
+    nw += (b["config"].get("clock_settle") or {}).get("launches", 0)
     per = b["roofline"]["launches"]
     return nw, min(n_dispatch, nw + b["reps"] * per)
 
@@ -66,7 +68,7 @@ for cfg in ("s20", "s1000"):
         rr = [r for r in rows(f"{d}/{cfg}/{sub}/**/*counter_collection.csv")
               if r["Counter_Name"] == name and STEP.search(r["Kernel_Name"])]
         rr.sort(key=lambda r: int(r["Dispatch_Id"]))
-        a2, z2 = timed_slice(b, len(rr))
+        a2, z2 = timed_slice(line(f"{d}/{cfg}/{sub}.json") or b, len(rr))  # that pass's own settle launches
         pm[name] = [float(r["Counter_Value"]) for r in rr[a2:z2]]
     if pm.get("FETCH_SIZE") and pm.get("WRITE_SIZE"):
         f = sum(pm["FETCH_SIZE"]) / len(pm["FETCH_SIZE"]) * 1024 * 2
@@ -84,7 +86,7 @@ for cfg in ("s20", "s1000"):
             e = by.setdefault(int(r["Dispatch_Id"]), {"ns": int(r["End_Timestamp"]) - int(r["Start_Timestamp"])})
             e[r["Counter_Name"]] = e.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
         ds = [by[k] for k in sorted(by)]
-        a3, z3 = timed_slice(b, len(ds))
+        a3, z3 = timed_slice(line(f"{d}/{cfg}/clock.json") or b, len(ds))
         ds = ds[a3:z3]
         if ds:
             clk = [e["GRBM_GUI_ACTIVE"] / 8 / e["ns"] for e in ds if "GRBM_GUI_ACTIVE" in e]

@@ -1,0 +1,46 @@
+"""RCCL on hardware at one rank: a fresh `torchrun --nproc-per-node 1` child runs
+bench.py with the nccl process group forced at world size 1 (RCCL init, the device
+all_gather_into_tensor of the split-R̂ moments, libemcmc beside torch's HIP context),
+and its diagnostics equal those of the plain single-process line bit for bit."""
+import json
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+ARGS = ["--gpus", "1", "--steps", "20", "--warmup", "5", "--no-cpu", "--settle-ms", "0", "--reps", "1"]
+
+
+@pytest.fixture(autouse=True)
+def _gpu(require_gpu):
+    pass
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _line(cmd, env):
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+
+
+def test_nccl_process_group_at_one_rank_matches_the_single_process_line():
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("WORLD_SIZE", None)
+    single = _line([sys.executable, "bench.py", *ARGS], env)
+    env_n = dict(env, EMCMC_BENCH_FORCE_NCCL="1")
+    rccl = _line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                  "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", *ARGS], env_n)
+    assert single["config"]["process_group"] is None
+    assert rccl["config"]["process_group"] == "nccl" and rccl["n_gpus"] == 1
+    assert rccl["config"]["workload"] == single["config"]["workload"]
+    assert rccl["diagnostics"] == single["diagnostics"]

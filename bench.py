@@ -35,6 +35,7 @@ sys.path.insert(0, str(ROOT / "extensiblemcmc.jl_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (AMD spec; equal to the FP64 vector peak)
+FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak: 1,024 SIMDs x 16 fma lanes x 2 flop x 2.4 GHz
 
 
 def parse():
@@ -458,6 +459,30 @@ def main():
     if cfg4:  # HIP events bracket the launch group, and its bytes cover all three kernels
         out["roofline"]["timed_region"] = ("per launch group: mix_gsn_kernel (steps) + mix_moments_kernel (batched "
                                            "GenericChainStats mean/cov) + mix_readjust_kernel when Haario is due")
+    if cfg4:  # the group is VALU-issue bound, not HBM-bound: fp64 rate and VALU busy next to the HBM figure
+        pc = ROOT / "profiles" / "pmc_compute.json"
+        try:
+            ent = json.loads(pc.read_text()).get(kname) if pc.exists() else None
+        except Exception:
+            ent = None
+        if ent:
+            ks = ent["kernels"]
+            # measured fp64 flop of one launch group (step + moments, readjust when due) at this shape
+            grp = sum(k["fp64_tflops"] * k["avg_ns"] * 1e3 * (k.get("per_group", 1.0)) for k in ks.values())
+            step_k = next((v for n, v in ks.items() if n.startswith("mix_res") or n.startswith("mix_gsn")), None)
+            mom_k = next((v for n, v in ks.items() if n.startswith("mix_moments")), None)
+            live = grp / avg_launch_s / 1e12
+            out["roofline"]["compute"] = {
+                "bound": "valu issue (fp64)", "unit": "TFLOP/s", "peak": FP64_VALU_PEAK_TFS,
+                "achieved": live, "frac": live / FP64_VALU_PEAK_TFS,
+                "note": "fp64 flop per launch group from the PMC pass (64 lanes x (2 FMA + MUL + ADD) per "
+                        "wave-instruction) over this run's HIP-event group time; a fp64 mul or add issues like "
+                        "an fma, so the flop fraction understates the issue fraction: valu_busy is that",
+                "valu_busy": {"step_kernel": step_k and step_k["valu_busy"],
+                              "moments_kernel": mom_k and mom_k["valu_busy"]},
+                "fp64_share_of_valu": {"step_kernel": step_k and step_k["f64_share_of_valu"],
+                                       "moments_kernel": mom_k and mom_k["f64_share_of_valu"]},
+                "source": ent["source"]}
     if cfg3:  # MFMA-bound: the two contractions, 4·N·D flop per chain-step
         flops = 4.0 * w.nobs * w.D * Cg * (a.steps / launches)
         tfs = flops / avg_launch_s / 1e12

@@ -897,7 +897,9 @@ hipEvent_t get_event(emcmc_handle *h) {
         return e;
     }
     hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
+    // timing events only: no system-scope fence when one is recorded (the step kernels'
+    // own end-of-dispatch release covers their results)
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     return e;
 }
 

@@ -6,21 +6,28 @@
 // mix_gsn_kernel runs one lane per chain and streams the chain's 4.2 KB of
 // L_B from HBM on every step (random_walk.jl:229-232 needs L_B⁻¹(θ° − θ) on
 // every step whichever kernel was picked), which bounds it at the HBM roofline.
-// Here a chain owns one 16-lane DPP row; lane r holds rows 2r and 2r+1 of L_B
-// (zero-padded to D, 2·D doubles in VGPRs), loaded once per launch.
+// Here a chain owns one 16-lane DPP row; lane r holds the folded row pair r and
+// 31 − r of L_B (r + 1 and 32 − r nonzeros: 16 + 32 doubles in VGPRs with the
+// zero padding, loaded once per launch), so every lane carries the same share of
+// the triangle and columns j ≥ 16 touch one row per lane instead of two.
 //
 //   normals     lane r draws Philox block r: z_{2r}, z_{2r+1} (the pair layout of
 //               normals<D>); lane 0 the mixture pick, lanes ≥ 1 the accept Exp(1)
 //   θ° = θ + L z  column sweep: z_j broadcast from lane j/2 (row_newbcast), each
-//               lane fma's it into its two rows — every row still accumulates
-//               over j ascending from L_i0·z_0, the oracle's order; columns past
-//               a row's diagonal add 0·z_j, which changes nothing but the sign of
-//               an exact zero: a wave-uniform check redoes that (never seen) case
-//               with masks
-//   y_B = L_B⁻¹(θ° − θ)  column sweep: at column j lane j/2 forms y_j = acc_j /
-//               L_jj (as acc·(1/L_jj)), broadcasts it, every row i > j subtracts
-//               L_ij·y_j — the oracle's row order again; every lane sees every
-//               y_j, so Σ y_j² is accumulated redundantly in the canonical order
+//               lane fma's it into its rows r (j < 16) and 31 − r — every row
+//               still accumulates over j ascending from L_i0·z_0, the oracle's
+//               order; columns past a row's diagonal add 0·z_j, which changes
+//               nothing but the sign of an exact zero: a wave-uniform check redoes
+//               that (never seen) case with masks
+//   layouts     θ and θ° are kept per lane both as the pair (2r, 2r+1) — the HBM
+//               layout of θ, the histories and the Σ_A / target terms — and as
+//               the folded pair (r, 31 − r) of the L_B sweeps; θ° changes layout
+//               through the chain's LDS row (which the per-observation ll reads)
+//   y_B = L_B⁻¹(θ° − θ)  column sweep: at column j the owner of row j (lane j,
+//               or lane 31 − j for j ≥ 16) forms y_j = acc_j / L_jj (as
+//               acc·(1/L_jj)), broadcasts it, every row i > j subtracts L_ij·y_j —
+//               the oracle's row order again; every lane sees every y_j, so
+//               Σ y_j² is accumulated redundantly in the canonical order
 //   Σ_A, Σ_t    diagonal: y_A,i and the target terms sit on the owner lane;
 //               canonical blocks of 8 coordinates are exactly the row's quads
 //               (serial quad scan, then the blocks' pairwise tree via row_shr)
@@ -116,26 +123,33 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
     const double xb0 = cs[2 * DD + 2 * D + i0], xb1 = cs[2 * DD + 2 * D + i1];
     const double *iLt = cs + 2 * DD + D;  // wave-uniform reads (per-observation, non-unit Σ_t)
 
-    // rows 2r and 2r+1 of L_B (packed lower, state_pos layout), zero past the diagonal
-    double L0[D], L1[D];
+    // folded rows fa = r (columns 0..15) and fb = 31 − r (columns 0..31) of L_B
+    // (packed lower, state_pos layout), zero past the diagonal
+    constexpr int H = D / 2;
+    const int fa = r, fb = D - 1 - r;
+    double La[H], Lb[D];
 #pragma unroll
     for (int j = 0; j < D; ++j) {
         // lo_idx(i, j) ≤ lo_idx(31, 31) = DP − 1 for every j: the loads stay in bounds
-        const double v0 = a.LB[state_pos((uint64_t)lo_idx(i0, j), chain, C, DP)];
-        const double v1 = a.LB[state_pos((uint64_t)lo_idx(i1, j), chain, C, DP)];
-        L0[j] = (j <= i0) ? v0 : 0.0;
-        L1[j] = (j <= i1) ? v1 : 0.0;
+        if (j < H) {
+            const double v = a.LB[state_pos((uint64_t)lo_idx(fa, j), chain, C, DP)];
+            La[j] = (j <= fa) ? v : 0.0;
+        }
+        const double v = a.LB[state_pos((uint64_t)lo_idx(fb, j), chain, C, DP)];
+        Lb[j] = (j <= fb) ? v : 0.0;
     }
-    const double iLB0 = a.iLB[(uint64_t)i0 * C + chain], iLB1 = a.iLB[(uint64_t)i1 * C + chain];
+    const double iLBa = a.iLB[(uint64_t)fa * C + chain], iLBb = a.iLB[(uint64_t)fb * C + chain];
     const double c0B = a.c0B[chain];
 
     const uint64_t po = ((uint64_t)r * C + chain) * 16u;  // the lane's pair word in a slot (64-bit: any C)
-    double th0, th1;
+    double th0, th1;  // θ at coordinates 2r, 2r+1
     {
         const d2v t = *reinterpret_cast<const d2v *>(reinterpret_cast<const char *>(a.theta) + po);
         th0 = t.x;
         th1 = t.y;
     }
+    double tfa = a.theta[state_pos((uint64_t)fa, chain, C, D)];  // θ at the folded rows
+    double tfb = a.theta[state_pos((uint64_t)fb, chain, C, D)];
     double ll = a.ll[chain];
     double ra = a.ra[chain];
     uint64_t rg0 = a.ring[2 * chain], rg1 = a.ring[2 * chain + 1];
@@ -178,51 +192,72 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
         const double E = rbcast<1>(ue);
 
         // ---- θ° = θ + L z (random_walk.jl:145-151), L = L_A (diagonal) or L_B
-        double lz0 = 0.0, lz1 = 0.0;
+        double lza = 0.0, lzb = 0.0;  // folded rows fa, fb of L_B z
         static_for<0, D>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
             const double zj = rbcast<j / 2>((j & 1) ? z1 : z0);
             if constexpr (j == 0) {
-                lz0 = L0[0] * zj;
-                lz1 = L1[0] * zj;
+                lza = La[0] * zj;
+                lzb = Lb[0] * zj;
             } else {
-                lz0 = fma(L0[j], zj, lz0);
-                lz1 = fma(L1[j], zj, lz1);
+                if constexpr (j < H) lza = fma(La[j], zj, lza);
+                lzb = fma(Lb[j], zj, lzb);
             }
         });
-        if (__ballot(useB && (lz0 == 0.0 || lz1 == 0.0)) != 0) {
+        if (__ballot(useB && (lza == 0.0 || lzb == 0.0)) != 0) {
             // an exact zero may carry the wrong sign after the padding columns: redo with masks
             static_for<0, D>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
                 const double zj = rbcast<j / 2>((j & 1) ? z1 : z0);
                 if constexpr (j == 0) {
-                    lz0 = L0[0] * zj;
-                    lz1 = L1[0] * zj;
+                    lza = La[0] * zj;
+                    lzb = Lb[0] * zj;
                 } else {
-                    const double n0 = fma(L0[j], zj, lz0), n1 = fma(L1[j], zj, lz1);
-                    lz0 = (j <= i0) ? n0 : lz0;
-                    lz1 = (j <= i1) ? n1 : lz1;
+                    if constexpr (j < H) {
+                        const double n = fma(La[j], zj, lza);
+                        lza = (j <= fa) ? n : lza;
+                    }
+                    const double n = fma(Lb[j], zj, lzb);
+                    lzb = (j <= fb) ? n : lzb;
                 }
             });
         }
-        const double thp0 = th0 + (useB ? lz0 : LA0 * z0);
-        const double thp1 = th1 + (useB ? lz1 : LA1 * z1);
-        const double rr0 = thp0 - th0, rr1 = thp1 - th1;
+        // θ° in the layout its kernel produced it in, then through the chain's LDS row
+        // into the other one (every lane of the row writes before any reads)
+        double thp0 = th0 + LA0 * z0, thp1 = th1 + LA1 * z1;  // pair layout (kernel A)
+        double tpa = tfa + lza, tpb = tfb + lzb;              // folded layout (kernel B)
+        if (useB) {
+            tprow[fa] = tpa;
+            tprow[fb] = tpb;
+        } else {
+            *reinterpret_cast<d2v *>(tprow + i0) = d2v{thp0, thp1};
+        }
+        wave_lds_sync();
+        {
+            const d2v t = *reinterpret_cast<const d2v *>(tprow + i0);
+            thp0 = t.x;
+            thp1 = t.y;
+            tpa = tprow[fa];
+            tpb = tprow[fb];
+        }
+        const double rr0 = thp0 - th0, rr1 = thp1 - th1;  // pair layout (Σ_A term)
+        const double rra = tpa - tfa, rrb = tpb - tfb;    // folded layout (L_B solve)
 
         // ---- log_transition_density of the mixture (random_walk.jl:229-232)
         const double qa = row_sumsq32(rr0 * iLA0, rr1 * iLA1, qlead);
         double qbb[4];
         {
-            double acc0 = rr0, acc1 = rr1;
+            double acca = rra, accb = rrb;
             static_for<0, D>([&](auto jc) {
                 constexpr int j = decltype(jc)::value;
-                const double t = (j & 1) ? acc1 * iLB1 : acc0 * iLB0;
-                const double y = rbcast<j / 2>(t);  // y_B,j
+                // row j's owner: lane j (row fa) for j < 16, lane 31 − j (row fb) above
+                const double t = (j < H) ? acca * iLBa : accb * iLBb;
+                const double y = rbcast<(j < H) ? j : D - 1 - j>(t);  // y_B,j
                 if constexpr (j % 8 == 0) qbb[j / 8] = y * y;
                 else qbb[j / 8] = fma(y, y, qbb[j / 8]);
                 if constexpr (j + 1 < D) {
-                    acc0 = fma(-L0[j], y, acc0);
-                    acc1 = fma(-L1[j], y, acc1);
+                    if constexpr (j < H) acca = fma(-La[j], y, acca);
+                    accb = fma(-Lb[j], y, accb);
                 }
             });
         }
@@ -244,9 +279,7 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
         // ---- compute_ll! (gsn_target.jl:23-29)
         double llp;
         if constexpr (LLMODE == LL_PER_OBS) {
-            *reinterpret_cast<d2v *>(tprow + i0) = d2v{thp0, thp1};
-            wave_lds_sync();
-            llp = 0.0;
+            llp = 0.0;  // θ° is in the chain's LDS row already
             for (uint32_t k0 = 0; k0 < nobs; k0 += kResLanes) {
                 const uint32_t k = k0 + (uint32_t)r;
                 const double *xr = X + (size_t)(k < nobs ? k : 0u) * XS;
@@ -276,7 +309,6 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
                     llp = llp + rbcast<q>(f);
                 });
             }
-            wave_lds_sync();  // the next step's θ° write stays behind this step's reads
         } else {
             double y0 = xb0 - thp0, y1 = xb1 - thp1;
             if constexpr (!UNIT_T) {
@@ -286,6 +318,7 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
             const double qv = row_sumsq32(y0, y1, qlead);
             llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
         }
+        wave_lds_sync();  // the next step's θ° write stays behind this step's reads of the row
         if (!(llp - llp == 0.0)) faults |= 1u;
         // ---- accept_reject! (run.jl:271-278)
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
@@ -295,6 +328,8 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
                                         reinterpret_cast<d2v *>(reinterpret_cast<char *>(a.hist_prop + slot * D * C) + po));
         th0 = acc ? thp0 : th0;
         th1 = acc ? thp1 : th1;
+        tfa = acc ? tpa : tfa;
+        tfb = acc ? tpb : tfb;
         if (s + 1 == a.nsteps && r == 0) a.ll_prop[chain] = llp;
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;

@@ -79,6 +79,10 @@ class LogisticWorkload:
     def nobs(self):
         return self.X.shape[0]
 
+    @property
+    def theta_init(self):  # θinit = 0 (BASELINE cfg 3)
+        return np.zeros(self.D)
+
 
 def cfg3(num_chains: int = 1 << 15, D: int = 64, nobs: int = 100_000, eps: float = None) -> LogisticWorkload:
     """BASELINE cfg 3: MALA on a logistic-regression log-likelihood, N = 1e5, D = 64.

@@ -20,5 +20,5 @@ step bench_driver python3 bench.py --gpus 1 --steps 20 --warmup 5 > $OUT/bench_s
 step bench_default python3 bench.py > $OUT/bench.json 2> $OUT/bench.err
 step bench_cfg4 python3 bench.py --workload cfg4 > $OUT/bench_cfg4.json 2> $OUT/bench_cfg4.err
 for f in bench_s20 bench bench_cfg4; do
-  python3 -c "import json; b=json.load(open('$OUT/$f.json')); print('$f', '%.4g' % b['value'], 'frac %.3f' % b['roofline']['frac'], 'kernel %.4g' % b['kernel_chain_steps_per_s'])"
+  python3 -c "import json; b=json.loads([l for l in open('$OUT/$f.json') if l.startswith('{')][-1]); print('$f', '%.4g' % b['value'], 'frac %.3f' % b['roofline']['frac'], 'kernel %.4g' % b['kernel_chain_steps_per_s'])"
 done

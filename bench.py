@@ -35,6 +35,7 @@ sys.path.insert(0, str(ROOT / "extensiblemcmc.jl_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (AMD spec; equal to the FP64 vector peak)
+FP64_MFMA_MEASURED_TFS = 47.8  # v_mfma_f64_16x16x4f64 issue ceiling measured on MI355X (profiles/r3_mfma_f64_ubench.txt)
 FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak: 1,024 SIMDs x 16 fma lanes x 2 flop x 2.4 GHz
 
 
@@ -492,6 +493,11 @@ def main():
         tfs = flops / avg_launch_s / 1e12
         out["roofline"] = {"bound": "mfma", "achieved": tfs, "peak": FP64_MFMA_PEAK_TFS, "unit": "TFLOP/s",
                            "frac": tfs / FP64_MFMA_PEAK_TFS, "traffic": traffic, "kernel": kname,
+                           "measured_mfma_ceiling": {
+                               "value": FP64_MFMA_MEASURED_TFS, "frac": tfs / FP64_MFMA_MEASURED_TFS,
+                               "source": "profiles/r3_mfma_f64_ubench.txt (scripts/ubench/mfma_f64_chain.hip: "
+                                         "back-to-back v_mfma_f64_16x16x4f64, 8 independent accumulators, "
+                                         "4 waves/SIMD)"},
                            "algorithmic_flops_per_launch": flops, "avg_launch_ms": avg_launch_s * 1e3,
                            "launches": launches, "flops_per_chain_step": 4.0 * w.nobs * w.D}
     if stream_bufs is not None:

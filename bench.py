@@ -36,6 +36,7 @@ sys.path.insert(0, str(ROOT / "extensiblemcmc.jl_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_MFMA_PEAK_TFS = 78.6  # MI355X FP64 matrix peak (AMD spec; equal to the FP64 vector peak)
 FP64_MFMA_MEASURED_TFS = 47.8  # v_mfma_f64_16x16x4f64 issue ceiling measured on MI355X (profiles/r3_mfma_f64_ubench.txt)
+FP64_VALU_MEASURED_TFS = 50.5  # v_fma_f64, 8 independent chains, 2 waves/SIMD (profiles/r3_valu_f64_ubench.txt)
 FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak: 1,024 SIMDs x 16 fma lanes x 2 flop x 2.4 GHz
 
 
@@ -487,6 +488,10 @@ def main():
                               "moments_kernel": mom_k and mom_k["valu_busy"]},
                 "fp64_share_of_valu": {"step_kernel": step_k and step_k["f64_share_of_valu"],
                                        "moments_kernel": mom_k and mom_k["f64_share_of_valu"]},
+                "measured_valu_ceiling": {
+                    "value": FP64_VALU_MEASURED_TFS, "frac": live / FP64_VALU_MEASURED_TFS,
+                    "source": "profiles/r3_valu_f64_ubench.txt (scripts/ubench/valu_f64_rate.hip: v_fma_f64, 8 "
+                              "independent chains per lane, 2 waves/SIMD as these kernels run; 59.5 at 4)"},
                 "source": ent["source"]}
     if cfg3:  # MFMA-bound: the two contractions, 4·N·D flop per chain-step
         flops = 4.0 * w.nobs * w.D * Cg * (a.steps / launches)

@@ -463,12 +463,18 @@ emcmc_status select_mwg(emcmc_handle *h) {
     const bool user = h->target.kind == EMCMC_TARGET_USER;
     std::string usrc, uopts;  // a user update's source: compiled into the same kernel
     bool xt = h->cfg.chain_moments != 0;  // GaussianRandomWalkMix / Haario / chain moments: compiled at run time
+    bool mala = false;                    // MALA updates: compiled at run time with the target's gradient
     for (const auto &u : h->updates) {
         if (u.kernel == EMCMC_USER_UPDATE) usrc = u.usrc, uopts = u.uopts;
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) xt = true;
+        if (u.kernel == EMCMC_MALA) mala = true;
     }
+    if (mala && user && h->target.src.find("EMCMC_USER_GRAD") == std::string::npos)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "MALA needs the target's gradient (compute_gradients_and_momenta!): the user law defines none "
+                    "(EMCMC_USER_GRAD { … })");
     for (const auto &e : mwg_table()) {
-        if (user || !usrc.empty() || xt) break;
+        if (user || !usrc.empty() || xt || mala) break;
         if (e.D != D) continue;
         if (e.nu != 0 && ((size_t)e.nu < nmax || e.nu >= best_nu)) continue;  // smallest NU that fits
         if (e.nu != 0) best_nu = e.nu;
@@ -477,11 +483,12 @@ emcmc_status select_mwg(emcmc_handle *h) {
     }
     // a user law, or a dimension without an ahead-of-time instantiation: the
     // same kernel compiled at run time (emcmc_rtc.hip, cached per process)
-    if (user || !usrc.empty() || xt || (!v.mfn && D <= kMwgMaxD)) {
+    if (user || !usrc.empty() || xt || mala || (!v.mfn && D <= kMwgMaxD)) {
         RtcKernel k;
         const int nu = rtc_wide_nu(D, (int)nmax);
-        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k, usrc, uopts, xt)
-                                     : rtc_compile_gsn(D, full, ll, nu, k, usrc, uopts, xt);
+        const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k, usrc, uopts, xt,
+                                                        mala)
+                                     : rtc_compile_gsn(D, full, ll, nu, k, usrc, uopts, xt, mala);
         if (!log.empty()) {
             h->err = std::string(user || !usrc.empty() ? "user target / update does not compile:\n"
                                                         : "run-time kernel build failed:\n") +
@@ -524,6 +531,15 @@ emcmc_status select_mwg(emcmc_handle *h) {
         }
         if (u.kernel == EMCMC_USER_UPDATE) {
             for (size_t q = 0; q < u.uparams.size(); ++q) m.L[q] = u.uparams[q];
+        } else if (u.kernel == EMCMC_MALA) {  // ϵ, h and the diagonal factor ϵI of its densities
+            m.eps0[0] = u.eps[0];
+            m.eps0[1] = u.eps[1];
+            for (uint32_t i = 0; i < m.nc; ++i) {
+                m.L[i * kMwgMaxD + i] = u.L[(size_t)i * m.nc + i];
+                m.iL[i] = u.invdiag[i];
+            }
+            m.c0 = u.c0;
+            m.diag = 1u;
         } else if (u.kernel == EMCMC_RW_UNIFORM) {
             for (uint32_t j = 0; j < m.nc; ++j) m.eps0[j] = u.eps[j];
             for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1ull << j) : 0ull;
@@ -694,6 +710,10 @@ emcmc_status select_mala(emcmc_handle *h) {
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA runs on device as the single joint update on coords 1:D");
     if (h->target.kind != EMCMC_TARGET_LOGISTIC)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA on device needs the logistic-regression target");
+    if (h->updates[0].prior != EMCMC_PRIOR_IMPROPER)
+        return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
+                    "MALA on the logistic-regression kernel runs with ImproperPrior only (priors: a user law with "
+                    "EMCMC_USER_GRAD on the general kernel)");
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     Variant v;
     v.afn = mala_lookup(D, full, 0);
@@ -725,8 +745,11 @@ emcmc_status select_mala(emcmc_handle *h) {
 
 emcmc_status select_variant(emcmc_handle *h) {
     if (!h->target_set || h->updates.empty()) return EMCMC_OK;
+    // MALA: the fused MFMA kernel on the logistic-regression target (cfg 3); on any
+    // other target the general kernel with the target's gradient (the built-in
+    // GsnTargetLaw's or a user law's EMCMC_USER_GRAD)
     for (const auto &u : h->updates)
-        if (u.kernel == EMCMC_MALA) return select_mala(h);
+        if (u.kernel == EMCMC_MALA && h->target.kind == EMCMC_TARGET_LOGISTIC) return select_mala(h);
     if (h->target.kind == EMCMC_TARGET_LOGISTIC)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "the logistic-regression target runs on device with MALA only");
     if (h->target.kind == EMCMC_TARGET_USER) return select_mwg(h);  // mix, Haario, chain moments included
@@ -1547,8 +1570,6 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     }
     if (u->prior > EMCMC_PRIOR_STANDARD)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "prior %u has no device plugin", u->prior);
-    if (u->prior != EMCMC_PRIOR_IMPROPER && u->kernel == EMCMC_MALA)
-        return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA runs on device with ImproperPrior only");
     if (u->adaptation != EMCMC_ADPT_NONE &&
         !((u->adaptation == EMCMC_ADPT_UNIF_RW || u->adaptation == EMCMC_ADPT_UNIF_RW_VEC) &&
           u->kernel == EMCMC_RW_UNIFORM) &&
@@ -1609,7 +1630,14 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
     } else if (u->kernel == EMCMC_MALA) {
         if (!u->epsilon || !(u->epsilon[0] > 0.0)) return fail(h, EMCMC_INVALID_ARG, "MALA needs a step size ϵ > 0");
         if (u->adaptation != EMCMC_ADPT_NONE) return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "MALA adaptation");
-        uh.eps.assign(1, u->epsilon[0]);
+        const double e = u->epsilon[0];
+        uh.eps = {e, (e * e) / 2.0};  // ϵ, h = ϵ²/2
+        // the transition density's MvNormal(·, ϵ²I) as the update's diagonal factor L = ϵI
+        uh.L.assign((size_t)n * n, 0.0);
+        for (int i = 0; i < n; ++i) uh.L[(size_t)i * n + i] = e;
+        uh.invdiag.assign(n, 1.0 / e);
+        uh.diag = true;
+        uh.c0 = mvnormal_c0(n, logdet_chol(uh.L, n));
     } else {
         if (!u->epsilon) return fail(h, EMCMC_INVALID_ARG, "UniformRandomWalk needs ϵ");
         uh.eps.assign(u->epsilon, u->epsilon + n);
@@ -1778,7 +1806,10 @@ emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const cha
                                      size_t log_len) {
     if (!source) return EMCMC_INVALID_ARG;
     RtcKernel k;
-    const std::string log = rtc_compile_user(source, options ? options : "", (int)dim, true, (int)dim, k);
+    // a law with a gradient (EMCMC_USER_GRAD) is checked with MALA compiled in
+    const bool mala = std::string(source).find("EMCMC_USER_GRAD") != std::string::npos;
+    const std::string log = rtc_compile_user(source, options ? options : "", (int)dim, true, (int)dim, k,
+                                             std::string(), std::string(), false, mala);
     if (log_out && log_len) {
         const size_t n = std::min(log.size(), log_len - 1);
         std::memcpy(log_out, log.data(), n);

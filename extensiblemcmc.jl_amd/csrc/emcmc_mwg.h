@@ -60,8 +60,9 @@ constexpr uint32_t kPriorImproper = 0u, kPriorImproperPos = 1u, kPriorProduct = 
 constexpr uint32_t kDistNormal = 1u, kDistUniform = 2u, kDistExponential = 3u, kDistGamma = 4u, kDistLogNormal = 5u,
                    kDistBeta = 6u, kDistInverseGamma = 7u, kDistCauchy = 8u, kDistLaplace = 9u, kDistTDist = 10u;
 
-// update kinds (include/emcmc.h): EMCMC_RW_UNIFORM 1, EMCMC_RW_GAUSSIAN 2, a user update 5
-constexpr uint32_t kKindUser = 5u, kKindMix = 3u;
+// update kinds (include/emcmc.h): EMCMC_RW_UNIFORM 1, EMCMC_RW_GAUSSIAN 2, a user update 5,
+// MALA 4 (with the target's gradient: the built-in GsnTargetLaw or a user law's EMCMC_USER_GRAD)
+constexpr uint32_t kKindUser = 5u, kKindMix = 3u, kKindMala = 4u;
 constexpr uint32_t kFaultPosdefMwg = 4u;  // EMCMC_FAULT_POSDEF
 
 // One RandomWalkUpdate (or user update), host-built; read with scalar (uniform) loads.
@@ -421,7 +422,99 @@ struct GsnTarget {
             return a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
         }
     }
+    // ∇_μ loglikelihood(P°, obs) = Σ_k Σ⁻¹(x_k − μ) = n·Σ⁻¹(x̄ − μ) (both likelihood
+    // modes): y = L⁻¹(x̄ − μ) forward (as mwg_sqmahal_t), w = L⁻ᵀy backward
+    // (w_i = (y_i − Σ_{j>i} L_ji w_j)/L_ii, j descending), g = n·w
+    // (oracle orc_gsn_grad).  The hook MALA reads (compute_gradients_and_momenta!).
+    template <int D, int LLMODE, bool ROLL = false>
+    __device__ __forceinline__ static void grad(const MwgParams &a, const double (&mp)[D], double (&g)[D]) {
+        constexpr int UJ = ROLL ? 1 : D;
+        double y[D];
+#pragma unroll UJ
+        for (int i = 0; i < D; ++i) {
+            double acc = a.xbar[i] - mp[i];
+            if (!a.tdiag) {
+#pragma unroll UJ
+                for (int j = 0; j < i; ++j) acc = fma(-a.Lt[i * D + j], y[j], acc);
+            }
+            y[i] = acc * a.iLt[i];
+        }
+#pragma unroll UJ
+        for (int ii = 0; ii < D; ++ii) {
+            const int i = D - 1 - ii;
+            double acc = y[i];
+            if (!a.tdiag) {
+#pragma unroll UJ
+                for (int j = D - 1; j > i; --j) acc = fma(-a.Lt[j * D + i], g[j], acc);
+            }
+            g[i] = acc * a.iLt[i];
+        }
+#pragma unroll UJ
+        for (int i = 0; i < D; ++i) g[i] = a.nobs_d * g[i];
+    }
 };
+
+// ---- MALA (kind 4) on the general kernel -------------------------------------
+// The reference stubs MALAUpdate (updates.jl:216-218) and gives a gradient-based
+// update one hook, compute_gradients_and_momenta!, called on the current state
+// in update_workspaces! (run.jl:110, __PREVIOUS) and on the proposal in
+// compute_ll! (run.jl:259, __PROPOSAL).  The engine's definition over the
+// update's n local coordinates (oracle orc_run_mwg kind 4):
+//   g  = ∇ℓ(x)[coords], x = P°.θ with coords ← θ   (the vector whose ℓ the ratio
+//        pairs with θ: the coordinates outside the update are P°'s)
+//   θ° = m + ϵz, m = θ + h·g, h = ϵ²/2, z_j normal j of (chain, iter, update)
+//   ltd_fwd = logpdf(MvNormal(m, ϵ²I), θ°), g° = ∇ℓ(P°.θ)[coords] after
+//   set_proposal!, ltd_rev = logpdf(MvNormal(θ° + h·g°, ϵ²I), θ); both as the
+//   update's diagonal Gaussian (L = ϵI: c0 − ‖(·)/ϵ‖²/2, the canonical sum).
+// The prior enters the ratio as for any update; MALA has no proposal! redraw.
+// eps0[0] = ϵ, eps0[1] = h (host-computed).
+template <int NU, bool ROLL>
+__device__ __forceinline__ void mwg_mala_forward(const MwgParams &a, const ZigTabs &zt, const MwgUpdate &u,
+                                                 uint32_t n, uint32_t gid, uint32_t iter, uint32_t p,
+                                                 const double (&tl)[NU], const double (&gl)[NU], double (&tp)[NU],
+                                                 double &ltd_fwd, uint32_t &faults) {
+    constexpr int UJ = ROLL ? 1 : NU;
+    const double eps = u.eps0[0], h = u.eps0[1];
+    double r[NU];
+#pragma unroll UJ
+    for (int j = 0; j < NU; ++j) {
+        if ((uint32_t)j < n) {
+            const double z = normal_draw(zt, a.key0, a.key1, gid, iter, p, (uint32_t)j, faults);
+            const double m = tl[j] + h * gl[j];
+            tp[j] = m + eps * z;
+            r[j] = tp[j] - m;
+        } else {
+            tp[j] = 0.0;
+            r[j] = 0.0;
+        }
+    }
+    ltd_fwd = u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0;
+}
+template <int NU, bool ROLL>
+__device__ __forceinline__ double mwg_mala_reverse(const MwgUpdate &u, uint32_t n, const double (&tl)[NU],
+                                                   const double (&tp)[NU], const double (&gp)[NU]) {
+    constexpr int UJ = ROLL ? 1 : NU;
+    const double h = u.eps0[1];
+    double r[NU];
+#pragma unroll UJ
+    for (int j = 0; j < NU; ++j) r[j] = ((uint32_t)j < n) ? tl[j] - (tp[j] + h * gp[j]) : 0.0;
+    return u.c0 - mwg_sqmahal_u<NU, ROLL>(u, n, r) / 2.0;
+}
+// gl[j] = g[coords[j]] for the update's local coordinates (selects over D)
+template <int D, int NU, bool ROLL>
+__device__ __forceinline__ void mwg_gather(const MwgUpdate &u, uint32_t n, const double (&g)[D], double (&gl)[NU]) {
+    constexpr int UJ = ROLL ? 1 : NU;
+#pragma unroll UJ
+    for (int j = 0; j < NU; ++j) {
+        double v = 0.0;
+        if ((uint32_t)j < n) {
+            const uint32_t cj = u.coords[j];
+#pragma unroll
+            for (int d = 0; d < D; ++d) v = (cj == (uint32_t)d) ? g[d] : v;
+        }
+        gl[j] = v;
+    }
+}
 
 // ---- user updates (EMCMC_USER_UPDATE; emcmc_rtc.hip compiles the source) -----
 // The draws a user proposal! makes come from the engine's counter-based stream,
@@ -444,8 +537,13 @@ __device__ __forceinline__ double user_rand(const UserRng &r, uint32_t j) {
 // no user update in this kernel: the branch compiles away
 struct NoUserUpdate {
     static constexpr bool kEnabled = false;
+    static constexpr bool kMala = false;  // MALA updates (kind 4) compiled in
     __device__ __forceinline__ static void propose(UserRng &, const double *, double *, int, const double *) {}
     __device__ __forceinline__ static double ltd(const double *, const double *, int, const double *) { return 0.0; }
+};
+// MALA updates on the general kernel, no user update (compiled at run time)
+struct MalaOnly : NoUserUpdate {
+    static constexpr bool kMala = true;
 };
 
 // ---- one update step on the update's local coordinates (shared by both kernels)
@@ -899,10 +997,40 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
             tl[j] = v;
         }
         double ltd_fwd, ltd_rev, lpp, lpc;
+        bool mala = false;
+        if constexpr (UPD::kMala) mala = (u.kind == kKindMala);  // wave-uniform
+        if constexpr (UPD::kMala) {
+            if (mala) {  // compute_gradients_and_momenta!(__PREVIOUS) at P°.θ with coords ← θ
+                double x[D], g[D], gl[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) x[d] = mp[d];
+#pragma unroll
+                for (int j = 0; j < D; ++j) {
+                    if ((uint32_t)j < n) {
+                        const uint32_t cj = u.coords[j];
+#pragma unroll
+                        for (int d = 0; d < D; ++d) x[d] = (cj == (uint32_t)d) ? tl[j] : x[d];
+                    }
+                }
+                TGT::template grad<D, LLMODE>(a, x, g);
+                mwg_gather<D, D, false>(u, n, g, gl);
+                mwg_mala_forward<D, false>(a, zt, u, n, gid, iter, p, tl, gl, tp, ltd_fwd, faults);
+#pragma unroll
+                for (int j = 0; j < D; ++j) ta[j] = tp[j];
+                ltd_rev = 0.0;
+                lpp = 0.0;
+                lpc = 0.0;
+                if (u.prior != kPriorImproper) {
+                    lpp = mwg_log_prior<D, false>(u, n, tp);
+                    lpc = mwg_log_prior<D, false>(u, n, tl);
+                }
+            }
+        }
         // XT kernels keep the update-local loops rolled: the mixture densities would
         // otherwise unroll four triangular solves per direction (minutes of hiprtc time)
-        mwg_local_step<D, XT, UPD, XT>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
-                                       faults);
+        if (!mala)
+            mwg_local_step<D, XT, UPD, XT>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
+                                           faults);
         // ---- set_proposal!: proposal history and P°.θ[coords] ← θ°
         double prop[D], nst[D];
 #pragma unroll
@@ -921,6 +1049,14 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         }
         // ---- compute_ll!: loglikelihood(P°, obs)
         const double llp = TGT::template loglik<D, LLMODE>(a, mp);
+        if constexpr (UPD::kMala) {
+            if (mala) {  // compute_gradients_and_momenta!(__PROPOSAL) at P°.θ
+                double g[D], gp[D];
+                TGT::template grad<D, LLMODE>(a, mp, g);
+                mwg_gather<D, D, false>(u, n, g, gp);
+                ltd_rev = mwg_mala_reverse<D, false>(u, n, tl, tp, gp);
+            }
+        }
         if (!(llp - llp == 0.0)) faults |= 1u;
         a.ll_prop[(uint64_t)p * C + chain] = llp;
         // ---- accept_reject! (run.jl:268-281)
@@ -998,8 +1134,31 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
         double tl[NU], tp[NU], ta[NU];
         for (int j = 0; j < NU; ++j) tl[j] = ((uint32_t)j < n) ? a.theta[state_pos(u.coords[j], chain, C, D)] : 0.0;
         double ltd_fwd, ltd_rev, lpp, lpc;
-        mwg_local_step<NU, RU, UPD, XT>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
-                                        faults);
+        bool mala = false;
+        if constexpr (UPD::kMala) mala = (u.kind == kKindMala);  // wave-uniform
+        if constexpr (UPD::kMala) {
+            if (mala) {  // compute_gradients_and_momenta!(__PREVIOUS) at P°.θ with coords ← θ
+                for (int j = 0; j < NU; ++j)
+                    if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tl[j];
+                double x[D], g[D], gl[NU];
+#pragma unroll
+                for (int d = 0; d < D; ++d) x[d] = a.mu_p[state_pos(d, chain, C, D)];
+                TGT::template grad<D, LLMODE, RT>(a, x, g);
+                mwg_gather<D, NU, RU>(u, n, g, gl);
+                mwg_mala_forward<NU, RU>(a, zt, u, n, gid, iter, p, tl, gl, tp, ltd_fwd, faults);
+                for (int j = 0; j < NU; ++j) ta[j] = tp[j];
+                ltd_rev = 0.0;
+                lpp = 0.0;
+                lpc = 0.0;
+                if (u.prior != kPriorImproper) {
+                    lpp = mwg_log_prior<NU, RU>(u, n, tp);
+                    lpc = mwg_log_prior<NU, RU>(u, n, tl);
+                }
+            }
+        }
+        if (!mala)
+            mwg_local_step<NU, RU, UPD, XT>(a, zt, u, n, chain, gid, iter, p, tl, tp, ta, ltd_fwd, ltd_rev, lpp, lpc,
+                                            faults);
         // ---- set_proposal!: P°.θ[coords] ← θ°, then all of P°.θ for the likelihood
         for (int j = 0; j < NU; ++j)
             if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tp[j];
@@ -1008,6 +1167,14 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
         for (int d = 0; d < D; ++d) mp[d] = a.mu_p[state_pos(d, chain, C, D)];
         // ---- compute_ll!
         const double llp = TGT::template loglik<D, LLMODE, RT>(a, mp);
+        if constexpr (UPD::kMala) {
+            if (mala) {  // compute_gradients_and_momenta!(__PROPOSAL) at P°.θ
+                double g[D], gp[NU];
+                TGT::template grad<D, LLMODE, RT>(a, mp, g);
+                mwg_gather<D, NU, RU>(u, n, g, gp);
+                ltd_rev = mwg_mala_reverse<NU, RU>(u, n, tl, tp, gp);
+            }
+        }
         if (!(llp - llp == 0.0)) faults |= 1u;
         a.ll_prop[(uint64_t)p * C + chain] = llp;
         // ---- accept_reject! (run.jl:268-281)

@@ -39,9 +39,11 @@ struct RtcKernel {
 int rtc_wide_nu(int D, int nmax);
 // usrc / uopts: a user update's EMCMC_USER_PROPOSAL + EMCMC_USER_LTD source (empty: none)
 // xt: compile GaussianRandomWalkMix / Haario / chain moments in (emcmc_mwg.h XT)
+// mala: compile MALA updates in (kind 4; the target's gradient: GsnTarget::grad or
+// the user law's EMCMC_USER_GRAD, which the source then defines)
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
                              RtcKernel &out, const std::string &usrc = std::string(),
-                             const std::string &uopts = std::string(), bool xt = false);
+                             const std::string &uopts = std::string(), bool xt = false, bool mala = false);
 
 // The text of a law the library ships as an EMCMC_USER_LOGLIK source
 // (csrc/laws/<name>), or nullptr.
@@ -51,6 +53,6 @@ const char *rtc_builtin_law(const char *name);
 // dimension the library has no ahead-of-time instantiation of (inst_mwg.hip).
 std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out,
                             const std::string &usrc = std::string(), const std::string &uopts = std::string(),
-                            bool xt = false);
+                            bool xt = false, bool mala = false);
 
 }  // namespace emcmc

@@ -27,6 +27,10 @@ const char *const kPrelude = R"EMCMC_RTC(#include "emcmc_mwg.h"
     extern "C" __device__ __attribute__((always_inline)) inline double emcmc_user_loglik(                 \
         const double *__restrict__ theta, int D, const double *__restrict__ obs, uint64_t nobs,            \
         const double *__restrict__ params)
+#define EMCMC_USER_GRAD                                                                                    \
+    extern "C" __device__ __attribute__((always_inline)) inline void emcmc_user_grad(                     \
+        const double *__restrict__ theta, int D, const double *__restrict__ obs, uint64_t nobs,            \
+        const double *__restrict__ params, double *__restrict__ grad)
 #define EMCMC_USER_PROPOSAL                                                                                \
     extern "C" __device__ __attribute__((always_inline)) inline void emcmc_user_proposal(                 \
         const double *__restrict__ theta, double *__restrict__ theta_prop, int n,                          \
@@ -48,6 +52,17 @@ struct UserTarget {
     __device__ __forceinline__ static double loglik(const MwgParams &a, const double (&mp)[D]) {
         return emcmc_user_loglik(mp, D, a.obs, (uint64_t)a.nobs, a.user_params);
     }
+    // ∇ loglikelihood(P°, obs) of the user's law (EMCMC_USER_GRAD), the hook
+    // MALA reads (compute_gradients_and_momenta!, updates.jl:123-133); the host
+    // refuses MALA on a law without one
+    template <int D, int LLMODE, bool ROLL = false>
+    __device__ __forceinline__ static void grad(const MwgParams &a, const double (&mp)[D], double (&g)[D]) {
+#ifdef EMCMC_HAS_USER_GRAD
+        emcmc_user_grad(mp, D, a.obs, (uint64_t)a.nobs, a.user_params, g);
+#else
+        for (int d = 0; d < D; ++d) g[d] = __builtin_nan("");
+#endif
+    }
 };
 }  // namespace emcmc
 )EMCMC_RTC";
@@ -57,6 +72,11 @@ namespace emcmc {
 // proposal! / log_transition_density of the user's update (updates.jl:42-93)
 struct UserUpdate {
     static constexpr bool kEnabled = true;
+#ifdef EMCMC_RTC_MALA
+    static constexpr bool kMala = true;  // MALA updates in the same schedule
+#else
+    static constexpr bool kMala = false;
+#endif
     __device__ __forceinline__ static void propose(UserRng &rng, const double *th, double *tp, int n,
                                                    const double *params) {
         emcmc_user_proposal(th, tp, n, params, &rng);
@@ -87,12 +107,12 @@ int rtc_wide_nu(int D, int nmax) { return (D > 16 && nmax <= 16) ? 16 : D; }
 
 std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
                         RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string(),
-                        bool xt = false) {
+                        bool xt = false, bool mala = false) {
     if (D < 1 || D > 64) return "the general schedule kernel runs 1 ≤ D ≤ 64";
     if (nu < 1 || nu > D) nu = D;
     const bool user = !src.empty(), upd = !usrc.empty();
     std::ostringstream key;
-    key << D << '|' << nu << '|' << full << '|' << ll << '|' << xt << '|' << opts << '|' << src << '|' << uopts << '|'
+    key << D << '|' << nu << '|' << full << '|' << ll << '|' << xt << '|' << mala << '|' << opts << '|' << src << '|' << uopts << '|'
         << usrc;
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -105,7 +125,7 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     std::ostringstream expr, name;
     const char *fl = full ? "true" : "false";
     const char *tgt = user ? "emcmc::UserTarget" : "emcmc::GsnTarget";
-    const char *ut = upd ? "emcmc::UserUpdate" : "emcmc::NoUserUpdate";
+    const char *ut = upd ? "emcmc::UserUpdate" : mala ? "emcmc::MalaOnly" : "emcmc::NoUserUpdate";
     const char *xs = xt ? "true" : "false";
     if (D <= 16) {
         expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ", " << ut << ", " << xs
@@ -118,7 +138,7 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     }
     name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << (upd ? ",UserUpdate" : "")
-         << (xt ? ",MIX_MOMENTS" : "") << "[hiprtc]>";
+         << (xt ? ",MIX_MOMENTS" : "") << (mala ? ",MALA" : "") << "[hiprtc]>";
     std::string prog_src = std::string(kPrelude);
     if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
     if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
@@ -130,6 +150,8 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     hiprtcAddNameExpression(prog, ex.c_str());
     // -ffp-contract=off: the parity contract with oracle/ (no implicit fma)
     std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    if (mala) o.push_back("-DEMCMC_RTC_MALA=1");
+    if (user && src.find("EMCMC_USER_GRAD") != std::string::npos) o.push_back("-DEMCMC_HAS_USER_GRAD=1");
     for (const std::string *op : {&opts, &uopts}) {
         std::istringstream is(*op);
         for (std::string w; is >> w;) o.push_back(w);
@@ -167,9 +189,9 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
 }
 
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
-                             RtcKernel &out, const std::string &usrc, const std::string &uopts, bool xt) {
+                             RtcKernel &out, const std::string &usrc, const std::string &uopts, bool xt, bool mala) {
     if (src.empty()) return "empty user source";
-    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts, xt);
+    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts, xt, mala);
 }
 
 const char *rtc_builtin_law(const char *name) {
@@ -179,8 +201,8 @@ const char *rtc_builtin_law(const char *name) {
 }
 
 std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &out, const std::string &usrc,
-                            const std::string &uopts, bool xt) {
-    return rtc_compile("", "", D, full, ll_mode, nu, out, usrc, uopts, xt);
+                            const std::string &uopts, bool xt, bool mala) {
+    return rtc_compile("", "", D, full, ll_mode, nu, out, usrc, uopts, xt, mala);
 }
 
 }  // namespace emcmc

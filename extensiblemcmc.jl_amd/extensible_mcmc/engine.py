@@ -244,14 +244,18 @@ class Engine:
         self.num_updates += 1
         self._update_n.append(int(len(coords)))
 
-    def add_mala_update(self, coords0, eps, prior=L.PRIOR_IMPROPER):
+    def add_mala_update(self, coords0, eps, prior=L.PRIOR_IMPROPER, prior_factors=None):
         """MALA with step size ϵ on coords0 (0-based; the engine's definition of
-        the reference's stub MALAUpdate, updates.jl:216-218)."""
+        the reference's stub MALAUpdate, updates.jl:216-218).  On the logistic
+        target: the fused MFMA kernel (one joint update, ImproperPrior); on
+        GsnTargetLaw or a user law with EMCMC_USER_GRAD: the general kernel (any
+        coordinates, any prior, beside other updates)."""
+        keep = []
         coords = np.ascontiguousarray(coords0, dtype=np.uint32)
         e = np.array([float(eps)])
         u = L.EmcmcUpdateDesc()
         u.kernel = L.MALA
-        u.prior = prior
+        self._prior_desc(u, prior, prior_factors, keep)
         u.num_coords = len(coords)
         u.coords = L.u32ptr(coords)
         u.epsilon = L.dptr(e)

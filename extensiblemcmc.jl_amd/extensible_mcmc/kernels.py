@@ -666,7 +666,10 @@ class MALAUpdate(MCMCGradientBasedUpdate):
     updates.jl:7) whose hook is ``compute_gradients_and_momenta!`` (run.jl:110,
     259).  The engine's definition: θ° = θ + (ϵ²/2)∇ℓ(θ) + ϵz with the MvNormal
     transition density both ways and the reference's accept_reject!
-    (DESIGN.md §2).  Device plugin: the logistic-regression target."""
+    (DESIGN.md §2).  Device plugins: the logistic-regression target (fused fp64
+    MFMA kernel, one joint update), and GsnTargetLaw or any user law whose source
+    defines ``EMCMC_USER_GRAD`` — the law's ``compute_gradients_and_momenta!`` —
+    on the general kernel (any coordinates and prior, in any schedule)."""
 
     eps: float
     coords: Sequence[int]
@@ -678,11 +681,11 @@ class MALAUpdate(MCMCGradientBasedUpdate):
         assert self.eps > 0.0
 
     def to_device(self, engine):
-        if not isinstance(self.prior, ImproperPrior):
-            raise UnsupportedPlugin(f"prior {type(self.prior).__name__} has no device plugin yet")
         if not isinstance(self.adpt, NoAdaptation):
             raise UnsupportedPlugin("MALA step-size adaptation has no device plugin yet")
-        engine.add_mala_update(np.asarray(self.coords, dtype=np.int64) - 1, self.eps, prior=L.PRIOR_IMPROPER)
+        prior, factors = prior_to_device(self.prior, len(self.coords))
+        engine.add_mala_update(np.asarray(self.coords, dtype=np.int64) - 1, self.eps, prior=prior,
+                               prior_factors=factors)
 
 
 class HamiltonianMCUpdate(MCMCGradientBasedUpdate):

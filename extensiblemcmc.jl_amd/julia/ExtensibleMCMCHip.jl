@@ -118,6 +118,7 @@ end
 
 const RW_GAUSSIAN = UInt32(2)
 const RW_GAUSSIAN_MIX = UInt32(3)
+const MALA = UInt32(4)
 const USER_UPDATE = UInt32(5)
 const ADPT_HAARIO = UInt32(2)
 const PRIOR_IMPROPER, PRIOR_IMPROPER_POS, PRIOR_PRODUCT, PRIOR_STANDARD = UInt32(0), UInt32(1), UInt32(2), UInt32(3)
@@ -135,7 +136,9 @@ const H_STATE, H_PROPOSAL, H_LL, H_ACCEPT = UInt32(0), UInt32(1), UInt32(2), UIn
 A user-defined target law for `MI355XBackend`: the law's parameter vector θ
 (`set_parameters!(P, idx, θ)` writes into it, as for any law of the reference,
 src/example/gsn_target.jl:15-21) and its `loglikelihood(P, obs)` written as an
-`EMCMC_USER_LOGLIK { … }` body (include/emcmc.h emcmc_user_target_desc), which the
+`EMCMC_USER_LOGLIK { … }` body — plus, for `HipMALAUpdate`, its gradient as an
+`EMCMC_USER_GRAD { … }` body (the law's `compute_gradients_and_momenta!`) —
+(include/emcmc.h emcmc_user_target_desc), which the
 engine compiles for the device.  `obs` is the `data.obs` vector of observation
 vectors (all of one length).
 """
@@ -199,6 +202,37 @@ function _update_desc(updt::HipUpdate, keep)
     push!(keep, coords, ud, updt)
     EmcmcUpdateDesc(USER_UPDATE, pk, ADPT_NONE, UInt32(length(coords)), pointer(coords), C_NULL, C_NULL, C_NULL,
                     C_NULL, C_NULL, pp, Base.unsafe_convert(Ptr{Cvoid}, ud), 0.0, (0.0, 0.0, 0.0))
+end
+
+"""
+    HipMALAUpdate(ϵ, coords; prior = ImproperPrior())
+
+MALA for `MI355XBackend`: the reference declares `MALAUpdate <: MCMCGradientBasedUpdate`
+without fields or methods (src/updates.jl:216-218) and gives gradient-based
+updates one hook, `compute_gradients_and_momenta!` (updates.jl:123-133, called at
+run.jl:110 and run.jl:259).  The engine's definition (DESIGN.md §2): θ° = θ +
+(ϵ²/2)∇ℓ + ϵz, MvNormal(·, ϵ²I) transition densities both ways, the prior in the
+ratio.  ∇ℓ is the target's: the built-in GsnTargetLaw's, or a `HipTargetLaw`
+whose source also defines `EMCMC_USER_GRAD { … }` (include/emcmc.h); on the
+logistic-regression target the fused MFMA kernel runs it.
+"""
+struct HipMALAUpdate{K,P} <: eMCMC.MCMCGradientBasedUpdate
+    ϵ::Float64
+    coords::K
+    invcoords::Dict{Int,Int}
+    prior::P
+    adpt::eMCMC.NoAdaptation
+end
+HipMALAUpdate(ϵ::Real, coords; prior = eMCMC.ImproperPrior()) =
+    HipMALAUpdate(Float64(ϵ), coords, Dict(c => i for (i, c) in enumerate(coords)), prior, eMCMC.NoAdaptation())
+
+function _update_desc(updt::HipMALAUpdate, keep)
+    coords = UInt32.(collect(updt.coords) .- 1)
+    pk, pp = _prior_desc(updt.prior, length(coords), keep)
+    eps = [updt.ϵ]
+    push!(keep, coords, eps, updt)
+    EmcmcUpdateDesc(MALA, pk, ADPT_NONE, UInt32(length(coords)), pointer(coords), C_NULL, pointer(eps), C_NULL,
+                    C_NULL, C_NULL, pp, C_NULL, 0.0, (0.0, 0.0, 0.0))
 end
 
 function check(st, h, where)
@@ -821,6 +855,6 @@ eMCMC.name_of_update(lws::MI355XLocalWorkspace) = lws.updt_name
 
 export MI355XBackend, state_history, proposal_history, ll_history, acceptance_history, rolling_acceptance,
        adaptation_state, chain_moments, adaptation_moments, mix_state, faults, moments_window, kernel_name, device_count,
-       HipTargetLaw, HipUpdate
+       HipTargetLaw, HipUpdate, HipMALAUpdate
 
 end # module

@@ -59,7 +59,12 @@ typedef enum emcmc_status {
 #define EMCMC_RW_GAUSSIAN 2u      /* GaussianRandomWalk       random_walk.jl:123-171 */
 #define EMCMC_RW_GAUSSIAN_MIX 3u  /* GaussianRandomWalkMix    random_walk.jl:193-232 */
 #define EMCMC_MALA 4u             /* MALAUpdate: a stub in the reference (updates.jl:216-218); the engine's
-                                     definition is in DESIGN.md §2.  epsilon[0] = step size ϵ. */
+                                     definition is in DESIGN.md §2.  epsilon[0] = step size ϵ.  ∇ℓ is the
+                                     target's compute_gradients_and_momenta! (updates.jl:123-133): on the
+                                     logistic-regression target the fused MFMA kernel (one joint update,
+                                     ImproperPrior); on GsnTargetLaw (built-in ∇) or a user law whose source
+                                     defines EMCMC_USER_GRAD, the general kernel (any coords and prior, any
+                                     schedule); a user law without one: EMCMC_UNSUPPORTED_PLUGIN */
 #define EMCMC_USER_UPDATE 5u      /* a user-defined MCMCParamUpdate: its proposal! and log_transition_density
                                      (updates.jl:42-93, the methods an update MUST implement) as device source
                                      compiled at run time; emcmc_update_desc.user_update */
@@ -318,8 +323,13 @@ typedef struct emcmc_target_desc {
  * in the C subset both hiprtc and a C compiler accept: + − × ÷, fma, sqrt, fabs,
  * copysign, em_exp(x), em_log(x) (the engine's exp / log, NaN below 0;
  * oracle/user_prelude.h maps them to their CPU restatement).  Every update kind, prior and adaptation
- * of the general kernel runs with it; D ≤ 64.  GaussianRandomWalkMix and MALA
- * raise EMCMC_UNSUPPORTED_PLUGIN with a user target. */
+ * of the general kernel runs with it; D ≤ 64.  A law may also define its gradient, the
+ * compute_gradients_and_momenta! hook MALA reads (updates.jl:123-133, run.jl:110, 259):
+ *
+ *     EMCMC_USER_GRAD {     // in scope: theta, D, obs, nobs, params as above and
+ *         …                 //   double *grad (out, D entries): ∇ loglikelihood(P°, obs)
+ *     }
+ */
 typedef struct emcmc_user_target_desc {
     uint32_t dim;           /* length(P.θ) = D */
     uint32_t obs_dim;       /* doubles per observation row (the source's business) */

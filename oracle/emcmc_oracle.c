@@ -835,6 +835,9 @@ typedef double (*orc_user_loglik_fn)(const double *theta, int D, const double *o
 typedef void (*orc_user_prop_fn)(const double *theta, double *theta_prop, int n, const double *params,
                                  emcmc_rng *rng);
 typedef double (*orc_user_ltd_fn)(const double *x, const double *y, int n, const double *params);
+/* a user law's gradient (EMCMC_USER_GRAD): ∇ loglikelihood(P°, obs) into grad[D] */
+typedef void (*orc_user_grad_fn)(const double *theta, int D, const double *obs, uint64_t nobs, const double *params,
+                                 double *grad);
 
 #define ORC_FAULT_POSDEF 4u
 
@@ -858,7 +861,29 @@ typedef struct orc_mwg_ext {
     int chain_moments;
     int reserved;
     double *smean, *scov;
+    orc_user_grad_fn user_grad; /* MALA (kind 4) with a user target: the law's EMCMC_USER_GRAD */
 } orc_mwg_ext;
+
+/* ∇_μ loglikelihood(GsnTargetLaw, obs) = Σ_k Σ⁻¹(x_k − μ) = n·Σ⁻¹(x̄ − μ), both
+ * likelihood modes: y = L⁻¹(x̄ − μ) forward, w = L⁻ᵀy backward (w_i = (y_i −
+ * Σ_{j>i} L_ji w_j)/L_ii, j descending), g = n·w — the device's GsnTarget::grad
+ * (emcmc_mwg.h), the hook MALA reads (compute_gradients_and_momenta!). */
+static void orc_gsn_grad(const orc_gsn *g, int D, int tdiag, const double *mp, double *out) {
+    double y[64];
+    for (int i = 0; i < D; ++i) {
+        double acc = g->xbar[i] - mp[i];
+        if (!tdiag)
+            for (int j = 0; j < i; ++j) acc = fma(-g->Lt[(size_t)i * D + j], y[j], acc);
+        y[i] = acc * g->iLt[i];
+    }
+    for (int i = D - 1; i >= 0; --i) {
+        double acc = y[i];
+        if (!tdiag)
+            for (int j = D - 1; j > i; --j) acc = fma(-g->Lt[(size_t)j * D + i], out[j], acc);
+        out[i] = acc * g->iLt[i];
+    }
+    for (int i = 0; i < D; ++i) out[i] = (double)g->nobs * out[i];
+}
 
 /* logpdf(rw::GaussianRandomWalk, a, b) (random_walk.jl:161-171) with its
  * in-place round trips: logJ = −sum(log b[pos]) (left fold; only where a
@@ -967,6 +992,22 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
             free(U);
             return -2;
         }
+        if (u->kind == 4) { /* MALA: ϵ = eps[0]; its densities' MvNormal(·, ϵ²I) as the factor ϵI */
+            const int n = (int)u->nc;
+            const double e = u->eps0[0];
+            if (!(e > 0.0) || (user_ll && !(ext && ext->user_grad))) {
+                free(g);
+                free(U);
+                return -2;
+            }
+            memset(u->L, 0, sizeof(double) * (size_t)n * n);
+            for (int i = 0; i < n; ++i) {
+                u->L[(size_t)i * n + i] = e;
+                u->iL[i] = 1.0 / e;
+            }
+            u->c0 = mvnormal_c0(n, logdet_chol(u->L, n));
+            u->diag = 1;
+        }
         if (u->kind == 2 || u->kind == 3) {
             const int n = (int)u->nc;
             if (orc_cholesky(sigma + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD, n, u->L)) {
@@ -1045,7 +1086,26 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 ltd_fwd = user_ltd(tl, tp, (int)n, user_uparams + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD);
                 ltd_rev = user_ltd(tp, tl, (int)n, user_uparams + (size_t)p * ORC_MWG_MAXD * ORC_MWG_MAXD);
             }
-            for (uint32_t rs = 0; u->kind != 5; ++rs) {
+            /* MALA (kind 4; the reference stubs MALAUpdate, updates.jl:216-218): g =
+             * ∇ℓ(x)[coords] at x = P°.θ with coords ← θ (compute_gradients_and_momenta!
+             * (__PREVIOUS), run.jl:110), m = θ + h·g, θ° = m + ϵz (normal j of (chain,
+             * iter, update)), ltd_fwd = logpdf(MvNormal(m, ϵ²I), θ°); no redraw loop */
+            const double mala_h = (u->eps0[0] * u->eps0[0]) / 2.0;
+            if (u->kind == 4) {
+                double x[ORC_MWG_MAXD], gg[ORC_MWG_MAXD], r[ORC_MWG_MAXD];
+                memcpy(x, mp, sizeof(double) * D);
+                for (uint32_t j = 0; j < n; ++j) x[u->coords[j]] = tl[j];
+                if (user_ll) ext->user_grad(x, D, obs, nobs, user_params, gg);
+                else orc_gsn_grad(g, D, tdiag, x, gg);
+                for (uint32_t j = 0; j < n; ++j) {
+                    const double z = orc_normal(zt, k0, k1, chain_id, iter, p, j, &f);
+                    const double m = tl[j] + mala_h * gg[u->coords[j]];
+                    tp[j] = m + u->eps0[0] * z;
+                    r[j] = tp[j] - m;
+                }
+                ltd_fwd = u->c0 - sqmahal(u->L, u->iL, r, (int)n, 1) / 2.0;
+            }
+            for (uint32_t rs = 0; u->kind != 5 && u->kind != 4; ++rs) {
                 if (u->kind == 1) { /* UniformRandomWalk */
                     for (uint32_t j = 0; j < n; ++j) {
                         const orc_u32x4 r = orc_draw(k0, k1, chain_id, iter, (rs << 16) | (j >> 1), p, 0);
@@ -1092,8 +1152,8 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 }
             }
             double t3[ORC_MWG_MAXD]; /* θ as log_prior(::Previous) reads it */
-            if (u->kind == 5) {
-                /* transition densities done above */
+            if (u->kind == 5 || u->kind == 4) {
+                /* transition densities done above (MALA's reverse one after compute_ll!) */
             } else if (u->kind == 3) {
                 /* logpdf(rw::GaussianRandomWalkMix, a, b) = log((1−λ)·exp(logpdf(gsn_A, a, b)) +
                  * λ·exp(logpdf(gsn_B, a, b))) (random_walk.jl:229-232), each component's logpdf
@@ -1212,6 +1272,15 @@ ORC_EXPORT int orc_run_mwg(int D, uint64_t C, uint32_t chain0, uint64_t seed, ui
                 for (int i = 0; i < D; ++i) r[i] = g->xbar[i] - mp[i];
                 const double qv = sqmahal(g->Lt, g->iLt, r, D, tdiag);
                 llp = (double)nobs * g->t_c0 - (g->S_c + (double)nobs * qv) * 0.5;
+            }
+            if (u->kind == 4) {
+                /* compute_gradients_and_momenta!(__PROPOSAL) (run.jl:259) at P°.θ:
+                 * ltd_rev = logpdf(MvNormal(θ° + h·g°, ϵ²I), θ) */
+                double gg[ORC_MWG_MAXD], rr[ORC_MWG_MAXD];
+                if (user_ll) ext->user_grad(mp, D, obs, nobs, user_params, gg);
+                else orc_gsn_grad(g, D, tdiag, mp, gg);
+                for (uint32_t j = 0; j < n; ++j) rr[j] = tl[j] - (tp[j] + mala_h * gg[u->coords[j]]);
+                ltd_rev = u->c0 - sqmahal(u->L, u->iL, rr, (int)n, 1) / 2.0;
             }
             if (!isfinite(llp)) f |= 1u;
             if (ll_prop) ll_prop[(size_t)p * C + c] = llp;

@@ -118,6 +118,20 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100,
             ltd_fwd, ltd_rev = fwd[0], rev[0]
             for j in range(1, len(cs)):
                 ltd_fwd, ltd_rev = ltd_fwd + fwd[j], ltd_rev + rev[j]
+        elif u["kind"] == 4:                   # MALA (the engine's definition; the reference stubs it)
+            # compute_gradients_and_momenta!(__PREVIOUS) (run.jl:110) at P°.θ with coords ← θ:
+            # ∇ℓ(μ) = Σ_k Σ⁻¹(x_k − μ); θ° = θ + (ϵ²/2)g + ϵz; MvNormal(·, ϵ²I) both ways
+            e = float(u["eps"][0])
+            hm = e * e / 2.0
+            Le = e * np.eye(len(cs))
+            x = mp.copy()
+            x[cs] = tl
+            g = sum(np.linalg.solve(Lt @ Lt.T, xo - x) for xo in obs)[cs]
+            z, _, _ = _oracle.step_variates(seed, chain, it, len(cs), pidx0=p)
+            m = tl + hm * g
+            tp = m + e * z
+            ltd_fwd = mvnormal_logpdf(tp, m, Le)
+            ltd_rev = None                     # after set_proposal! (run.jl:259)
         elif u["kind"] == 3:                   # GaussianRandomWalkMix (random_walk.jl:193-232)
             n = len(cs)
             pos = np.array(u["pos"], dtype=bool) if u.get("pos") is not None else np.zeros(n, dtype=bool)
@@ -185,6 +199,9 @@ def run_mwg_chain(seed, chain, theta0, mu0, updates, t_sigma, obs, steps, W=100,
         llp = 0.0
         for x in obs:
             llp += mvnormal_logpdf(x, mp, Lt)
+        if u["kind"] == 4:                     # compute_gradients_and_momenta!(__PROPOSAL) at P°.θ
+            gp = sum(np.linalg.solve(Lt @ Lt.T, xo - mp) for xo in obs)[cs]
+            ltd_rev = mvnormal_logpdf(tl, tp + hm * gp, Le)
         _, E, _ = _oracle.step_variates(seed, chain, it, 1, pidx0=p)
         llr = llp - ll + ltd_rev - ltd_fwd + 0.0 - 0.0
         acc = bool(E > -llr)

@@ -269,6 +269,7 @@ KIND_USER = 5
 
 
 KIND_MIX = 3
+KIND_MALA = 4
 
 
 def mwg_update(kind, coords0, eps=None, sigma=None, adapt=None, pos=None, prior=PRIOR_IMPROPER, factors=None,
@@ -351,7 +352,7 @@ class _MwgExt(C.Structure):
                 ("M_io", C.POINTER(C.c_uint32)), ("LB", C.POINTER(C.c_double)), ("hmean", C.POINTER(C.c_double)),
                 ("hcov", C.POINTER(C.c_double)), ("off_sq", C.POINTER(C.c_uint64)),
                 ("off_v", C.POINTER(C.c_uint64)), ("chain_moments", C.c_int), ("reserved", C.c_int),
-                ("smean", C.POINTER(C.c_double)), ("scov", C.POINTER(C.c_double))]
+                ("smean", C.POINTER(C.c_double)), ("scov", C.POINTER(C.c_double)), ("user_grad", C.c_void_p)]
 
 
 def _mwg_tables(updates):
@@ -454,10 +455,11 @@ USER_LL_FN = C.CFUNCTYPE(C.c_double, C.POINTER(C.c_double), C.c_int, C.POINTER(C
 
 
 def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll_mode=0, W=100, history=True,
-            nthreads=1, user_ll=None, user_params=None, user_upd=None):
+            nthreads=1, user_ll=None, user_params=None, user_upd=None, user_grad=None):
     """Advance `state` over `steps` [(mcmciter, pidx 1-based), …]; histories per step.
     user_ll: a C function pointer (ctypes) of the user target's loglikelihood, or None
-    for GsnTargetLaw; state.ll_prop receives sub_ws°.ll of every update."""
+    for GsnTargetLaw; user_grad: the law's EMCMC_USER_GRAD (MALA updates, kind 4, on a user
+    law); state.ll_prop receives sub_ws°.ll of every update."""
     L = lib()
     if not hasattr(L, "_mwg_ready"):
         dp, u32p, u64p, u8p = (C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
@@ -484,7 +486,7 @@ def run_mwg(state: MWGState, updates, *, seed, t_sigma, obs, steps, chain0=0, ll
                   state.M.ctypes.data_as(C.POINTER(C.c_uint32)), _d(state.LB), _d(state.hmean), _d(state.hcov),
                   state.off_sq.ctypes.data_as(C.POINTER(C.c_uint64)),
                   state.off_v.ctypes.data_as(C.POINTER(C.c_uint64)), int(state.chain_moments), 0, _d(state.smean),
-                  _d(state.scov))
+                  _d(state.scov), None if user_grad is None else C.cast(user_grad, C.c_void_p))
     up = None if user_params is None else np.ascontiguousarray(user_params, dtype=np.float64)
     steps = np.asarray(steps, dtype=np.uint32).reshape(-1, 2)
     si = np.ascontiguousarray(steps[:, 0])
@@ -536,6 +538,22 @@ def user_loglik(name):
     fn = USER_LL_FN(("emcmc_user_loglik", dll))
     fn._dll = dll  # keep the library loaded
     return fn, src.read_text()
+
+
+USER_GRAD_FN = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.c_uint64,
+                           C.POINTER(C.c_double), C.POINTER(C.c_double))
+
+
+def user_grad(name):
+    """The oracle build's emcmc_user_grad of user target tests/user_targets/<name>.c
+    (a law whose source defines EMCMC_USER_GRAD), as a ctypes function."""
+    so = Path(__file__).resolve().parent / "lib" / f"user_{name}.so"
+    if not so.exists():
+        raise ImportError(f"{so} not built (make -C oracle)")
+    dll = C.CDLL(str(so))
+    fn = USER_GRAD_FN(("emcmc_user_grad", dll))
+    fn._dll = dll
+    return fn
 
 
 USER_PROP_FN = C.CFUNCTYPE(None, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double),

@@ -22,6 +22,10 @@
 #define EMCMC_USER_LOGLIK                                                                              \
     double emcmc_user_loglik(const double *restrict theta, int D, const double *restrict obs, uint64_t nobs, \
                              const double *restrict params)
+/* the law's gradient, ∇ loglikelihood(P°, obs) into grad[D] (optional; MALA reads it) */
+#define EMCMC_USER_GRAD                                                                                \
+    void emcmc_user_grad(const double *restrict theta, int D, const double *restrict obs, uint64_t nobs,   \
+                         const double *restrict params, double *restrict grad)
 /* a user update (include/emcmc.h emcmc_user_update_desc): proposal! and
  * log_transition_density, with the engine's draws by index (oracle_math.h) */
 #define EMCMC_USER_PROPOSAL                                                                                  \

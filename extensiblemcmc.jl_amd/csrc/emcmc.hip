@@ -148,6 +148,8 @@ struct Variant {
     MomentsFn mofn = nullptr;  // batched chain mean/cov (mix_moments_kernel)
     int mo_tiles = 0;
     MalaFn afn = nullptr, ainit = nullptr;  // MALA step / ∇ℓ initialisation kernels
+    hipFunction_t ffn = nullptr;  // a fused single-update kernel compiled at run time (rwm_gsn_chol_kernel
+                                  // at a D without an ahead-of-time instantiation)
     bool mix = false;
     bool xres = false;  // xfn is mix_res_kernel (16 lanes per chain, L_B in registers)
     int lpc = 1;
@@ -452,6 +454,21 @@ emcmc_status allow_lds(emcmc_handle *h, const void *fn, size_t bytes) {
     return EMCMC_OK;
 }
 
+// Load a run-time compiled code object as the handle's module (kept while the
+// same kernel stays selected).
+emcmc_status load_rtc_module(emcmc_handle *h, const RtcKernel &k) {
+    const std::string key = k.name + '|' + k.lowered + '|' + std::to_string(std::hash<std::string>{}(
+                                std::string(k.code.begin(), k.code.end())));
+    if (key == h->umod_key) return EMCMC_OK;
+    if (h->umod) (void)hipModuleUnload(h->umod);
+    h->umod = nullptr;
+    h->umod_key.clear();
+    HIPCHK(h, hipSetDevice(h->cfg.device));
+    HIPCHK(h, hipModuleLoadData(&h->umod, k.code.data()));
+    h->umod_key = key;
+    return EMCMC_OK;
+}
+
 emcmc_status select_mwg(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
@@ -495,16 +512,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
                      log;
             return (user || !usrc.empty()) ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
         }
-        const std::string key = k.name + '|' + k.lowered + '|' + std::to_string(std::hash<std::string>{}(
-                                    std::string(k.code.begin(), k.code.end())));
-        if (key != h->umod_key) {
-            if (h->umod) (void)hipModuleUnload(h->umod);
-            h->umod = nullptr;
-            h->umod_key.clear();
-            HIPCHK(h, hipSetDevice(h->cfg.device));
-            HIPCHK(h, hipModuleLoadData(&h->umod, k.code.data()));
-            h->umod_key = key;
-        }
+        if (emcmc_status st = load_rtc_module(h, k)) return st;
         HIPCHK(h, hipModuleGetFunction(&v.ufn, h->umod, k.lowered.c_str()));
         v.name = k.name;
         best_nu = 1 << 30;
@@ -772,7 +780,10 @@ emcmc_status select_variant(emcmc_handle *h) {
     // a correlated Σ (proposal or target) beyond the fused dense kernel's D ≤ 8:
     // rwm_gsn_chol_kernel (factors through the scalar cache) where instantiated,
     // else the general kernel (forward substitutions from the factors, D ≤ 64)
-    if (!(u.diag && h->target.diag) && D > 8 && !lookup(D, 1, full, ll, 2, false)) return select_mwg(h);
+    // (the chol kernel compiled at run time for other D ≤ kCholRtcMaxD: registers
+    // hold θ, θ° and one substitution vector, 6·D VGPRs)
+    const bool chol_rtc = !(u.diag && h->target.diag) && D > 8 && !lookup(D, 1, full, ll, 2, false);
+    if (chol_rtc && (D > kCholRtcMaxD || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_RTC_CHOL))) return select_mwg(h);
     const bool diag = u.diag && h->target.diag;
     Variant v;
     if (diag) {
@@ -807,17 +818,24 @@ emcmc_status select_variant(emcmc_handle *h) {
         v.dense = D > 8 ? 2 : 1;
         v.fn = lookup(D, 1, full, ll, v.dense, false);
         v.lpc = 1;
+        if (!v.fn && chol_rtc) {
+            RtcKernel k;
+            const std::string log = rtc_compile_chol(D, full, ll, k);
+            if (!log.empty()) return fail(h, EMCMC_HIP_ERROR, "run-time kernel build failed:\n%s", log.c_str());
+            if (emcmc_status st = load_rtc_module(h, k)) return st;
+            HIPCHK(h, hipModuleGetFunction(&v.ffn, h->umod, k.lowered.c_str()));
+        }
     }
-    if (!v.fn)
+    if (!v.fn && !v.ffn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "no device kernel for D=%d (%s, lanes_per_chain=%u); instantiated: diag D∈{1,2,3,4,8,16,32,64}, "
                     "dense D∈{1,2,3,4,8,16,24,32}",
                     D, diag ? "diagonal" : "dense", h->cfg.lanes_per_chain);
     char nm[160];
-    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>",
+    snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>%s",
              v.dense == 3 ? "diag_s" : v.dense == 2 ? "chol" : v.dense ? "dense" : "diag", D, v.lpc,
              full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
-             v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : "");
+             v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : "", v.ffn ? "[hiprtc]" : "");
     v.name = nm;
     // constants for this variant
     std::vector<double> c;
@@ -940,6 +958,25 @@ hipError_t launch_step(emcmc_handle *h, const void *fn, dim3 grid, dim3 block, v
         h->pending_bytes += bytes;
     }
     return e;
+}
+
+// The same for a kernel of a run-time compiled module: event markers around the launch.
+hipError_t launch_module(emcmc_handle *h, hipFunction_t fn, dim3 grid, dim3 block, void **args, size_t lds,
+                         uint64_t bytes) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (h->timing) {
+        e0 = get_event(h);
+        e1 = get_event(h);
+        if (hipError_t e = hipEventRecord(e0, h->stream)) return e;
+    }
+    if (hipError_t e = hipModuleLaunchKernel(fn, grid.x, 1, 1, block.x, 1, 1, (unsigned)lds, h->stream, args, nullptr))
+        return e;
+    if (h->timing) {
+        if (hipError_t e = hipEventRecord(e1, h->stream)) return e;
+        h->ev.emplace_back(e0, e1);
+        h->pending_bytes += bytes;
+    }
+    return hipSuccess;
 }
 
 emcmc_status drain_timing(emcmc_handle *h) {
@@ -1328,20 +1365,8 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
             if (gs) return gs;
         }
         void *args[] = {&a};
-        if (h->var.ufn) {  // a run-time compiled module: event markers around the launch
-            hipEvent_t e0 = nullptr, e1 = nullptr;
-            if (h->timing) {
-                e0 = get_event(h);
-                e1 = get_event(h);
-                HIPCHK(h, hipEventRecord(e0, h->stream));
-            }
-            HIPCHK(h, hipModuleLaunchKernel(h->var.ufn, grid.x, 1, 1, block.x, 1, 1, (unsigned)h->lds_bytes, h->stream,
-                                            args, nullptr));
-            if (h->timing) {
-                HIPCHK(h, hipEventRecord(e1, h->stream));
-                h->ev.emplace_back(e0, e1);
-                h->pending_bytes += bytes_per_launch(h, n, false);
-            }
+        if (h->var.ufn) {  // a run-time compiled module
+            HIPCHK(h, launch_module(h, h->var.ufn, grid, block, args, h->lds_bytes, bytes_per_launch(h, n, false)));
         } else {
             HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.mfn), grid, block, args, h->lds_bytes,
                                   bytes_per_launch(h, n, false)));
@@ -1906,7 +1931,7 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
     if (!h || (!steps && num_steps)) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_state must precede emcmc_run");
     if (!h->target_set) return fail(h, EMCMC_STATE_ERROR, "emcmc_set_target must precede emcmc_run");
-    if (!h->var.fn && !h->var.mfn && !h->var.ufn && !h->var.xfn && !h->var.afn)
+    if (!h->var.fn && !h->var.ffn && !h->var.mfn && !h->var.ufn && !h->var.xfn && !h->var.afn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN, "no kernel variant selected");
     if (!h->d_zig) return fail(h, EMCMC_STATE_ERROR, "state not allocated");
     const uint32_t P = (uint32_t)h->updates.size();
@@ -1985,8 +2010,11 @@ emcmc_status emcmc_run(emcmc_handle *h, const emcmc_step *steps, uint64_t num_st
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[p.pidx0] = steps[j - 1].mcmciter;
         void *args[] = {&p};
-        HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.fn), grid, block, args, h->lds_bytes,
-                              bytes_per_launch(h, n, false)));
+        if (h->var.ffn)
+            HIPCHK(h, launch_module(h, h->var.ffn, grid, block, args, h->lds_bytes, bytes_per_launch(h, n, false)));
+        else
+            HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.fn), grid, block, args, h->lds_bytes,
+                                  bytes_per_launch(h, n, false)));
         h->stats_N += n;
         i = j;
     }

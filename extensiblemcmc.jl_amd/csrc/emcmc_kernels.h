@@ -988,7 +988,9 @@ __device__ __forceinline__ void static_for(F &&f) {
 // SGPRs), and every result is pinned with vpin, so the stream keeps its order.
 // fpre(IntC<i>, x_i) for the prefix, ftab(IntC<j>, IntC<i>, T_ij) for the table.
 template <int D>
-constexpr int chol_chunk() { return D % 16 == 0 ? 16 : 8; }
+constexpr int chol_chunk() {  // the largest of 16, 8, 4, 2, 1 dividing D (the prefix is whole chunks)
+    return D % 16 == 0 ? 16 : D % 8 == 0 ? 8 : D % 4 == 0 ? 4 : D % 2 == 0 ? 2 : 1;
+}
 template <int D, int NA, typename FP, typename FT>
 __device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, FT &&ftab) {
     constexpr int CH = chol_chunk<D>();

@@ -55,4 +55,11 @@ std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &ou
                             const std::string &usrc = std::string(), const std::string &uopts = std::string(),
                             bool xt = false, bool mala = false);
 
+// rwm_gsn_chol_kernel<D, FULL, LL> (emcmc_kernels.h) for a D without an
+// ahead-of-time instantiation (inst_chol.hip: 16, 24, 32): correlated Σ_rw / Σ_t
+// on the fused single-update path.  Up to D = 48 (θ, θ° and one substitution
+// vector in registers; beyond, the general kernel).
+constexpr int kCholRtcMaxD = 48;
+std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out);
+
 }  // namespace emcmc

@@ -194,6 +194,59 @@ std::string rtc_compile_user(const std::string &src, const std::string &opts, in
     return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts, xt, mala);
 }
 
+std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
+    if (D < 2 || D > kCholRtcMaxD) return "rwm_gsn_chol_kernel is compiled at run time for 2 ≤ D ≤ 48";
+    std::ostringstream key, expr, name;
+    key << "chol|" << D << '|' << full << '|' << ll_mode;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto it = g_cache.find(key.str());
+        if (it != g_cache.end()) {
+            out = it->second;
+            return "";
+        }
+    }
+    expr << "emcmc::rwm_gsn_chol_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ">";
+    name << "rwm_gsn_chol_kernel<D=" << D << ",LPC=1," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
+    const std::string src = "#include \"emcmc_kernels.h\"\n";
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "chol_kernel.hip", kRtcHeaderCount, kRtcHeaderSrc, kRtcHeaderNames) !=
+        HIPRTC_SUCCESS)
+        return "hiprtcCreateProgram failed";
+    const std::string ex = expr.str();
+    hiprtcAddNameExpression(prog, ex.c_str());
+    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+    const std::string log = program_log(prog);
+    if (rc != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        return std::string("hiprtc: ") + hiprtcGetErrorString(rc) + "\n" + log;
+    }
+    RtcKernel k;
+    const char *low = nullptr;
+    size_t n = 0;
+    if (hiprtcGetLoweredName(prog, ex.c_str(), &low) != HIPRTC_SUCCESS || !low ||
+        hiprtcGetCodeSize(prog, &n) != HIPRTC_SUCCESS || n == 0) {
+        hiprtcDestroyProgram(&prog);
+        return "hiprtc: no code object for " + ex;
+    }
+    k.lowered = low;
+    k.code.resize(n);
+    if (hiprtcGetCode(prog, k.code.data()) != HIPRTC_SUCCESS) {
+        hiprtcDestroyProgram(&prog);
+        return "hiprtcGetCode failed";
+    }
+    hiprtcDestroyProgram(&prog);
+    k.name = name.str();
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_cache[key.str()] = k;
+    }
+    out = std::move(k);
+    return "";
+}
+
 const char *rtc_builtin_law(const char *name) {
     for (int i = 0; i < kRtcHeaderCount; ++i)
         if (std::string(kRtcHeaderNames[i]) == name) return kRtcHeaderSrc[i];

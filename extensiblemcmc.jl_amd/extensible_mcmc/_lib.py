@@ -56,6 +56,7 @@ VARIANT_OCCUPANCY3 = 2
 VARIANT_SCALAR_OBS = 4
 VARIANT_MIX_STREAM = 8
 VARIANT_NO_XCD_ORDER = 16
+VARIANT_NO_RTC_CHOL = 32
 
 
 class EmcmcConfig(C.Structure):

@@ -173,6 +173,8 @@ typedef struct emcmc_config {
 #define EMCMC_VARIANT_MIX_STREAM 8u      /* GaussianRandomWalkMix: stream L_B from HBM every step (mix_gsn_kernel)
                                             instead of keeping it in registers (mix_res_kernel) */
 #define EMCMC_VARIANT_NO_XCD_ORDER 16u   /* blocks in blockIdx order instead of one contiguous chain range per XCD */
+#define EMCMC_VARIANT_NO_RTC_CHOL 32u    /* a correlated Σ at a D without an ahead-of-time rwm_gsn_chol_kernel runs on
+                                            the general kernel instead of the chol kernel compiled at run time */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,

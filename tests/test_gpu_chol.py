@@ -69,3 +69,27 @@ def test_chol_kernel_overdispersed_start_and_shards(oracle):
     th0 = w.mu_true + 3.0 * np.random.default_rng(3).standard_normal((512, 32))
     e = run_engine(w, 512, 60, chain0=4096, theta0=th0)
     assert_bitwise(e, run_oracle(oracle, w, 512, 60, chain0=4096, theta0=th0))
+
+
+@pytest.mark.parametrize("D,ll_mode", [(9, L.LL_PER_OBS), (12, L.LL_SUFFSTAT), (20, L.LL_PER_OBS),
+                                       (40, L.LL_SUFFSTAT), (48, L.LL_PER_OBS)])
+def test_chol_kernel_compiled_at_run_time(oracle, D, ll_mode):
+    """A correlated Σ at a D without an ahead-of-time instantiation: the same
+    rwm_gsn_chol_kernel compiled with hiprtc (chunks of 16/8/4/2/1 doubles as D
+    allows), bitwise against the oracle — where round 2 ran the general kernel."""
+    w = _corr(D, 100 + D)
+    e = run_engine(w, 1536, 60, ll_mode=ll_mode)
+    assert e["kernel"].startswith(f"rwm_gsn_chol_kernel<D={D},") and "[hiprtc]" in e["kernel"]
+    assert_bitwise(e, run_oracle(oracle, w, 1536, 60, ll_mode=ll_mode))
+    assert 0.02 < e["acc"][10:].mean() < 0.9
+
+
+def test_chol_rtc_equals_general_kernel(oracle):
+    """EMCMC_VARIANT_NO_RTC_CHOL keeps the round-2 route (the general kernel); both
+    routes give the same bits at D = 20."""
+    w = _corr(20, 5)
+    a = run_engine(w, 512, 40)
+    b = run_engine(w, 512, 40, variant=L.VARIANT_NO_RTC_CHOL)
+    assert "chol" in a["kernel"] and "mwg" in b["kernel"]
+    for k in ("acc", "theta", "ll", "ra", "nacc", "theta_hist", "prop_hist", "ll_hist"):
+        assert np.array_equal(a[k], b[k]), k

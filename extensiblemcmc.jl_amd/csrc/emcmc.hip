@@ -780,8 +780,8 @@ emcmc_status select_variant(emcmc_handle *h) {
     // a correlated Σ (proposal or target) beyond the fused dense kernel's D ≤ 8:
     // rwm_gsn_chol_kernel (factors through the scalar cache) where instantiated,
     // else the general kernel (forward substitutions from the factors, D ≤ 64)
-    // (the chol kernel compiled at run time for other D ≤ kCholRtcMaxD: registers
-    // hold θ, θ° and one substitution vector, 6·D VGPRs)
+    // (the chol kernel compiled at run time for other D ≤ kCholRtcMaxD = 64:
+    // registers hold θ, θ° and one substitution vector, 6·D VGPRs)
     const bool chol_rtc = !(u.diag && h->target.diag) && D > 8 && !lookup(D, 1, full, ll, 2, false);
     if (chol_rtc && (D > kCholRtcMaxD || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_RTC_CHOL))) return select_mwg(h);
     const bool diag = u.diag && h->target.diag;

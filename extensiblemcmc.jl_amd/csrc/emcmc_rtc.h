@@ -57,9 +57,10 @@ std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &ou
 
 // rwm_gsn_chol_kernel<D, FULL, LL> (emcmc_kernels.h) for a D without an
 // ahead-of-time instantiation (inst_chol.hip: 16, 24, 32): correlated Σ_rw / Σ_t
-// on the fused single-update path.  Up to D = 48 (θ, θ° and one substitution
-// vector in registers; beyond, the general kernel).
-constexpr int kCholRtcMaxD = 48;
+// on the fused single-update path, any D ≤ 64 (θ, θ° and one substitution vector
+// in registers: no spills to D = 40, AGPR and scratch spills above — still 20–45×
+// the general kernel).
+constexpr int kCholRtcMaxD = 64;
 std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out);
 
 }  // namespace emcmc

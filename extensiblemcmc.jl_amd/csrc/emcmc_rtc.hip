@@ -195,7 +195,7 @@ std::string rtc_compile_user(const std::string &src, const std::string &opts, in
 }
 
 std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
-    if (D < 2 || D > kCholRtcMaxD) return "rwm_gsn_chol_kernel is compiled at run time for 2 ≤ D ≤ 48";
+    if (D < 2 || D > kCholRtcMaxD) return "rwm_gsn_chol_kernel is compiled at run time for 2 ≤ D ≤ 64";
     std::ostringstream key, expr, name;
     key << "chol|" << D << '|' << full << '|' << ll_mode;
     {

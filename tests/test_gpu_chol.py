@@ -72,7 +72,7 @@ def test_chol_kernel_overdispersed_start_and_shards(oracle):
 
 
 @pytest.mark.parametrize("D,ll_mode", [(9, L.LL_PER_OBS), (12, L.LL_SUFFSTAT), (20, L.LL_PER_OBS),
-                                       (40, L.LL_SUFFSTAT), (48, L.LL_PER_OBS)])
+                                       (40, L.LL_SUFFSTAT), (48, L.LL_PER_OBS), (64, L.LL_PER_OBS)])
 def test_chol_kernel_compiled_at_run_time(oracle, D, ll_mode):
     """A correlated Σ at a D without an ahead-of-time instantiation: the same
     rwm_gsn_chol_kernel compiled with hiprtc (chunks of 16/8/4/2/1 doubles as D

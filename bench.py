@@ -60,7 +60,9 @@ def parse():
     ap.add_argument("--history", choices=["full", "accept_only"], default="full")
     ap.add_argument("--ll-mode", choices=["per_obs", "suffstat"], default="per_obs")
     ap.add_argument("--lpc", type=int, default=0)
-    ap.add_argument("--steps-per-launch", type=int, default=100)
+    ap.add_argument("--steps-per-launch", type=int, default=None,
+                    help="steps per kernel launch (default 100; cfg 4: its readjust period k = 200, so every "
+                         "launch group runs up to a readjust — +2.5%% against 100, profiles/r3_cfg4_k)")
     ap.add_argument("--variant", type=int, default=0,
                     help="emcmc_config.kernel_variant (EMCMC_VARIANT_* flags; same results, for A/B timing)")
     ap.add_argument("--reps", type=int, default=0,
@@ -282,6 +284,8 @@ def main():
         w.num_chains = Cg
     else:
         w = W.cfg2(Cg)
+    if a.steps_per_launch is None:  # cfg 4: one launch group per readjust period
+        a.steps_per_launch = w.haario_k if cfg4 else 100
     theta0 = np.broadcast_to(np.asarray(w.theta_init, dtype=np.float64), (Cg, w.D))
     ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
     hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
@@ -473,8 +477,10 @@ def main():
             ent = None
         if ent:
             ks = ent["kernels"]
-            # measured fp64 flop of one launch group (step + moments, readjust when due) at this shape
+            # measured fp64 flop of one launch group (step + moments, readjust when due) at this shape,
+            # per step of the PMC pass's launch length, times this run's steps per launch
             grp = sum(k["fp64_tflops"] * k["avg_ns"] * 1e3 * (k.get("per_group", 1.0)) for k in ks.values())
+            grp *= (a.steps / launches) / float(ent.get("steps_per_launch", 100))
             step_k = next((v for n, v in ks.items() if n.startswith("mix_res") or n.startswith("mix_gsn")), None)
             mom_k = next((v for n, v in ks.items() if n.startswith("mix_moments")), None)
             live = grp / avg_launch_s / 1e12

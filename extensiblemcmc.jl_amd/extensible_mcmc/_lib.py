@@ -265,6 +265,16 @@ class EMCMCError(RuntimeError):
         super().__init__(f"{where}: {STATUS_NAMES.get(status, status)}" + (f" — {message}" if message else ""))
 
 
+class UnsupportedPlugin(NotImplementedError):
+    """A plugin (update, transition kernel, prior, target) with no device
+    implementation: raised instead of any CPU fallback."""
+
+
+class UnsupportedPluginError(EMCMCError, UnsupportedPlugin):
+    """EMCMC_UNSUPPORTED_PLUGIN from the library: both an EMCMCError (with the
+    status and message) and an UnsupportedPlugin."""
+
+
 _lib = None
 
 

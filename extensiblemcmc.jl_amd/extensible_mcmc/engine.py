@@ -94,7 +94,8 @@ class Engine:
     def _check(self, st: int, where: str):
         if st != L.OK:
             msg = self._lib.emcmc_last_error(self._h)
-            raise L.EMCMCError(st, where, msg.decode() if msg else "")
+            cls = L.UnsupportedPluginError if st == L.UNSUPPORTED_PLUGIN else L.EMCMCError
+            raise cls(st, where, msg.decode() if msg else "")
 
     def close(self):
         if getattr(self, "_h", None):

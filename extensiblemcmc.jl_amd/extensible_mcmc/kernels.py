@@ -19,8 +19,7 @@ from math import lgamma  # noqa: E402
 from . import _lib as L
 
 
-class UnsupportedPlugin(NotImplementedError):
-    pass
+UnsupportedPlugin = L.UnsupportedPlugin  # also raised, as UnsupportedPluginError, for EMCMC_UNSUPPORTED_PLUGIN
 
 
 # ---------------------------------------------------------------------------

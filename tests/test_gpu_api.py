@@ -57,10 +57,15 @@ def test_unsupported_plugins_raise_not_fallback():
                  RandomWalkUpdate(GaussianRandomWalk(np.eye(1)), [2])], backend=MI355XBackend(num_chains=8))
     with pytest.raises(UnsupportedPlugin):
         run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [0.0, 0.0])
-    # MALA's device plugin takes ImproperPrior only
-    mcmc = MCMC([MALAUpdate(0.1, [1, 2], prior=ProductPrior([Normal()], [1]))], backend=MI355XBackend(num_chains=8))
+    # MALA's fused logistic-regression kernel takes ImproperPrior only (the library's
+    # EMCMC_UNSUPPORTED_PLUGIN surfaces as UnsupportedPlugin)
+    from extensible_mcmc import LogisticRegressionLaw
+    X = np.random.default_rng(0).normal(size=(64, 16))
+    y = (X[:, 0] > 0).astype(float)
+    mcmc = MCMC([MALAUpdate(0.1, list(range(1, 17)), prior=ProductPrior([Normal()], [1]))],
+                backend=MI355XBackend(num_chains=64))
     with pytest.raises(UnsupportedPlugin):
-        run(mcmc, 10, dict(P=GsnTargetLaw([1.0, 2.0]), obs=w.obs), [1.0, 0.0])
+        run(mcmc, 10, dict(P=LogisticRegressionLaw(16), obs=(X, y)), np.zeros(16))
 
 
 def test_positive_mixture_walk_beside_a_gaussian_walk_through_the_api(oracle):

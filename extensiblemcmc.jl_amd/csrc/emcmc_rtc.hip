@@ -105,119 +105,32 @@ std::string program_log(hiprtcProgram p) {
 // src empty: the built-in GsnTarget with likelihood mode ll; else the user's law
 int rtc_wide_nu(int D, int nmax) { return (D > 16 && nmax <= 16) ? 16 : D; }
 
-std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
-                        RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string(),
-                        bool xt = false, bool mala = false) {
-    if (D < 1 || D > 64) return "the general schedule kernel runs 1 ≤ D ≤ 64";
-    if (nu < 1 || nu > D) nu = D;
-    const bool user = !src.empty(), upd = !usrc.empty();
-    std::ostringstream key;
-    key << D << '|' << nu << '|' << full << '|' << ll << '|' << xt << '|' << mala << '|' << opts << '|' << src << '|' << uopts << '|'
-        << usrc;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        auto it = g_cache.find(key.str());
-        if (it != g_cache.end()) {
-            out = it->second;
-            return "";
-        }
-    }
-    std::ostringstream expr, name;
-    const char *fl = full ? "true" : "false";
-    const char *tgt = user ? "emcmc::UserTarget" : "emcmc::GsnTarget";
-    const char *ut = upd ? "emcmc::UserUpdate" : mala ? "emcmc::MalaOnly" : "emcmc::NoUserUpdate";
-    const char *xs = xt ? "true" : "false";
-    if (D <= 16) {
-        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ", " << ut << ", " << xs
-             << ">";
-        name << "mwg_gsn_kernel<D=" << D;
-    } else {
-        expr << "emcmc::mwg_wide_kernel<" << D << ", " << nu << ", " << fl << ", " << ll << ", " << tgt << ", " << ut
-             << ", " << xs << ">";
-        name << "mwg_wide_kernel<D=" << D << ",NU=" << nu;
-    }
-    name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
-         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << (upd ? ",UserUpdate" : "")
-         << (xt ? ",MIX_MOMENTS" : "") << (mala ? ",MALA" : "") << "[hiprtc]>";
-    std::string prog_src = std::string(kPrelude);
-    if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
-    if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, prog_src.c_str(), user ? "user_target.hip" : upd ? "user_update.hip" : "gsn_target.hip",
-                            kRtcHeaderCount, kRtcHeaderSrc, kRtcHeaderNames) != HIPRTC_SUCCESS)
-        return "hiprtcCreateProgram failed";
-    const std::string ex = expr.str();
-    hiprtcAddNameExpression(prog, ex.c_str());
-    // -ffp-contract=off: the parity contract with oracle/ (no implicit fma)
-    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
-    if (mala) o.push_back("-DEMCMC_RTC_MALA=1");
-    if (user && src.find("EMCMC_USER_GRAD") != std::string::npos) o.push_back("-DEMCMC_HAS_USER_GRAD=1");
-    for (const std::string *op : {&opts, &uopts}) {
-        std::istringstream is(*op);
-        for (std::string w; is >> w;) o.push_back(w);
-    }
-    std::vector<const char *> ov;
-    for (const auto &s : o) ov.push_back(s.c_str());
-    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)ov.size(), ov.data());
-    std::string log = program_log(prog);
-    if (rc != HIPRTC_SUCCESS) {
-        hiprtcDestroyProgram(&prog);
-        return std::string("hiprtc: ") + hiprtcGetErrorString(rc) + "\n" + log;
-    }
-    RtcKernel k;
-    const char *low = nullptr;
-    size_t n = 0;
-    if (hiprtcGetLoweredName(prog, ex.c_str(), &low) != HIPRTC_SUCCESS || !low ||
-        hiprtcGetCodeSize(prog, &n) != HIPRTC_SUCCESS || n == 0) {
-        hiprtcDestroyProgram(&prog);
-        return "hiprtc: no code object for " + ex;
-    }
-    k.lowered = low;
-    k.code.resize(n);
-    if (hiprtcGetCode(prog, k.code.data()) != HIPRTC_SUCCESS) {
-        hiprtcDestroyProgram(&prog);
-        return "hiprtcGetCode failed";
-    }
-    hiprtcDestroyProgram(&prog);
-    k.name = name.str();
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        g_cache[key.str()] = k;
-    }
-    out = std::move(k);
-    return "";
+namespace {
+
+bool cache_get(const std::string &key, RtcKernel &out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_cache.find(key);
+    if (it == g_cache.end()) return false;
+    out = it->second;
+    return true;
 }
 
-std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
-                             RtcKernel &out, const std::string &usrc, const std::string &uopts, bool xt, bool mala) {
-    if (src.empty()) return "empty user source";
-    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts, xt, mala);
-}
-
-std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
-    if (D < 2 || D > kCholRtcMaxD) return "rwm_gsn_chol_kernel is compiled at run time for 2 ≤ D ≤ 64";
-    std::ostringstream key, expr, name;
-    key << "chol|" << D << '|' << full << '|' << ll_mode;
-    {
-        std::lock_guard<std::mutex> lk(g_mu);
-        auto it = g_cache.find(key.str());
-        if (it != g_cache.end()) {
-            out = it->second;
-            return "";
-        }
-    }
-    expr << "emcmc::rwm_gsn_chol_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ">";
-    name << "rwm_gsn_chol_kernel<D=" << D << ",LPC=1," << (full ? "FULL" : "ACCEPT_ONLY") << ","
-         << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
-    const std::string src = "#include \"emcmc_kernels.h\"\n";
+// Compile prog_src for gfx950 and fetch the code object of the kernel named by
+// the expression ex; cache it under key.  Returns "" or the compiler's log.
+// -ffp-contract=off: the parity contract with oracle/ (no implicit fma).
+std::string compile_kernel(const std::string &key, const std::string &prog_src, const char *file,
+                           const std::string &ex, const std::string &name, const std::vector<std::string> &extra,
+                           RtcKernel &out) {
     hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "chol_kernel.hip", kRtcHeaderCount, kRtcHeaderSrc, kRtcHeaderNames) !=
+    if (hiprtcCreateProgram(&prog, prog_src.c_str(), file, kRtcHeaderCount, kRtcHeaderSrc, kRtcHeaderNames) !=
         HIPRTC_SUCCESS)
         return "hiprtcCreateProgram failed";
-    const std::string ex = expr.str();
     hiprtcAddNameExpression(prog, ex.c_str());
-    const char *opts[] = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
-    const hiprtcResult rc = hiprtcCompileProgram(prog, 4, opts);
+    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    o.insert(o.end(), extra.begin(), extra.end());
+    std::vector<const char *> ov;
+    for (const auto &w : o) ov.push_back(w.c_str());
+    const hiprtcResult rc = hiprtcCompileProgram(prog, (int)ov.size(), ov.data());
     const std::string log = program_log(prog);
     if (rc != HIPRTC_SUCCESS) {
         hiprtcDestroyProgram(&prog);
@@ -238,13 +151,74 @@ std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
         return "hiprtcGetCode failed";
     }
     hiprtcDestroyProgram(&prog);
-    k.name = name.str();
+    k.name = name;
     {
         std::lock_guard<std::mutex> lk(g_mu);
-        g_cache[key.str()] = k;
+        g_cache[key] = k;
     }
     out = std::move(k);
     return "";
+}
+
+}  // namespace
+
+std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
+                        RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string(),
+                        bool xt = false, bool mala = false) {
+    if (D < 1 || D > 64) return "the general schedule kernel runs 1 ≤ D ≤ 64";
+    if (nu < 1 || nu > D) nu = D;
+    const bool user = !src.empty(), upd = !usrc.empty();
+    std::ostringstream key;
+    key << D << '|' << nu << '|' << full << '|' << ll << '|' << xt << '|' << mala << '|' << opts << '|' << src << '|'
+        << uopts << '|' << usrc;
+    if (cache_get(key.str(), out)) return "";
+    std::ostringstream expr, name;
+    const char *fl = full ? "true" : "false";
+    const char *tgt = user ? "emcmc::UserTarget" : "emcmc::GsnTarget";
+    const char *ut = upd ? "emcmc::UserUpdate" : mala ? "emcmc::MalaOnly" : "emcmc::NoUserUpdate";
+    const char *xs = xt ? "true" : "false";
+    if (D <= 16) {
+        expr << "emcmc::mwg_gsn_kernel<" << D << ", " << fl << ", " << ll << ", " << tgt << ", " << ut << ", " << xs
+             << ">";
+        name << "mwg_gsn_kernel<D=" << D;
+    } else {
+        expr << "emcmc::mwg_wide_kernel<" << D << ", " << nu << ", " << fl << ", " << ll << ", " << tgt << ", " << ut
+             << ", " << xs << ">";
+        name << "mwg_wide_kernel<D=" << D << ",NU=" << nu;
+    }
+    name << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (user ? "UserTarget" : ll == 0 ? "PER_OBS" : "SUFFSTAT") << (upd ? ",UserUpdate" : "")
+         << (xt ? ",MIX_MOMENTS" : "") << (mala ? ",MALA" : "") << "[hiprtc]>";
+    std::string prog_src = std::string(kPrelude);
+    if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
+    if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
+    std::vector<std::string> extra;
+    if (mala) extra.push_back("-DEMCMC_RTC_MALA=1");
+    if (user && src.find("EMCMC_USER_GRAD") != std::string::npos) extra.push_back("-DEMCMC_HAS_USER_GRAD=1");
+    for (const std::string *op : {&opts, &uopts}) {
+        std::istringstream is(*op);
+        for (std::string w; is >> w;) extra.push_back(w);
+    }
+    return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : upd ? "user_update.hip" : "gsn_target.hip",
+                          expr.str(), name.str(), extra, out);
+}
+
+std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
+                             RtcKernel &out, const std::string &usrc, const std::string &uopts, bool xt, bool mala) {
+    if (src.empty()) return "empty user source";
+    return rtc_compile(src, opts, D, full, 0, nu, out, usrc, uopts, xt, mala);
+}
+
+std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
+    if (D < 2 || D > kCholRtcMaxD) return "rwm_gsn_chol_kernel is compiled at run time for 2 ≤ D ≤ 64";
+    std::ostringstream key, expr, name;
+    key << "chol|" << D << '|' << full << '|' << ll_mode;
+    if (cache_get(key.str(), out)) return "";
+    expr << "emcmc::rwm_gsn_chol_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ">";
+    name << "rwm_gsn_chol_kernel<D=" << D << ",LPC=1," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
+    return compile_kernel(key.str(), "#include \"emcmc_kernels.h\"\n", "chol_kernel.hip", expr.str(), name.str(), {},
+                          out);
 }
 
 const char *rtc_builtin_law(const char *name) {

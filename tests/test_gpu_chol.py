@@ -93,3 +93,14 @@ def test_chol_rtc_equals_general_kernel(oracle):
     assert "chol" in a["kernel"] and "mwg" in b["kernel"]
     for k in ("acc", "theta", "ll", "ra", "nacc", "theta_hist", "prop_hist", "ll_hist"):
         assert np.array_equal(a[k], b[k]), k
+
+
+def test_chol_rtc_accept_only_and_launch_splits(oracle):
+    """The run-time compiled kernel (D = 20) with accept-only histories, a ragged chain
+    count and launches of 1, 7 and 64 steps: the same bits as one full-history launch."""
+    w = _corr(20, 17)
+    o = run_oracle(oracle, w, 999, 50)
+    for spl in (1, 7, 64):
+        e = run_engine(w, 999, 50, hist=L.HIST_ACCEPT_ONLY, spl=spl)
+        assert "[hiprtc]" in e["kernel"] and "ACCEPT_ONLY" in e["kernel"]
+        assert_bitwise(e, o, full=False)

@@ -160,3 +160,32 @@ def test_mala_update_through_the_api(oracle):
                    user_grad=gfn, history=False)
     assert np.array_equal(gws.state, st.theta)
     assert np.array_equal(lws[0].ll, st.ll)
+
+
+def test_mala_on_a_user_law_on_the_wide_kernel(oracle):
+    """D = 20 (mwg_wide_kernel, NU = 20): the user logistic law with its gradient, a MALA
+    block of 12 coordinates and a Gaussian block of 8, accept-only then full histories."""
+    rng = np.random.default_rng(21)
+    D, n, C, M = 20, 80, 2048, 40
+    X = np.column_stack([np.ones(n), rng.normal(size=(n, D - 1))])
+    beta = rng.normal(scale=0.3, size=D)
+    y = (rng.uniform(size=n) < 1.0 / (1.0 + np.exp(-(X @ beta)))).astype(float)
+    obs = np.column_stack([X, y])
+    fn, src = oracle.user_loglik("logistic_regression")
+    gfn = oracle.user_grad("logistic_regression")
+    perm = rng.permutation(D)
+    ups = [oracle.mwg_update(oracle.KIND_MALA, perm[:12], eps=[0.08]),
+           oracle.mwg_update(2, perm[12:], sigma=0.004 * np.eye(8))]
+    steps = full_steps(M, 2)
+    for hist in (L.HIST_ACCEPT_ONLY, L.HIST_FULL):
+        eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=41, history_mode=hist))
+        for u in ups:
+            _add(eng, u)
+        eng.set_user_target(src, obs=obs, theta0=np.zeros(D))
+        eng.set_state(np.zeros((C, D)))
+        eng.run(steps)
+        assert "mwg_wide_kernel<D=20" in eng.kernel_name() and "MALA" in eng.kernel_name()
+        st = oracle.MWGState(np.zeros((C, D)), np.zeros(D), ups)
+        h = oracle.run_mwg(st, ups, seed=41, t_sigma=None, obs=obs, steps=steps, nthreads=8, user_ll=fn,
+                           user_grad=gfn)
+        check(oracle, eng, st, h, steps, ups, 2, full=hist == L.HIST_FULL)

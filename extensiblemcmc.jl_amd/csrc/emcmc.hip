@@ -782,8 +782,13 @@ emcmc_status select_variant(emcmc_handle *h) {
     // else the general kernel (forward substitutions from the factors, D ≤ 64)
     // (the chol kernel compiled at run time for other D ≤ kCholRtcMaxD = 64:
     // registers hold θ, θ° and one substitution vector, 6·D VGPRs)
+    // The kernel's scalar-load stream is unrolled at compile time in chunks of the largest of
+    // 16/8/4/2/1 doubles dividing D; above kCholRtcMaxChunks chunks per observation sweep (odd
+    // D > 25, D ≡ 2 mod 4 above 38) the compile takes minutes, and the general kernel runs instead.
     const bool chol_rtc = !(u.diag && h->target.diag) && D > 8 && !lookup(D, 1, full, ll, 2, false);
-    if (chol_rtc && (D > kCholRtcMaxD || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_RTC_CHOL))) return select_mwg(h);
+    if (chol_rtc && (D > kCholRtcMaxD || chol_rtc_chunks(D) > kCholRtcMaxChunks ||
+                     (h->cfg.kernel_variant & EMCMC_VARIANT_NO_RTC_CHOL)))
+        return select_mwg(h);
     const bool diag = u.diag && h->target.diag;
     Variant v;
     if (diag) {

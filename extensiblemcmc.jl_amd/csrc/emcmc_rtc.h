@@ -61,6 +61,12 @@ std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &ou
 // in registers: no spills to D = 40, AGPR and scratch spills above — still 20–45×
 // the general kernel).
 constexpr int kCholRtcMaxD = 64;
+constexpr int kCholRtcMaxChunks = 400;
+// chunks of one observation sweep (prefix D + the packed factor), as chol_stream cuts them
+inline int chol_rtc_chunks(int D) {
+    const int ch = D % 16 == 0 ? 16 : D % 8 == 0 ? 8 : D % 4 == 0 ? 4 : D % 2 == 0 ? 2 : 1;
+    return (D + D * (D + 1) / 2 + ch - 1) / ch;
+}
 std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out);
 
 }  // namespace emcmc

@@ -217,8 +217,8 @@ std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
     expr << "emcmc::rwm_gsn_chol_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ">";
     name << "rwm_gsn_chol_kernel<D=" << D << ",LPC=1," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
-    return compile_kernel(key.str(), "#include \"emcmc_kernels.h\"\n", "chol_kernel.hip", expr.str(), name.str(), {},
-                          out);
+    return compile_kernel(key.str(), "#include \"emcmc_kernels.h\"\n", "chol_kernel.hip", expr.str(), name.str(),
+                          {"-ftemplate-depth=2048"}, out);
 }
 
 const char *rtc_builtin_law(const char *name) {

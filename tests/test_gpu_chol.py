@@ -104,3 +104,12 @@ def test_chol_rtc_accept_only_and_launch_splits(oracle):
         e = run_engine(w, 999, 50, hist=L.HIST_ACCEPT_ONLY, spl=spl)
         assert "[hiprtc]" in e["kernel"] and "ACCEPT_ONLY" in e["kernel"]
         assert_bitwise(e, o, full=False)
+
+
+def test_chol_rtc_compile_limit_routes_to_general_kernel(oracle):
+    """D = 27 (odd: one-double scalar-load chunks, 405 per sweep) is above the run-time
+    chol kernel's compile budget: the general kernel runs it, bitwise."""
+    w = _corr(27, 27)
+    e = run_engine(w, 256, 12)
+    assert "mwg" in e["kernel"]
+    assert_bitwise(e, run_oracle(oracle, w, 256, 12))

@@ -12,8 +12,8 @@ log-prior, log-likelihood, MH accept/reject, rolling acceptance and the full
 per-step histories (θ, θ°, ll, accept bit) written to HBM — the reference's
 run! outputs (src/run.jl:237-239, 319, 333-334).  Chains are sharded
 embarrassingly: rank r owns global chain ids [r·C, (r+1)·C) (weak scaling,
-no data-path collective).  Diagnostics (split-R̂, acceptance) are reduced once
-after the timed region with one all-reduce.
+no data-path collective).  Diagnostics (split-R̂, acceptance) are combined once
+after the timed region: an all-gather of every rank's moments, Chan-merged.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -46,7 +46,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "cfg5"], default="cfg2",
-                    help="cfg2 at N=1; with N>1 GPUs cfg2 means cfg5 (131,072 chains per GPU)")
+                    help="cfg2: 65,536 chains per GPU at every N (the scaling line: the per-GPU shape does "
+                         "not change with N); cfg5: 131,072 chains per GPU, overdispersed θinit (1,048,576 "
+                         "chains at 8 GPUs), its own line")
     ap.add_argument("--shard", type=int, default=-1,
                     help="single-process run of shard r: global chains [r·C, (r+1)·C) (default: this rank's)")
     ap.add_argument("--chains-per-gpu", type=int, default=0,
@@ -69,6 +71,7 @@ def parse():
                     help="repeat the timed region, report the median (0: 5 when the histories fit in 96 GB, else 1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-parity", action="store_true", help="skip the oracle replay of 8 chains per rank")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="A/B only: no dispatch events in the timed region (the line then has no kernel roofline)")
     ap.add_argument("--settle-ms", type=float, default=150.0,
@@ -198,6 +201,41 @@ def cpu_baseline(w, seconds, ll_mode):
     return out
 
 
+def chains_per_gpu(workload, override=0):
+    """Chains per GPU of a workload: the same for every world size, so a 1→8 GPU
+    run is weak scaling of one per-GPU shape (cfg 5's 131,072 only when asked for)."""
+    if override:
+        return override
+    return {"cfg2": 65536, "cfg3": 32768, "cfg4": 131072, "cfg5": 131072}[workload]
+
+
+def timed_rep(eng, steps, barrier, run=None):
+    """One timed repetition: barrier and synchronize on both sides, the clock
+    between the two synchronizes only, so neither barrier's latency is inside the
+    window (in a 0.18 ms window it would be a visible share).  Returns (this rank's
+    seconds, the closing barrier's seconds); the caller takes the max over ranks."""
+    barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    (run or eng.run)(steps)
+    eng.synchronize()
+    dt = time.perf_counter() - t0
+    tb = time.perf_counter()
+    barrier()
+    return dt, time.perf_counter() - tb
+
+
+def reduce_over_ranks(x, dist, dev=None, op="max"):
+    """max (times) or min (AND of 0/1 flags) of a float over every rank."""
+    if dist is None:
+        return x
+    import torch
+
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.MIN)
+    return float(t.item())
+
+
 def settle_clock(w, Cg, device, a, first, cfg3, cfg4, ll_mode):
     """Bring the GPU to its steady-state clock right before the timed steps: the same step
     kernel (same workload shape, full histories into a ring of one launch) on a throwaway
@@ -270,9 +308,10 @@ def main():
 
     cfg4 = a.workload == "cfg4"
     cfg3 = a.workload == "cfg3"
-    # N > 1 GPUs: BASELINE cfg 5, 131,072 chains per GPU (1,048,576 over 8), overdispersed θinit
-    cfg5 = a.workload == "cfg5" or (a.workload == "cfg2" and world > 1)
-    Cg = a.chains_per_gpu or (131072 if (cfg4 or cfg5) else 32768 if cfg3 else 65536)
+    # cfg 5 (131,072 chains per GPU, 1,048,576 over 8, overdispersed θinit) only when asked for:
+    # the default line keeps cfg 2's 65,536 chains per GPU at every N
+    cfg5 = a.workload == "cfg5"
+    Cg = chains_per_gpu(a.workload, a.chains_per_gpu)
     first = (a.shard if a.shard >= 0 else rank) * Cg  # global id of this process's chain 0
     if cfg4:
         w = W.cfg4(Cg, k=a.haario_k)
@@ -327,18 +366,22 @@ def main():
             else:
                 dist.barrier(device_ids=[local])
 
-    times, kern = [], []
+    class _Sync:  # the engine's synchronize for timed_rep (cfg 4: PosDef faults are counted, not raised)
+        def synchronize(self):
+            eng.synchronize(allow_faults=cfg4)  # hipStreamSynchronize of the engine's stream (+ a 4-byte fault flag)
+
+    times, kern, barrier_s = [], [], []
     it = a.warmup + 1
     for _ in range(reps):
         # the rep's (mcmciter, pidx) schedule is built before the clock starts
         steps = np.stack([np.arange(it, it + a.steps, dtype=np.uint32), np.ones(a.steps, dtype=np.uint32)], axis=1)
         eng.set_timing(not a.no_kernel_timing)
-        barrier()
-        eng.synchronize()
-        t0 = time.perf_counter()
-        if stream_bufs is None:
-            eng.run(steps)
-        else:  # half a ring per chunk: a chunk's thinned θ history leaves while the next chunk runs
+
+        def run(steps, it=it):
+            if stream_bufs is None:
+                eng.run(steps)
+                return
+            # half a ring per chunk: a chunk's thinned θ history leaves while the next chunk runs
             ch = a.history_ring // 2 if a.history_ring >= 2 * a.stream_thin else a.history_ring
             for c0 in range(0, a.steps, ch):
                 eng.run(steps[c0:c0 + ch])
@@ -346,21 +389,15 @@ def main():
                 eng.stream_history(L.H_STATE, it + c0 + a.stream_thin - 1, ch // a.stream_thin, thin=a.stream_thin,
                                    out=stream_bufs[k0:k0 + ch // a.stream_thin])
             eng.stream_wait()
-        eng.synchronize(allow_faults=cfg4)  # hipStreamSynchronize of the engine's stream (+ a 4-byte fault flag)
-        barrier()
-        dt = time.perf_counter() - t0
+
+        dt, bs = timed_rep(_Sync(), steps, barrier, run)
         ms, launches, nbytes = eng.get_timing(reset=True)
         if a.no_kernel_timing:  # placeholders: the wall clock stands in for the kernel time
             ms, launches, nbytes = dt * 1e3, 1, 1.0
         eng.set_timing(False)
         kern.append((ms, launches, nbytes))
-        if dist is not None:
-            import torch
-
-            t = torch.tensor([dt], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        times.append(dt)
+        times.append(reduce_over_ranks(dt, dist, dev, "max"))  # the slowest rank's window
+        barrier_s.append(bs)
         it += a.steps
     if settle_eng is not None:
         settle_eng.close()
@@ -375,6 +412,19 @@ def main():
     if mom is not None and dist is not None:
         mom = DG.allgather_moments(mom, w.D, device=dev)
     diag = DG.rhat_from_moments(mom) if mom is not None else None
+
+    # parity on every rank: 8 of its chains replayed on the oracle after the timed
+    # region (global ids first + c), AND-reduced over the ranks
+    par = None
+    if not a.history_ring and not a.no_parity:
+        try:
+            par = parity_sample(eng, w, a, ll_mode, first, reps)
+            ok = all(v for k, v in par.items() if k.endswith("bitwise"))
+        except Exception as e:
+            par, ok = {"error": repr(e)}, False
+        if dist is not None:
+            par["ranks"] = world
+            par["all_ranks_bitwise"] = reduce_over_ranks(1.0 if ok else 0.0, dist, dev, "min") == 1.0
 
     if rank != 0:
         dist.destroy_process_group()
@@ -424,7 +474,9 @@ def main():
                          (f"BASELINE cfg 5: chains sharded over MI355X GPUs, {Cg} per GPU (1,048,576 at 8 GPUs), "
                           f"here {world} GPU(s) = {Cg * world} chains, D=32 Gaussian target, fp64; cross-chain "
                           "split-R̂ moments all-gathered once after the timed region" if cfg5 else
-                          f"BASELINE cfg 2: {Cg} independent RWM chains per GPU, D=32 Gaussian target, fp64")),
+                          f"BASELINE cfg 2: {Cg} independent RWM chains per GPU at every GPU count (weak "
+                          f"scaling of one per-GPU shape), here {world} GPU(s) = {Cg * world} chains, D=32 "
+                          "Gaussian target, fp64")),
             "chains_per_gpu": Cg,
             "total_chains": total_chains, "first_chain_id": first,
             "dim": w.D,
@@ -461,6 +513,9 @@ def main():
         "kernel_chain_steps_per_s": Cg * a.steps / (ms / 1e3),
         "reps": reps,
         "times_s": times,
+        "timing": {"window": "between the engine synchronizes after the opening barrier and before the closing "
+                             "one; max over ranks (barriers outside the window)",
+                   "closing_barrier_ms_rank0": [b * 1e3 for b in barrier_s]},
     }
     # the same bytes on the wall clock of the timed region (host launch + synchronize included)
     e2e = bytes_per_launch * launches / dt / 1e9
@@ -528,11 +583,8 @@ def main():
             out["gpu_over_cpu"] = value / out["cpu_baseline"]["value"]
         except Exception as e:  # the oracle is a reported baseline, never the measured path
             out["cpu_baseline"] = {"error": repr(e)}
-        if not a.history_ring:
-            try:
-                out["parity"] = parity_sample(eng, w, a, ll_mode, first, reps)
-            except Exception as e:
-                out["parity"] = {"error": repr(e)}
+    if par is not None:
+        out["parity"] = par
     print(json.dumps(out))
     eng.close()
     if dist is not None:

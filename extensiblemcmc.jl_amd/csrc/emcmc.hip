@@ -197,6 +197,7 @@ struct emcmc_handle {
     double *d_uparams = nullptr;
     std::vector<uint32_t> last_iter;                    // per update: last iteration it ran (uniform)
     std::vector<std::vector<uint32_t>> steps_staging;   // host step lists alive until synchronize
+    std::vector<std::vector<double>> lam_staging;       // fλ values of a run's launch cuts, alive until synchronize
     uint64_t steps_used = 0;
     // mix / chain-moments path (mix_gsn_kernel): GenericChainStats mean/cov,
     // per-chain Σ_B factor, Haario M (same for every chain)
@@ -334,6 +335,9 @@ uint64_t mwg_pool_layout(emcmc_handle *h) {
 // (N = 1, the phantom zero sample: chain_statistics.jl:30-35, adaptation.jl:387-395).
 emcmc_status reset_mwg_pool(emcmc_handle *h) {
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
+    // queued kernels read and write the pool on h->stream (non-blocking: the null
+    // stream's copies below would not wait for them)
+    if (h->allocated) HIPCHK(h, hipStreamSynchronize(h->stream));
     const uint64_t elems = mwg_pool_layout(h);
     if (elems != h->mixpool_elems) {
         if (h->d_mixpool) (void)hipFree(h->d_mixpool);
@@ -471,6 +475,16 @@ emcmc_status load_rtc_module(emcmc_handle *h, const RtcKernel &k) {
 
 emcmc_status select_mwg(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
+    if (h->allocated) {
+        // Re-selected after emcmc_set_state (a new target or variant): kernels still
+        // queued on the non-blocking h->stream read the update table and the pool
+        // replaced below. The pool restarts (L_B = user Σ_B, Haario M = 0, moments =
+        // phantom zero sample), so the adaptation state restarts with it: N = 1 and
+        // λ as constructed, as emcmc_set_state does.
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->stats_N = 1;
+        for (auto &u : h->updates) u.lam = u.lam0;
+    }
     const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
     const int ll = (int)h->target.ll_mode;
     Variant v;
@@ -486,7 +500,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) xt = true;
         if (u.kernel == EMCMC_MALA) mala = true;
     }
-    if (mala && user && h->target.src.find("EMCMC_USER_GRAD") == std::string::npos)
+    if (mala && user && !rtc_defines_user_grad(h->target.src))
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "MALA needs the target's gradient (compute_gradients_and_momenta!): the user law defines none "
                     "(EMCMC_USER_GRAD { … })");
@@ -1339,13 +1353,17 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
     const uint64_t K = h->cfg.steps_per_launch;
     size_t ci = 0;  // next λ cut
+    if (!cuts.empty()) {  // the cut values stay alive until emcmc_synchronize: no host wait per readjust
+        std::vector<double> lv(cuts.size());
+        for (size_t k = 0; k < cuts.size(); ++k) lv[k] = cuts[k].second.second;
+        h->lam_staging.push_back(std::move(lv));
+    }
+    const double *lam_src = cuts.empty() ? nullptr : h->lam_staging.back().data();
     for (uint64_t i = 0, n = 0; i < num_steps; i += n) {
         while (ci < cuts.size() && cuts[ci].first <= i) {  // λ after an fλ readjust, in stream order
             const uint32_t q = cuts[ci].second.first;
-            const double lam = cuts[ci].second.second;
-            HIPCHK(h, hipMemcpyAsync(reinterpret_cast<char *>(h->d_mwg + q) + offsetof(MwgUpdate, lam), &lam,
+            HIPCHK(h, hipMemcpyAsync(reinterpret_cast<char *>(h->d_mwg + q) + offsetof(MwgUpdate, lam), lam_src + ci,
                                      sizeof(double), hipMemcpyHostToDevice, h->stream));
-            HIPCHK(h, hipStreamSynchronize(h->stream));  // the host value is a loop temporary
             ++ci;
         }
         const uint64_t lim = (ci < cuts.size()) ? cuts[ci].first : num_steps;  // end the launch at the next cut
@@ -1466,7 +1484,7 @@ emcmc_status univariate_consts(emcmc_handle *h, uint32_t fam, double a, double b
         return EMCMC_OK;
     case EMCMC_DIST_CAUCHY:
         if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Cauchy prior: σ must be > 0");
-        pc = 1.1447298858494002 + log_pos(b);  // log π + log σ
+        pc = log_pos(b);  // log σ (log π enters in Distributions.jl's order on the device)
         return EMCMC_OK;
     case EMCMC_DIST_LAPLACE:
         if (!(b > 0.0)) return fail(h, EMCMC_INVALID_ARG, "Laplace prior: θ must be > 0");
@@ -1837,7 +1855,7 @@ emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const cha
     if (!source) return EMCMC_INVALID_ARG;
     RtcKernel k;
     // a law with a gradient (EMCMC_USER_GRAD) is checked with MALA compiled in
-    const bool mala = std::string(source).find("EMCMC_USER_GRAD") != std::string::npos;
+    const bool mala = rtc_defines_user_grad(source);
     const std::string log = rtc_compile_user(source, options ? options : "", (int)dim, true, (int)dim, k,
                                              std::string(), std::string(), false, mala);
     if (log_out && log_len) {
@@ -2030,6 +2048,7 @@ emcmc_status emcmc_synchronize(emcmc_handle *h) {
     if (!h) return EMCMC_INVALID_ARG;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->steps_staging.clear();
+    h->lam_staging.clear();
     if (!h->allocated) return EMCMC_OK;
     // O(1): the kernels set the mapped flag when a chain ends a launch with a fault bit
     if (*static_cast<volatile uint32_t *>(h->h_fault_flag))

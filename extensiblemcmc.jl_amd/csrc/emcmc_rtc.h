@@ -55,6 +55,37 @@ std::string rtc_compile_gsn(int D, bool full, int ll_mode, int nu, RtcKernel &ou
                             const std::string &usrc = std::string(), const std::string &uopts = std::string(),
                             bool xt = false, bool mala = false);
 
+// Does a user law's source define a gradient body (`EMCMC_USER_GRAD { … }`)?
+// Comments, string and character literals are skipped, and the name must stand
+// as a whole token, so a law that only mentions the macro in a comment gets the
+// "MALA needs the target's gradient" refusal instead of a compile error.
+inline bool rtc_defines_user_grad(const std::string &src) {
+    static const char kTok[] = "EMCMC_USER_GRAD";
+    const size_t n = src.size(), tn = sizeof kTok - 1;
+    auto ident = [](char c) { return c == '_' || (c >= '0' && c <= '9') || ((c | 32) >= 'a' && (c | 32) <= 'z'); };
+    for (size_t i = 0; i < n;) {
+        const char c = src[i];
+        if (c == '/' && i + 1 < n && src[i + 1] == '/') {
+            while (i < n && src[i] != '\n') ++i;
+        } else if (c == '/' && i + 1 < n && src[i + 1] == '*') {
+            const size_t e = src.find("*/", i + 2);
+            i = (e == std::string::npos) ? n : e + 2;
+        } else if (c == '"' || c == '\'') {
+            for (++i; i < n && src[i] != c; ++i)
+                if (src[i] == '\\') ++i;
+            ++i;
+        } else if (ident(c)) {
+            size_t j = i;
+            while (j < n && ident(src[j])) ++j;
+            if (j - i == tn && src.compare(i, tn, kTok) == 0) return true;
+            i = j;
+        } else {
+            ++i;
+        }
+    }
+    return false;
+}
+
 // rwm_gsn_chol_kernel<D, FULL, LL> (emcmc_kernels.h) for a D without an
 // ahead-of-time instantiation (inst_chol.hip: 16, 24, 32): correlated Σ_rw / Σ_t
 // on the fused single-update path, any D ≤ 64 (θ, θ° and one substitution vector

@@ -194,7 +194,7 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
     if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
     std::vector<std::string> extra;
     if (mala) extra.push_back("-DEMCMC_RTC_MALA=1");
-    if (user && src.find("EMCMC_USER_GRAD") != std::string::npos) extra.push_back("-DEMCMC_HAS_USER_GRAD=1");
+    if (user && rtc_defines_user_grad(src)) extra.push_back("-DEMCMC_HAS_USER_GRAD=1");
     for (const std::string *op : {&opts, &uopts}) {
         std::istringstream is(*op);
         for (std::string w; is >> w;) extra.push_back(w);

@@ -279,7 +279,7 @@ class Engine:
     def add_update_desc(self, u: L.EmcmcUpdateDesc, keepalive=()):
         self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
         self.num_updates += 1
-        self._update_n.append(int(len(coords)))
+        self._update_n.append(int(u.num_coords))
 
     def set_gsn_target(self, mu, sigma, obs, ll_mode=L.LL_PER_OBS):
         mu = np.ascontiguousarray(mu, dtype=np.float64)

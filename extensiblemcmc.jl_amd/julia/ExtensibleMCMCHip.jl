@@ -404,6 +404,12 @@ function _update_desc(updt::eMCMC.RandomWalkUpdate, keep)
     error("no device plugin for $(typeof(updt.rw))")
 end
 
+# Field reads that only a RandomWalkUpdate has (`rw`, its λ, the Haario `adpt`)
+# go through these predicates: HipUpdate and HipMALAUpdate have no `rw`
+# (updates.jl:42-93 and :129-133 define no such field for a plugin update).
+_mix(u) = u isa eMCMC.RandomWalkUpdate && u.rw isa eMCMC.GaussianRandomWalkMix
+_haario_mix(u) = _mix(u) && u.adpt isa eMCMC.HaarioTypeAdaptation
+
 # emcmc_lambda_fn trampoline: ctx is a HaarioTypeAdaptation, kept alive by the
 # MCMC object for the whole run!
 function _flam_trampoline(λ::Float64, N::Int64, it::Int64, ctx::Ptr{Cvoid})::Float64
@@ -429,7 +435,7 @@ function eMCMC.init_global_workspace(be::MI355XBackend, num_mcmc_steps,
             desc = Ref(_update_desc(u, keep))
             check(ccall((:emcmc_add_update, LIB), Cint, (Ptr{Cvoid}, Ref{EmcmcUpdateDesc}), h[], desc),
                   h[], "emcmc_add_update")
-            if u.rw isa eMCMC.GaussianRandomWalkMix && u.adpt isa eMCMC.HaarioTypeAdaptation
+            if _haario_mix(u)
                 # fλ (adaptation.jl:425) runs in Julia at every readjust: the library
                 # calls back with (λ, N, mcmc_iter); ctx is the (mutable) adaptation
                 check(ccall((:emcmc_set_mix_lambda_fn, LIB), Cint, (Ptr{Cvoid}, UInt32, Ptr{Cvoid}, Ptr{Cvoid}),
@@ -506,7 +512,7 @@ function eMCMC.__run!(gws::MI355XGlobalWorkspace, local_wss, updates, schedule, 
     end
     flush!()
     for (i, u) in enumerate(updates)   # readjust! mutates rw.λ (adaptation.jl:425)
-        if u.rw isa eMCMC.GaussianRandomWalkMix
+        if _mix(u)
             λ = Ref(0.0)
             check(ccall((:emcmc_get_mix_lambda, LIB), Cint, (Ptr{Cvoid}, UInt32, Ref{Float64}), h, UInt32(i), λ),
                   h, "emcmc_get_mix_lambda")

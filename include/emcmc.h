@@ -351,8 +351,10 @@ typedef struct emcmc_step {
 } emcmc_step;
 
 /* Cross-chain moments of θ over an iteration window, for split-R̂
- * (new functionality; BASELINE cfg 5).  Each field is a sum over the chains
- * of this handle, so shards combine by summation (allreduce). */
+ * (new functionality; BASELINE cfg 5).  out3d = [m̄ | M2 | Σ var] over the
+ * chains of this handle: not sums.  Shards combine by an all-gather of every
+ * rank's 3·D + 3 doubles and chain count, merged in rank order with Chan's
+ * pairwise update (extensible_mcmc/diagnostics.py). */
 typedef struct emcmc_moments {
     uint64_t num_chains;   /* chains summed (×2 halves when split) */
     uint64_t num_draws;    /* draws per (half-)chain */

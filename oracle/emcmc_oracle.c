@@ -592,7 +592,7 @@ static double orc_log_real(double x) { return (x < 0.0) ? NAN : orc_log_any(x); 
  *   LogNormal(μ, σ): x ≤ 0 ? −Inf : normlogpdf(μ, σ, log x) − log x
  *   Beta(α, β): x ∉ [0, 1] ? −Inf : xlogy(α − 1, x) + xlog1py(β − 1, −x) − logbeta(α, β)
  *   InverseGamma(α, θ): x ≤ 0 ? −Inf : α log θ − loggamma(α) − (α + 1) log x − θ/x
- *   Cauchy(μ, σ): −(log π + log σ + log1p(z²))
+ *   Cauchy(μ, σ): −((log1p(z²) + log π) + log σ)  (Distributions.jl: −(log1psq(z) + logπ + log(σ)))
  *   Laplace(μ, θ): −(|x − μ|/θ + log(2θ))
  *   TDist(ν): loggamma((ν+1)/2) − loggamma(ν/2) − log(νπ)/2 − (ν+1)/2 · log1p(x²/ν)
  * (a, b) are the parameters as the device holds them (Exponential: b = 1/θ,
@@ -625,7 +625,7 @@ static double orc_univariate_logpdf(uint32_t fam, double a, double b, double c, 
         return (c - (a + 1.0) * orc_log_any(x)) - b / x;
     case ORC_DIST_CAUCHY: {
         const double z = (x - a) / b;
-        return -(c + orc_log1p_any(z * z));
+        return -((orc_log1p_any(z * z) + ORC_LOGPI) + c);
     }
     case ORC_DIST_LAPLACE: return -(fabs(x - a) / b + c);
     default: /* TDist */
@@ -665,7 +665,7 @@ static int orc_prior_factor_consts(uint32_t fam, double a, double b, double *pa,
         return 0;
     case ORC_DIST_CAUCHY:
         if (!(b > 0.0)) return -1;
-        *pc = ORC_LOGPI + orc_log(b);
+        *pc = orc_log(b);
         return 0;
     case ORC_DIST_LAPLACE:
         if (!(b > 0.0)) return -1;

@@ -81,7 +81,7 @@ def test_two_rank_sharding_and_diagnostics(tmp_path, oracle):
     # per-chain results do not depend on the sharding
     sharded = np.concatenate([np.load(tmp_path / "theta_0.npy"), np.load(tmp_path / "theta_1.npy")])
     assert np.array_equal(sharded, st.theta)
-    # the all-reduced diagnostics equal the single-process reduction
+    # the all-gathered, merged diagnostics equal the single-process reduction
     ref = shard_moments(h["theta"][20:])
     ref["accepted"], ref["proposed"] = int(h["acc"][20:].sum()), int(h["acc"][20:].size)
     got = DG.unpack(np.load(tmp_path / "reduced.npy"), w.D, ref["num_draws"])
@@ -109,3 +109,59 @@ def test_chan_merge_does_not_cancel():
     naive = (means * means).sum(0) - means.sum(0) ** 2 / means.shape[0]
     assert np.all(np.abs(naive - exact) > 1e3 * np.abs(got["m2"] - exact))
     assert got["num_chains"] == 1 << 20
+
+
+class _SleepEngine:
+    """A stand-in for one rank's engine: run() takes a fixed time."""
+
+    def __init__(self, secs):
+        self.secs = secs
+
+    def synchronize(self):
+        pass
+
+    def run(self, steps):
+        import time
+
+        time.sleep(self.secs)
+
+
+def _bench_worker(rank, world, port, out_dir):
+    sys.path[:0] = [str(ROOT), str(ROOT / "extensiblemcmc.jl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import json
+
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = _SleepEngine(0.02 if rank == 0 else 0.4)
+    dt, bs = bench.timed_rep(eng, None, dist.barrier)
+    dmax = bench.reduce_over_ranks(dt, dist, None, "max")
+    # rank 1's replay disagrees: the AND over ranks is false on every rank
+    all_ok = bench.reduce_over_ranks(0.0 if rank == 1 else 1.0, dist, None, "min") == 1.0
+    with open(os.path.join(out_dir, f"bench_{rank}.json"), "w") as f:
+        json.dump({"dt": dt, "barrier": bs, "dmax": dmax, "all_ok": all_ok,
+                   "cg": [bench.chains_per_gpu(wl) for wl in ("cfg2", "cfg3", "cfg4", "cfg5")]}, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_scaling_line_two_ranks(tmp_path):
+    """bench.py's N > 1 path on 2 gloo ranks: the timed window holds no barrier (a
+    fast rank's own window is its own run, the wait for the slow rank shows up in
+    the closing barrier), the line's time is the max over ranks, the per-GPU chain
+    count does not depend on the world size, and parity is AND-reduced over ranks."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    mp.spawn(_bench_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (json.loads((tmp_path / f"bench_{r}.json").read_text()) for r in (0, 1))
+    assert r0["dt"] < 0.2, r0  # rank 0 did not wait for rank 1 inside its window
+    assert r0["barrier"] > 0.2, r0  # it waited in the closing barrier instead
+    assert r1["dt"] >= 0.4
+    assert r0["dmax"] == r1["dmax"] == max(r0["dt"], r1["dt"])
+    assert r0["all_ok"] is False and r1["all_ok"] is False
+    assert r0["cg"] == r1["cg"] == [65536, 32768, 131072, 131072]

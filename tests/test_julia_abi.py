@@ -129,3 +129,55 @@ def test_reference_accessors_are_defined():
     for prop in (":sub_ws", ":sub_ws°", ":acceptance_history", ":state_history", ":state_proposal_history",
                  ":ll_history"):
         assert prop in src, prop
+
+
+# The fields only a RandomWalkUpdate carries (updates.jl:163-170): the plugin
+# updates HipUpdate / HipMALAUpdate have neither `rw` nor a Haario `adpt`.
+_RW_ONLY = re.compile(r"\b(?:u|updt)\.(?:rw|adpt)\b")
+_ALLOWED_DEF = re.compile(r"^(function _update_desc\(updt::eMCMC\.RandomWalkUpdate|_mix\(u\) =|_haario_mix\(u\) =)")
+_GUARD = re.compile(r"^\s*(?:if|elseif)\s+(?:_mix\(u\)|_haario_mix\(u\)|u isa eMCMC\.RandomWalkUpdate)")
+
+
+def _indent(line):
+    return len(line) - len(line.lstrip(" "))
+
+
+def test_rw_field_reads_are_guarded():
+    """Every read of `.rw` / `.adpt` on an update sits inside
+    `_update_desc(::RandomWalkUpdate)`, the `_mix` / `_haario_mix` predicates, or an
+    `if` on one of them: init_global_workspace and __run! loop over every update,
+    user plugins included (round-3 defect: a FieldError on `u.rw` before the first
+    ccall of a HipUpdate / HipMALAUpdate run)."""
+    lines = SHIM.read_text().split("\n")
+    bad = []
+    for i, line in enumerate(lines):
+        code = line.split("#")[0]
+        if not _RW_ONLY.search(code):
+            continue
+        if _ALLOWED_DEF.match(code):
+            continue
+        ok, level = False, _indent(line)
+        for j in range(i - 1, -1, -1):  # the enclosing lines, innermost first
+            up = lines[j]
+            if not up.strip() or _indent(up) >= level:
+                continue
+            level = _indent(up)
+            if _GUARD.match(up) or _ALLOWED_DEF.match(up):
+                ok = True
+                break
+            if level == 0:
+                break
+        if not ok:
+            bad.append(f"{i + 1}: {line.strip()}")
+    assert not bad, "unguarded RandomWalkUpdate field reads:\n" + "\n".join(bad)
+
+
+def test_plugin_updates_reach_emcmc_add_update():
+    """HipUpdate and HipMALAUpdate have a `_update_desc` method, and the loop that
+    passes each update to emcmc_add_update reads no RandomWalkUpdate field before
+    the ccall."""
+    src = SHIM.read_text()
+    for t in ("HipUpdate", "HipMALAUpdate"):
+        assert re.search(rf"^function _update_desc\(updt::{t}, keep\)", src, flags=re.M), t
+    loop = src[src.index("for (i, u) in enumerate(updates)"):src.index(":emcmc_add_update")]
+    assert not _RW_ONLY.search(loop), loop

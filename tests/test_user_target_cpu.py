@@ -25,6 +25,15 @@ def test_user_source_compile_error_is_reported():
     assert "undefined_symbol" in str(e.value)
 
 
+def test_gradient_named_only_in_a_comment_is_not_a_gradient():
+    """A law that mentions EMCMC_USER_GRAD only in a comment or a string defines no
+    gradient: it compiles as a plain law (before, a text search compiled the MALA
+    path in and the build failed on an undefined emcmc_user_grad)."""
+    src = ("/* no EMCMC_USER_GRAD here */\n// nor EMCMC_USER_GRAD here\n"
+           "EMCMC_USER_LOGLIK { const char *s = \"EMCMC_USER_GRAD\"; (void)s; return -0.5 * theta[0] * theta[0]; }")
+    L.check_user_target(src, 2)
+
+
 def test_user_target_rejects_too_large_dim(oracle):
     _, src = oracle.user_loglik("banana")
     with pytest.raises(L.EMCMCError):

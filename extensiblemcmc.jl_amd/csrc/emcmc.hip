@@ -194,6 +194,8 @@ struct emcmc_handle {
     // user target (EMCMC_TARGET_USER): the loaded code object and the law's constants
     hipModule_t umod = nullptr;
     std::string umod_key;
+    uint32_t rtc_origin = 0;  // emcmc_rtc_info of the loaded module
+    double rtc_seconds = 0.0;
     double *d_uparams = nullptr;
     std::vector<uint32_t> last_iter;                    // per update: last iteration it ran (uniform)
     std::vector<std::vector<uint32_t>> steps_staging;   // host step lists alive until synchronize
@@ -463,6 +465,8 @@ emcmc_status allow_lds(emcmc_handle *h, const void *fn, size_t bytes) {
 emcmc_status load_rtc_module(emcmc_handle *h, const RtcKernel &k) {
     const std::string key = k.name + '|' + k.lowered + '|' + std::to_string(std::hash<std::string>{}(
                                 std::string(k.code.begin(), k.code.end())));
+    h->rtc_origin = k.origin;
+    h->rtc_seconds = k.seconds;
     if (key == h->umod_key) return EMCMC_OK;
     if (h->umod) (void)hipModuleUnload(h->umod);
     h->umod = nullptr;
@@ -1879,6 +1883,19 @@ emcmc_status emcmc_check_user_update(const char *source, uint32_t dim, const cha
     return log.empty() ? EMCMC_OK : EMCMC_INVALID_ARG;
 }
 
+emcmc_status emcmc_prebuild_chol_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, char *log_out,
+                                        size_t log_len) {
+    if (dim < 2 || dim > (uint32_t)kCholRtcMaxD || history_mode > 1 || ll_mode > 1) return EMCMC_INVALID_ARG;
+    RtcKernel k;
+    const std::string log = rtc_compile_chol((int)dim, history_mode == EMCMC_HIST_FULL, (int)ll_mode, k);
+    if (log_out && log_len) {
+        const size_t n = std::min(log.size(), log_len - 1);
+        std::memcpy(log_out, log.data(), n);
+        log_out[n] = '\0';
+    }
+    return log.empty() ? EMCMC_OK : EMCMC_HIP_ERROR;
+}
+
 emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {
     if (!h || !theta) return EMCMC_INVALID_ARG;
     emcmc_status st = ensure_alloc(h);
@@ -2574,6 +2591,14 @@ emcmc_status emcmc_get_timing(emcmc_handle *h, double *total_ms, uint64_t *launc
 emcmc_status emcmc_kernel_name(emcmc_handle *h, char *buf, size_t buflen) {
     if (!h || !buf || buflen == 0) return EMCMC_INVALID_ARG;
     snprintf(buf, buflen, "%s", h->var.name.empty() ? "(none)" : h->var.name.c_str());
+    return EMCMC_OK;
+}
+
+emcmc_status emcmc_rtc_info(emcmc_handle *h, uint32_t *origin, double *seconds) {
+    if (!h || !origin || !seconds) return EMCMC_INVALID_ARG;
+    if (!h->var.ufn && !h->var.ffn) return fail(h, EMCMC_STATE_ERROR, "the selected kernel is compiled ahead of time");
+    *origin = h->rtc_origin;
+    *seconds = h->rtc_seconds;
     return EMCMC_OK;
 }
 

@@ -987,22 +987,34 @@ __device__ __forceinline__ void static_for(F &&f) {
 // nothing, so the IR would otherwise hoist and merge a whole sweep's loads into
 // SGPRs), and every result is pinned with vpin, so the stream keeps its order.
 // fpre(IntC<i>, x_i) for the prefix, ftab(IntC<j>, IntC<i>, T_ij) for the table.
-template <int D>
-constexpr int chol_chunk() {  // the largest of 16, 8, 4, 2, 1 dividing D (the prefix is whole chunks)
-    return D % 16 == 0 ? 16 : D % 8 == 0 ? 8 : D % 4 == 0 ? 4 : D % 2 == 0 ? 2 : 1;
-}
+// Chunks are 16 doubles at any D: the prefix takes ⌈NA/16⌉ chunks (the last one
+// partial) and the table starts on a chunk of its own, so an odd D streams the
+// same ≤ 134 chunks per sweep as an even one (SMEM needs 4-byte alignment only).
+constexpr int kCholChunk = 16;
+template <int D, int NA>
+struct CholChunks {
+    static constexpr int NCA = (NA + kCholChunk - 1) / kCholChunk;  // prefix chunks
+    static constexpr int P = D * (D + 1) / 2;
+    static constexpr int NCH = NCA + (P + kCholChunk - 1) / kCholChunk;
+    // first element (stream index: prefix 0..NA−1, table NA..) and length of chunk t
+    static constexpr int first(int t) { return t < NCA ? t * kCholChunk : NA + (t - NCA) * kCholChunk; }
+    static constexpr int len(int t) {
+        return t < NCA ? ((NA - t * kCholChunk) < kCholChunk ? NA - t * kCholChunk : kCholChunk)
+                       : ((P - (t - NCA) * kCholChunk) < kCholChunk ? P - (t - NCA) * kCholChunk : kCholChunk);
+    }
+};
 template <int D, int NA, typename FP, typename FT>
 __device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, FT &&ftab) {
-    constexpr int CH = chol_chunk<D>();
-    static_assert(NA % CH == 0, "prefix must be whole chunks");
-    constexpr int NT = NA + D * (D + 1) / 2, NCH = (NT + CH - 1) / CH;
+    constexpr int CH = kCholChunk;
+    using S = CholChunks<D, NA>;
+    constexpr int NCH = S::NCH;
     auto load = [&](auto TC, double(&buf)[CH]) {
-        constexpr int e0 = decltype(TC)::value * CH;
+        constexpr int t = decltype(TC)::value, e0 = S::first(t), n = S::len(t);
         cdouble *p = (e0 < NA) ? X + e0 : T + (e0 - NA);
         asm volatile("" : "+s"(p));
 #pragma unroll
         for (int r = 0; r < CH; ++r)
-            if (e0 + r < NT) buf[r] = p[r];
+            if (r < n) buf[r] = p[r];
     };
     auto elem = [&](auto EC, double v) {
         constexpr int e = decltype(EC)::value;
@@ -1016,8 +1028,7 @@ __device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, F
     double cur[CH], nxt[CH];
     load(IntC<0>{}, cur);
     static_for<0, NCH>([&](auto TC) {
-        constexpr int t = decltype(TC)::value, e0 = t * CH;
-        constexpr int n = (NT - e0) < CH ? (NT - e0) : CH;
+        constexpr int t = decltype(TC)::value, e0 = S::first(t), n = S::len(t);
         elem(IntC<e0>{}, cur[0]);
         sbar();
         if constexpr (t + 1 < NCH) load(IntC<t + 1>{}, nxt);

@@ -29,7 +29,19 @@ struct RtcKernel {
     std::vector<char> code;  // gfx950 code object
     std::string lowered;     // mangled kernel name inside it
     std::string name;        // readable name for emcmc_kernel_name
+    // how this process obtained it (emcmc_rtc_info): the process cache, the
+    // on-disk code-object cache, or a hiprtc compile; seconds spent getting it
+    uint32_t origin = 0;
+    double seconds = 0.0;
 };
+enum : uint32_t { kRtcFromProcess = 0, kRtcFromDisk = 1, kRtcCompiled = 2 };
+
+// The on-disk code-object cache: EMCMC_RTC_CACHE (a directory; "off" disables
+// it), else rtc_cache/ beside libemcmc.so.  Entries are keyed by a 128-bit
+// digest of everything the code depends on (program text, embedded headers,
+// name expression, options, hiprtc version, target arch), so a second process,
+// the other ranks of a node and later runs load instead of compiling.
+std::string rtc_cache_dir();
 
 // Compile (or fetch from the process-wide cache) the general schedule kernel
 // for dimension D with the user's log-likelihood: mwg_gsn_kernel<D> for
@@ -93,11 +105,10 @@ inline bool rtc_defines_user_grad(const std::string &src) {
 // the general kernel).
 constexpr int kCholRtcMaxD = 64;
 constexpr int kCholRtcMaxChunks = 400;
-// chunks of one observation sweep (prefix D + the packed factor), as chol_stream cuts them
-inline int chol_rtc_chunks(int D) {
-    const int ch = D % 16 == 0 ? 16 : D % 8 == 0 ? 8 : D % 4 == 0 ? 4 : D % 2 == 0 ? 2 : 1;
-    return (D + D * (D + 1) / 2 + ch - 1) / ch;
-}
+// chunks of one observation sweep (prefix D + the packed factor), as chol_stream
+// cuts them: 16 doubles each, the prefix and the table on chunks of their own
+// (≤ 4 + 130 at D = 64, so every D ≤ 64 is within the compile budget)
+inline int chol_rtc_chunks(int D) { return (D + 15) / 16 + (D * (D + 1) / 2 + 15) / 16; }
 std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out);
 
 }  // namespace emcmc

@@ -9,7 +9,14 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <chrono>
 #include <cstdio>
+#include <cstdlib>
+#include <fstream>
 #include <map>
 #include <mutex>
 #include <sstream>
@@ -112,7 +119,68 @@ bool cache_get(const std::string &key, RtcKernel &out) {
     auto it = g_cache.find(key);
     if (it == g_cache.end()) return false;
     out = it->second;
+    out.origin = kRtcFromProcess;
+    out.seconds = 0.0;
     return true;
+}
+
+// ---- on-disk code-object cache ------------------------------------------------
+// 128-bit digest: two FNV-1a-64 streams with different offsets over the same bytes
+struct Digest {
+    uint64_t a = 0xcbf29ce484222325ull, b = 0x84222325cbf29ce4ull;
+    void add(const void *p, size_t n) {
+        const unsigned char *c = static_cast<const unsigned char *>(p);
+        for (size_t i = 0; i < n; ++i) {
+            a = (a ^ c[i]) * 0x100000001b3ull;
+            b = (b ^ c[i] ^ 0x5a) * 0x100000001b3ull;
+        }
+        const uint64_t len = n;  // length-delimited: ("ab","c") ≠ ("a","bc")
+        const unsigned char *l = reinterpret_cast<const unsigned char *>(&len);
+        for (int i = 0; i < 8; ++i) a = (a ^ l[i]) * 0x100000001b3ull, b = (b ^ l[i]) * 0x100000001b3ull;
+    }
+    void add(const std::string &s) { add(s.data(), s.size()); }
+    std::string hex() const {
+        char buf[33];
+        snprintf(buf, sizeof buf, "%016llx%016llx", (unsigned long long)a, (unsigned long long)b);
+        return buf;
+    }
+};
+
+const char kDiskMagic[8] = {'E', 'M', 'C', 'R', 'T', 'C', '1', '\n'};
+
+bool disk_get(const std::string &file, RtcKernel &k) {
+    std::ifstream f(file, std::ios::binary);
+    if (!f) return false;
+    char m[8];
+    uint64_t nl = 0, nc = 0;
+    if (!f.read(m, 8) || std::string(m, 8) != std::string(kDiskMagic, 8)) return false;
+    if (!f.read(reinterpret_cast<char *>(&nl), 8) || nl == 0 || nl > 4096) return false;
+    k.lowered.resize(nl);
+    if (!f.read(&k.lowered[0], (std::streamsize)nl)) return false;
+    if (!f.read(reinterpret_cast<char *>(&nc), 8) || nc == 0 || nc > (1ull << 30)) return false;
+    k.code.resize(nc);
+    if (!f.read(k.code.data(), (std::streamsize)nc)) return false;
+    return f.peek() == std::char_traits<char>::eof();  // a truncated or padded file is not an entry
+}
+
+void disk_put(const std::string &dir, const std::string &file, const RtcKernel &k) {
+    (void)mkdir(dir.c_str(), 0775);
+    const std::string tmp = file + ".tmp." + std::to_string((long)getpid());
+    {
+        std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+        if (!f) return;  // read-only location: the process cache still holds it
+        const uint64_t nl = k.lowered.size(), nc = k.code.size();
+        f.write(kDiskMagic, 8);
+        f.write(reinterpret_cast<const char *>(&nl), 8);
+        f.write(k.lowered.data(), (std::streamsize)nl);
+        f.write(reinterpret_cast<const char *>(&nc), 8);
+        f.write(k.code.data(), (std::streamsize)nc);
+        if (!f) {
+            (void)unlink(tmp.c_str());
+            return;
+        }
+    }
+    if (rename(tmp.c_str(), file.c_str()) != 0) (void)unlink(tmp.c_str());  // atomic: ranks may race
 }
 
 // Compile prog_src for gfx950 and fetch the code object of the kernel named by
@@ -121,6 +189,44 @@ bool cache_get(const std::string &key, RtcKernel &out) {
 std::string compile_kernel(const std::string &key, const std::string &prog_src, const char *file,
                            const std::string &ex, const std::string &name, const std::vector<std::string> &extra,
                            RtcKernel &out) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    // disk cache: the digest covers every input of the compile
+    const std::string dir = rtc_cache_dir();
+    std::string dfile;
+    if (!dir.empty()) {
+        Digest d;
+        static const std::string hdr_digest = [] {
+            Digest h;
+            for (int i = 0; i < kRtcHeaderCount; ++i) {
+                h.add(std::string(kRtcHeaderNames[i]));
+                h.add(std::string(kRtcHeaderSrc[i]));
+            }
+            return h.hex();
+        }();
+        int vmaj = 0, vmin = 0;
+        (void)hiprtcVersion(&vmaj, &vmin);
+        d.add(hdr_digest);
+        d.add(prog_src);
+        d.add(std::string(file));
+        d.add(ex);
+        for (const auto &w : extra) d.add(w);
+        d.add("gfx950|-O3|-ffp-contract=off|-std=c++17|hiprtc " + std::to_string(vmaj) + "." + std::to_string(vmin) +
+              "|HIP " + std::to_string(HIP_VERSION));
+        dfile = dir + "/" + d.hex() + ".co";
+        RtcKernel k;
+        if (disk_get(dfile, k)) {
+            k.name = name;
+            k.origin = kRtcFromDisk;
+            k.seconds = since();
+            {
+                std::lock_guard<std::mutex> lk(g_mu);
+                g_cache[key] = k;
+            }
+            out = std::move(k);
+            return "";
+        }
+    }
     hiprtcProgram prog;
     if (hiprtcCreateProgram(&prog, prog_src.c_str(), file, kRtcHeaderCount, kRtcHeaderSrc, kRtcHeaderNames) !=
         HIPRTC_SUCCESS)
@@ -152,6 +258,12 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
     }
     hiprtcDestroyProgram(&prog);
     k.name = name;
+    k.origin = kRtcCompiled;
+    k.seconds = since();
+    if (!dfile.empty()) disk_put(dir, dfile, k);
+    if (getenv("EMCMC_RTC_LOG"))
+        fprintf(stderr, "[emcmc rtc] compiled %s in %.1f s%s%s\n", name.c_str(), k.seconds,
+                dfile.empty() ? "" : ", cached as ", dfile.c_str());
     {
         std::lock_guard<std::mutex> lk(g_mu);
         g_cache[key] = k;
@@ -161,6 +273,16 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
 }
 
 }  // namespace
+
+std::string rtc_cache_dir() {
+    const char *e = getenv("EMCMC_RTC_CACHE");
+    if (e && *e) return std::string(e) == "off" ? std::string() : std::string(e);
+    Dl_info info;
+    if (!dladdr(reinterpret_cast<void *>(&rtc_wide_nu), &info) || !info.dli_fname) return std::string();
+    std::string lib = info.dli_fname;
+    const size_t s = lib.rfind('/');
+    return (s == std::string::npos ? std::string(".") : lib.substr(0, s)) + "/rtc_cache";
+}
 
 std::string rtc_compile(const std::string &src, const std::string &opts, int D, bool full, int ll, int nu,
                         RtcKernel &out, const std::string &usrc = std::string(), const std::string &uopts = std::string(),

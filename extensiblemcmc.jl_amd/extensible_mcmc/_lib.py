@@ -245,6 +245,8 @@ SIGNATURES = {
         [_H, C.POINTER(C.c_double), C.POINTER(C.c_uint64), C.POINTER(C.c_double), C.c_int],
     ),
     "emcmc_kernel_name": (_ST, [_H, C.c_char_p, C.c_size_t]),
+    "emcmc_rtc_info": (_ST, [_H, C.POINTER(C.c_uint32), C.POINTER(C.c_double)]),
+    "emcmc_prebuild_chol_kernel": (_ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t]),
     "emcmc_probe_variates": (
         _ST,
         [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -343,6 +345,15 @@ def check_user_update(source: str, dim: int, options: str = "") -> None:
     st = lib().emcmc_check_user_update(source.encode(), dim, options.encode(), buf, len(buf))
     if st != OK:
         raise EMCMCError(st, "emcmc_check_user_update", buf.value.decode(errors="replace"))
+
+
+def prebuild_chol_kernel(dim: int, history_mode: int = 0, ll_mode: int = 0) -> None:
+    """Compile the run-time chol kernel at dim into the on-disk code-object cache
+    (no device needed), so a handle at that D loads it instead of compiling."""
+    buf = C.create_string_buffer(1 << 16)
+    st = lib().emcmc_prebuild_chol_kernel(dim, history_mode, ll_mode, buf, len(buf))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_prebuild_chol_kernel", buf.value.decode(errors="replace"))
 
 
 def device_count() -> int:

@@ -397,6 +397,13 @@ emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const cha
 emcmc_status emcmc_check_user_update(const char *source, uint32_t dim, const char *options, char *log_out,
                                      size_t log_len);
 
+/* Compile (no device needed) the run-time rwm_gsn_chol_kernel for a correlated
+ * Σ at dimension dim (9 ≤ dim ≤ 64 without an ahead-of-time instantiation) into
+ * the on-disk code-object cache (emcmc_rtc_info), so the first handle of a
+ * deployment loads it instead of compiling it (≈ 1 minute at dim ≥ 40). */
+emcmc_status emcmc_prebuild_chol_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, char *log_out,
+                                        size_t log_len);
+
 /* θinit for every chain (row-major [C][D]); ll = NULL means the reference's
  * initial ll = -Inf (workspaces.jl:425), i.e. the first step always accepts.
  * Also resets the rolling-acceptance statistics (chain_statistics.jl:23-36). */
@@ -531,6 +538,13 @@ emcmc_status emcmc_get_timing(emcmc_handle *h, double *total_ms, uint64_t *launc
 
 /* Human-readable name of the kernel variant `emcmc_run` dispatches to. */
 emcmc_status emcmc_kernel_name(emcmc_handle *h, char *buf, size_t buflen);
+
+/* How the handle's run-time compiled kernel (hiprtc: user laws and updates, the
+ * general kernel at other D, the chol kernel at other D) was obtained: origin
+ * 0 = this process's cache, 1 = the on-disk code-object cache (EMCMC_RTC_CACHE,
+ * else rtc_cache/ beside libemcmc.so), 2 = compiled now; seconds = the time it
+ * took.  EMCMC_STATE_ERROR when the selected kernel is compiled ahead of time. */
+emcmc_status emcmc_rtc_info(emcmc_handle *h, uint32_t *origin, double *seconds);
 
 /* ---- self-test probes (run the device's own math on given inputs) ------- */
 

@@ -152,6 +152,7 @@ struct Variant {
                                   // at a D without an ahead-of-time instantiation)
     bool mix = false;
     bool xres = false;  // xfn is mix_res_kernel (16 lanes per chain, L_B in registers)
+    bool xchol = false;  // xfn is mix_chol_kernel (dense Σ_A / Σ_t through the scalar cache)
     int lpc = 1;
     int dense = 0;  // 0 rwm_gsn_diag_kernel, 1 rwm_gsn_dense_kernel, 2 rwm_gsn_chol_kernel
     bool unit = false;
@@ -673,6 +674,13 @@ emcmc_status select_mix(emcmc_handle *h) {
     Variant v;
     for (const auto &e : mix_table())
         if (e.D == D && e.full == (int)full && e.ll == ll && e.mix == (int)mix && e.adiag == (int)adiag) v.xfn = e.fn;
+    // a dense Σ_A or Σ_t at D ≥ 16: the factors through the scalar cache
+    if (!v.xfn && !adiag && !(h->cfg.kernel_variant & EMCMC_VARIANT_NO_MIX_CHOL))
+        for (const auto &e : mixchol_table())
+            if (e.D == D && e.full == (int)full && e.ll == ll && e.mix == (int)mix) {
+                v.xfn = e.fn;
+                v.xchol = true;
+            }
     if (!v.xfn)
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "no mix/chain-moments kernel for D=%d with %s Σ_A/Σ_t (instantiated: D ∈ {1,2,3,4,8} any, "
@@ -698,20 +706,40 @@ emcmc_status select_mix(emcmc_handle *h) {
             }
     }
     char nm[160];
-    snprintf(nm, sizeof nm, "%s<D=%d,%s,%s,%s,%s%s>+mix_moments_kernel%s", v.xres ? "mix_res_kernel" : "mix_gsn_kernel",
+    snprintf(nm, sizeof nm, "%s<D=%d,%s,%s,%s,%s%s>+mix_moments_kernel%s",
+             v.xres ? "mix_res_kernel" : v.xchol ? "mix_chol_kernel" : "mix_gsn_kernel",
              D, full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", mix ? "MIX" : "GSN_MOMENTS",
              adiag ? "DIAG" : "DENSE", v.xres && unit ? ",UNIT_T" : "", v.rfn ? "+mix_readjust_kernel" : "");
     v.name = nm;
     const size_t DD = (size_t)D * D;
-    std::vector<double> c(2 * DD + 3 * (size_t)D);
-    std::copy(u.L.begin(), u.L.end(), c.begin());
-    std::copy(u.invdiag.begin(), u.invdiag.end(), c.begin() + DD);
-    std::copy(t.L.begin(), t.L.end(), c.begin() + DD + D);
-    std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
-    std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
+    std::vector<double> c;
+    if (v.xchol) {
+        // emcmc_mix.h mix_chol_kernel: L_A rows (packed lower, row-major, with L_ii) | L_A and
+        // L_t packed column-major with 1/L_jj on the diagonal | x̄ | observations (row-major)
+        const size_t P = (size_t)D * (D + 1) / 2;
+        c.assign(3 * P + D + (ll == LL_PER_OBS ? t.nobs * (size_t)D : 0), 0.0);
+        for (int i = 0; i < D; ++i)
+            for (int j = 0; j <= i; ++j) c[(size_t)lo_idx(i, j)] = u.L[(size_t)i * D + j];
+        for (int j = 0; j < D; ++j)
+            for (int i = j; i < D; ++i) {
+                const size_t e = (size_t)chol_col(D, j) + (size_t)(i - j);
+                c[P + e] = (i == j) ? u.invdiag[j] : u.L[(size_t)i * D + j];
+                c[2 * P + e] = (i == j) ? t.invdiag[j] : t.L[(size_t)i * D + j];
+            }
+        std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 3 * P);
+        if (ll == LL_PER_OBS) std::copy(t.obs.begin(), t.obs.end(), c.begin() + 3 * P + D);
+    } else {
+        c.resize(2 * DD + 3 * (size_t)D);
+        std::copy(u.L.begin(), u.L.end(), c.begin());
+        std::copy(u.invdiag.begin(), u.invdiag.end(), c.begin() + DD);
+        std::copy(t.L.begin(), t.L.end(), c.begin() + DD + D);
+        std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * DD + D);
+        std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * DD + 2 * D);
+    }
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    const size_t lds = v.xres ? mixres_lds(D, t.nobs, h->cfg.steps_per_launch, ll == LL_PER_OBS)
-                              : (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
+    const size_t lds = v.xres    ? mixres_lds(D, t.nobs, h->cfg.steps_per_launch, ll == LL_PER_OBS)
+                       : v.xchol ? 0  // the ziggurat only, in static LDS
+                                 : (c.size() + obs_doubles) * sizeof(double);  // + kZigLdsBytes of static LDS
     if (kZigLdsBytes + lds > kMaxLds)
         return fail(h, EMCMC_INVALID_ARG,
                     "per-observation likelihood needs %zu B of LDS (> %zu); use EMCMC_LL_SUFFSTAT for n=%llu", lds,
@@ -1086,6 +1114,7 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     p.zig = h->d_zig;
     p.consts = h->d_consts;
     p.obs = h->d_obs;
+    p.sconsts = h->d_consts;  // mix_chol_kernel's layout when it is selected
     p.C = C;
     p.row_bytes = h->row_bytes;
     p.chain0 = (uint32_t)h->cfg.first_chain_id;

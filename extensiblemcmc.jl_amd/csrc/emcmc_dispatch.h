@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "emcmc_kernels.h"
+#include "emcmc_fused.h"
 #include "emcmc_mala.h"
 #include "emcmc_mix.h"
 #include "emcmc_mwg.h"
@@ -46,6 +47,9 @@ struct MixEntry {
     MixFn fn;
 };
 const std::vector<MixEntry> &mix_table();
+// the same step for a dense Σ_A / Σ_t at D ≥ 16 with the factors through the
+// scalar cache (mix_chol_kernel, emcmc_mix.h; adiag = 0)
+const std::vector<MixEntry> &mixchol_table();
 // the same step with the chain's L_B resident in registers, 16 lanes per chain
 // (mix_res_kernel, emcmc_mixres.h; D = 32, MIX, diagonal Σ_A / Σ_t)
 struct MixResEntry {

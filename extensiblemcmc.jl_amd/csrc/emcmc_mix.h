@@ -59,6 +59,7 @@ struct MixParams {
     const Ziggurat *zig;
     const double *consts;  // L_A (D×D row-major lower) | 1/L_A,ii | L_t | 1/L_t,ii | x̄
     const double *obs;     // [nobs][D]
+    const double *sconsts;  // mix_chol_kernel: the scalar-cache constants (layout there)
     uint64_t C;
     uint64_t row_bytes;
     uint64_t N0;  // GenericChainStats.N before the first step of the launch
@@ -298,6 +299,159 @@ __global__ void __launch_bounds__(256) mix_gsn_kernel(const MixParams a) {
         // update_stats!' mean/cov recurrence runs batched over the launch in
         // mix_moments_kernel; it reads θ from the θ history (FULL) or here:
         if constexpr (!FULL) store_slot<D>(a.mom_theta + (uint64_t)s * D * C, soff, th);
+    }
+    a.ll[chain] = ll;
+    a.ra[chain] = ra;
+    a.ring[2 * chain] = r0;
+    a.ring[2 * chain + 1] = r1;
+    a.nacc[chain] = nacc;
+    a.faults[chain] = faults;
+    if (faults) *a.fault_flag = 1u;
+    store_state<D>(a.theta, C, chain, 0, th, false);
+}
+
+// ---- correlated Σ_A / Σ_t at the headline D: mix_chol_kernel -------------------
+// The same step as mix_gsn_kernel<D, …, DIAG = false> (the same formulas, so the
+// same bits as orc_run_mix and the general kernel's kind 3), for a dense Σ_A and
+// a dense target Σ_t at D ≥ 16, where the LDS route of mix_gsn_kernel would read
+// one broadcast LDS word per fma (4× the LDS bandwidth the fp64 VALU consumes)
+// and D×D factors per lane.  L_A and L_t are the same for every chain, so they
+// come through the SCALAR cache and enter v_fma_f64 as SGPR operands, as in
+// rwm_gsn_chol_kernel; each chain's own L_B streams from HBM once per step, row
+// by row, as in mix_gsn_kernel (that stream, 4.2 KB per chain-step at D = 32, is
+// what bounds the kernel).  Scalar constants (a.sconsts, doubles):
+//   [0, DP)      L_A packed lower, row-major, with its diagonal (the proposal rows)
+//   [DP, 2DP)    L_A packed lower, column-major, 1/L_jj on the diagonal (solve)
+//   [2DP, 3DP)   L_t the same (solve)
+//   [3DP, 3DP+D) x̄   |   [3DP+D, …) the observations, row-major
+// Order of each quantity (as mix_gsn_kernel): the proposal row i over j
+// ascending for both factors, then the pick; y_B by rows (the L_B row loaded
+// once serves the proposal and the substitution); y_A = L_A⁻¹(θ° − θ) and the
+// target's L_t⁻¹(x_k − θ°) as column sweeps (each row still accumulates over
+// j ascending: the bits of the row forms, DESIGN.md §6 rwm_gsn_chol_kernel).
+template <int D, bool FULL, int LLMODE, bool MIX>
+__global__ void __launch_bounds__(256) mix_chol_kernel(const MixParams a) {
+    constexpr int DP = packed_n(D);
+    const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
+
+    const uint64_t chain = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (chain >= a.C) return;
+    const uint64_t C = a.C;
+    const uint32_t gid = a.chain0 + (uint32_t)chain;
+    const uint32_t nobs = a.nobs;
+
+    double th[D];
+    load_state<D>(a.theta, C, chain, 0, th);
+    double ll = a.ll[chain];
+    double ra = a.ra[chain];
+    uint64_t r0 = a.ring[2 * chain], r1 = a.ring[2 * chain + 1];
+    uint32_t nacc = a.nacc[chain];
+    uint32_t faults = a.faults[chain];
+    const double c0B = MIX ? a.c0B[chain] : 0.0;
+    const SlotOffset<D> soff(C, chain, 0);
+
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
+        const uint64_t N = a.N0 + s;
+        const uint64_t slot = (uint64_t)(iter - 1);
+        // ---- proposal!: pick the kernel, θ° = θ + L z
+        bool useB = false;
+        if constexpr (MIX) {
+            const u32x4 pr = draw(a.key0, a.key1, gid, iter, kBlockMixPick, 0, 0);
+            useB = u01_closed0(pr.x, pr.y) <= a.lam;
+        }
+        double thp[D];
+        double qb = 0.0;
+        {
+            double z[D];
+            normals<D>(zt, a.key0, a.key1, gid, iter, 0, z, faults);
+            double yB[MIX ? D : 1];
+            SumSqAcc<D> sb;
+#pragma unroll
+            for (int i = 0; i < D; ++i) {
+                // one row at a time (bounded live L_B loads; the opaque pointer keeps
+                // the row's scalar loads of L_A here, not hoisted out of the loops)
+                __builtin_amdgcn_sched_barrier(0);
+                cdouble *la = opaque_cptr(a.sconsts) + lo_idx(i, 0);
+                double lzA = la[0] * z[0];
+#pragma unroll
+                for (int j = 1; j <= i; ++j) lzA = fma(la[j], z[j], lzA);
+                double lz = lzA;
+                if constexpr (MIX) {
+                    const LaneSoA lb = lane_soa(C, chain, DP);
+                    const LaneSoA il = lane_plain(C, chain);
+                    double Lr[D];
+#pragma unroll
+                    for (int j = 0; j <= i; ++j) Lr[j] = *soa_ptr<DP>(a.LB, lb, lo_idx(i, j));
+                    double lzB = Lr[0] * z[0];
+#pragma unroll
+                    for (int j = 1; j <= i; ++j) lzB = fma(Lr[j], z[j], lzB);
+                    lz = useB ? lzB : lzA;
+                    thp[i] = th[i] + lz;
+                    double acc = thp[i] - th[i];
+#pragma unroll
+                    for (int j = 0; j < i; ++j) acc = fma(-Lr[j], yB[j], acc);
+                    yB[i] = acc * *plain_ptr(a.iLB, il, i);
+                    pin(yB[i]);
+                    sb.add(i, yB[i]);
+                } else {
+                    thp[i] = th[i] + lz;
+                }
+                pin(thp[i]);
+            }
+            if constexpr (MIX) qb = sb.finish();
+        }
+        // logpdf(gsn_A, θ, θ°): y_A = L_A⁻¹(θ° − θ) as a column sweep over the solve table
+        double ltd;
+        {
+            double acc[D];
+#pragma unroll
+            for (int i = 0; i < D; ++i) acc[i] = thp[i] - th[i];
+            cdouble *c = opaque_cptr(a.sconsts);
+            const double lpA = fma(-0.5, chol_sqmahal<D, 0>(c, c + DP, thp, acc), a.c0A);  // = c0 − q/2
+            ltd = lpA;
+            if constexpr (MIX) {
+                const double lpB = fma(-0.5, qb, c0B);
+                ltd = log_any(a.oml * exp_any(lpA) + a.lam * exp_any(lpB));
+            }
+        }
+        // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
+        double llp;
+        if constexpr (LLMODE == LL_PER_OBS) {
+            llp = 0.0;
+            for (uint32_t k = 0; k < nobs; ++k) {
+                cdouble *c = opaque_cptr(a.sconsts);
+                double acc[D];
+                llp = llp + fma(-0.5, chol_sqmahal<D, D>(c + 3 * DP + D + (size_t)k * D, c + 2 * DP, thp, acc),
+                                a.t_c0);
+            }
+        } else {
+            cdouble *c = opaque_cptr(a.sconsts);
+            double acc[D];
+            const double qv = chol_sqmahal<D, D>(c + 3 * DP, c + 2 * DP, thp, acc);
+            llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
+        if (!(llp - llp == 0.0)) faults |= 1u;
+        // ---- accept_reject!
+        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double E = exp_draw(zt, a.key0, a.key1, gid, iter, 0, faults);
+        const bool acc = E > -llr;
+        if constexpr (FULL) store_slot_late<D>(a.hist_prop + slot * D * C, soff, thp);
+#pragma unroll
+        for (int i = 0; i < D; ++i) th[i] = acc ? thp[i] : th[i];
+        if (s + 1 == a.nsteps) a.ll_prop[chain] = llp;
+        ll = acc ? llp : ll;
+        nacc += acc ? 1u : 0u;
+        if constexpr (FULL) {
+            store_slot_late<D>(a.hist_theta + slot * D * C, soff, th);
+            __builtin_nontemporal_store(ll, a.hist_ll + slot * C + chain);
+        }
+        {
+            const uint64_t m = __ballot(acc);
+            if ((threadIdx.x & 63) == 0) store_acc_bits<1>(a.hist_acc + slot * a.row_bytes, chain, m);
+        }
+        ra = rolling_update(ra, r0, r1, iter, a.W, N, a.rcp_W, acc);
+        if constexpr (!FULL) store_slot_late<D>(a.mom_theta + (uint64_t)s * D * C, soff, th);
     }
     a.ll[chain] = ll;
     a.ra[chain] = ra;

@@ -23,6 +23,25 @@ const std::vector<MixEntry> &mix_table() {
                                             MIX8(8, false), MIX8(16, true), MIX8(32, true)};
     return t;
 }
+template <int D, bool FULL, int LL, bool MIX>
+MixFn mixchol_fn() {
+    return &mix_chol_kernel<D, FULL, LL, MIX>;
+}
+// correlated Σ_A / Σ_t at D ≥ 16: factors through the scalar cache (the entry's
+// adiag field is 0: dense)
+#define MIXCHOL8(D)                                                                                         \
+    {D, true, 0, true, 0, mixchol_fn<D, true, 0, true>()}, {D, true, 1, true, 0, mixchol_fn<D, true, 1, true>()},   \
+        {D, false, 0, true, 0, mixchol_fn<D, false, 0, true>()},                                             \
+        {D, false, 1, true, 0, mixchol_fn<D, false, 1, true>()},                                             \
+        {D, true, 0, false, 0, mixchol_fn<D, true, 0, false>()},                                             \
+        {D, true, 1, false, 0, mixchol_fn<D, true, 1, false>()},                                             \
+        {D, false, 0, false, 0, mixchol_fn<D, false, 0, false>()},                                           \
+        {D, false, 1, false, 0, mixchol_fn<D, false, 1, false>()}
+const std::vector<MixEntry> &mixchol_table() {
+    static const std::vector<MixEntry> t = {MIXCHOL8(16), MIXCHOL8(32)};
+    return t;
+}
+
 template <int D, bool FULL, int LL, bool UNIT>
 MixFn mixres_fn() {
     return &mix_res_kernel<D, FULL, LL, UNIT>;

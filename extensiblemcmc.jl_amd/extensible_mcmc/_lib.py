@@ -57,6 +57,7 @@ VARIANT_SCALAR_OBS = 4
 VARIANT_MIX_STREAM = 8
 VARIANT_NO_XCD_ORDER = 16
 VARIANT_NO_RTC_CHOL = 32
+VARIANT_NO_MIX_CHOL = 64
 
 
 class EmcmcConfig(C.Structure):

@@ -175,6 +175,8 @@ typedef struct emcmc_config {
 #define EMCMC_VARIANT_NO_XCD_ORDER 16u   /* blocks in blockIdx order instead of one contiguous chain range per XCD */
 #define EMCMC_VARIANT_NO_RTC_CHOL 32u    /* a correlated Σ at a D without an ahead-of-time rwm_gsn_chol_kernel runs on
                                             the general kernel instead of the chol kernel compiled at run time */
+#define EMCMC_VARIANT_NO_MIX_CHOL 64u    /* GaussianRandomWalkMix / chain moments with a dense Σ_A or Σ_t at D = 16,
+                                            24, 32: the general kernel instead of mix_chol_kernel */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,

@@ -37,18 +37,105 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chains", type=int, default=65536)
     ap.add_argument("--iters", type=int, default=200)
+    ap.add_argument("--haario-chains", type=int, default=131072)
+    ap.add_argument("--haario-iters", type=int, default=400)
+    ap.add_argument("--only", default="", help="comma-separated workload names (default: all)")
     a = ap.parse_args()
     C, M = a.chains, a.iters
     w = W.cfg2(8)
     out = []
+    only = set(filter(None, a.only.split(",")))
 
-    def report(name, eng, P, ms, nbytes):
+    def want(name):
+        return not only or name in only
+
+    def report(name, eng, P, ms, nbytes, C=C, M=M, extra=None):
         n = C * M * P
         out.append({"workload": name, "kernel": eng.kernel_name(), "chains": C, "iters": M, "updates": P,
-                    "ms": ms, "update_steps_per_s": n / (ms / 1e3), "GBps_algorithmic": nbytes / (ms / 1e3) / 1e9})
+                    "ms": ms, "update_steps_per_s": n / (ms / 1e3), "GBps_algorithmic": nbytes / (ms / 1e3) / 1e9,
+                    **(extra or {})})
         print(json.dumps(out[-1]), flush=True)
 
     # (1) D = 32, two GaussianRandomWalk blocks of 16 coordinates (Metropolis-within-Gibbs)
+    if want("mwg_d32_two_blocks"):
+        mwg_two_blocks(C, M, w, report)
+    if want("dense_d32_joint"):
+        dense_joint(C, M, w, report)
+    if want("user_student_t_d4"):
+        user_student_t(C, M, report)
+    # (4) the round-3 verdict's correlated Haario case and its general-kernel route
+    for name, variant in (("haario_dense_d32", 0), ("haario_dense_d32_general", L.VARIANT_NO_MIX_CHOL)):
+        if want(name):
+            haario_dense(name, variant, a.haario_chains, a.haario_iters, report)
+    if want("mala_gsn_d32"):
+        mala_gsn(C, M, report)
+    if want("pcn_user_d32"):
+        pcn_user(C, M, report)
+
+
+def corr_d32(seed=32, D=32, nobs=10):
+    rng = np.random.default_rng(seed)
+    B = rng.standard_normal((D, D))
+    ts = B @ B.T / D + np.eye(D)
+    mu = rng.standard_normal(D)
+    obs = rng.multivariate_normal(mu, ts, size=nobs)
+    return mu, ts, obs
+
+
+def haario_dense(name, variant, C, M, report):
+    """GaussianRandomWalkMix(Σ_A dense, Σ_B, λ = 0.3) + HaarioTypeAdaptation(k = 100) on
+    GsnTargetLaw(μ, BBᵀ/32 + I), 10 observations, per-observation likelihood; the kernel
+    time covers step + moments (+ readjust) launch groups."""
+    D = 32
+    mu, ts, obs = corr_d32()
+    sa = 0.2 * (2.38 ** 2 / (D * 10)) * ts
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=3 * M, seed=321, kernel_variant=variant))
+    eng.add_gaussian_rw_mix_update(np.arange(D), sa, 0.5 * sa, lam=0.3, haario_k=100)
+    eng.set_gsn_target(mu, ts, obs)
+    eng.set_state(np.tile(obs.mean(0), (C, 1)))
+    eng.run([(i, 1) for i in range(1, M // 10 + 1)])  # warm-up (first launch compiles a run-time kernel)
+    eng.synchronize(allow_faults=True)
+    eng.set_timing(True)
+    eng.get_timing(reset=True)
+    it0 = M // 10 + 1
+    eng.run([(i, 1) for i in range(it0, it0 + M)])
+    eng.synchronize(allow_faults=True)
+    ms, n, b = eng.get_timing(reset=True)
+    faults = int(np.count_nonzero(eng.get_faults() & L.FAULT_POSDEF))
+    report(name, eng, 1, ms, b, C=C, M=M, extra={"posdef_faulted_chains": faults, "readjusts_in_window": M // 100})
+    eng.close()
+
+
+def mala_gsn(C, M, report):
+    """MALA (ϵ = 0.05) on GsnTargetLaw(μ, BBᵀ/32 + I) at D = 32 (general kernel, the target's
+    built-in gradient)."""
+    D = 32
+    mu, ts, obs = corr_d32(7)
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=5))
+    eng.add_mala_update(np.arange(D), 0.05)
+    eng.set_gsn_target(mu, ts, obs)
+    eng.set_state(np.tile(obs.mean(0), (C, 1)))
+    ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
+    report("mala_gsn_d32", eng, 1, ms, b)
+    eng.close()
+
+
+def pcn_user(C, M, report):
+    """The pCN user update (tests/user_updates/pcn.c, ρ = 0.9, σ = 0.3, centred at x̄) at D = 32
+    on the correlated GsnTargetLaw (general kernel, run-time compiled)."""
+    D = 32
+    mu, ts, obs = corr_d32(9)
+    src = (ROOT / "tests" / "user_updates" / "pcn.c").read_text()
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=6))
+    eng.add_user_update(np.arange(D), src, params=np.concatenate([[0.9, 0.3], obs.mean(0)]))
+    eng.set_gsn_target(mu, ts, obs)
+    eng.set_state(np.tile(obs.mean(0), (C, 1)))
+    ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
+    report("pcn_user_d32", eng, 1, ms, b)
+    eng.close()
+
+
+def mwg_two_blocks(C, M, w, report):
     eng = Engine(EngineConfig(dim=32, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed))
     for blk in (range(0, 16), range(16, 32)):
         eng.add_gaussian_rw_update(np.array(blk), np.asarray(w.rw_sigma)[:16, :16] * 2.0)
@@ -59,6 +146,8 @@ def main():
     report("mwg_d32_two_blocks", eng, 2, ms, b)
     eng.close()
 
+
+def dense_joint(C, M, w, report):
     # (2) D = 32, one joint update with correlated proposal and target Σ
     rng = np.random.default_rng(5)
     A = rng.standard_normal((32, 32))
@@ -80,6 +169,8 @@ def main():
     report("dense_d32_joint_suffstat", eng, 1, ms, b)
     eng.close()
 
+
+def user_student_t(C, M, report):
     # (3) user law: student-t regression, D = 4, 50 observations (run-time compiled)
     import user_target_cases as U
     case = U.student_t()
@@ -88,11 +179,8 @@ def main():
     eng.add_gaussian_rw_update(np.arange(case.D), 0.01 * np.eye(case.D))
     eng.set_user_target(src, obs=case.obs, params=case.params, theta0=case.theta0)
     eng.set_state(np.zeros((2 * C, case.D)))
-    C0 = C
-    C = 2 * C0
     ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
-    report("user_student_t_d4", eng, 1, ms, b)
-    C = C0
+    report("user_student_t_d4", eng, 1, ms, b, C=2 * C)
     eng.close()
 
 

@@ -205,6 +205,12 @@ def test_shapes_outside_the_fused_kernels_run_on_the_general_kernel():
     eng = Engine(EngineConfig(dim=32, num_chains=64, num_mcmc_steps=10, seed=seed))
     eng.add_gaussian_rw_mix_update(range(32), sa, sa)
     eng.set_gsn_target(mu, ts, obs)
+    assert eng.kernel_name().startswith("mix_chol_kernel<D=32")  # round 4: dense Σ at D = 16 / 32 fused
+    eng.close()
+    eng = Engine(EngineConfig(dim=32, num_chains=64, num_mcmc_steps=10, seed=seed,
+                              kernel_variant=L.VARIANT_NO_MIX_CHOL))
+    eng.add_gaussian_rw_mix_update(range(32), sa, sa)
+    eng.set_gsn_target(mu, ts, obs)
     assert eng.kernel_name().startswith("mwg_wide_kernel<D=32")
     eng.close()
 

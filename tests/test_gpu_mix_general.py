@@ -21,9 +21,10 @@ def _gpu(require_gpu):
     pass
 
 
-def build(oracle, D, C, M, ups, seed, hist=L.HIST_FULL, spl=0, chain_moments=False, ll_mode=L.LL_PER_OBS):
+def build(oracle, D, C, M, ups, seed, hist=L.HIST_FULL, spl=0, chain_moments=False, ll_mode=L.LL_PER_OBS,
+          variant=0):
     eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
-                              steps_per_launch=spl, chain_moments=chain_moments))
+                              steps_per_launch=spl, chain_moments=chain_moments, kernel_variant=variant))
     for u in ups:
         pr = dict(prior=u.get("prior", 0), prior_factors=u.get("factors") or None)
         if u["kind"] == oracle.KIND_MIX:
@@ -66,8 +67,10 @@ def run_both(oracle, D, C, M, ups, mu, ts, obs, steps, seed, theta0=None, chain_
 
 
 def test_haario_on_a_correlated_d32_target_through_two_readjusts(oracle):
-    """The verdict's case: HaarioTypeAdaptation on GsnTargetLaw(μ, BBᵀ/32 + I) at D = 32
-    with a dense Σ_A, k = 50, 140 steps (two readjusts): general kernel, bitwise."""
+    """The round-2 verdict's case: HaarioTypeAdaptation on GsnTargetLaw(μ, BBᵀ/32 + I) at
+    D = 32 with a dense Σ_A, k = 100, 230 steps (two readjusts): the general kernel
+    (EMCMC_VARIANT_NO_MIX_CHOL; the default is the fused mix_chol_kernel,
+    tests/test_gpu_mix_chol.py), bitwise."""
     rng = np.random.default_rng(32)
     D, C, M, k = 32, 1024, 230, 100
     B = rng.standard_normal((D, D))
@@ -77,7 +80,8 @@ def test_haario_on_a_correlated_d32_target_through_two_readjusts(oracle):
     sa = 0.2 * (2.38 ** 2 / (D * 10)) * ts  # ≈ 60 % acceptance: 100 registrations span the space
     ups = [oracle.mwg_update(oracle.KIND_MIX, range(D), sigma=sa, sigma_b=0.5 * sa, lam=0.3, haario_k=k)]
     steps = full_steps(M, 1)
-    eng, st, h = run_both(oracle, D, C, M, ups, mu, ts, obs, steps, 321, theta0=obs.mean(0), ll_mode=L.LL_SUFFSTAT)
+    eng, st, h = run_both(oracle, D, C, M, ups, mu, ts, obs, steps, 321, theta0=obs.mean(0), ll_mode=L.LL_SUFFSTAT,
+                          variant=L.VARIANT_NO_MIX_CHOL)
     assert "mwg_wide_kernel<D=32" in eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
     check_mix(oracle, eng, st, ups)

@@ -269,7 +269,7 @@ emcmc_status fail(emcmc_handle *h, emcmc_status st, const char *fmt, ...) {
     } while (0)
 
 KernelFn lookup(int D, int lpc, bool full, int ll, int dense, bool unit, int occ = 0) {
-    for (const auto *tab : {&diag_table(), &chol_table()})
+    for (const auto *tab : {&diag_table(), &diag2_table(), &chol_table()})
         for (const auto &e : *tab)
             if (e.k.D == D && e.k.lpc == lpc && e.k.full == (int)full && e.k.ll == ll && e.k.dense == dense &&
                 e.k.unit == (int)unit && e.k.occ == occ)
@@ -842,9 +842,11 @@ emcmc_status select_variant(emcmc_handle *h) {
         bool unit = true;
         for (int i = 0; i < D; ++i) unit = unit && h->target.invdiag[i] == 1.0;
         v.unit = unit;
+        // default: the 2-waves-per-SIMD register cap where instantiated (inst_diag2.hip)
         const int occ = (h->cfg.kernel_variant & EMCMC_VARIANT_HIGH_OCCUPANCY) ? 4
                         : (h->cfg.kernel_variant & EMCMC_VARIANT_OCCUPANCY3)   ? 3
-                                                                               : 0;
+                        : (h->cfg.kernel_variant & EMCMC_VARIANT_UNCAPPED)     ? 0
+                                                                               : 2;
         v.fn = lookup(D, lpc, full, ll, false, unit, occ);
         v.occ = occ;
         if (!v.fn && occ) {
@@ -886,7 +888,7 @@ emcmc_status select_variant(emcmc_handle *h) {
     snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>%s",
              v.dense == 3 ? "diag_s" : v.dense == 2 ? "chol" : v.dense ? "dense" : "diag", D, v.lpc,
              full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
-             v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : "", v.ffn ? "[hiprtc]" : "");
+             v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : v.occ == 2 ? ",MINW=2" : "", v.ffn ? "[hiprtc]" : "");
     v.name = nm;
     // constants for this variant
     std::vector<double> c;

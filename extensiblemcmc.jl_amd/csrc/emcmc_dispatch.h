@@ -31,6 +31,7 @@ struct Entry {
     KernelFn fn;
 };
 const std::vector<Entry> &diag_table();
+const std::vector<Entry> &diag2_table();  // occ = 2 (≤ 256 registers): inst_diag2.hip
 const std::vector<Entry> &chol_table();  // dense = 2 (chol) and 3 (diag_s): inst_chol.hip
 
 // general schedule kernel (mwg_gsn_kernel)

@@ -17,6 +17,29 @@ namespace emcmc {
 #define EMCMC_DIAG_BLOCK2 256  // threads per block at ≤ 2 waves/SIMD (512: one table copy per CU)
 #endif
 constexpr int diag_block(int MINW) { return MINW >= 3 ? 256 * MINW : EMCMC_DIAG_BLOCK2; }
+
+// Timing-only build (make trace → lib/libemcmc_trace.so, scripts/trace_diag.py):
+// every wave of rwm_gsn_diag_kernel records the 100 MHz real-time counter at its
+// start, after the table staging, after its carried state arrived, at the end of
+// every step and after its last stores drained.  Not a product path.
+#ifndef EMCMC_TRACE
+#define EMCMC_TRACE 0
+#endif
+#if EMCMC_TRACE
+constexpr int kTraceSlots = 128, kTraceWaves = 16384;
+static __device__ uint64_t emcmc_trace_buf[kTraceSlots * kTraceWaves];
+__device__ __forceinline__ void trace_mark(uint32_t wave, int idx) {
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kTraceWaves && idx < kTraceSlots)
+        emcmc_trace_buf[(size_t)wave * kTraceSlots + idx] = t;  // one lane: a vector store under exec
+}
+#define EMCMC_TRACE_MARK(w, i) trace_mark((w), (i))
+#else
+#define EMCMC_TRACE_MARK(w, i) ((void)0)
+#endif
+#ifndef EMCMC_TILED_HIST
+#define EMCMC_TILED_HIST 0
+#endif
 #ifndef EMCMC_EARLY_STATE
 #define EMCMC_EARLY_STATE 0  // 1: the carried state's loads are issued before the table staging
 #endif
@@ -33,10 +56,15 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 4 * D;
+#if EMCMC_TRACE
+    const uint32_t twave = (uint32_t)((xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x) >> 6);
+    EMCMC_TRACE_MARK(twave, 0);
+#endif
 #if !EMCMC_EARLY_STATE
     const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
 #endif
     const double *cst0 = lds;
+    EMCMC_TRACE_MARK(twave, 1);
 
     const uint64_t tid = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x;
 #if EMCMC_EARLY_STATE
@@ -55,6 +83,13 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
 
     const uint64_t C = a.C;
     const SlotOffset<D> soff(C, chain, d0);
+#if EMCMC_TILED_HIST  // timing-only A/B: history slots in 32-chain tiles (readers not adapted)
+    SlotOffset<D> hoff = soff;
+    hoff.o = (uint32_t)(((((uint64_t)chain >> 5) * (D / 2) + (uint64_t)(d0 / 2)) * 32u + (chain & 31u)) * 16u);
+    hoff.stride = 512u;
+#else
+    const SlotOffset<D> &hoff = soff;
+#endif
     const uint32_t c32 = (uint32_t)chain;  // C < 2^32 (emcmc_create)
     double th[DPL];
     load_slot<D>(a.theta, soff, th);
@@ -78,6 +113,10 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
 #else
     const PhiloxVKeys vkeys{};
+#endif
+#if EMCMC_TRACE
+    __builtin_amdgcn_s_waitcnt(0);  // the carried state has arrived
+    EMCMC_TRACE_MARK(twave, 2);
 #endif
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
@@ -165,7 +204,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         const double E = accs.next<EMCMC_VKEYS != 0>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
         const bool acc = E > -llr;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
-        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, soff, thp);
+        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)
 #pragma unroll
         for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
@@ -173,7 +212,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;
         if constexpr (FULL) {
-            store_slot<D>(a.hist_theta + slot * D * C, soff, th);
+            store_slot<D>(a.hist_theta + slot * D * C, hoff, th);
             if (sub == 0) __builtin_nontemporal_store(ll, &chain_elem(a.hist_ll + slot * a.C, c32));
         }
         {
@@ -183,6 +222,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         }
         // ---- update_stats! rolling acceptance (chain_statistics.jl:53-65)
         ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
+        EMCMC_TRACE_MARK(twave, 3 + (int)s);
     }
 
     if constexpr (kBatched) {
@@ -202,6 +242,11 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         if (faults) *a.fault_flag = 1u;
     }
     store_slot_cached<D>(a.theta, soff, th);
+#if EMCMC_TRACE
+    EMCMC_TRACE_MARK(twave, kTraceSlots - 2);
+    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged
+    EMCMC_TRACE_MARK(twave, kTraceSlots - 1);
+#endif
 }
 
 // ---------------------------------------------------------------------------

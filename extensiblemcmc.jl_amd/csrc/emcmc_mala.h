@@ -27,6 +27,9 @@ namespace emcmc {
 
 typedef double mala_d4 __attribute__((ext_vector_type(4)));
 
+#ifndef EMCMC_MALA_IEEE_DIV
+#define EMCMC_MALA_IEEE_DIV 0
+#endif
 #ifndef EMCMC_MALA_ABLATE
 #define EMCMC_MALA_ABLATE 0
 #endif
@@ -58,10 +61,11 @@ struct MalaParams {
     double rcp_W;
 };
 
-// ℓ_n = y·η − softplus(η), r_n = y − σ(η), one division: t = e^{−|η|},
-// u = 1 + t, v = 1/u, log1p(t) = log(u) − ((u − 1) − t)·v (t if u == 1),
-// σ = (η ≥ 0 ? 1 : t)·v.  exp and log are the table-driven forms
-// (emcmc_math.h exp_le0 / log_1_2) with their tables in LDS.
+// ℓ_n = y·η − softplus(η), r_n = y − σ(η), no division: t = e^{−|η|},
+// u = 1 + t, log(u) and v ≈ 1/u from one reduction (log_rcp_1_2), log1p(t) =
+// log(u) − ((u − 1) − t)·v (t if u == 1), σ = (η ≥ 0 ? 1 : t)·v.  exp and log
+// are the table-driven forms (emcmc_math.h exp_le0 / log_rcp_1_2) with their
+// tables in LDS.
 struct MathLds {
     double exp2_64[64];
     double invc[128];
@@ -72,8 +76,12 @@ struct MathLds {
 __device__ __forceinline__ void logistic_terms(double eta, double y, double &ell, double &r, const MathLds &mt) {
     const double t = exp_le0<false>(-fabs(eta), mt.exp2_64);
     const double u = 1.0 + t;
-    const double v = 1.0 / u;
-    const double lp1 = (u == 1.0) ? t : log_1_2(u, mt.invc, mt.logc) - ((u - 1.0) - t) * v;
+    double v;
+    const double lu = log_rcp_1_2(u, mt.invc, mt.logc, v);
+#if EMCMC_MALA_IEEE_DIV  // timing-only A/B build: the round-3 quotient (not the oracle's bits)
+    v = 1.0 / u;
+#endif
+    const double lp1 = (u == 1.0) ? t : lu - ((u - 1.0) - t) * v;
     const double sp = (eta > 0.0 ? eta : 0.0) + lp1;
     const double sig = (eta >= 0.0 ? 1.0 : t) * v;
     ell = y * eta - sp;

@@ -366,6 +366,35 @@ EMCMC_HD double log_1_2(double u, const double *invc, const double *logc) {
     const double l1 = fma(q * r, r, r);  // log1p(r)
     return fma(e, ln2_hi, logc[j]) + fma(e, ln2_lo, l1);
 }
+// log_1_2 and 1/u from the same reduction (the MALA logistic terms need both):
+// 1/u = 2^−e · RN(1/c_j) / (1 + r), 1/(1 + r) = Σ_{k≤6} (−r)^k (|r|^7 < 2^-56),
+// ≤ 2 ulp (tests/test_oracle_mala.py) with no division: 6 fma, a product and an
+// ldexp instead of the IEEE quotient's scale/reciprocal/refine/fixup sequence.
+EMCMC_HD double log_rcp_1_2(double u, const double *invc, const double *logc, double &rcp) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const uint64_t b = d2u(u);
+    const int ei = (int)(b >> 52) - 1023;  // 0, or 1 at u = 2
+    const double e = (double)ei;
+    const double w = u2d((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int j = (int)((b >> 45) & 127u);
+    const double ic = invc[j];
+    const double r = fma(w, ic, -1.0);
+    double q = 1.0 / 7.0;
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double l1 = fma(q * r, r, r);  // log1p(r)
+    double p = 1.0 - r;
+    p = fma(-r, p, 1.0);
+    p = fma(-r, p, 1.0);
+    p = fma(-r, p, 1.0);
+    p = fma(-r, p, 1.0);
+    p = fma(-r, p, 1.0);  // Σ_{k≤6} (−r)^k
+    rcp = ldexp(ic * p, -ei);
+    return fma(e, ln2_hi, logc[j]) + fma(e, ln2_lo, l1);
+}
 
 // ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ---------------
 // The same sampler family as Julia's randn/randexp (Random stdlib), fed by the

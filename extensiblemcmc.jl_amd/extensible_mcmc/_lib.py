@@ -58,6 +58,7 @@ VARIANT_MIX_STREAM = 8
 VARIANT_NO_XCD_ORDER = 16
 VARIANT_NO_RTC_CHOL = 32
 VARIANT_NO_MIX_CHOL = 64
+VARIANT_UNCAPPED = 128  # diag kernel without the 2-waves-per-SIMD register cap
 
 
 class EmcmcConfig(C.Structure):

@@ -177,6 +177,8 @@ typedef struct emcmc_config {
                                             the general kernel instead of the chol kernel compiled at run time */
 #define EMCMC_VARIANT_NO_MIX_CHOL 64u    /* GaussianRandomWalkMix / chain moments with a dense Σ_A or Σ_t at D = 16,
                                             24, 32: the general kernel instead of mix_chol_kernel */
+#define EMCMC_VARIANT_UNCAPPED 128u      /* diagonal fused kernel without the 2-waves-per-SIMD register cap
+                                            (D = 16, 32, 64 build it at MINW = 2 by default) */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,

@@ -491,6 +491,9 @@ ORC_EXPORT void orc_exp_le0_vec(const double *x, double *y, uint64_t n) {
 ORC_EXPORT void orc_log_1_2_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_log_1_2(x[i]);
 }
+ORC_EXPORT void orc_rcp_1_2_vec(const double *x, double *y, uint64_t n) {
+    for (uint64_t i = 0; i < n; ++i) (void)orc_log_rcp_1_2(x[i], &y[i]);
+}
 ORC_EXPORT void orc_exp_any_vec(const double *x, double *y, uint64_t n) {
     for (uint64_t i = 0; i < n; ++i) y[i] = orc_exp_any(x[i]);
 }
@@ -1598,16 +1601,17 @@ ORC_EXPORT int orc_run_mix(int D, uint64_t C, uint32_t chain0, uint64_t seed, co
  *   ∇ℓ_d  = fma chain over n = 0..N−1 from 0.0
  *   ℓ     = (S_0 + S_1) + (S_2 + S_3), S_g = Σ_{n ≡ g mod 4} ℓ_n in increasing n
  *   ‖v‖²  = (s_0 + s_1) + (s_2 + s_3), s_g = v_g² then fma over d ≡ g mod 4 ascending
- *   t = e^{−|η|} (orc_exp_le0), u = 1 + t, v = 1/u (the one division per element),
- *   log(u) by orc_log_1_2,
+ *   t = e^{−|η|} (orc_exp_le0), u = 1 + t, log(u) and v ≈ 1/u (≤ 2 ulp, no
+ *   division) by orc_log_rcp_1_2,
  *   log1p(t) = t if u == 1 else log(u) − ((u − 1) − t)·v,
  *   softplus(η) = max(η, 0) + log1p(t), σ(η) = (η ≥ 0 ? 1 : t)·v.
  */
 static inline void orc_logistic_terms(double eta, double y, double *ell, double *r) {
     const double t = orc_exp_le0(-fabs(eta));
     const double u = 1.0 + t;
-    const double v = 1.0 / u;
-    const double lp1 = (u == 1.0) ? t : orc_log_1_2(u) - ((u - 1.0) - t) * v;
+    double v;
+    const double lu = orc_log_rcp_1_2(u, &v);
+    const double lp1 = (u == 1.0) ? t : lu - ((u - 1.0) - t) * v;
     const double sp = (eta > 0.0 ? eta : 0.0) + lp1;
     const double sig = (eta >= 0.0 ? 1.0 : t) * v;
     *ell = y * eta - sp;

@@ -61,7 +61,8 @@ def lib():
         L.orc_normal_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
         L.orc_exp_vec.restype = None
         L.orc_exp_vec.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, dp]
-        for nm in ("orc_exp_any_vec", "orc_log_any_vec", "orc_exp_le0_vec", "orc_log_1_2_vec"):
+        for nm in ("orc_exp_any_vec", "orc_log_any_vec", "orc_exp_le0_vec", "orc_log_1_2_vec",
+                   "orc_rcp_1_2_vec"):
             getattr(L, nm).restype = None
             getattr(L, nm).argtypes = [dp, dp, C.c_uint64]
         L.orc_markstein_mismatches.restype = C.c_uint64
@@ -212,6 +213,14 @@ def log_1_2_vec(x):
     x = np.ascontiguousarray(x, dtype=np.float64)
     y = np.empty_like(x)
     lib().orc_log_1_2_vec(_d(x), _d(y), x.size)
+    return y
+
+
+def rcp_1_2_vec(x):
+    """1/u for u in [1, 2] as the MALA logistic terms form it (orc_log_rcp_1_2)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    y = np.empty_like(x)
+    lib().orc_rcp_1_2_vec(_d(x), _d(y), x.size)
     return y
 
 

@@ -220,6 +220,30 @@ static inline double orc_log_1_2(double u) {
     return fma(e, ln2_hi, ORC_LOG_LOGC[j]) + fma(e, ln2_lo, l1);
 }
 
+/* log u and 1/u from the same reduction (device log_rcp_1_2, emcmc_math.h):
+ * 1/u = 2^-e · RN(1/c_j) · Σ_{k<=6} (−r)^k, Horner from 1 − r. */
+static inline double orc_log_rcp_1_2(double u, double *rcp) {
+    const double ln2_hi = 6.93147180369123816490e-01, ln2_lo = 1.90821492927058770002e-10;
+    const uint64_t b = orc_d2u(u);
+    const int ei = (int)(b >> 52) - 1023;
+    const double e = (double)ei;
+    const double w = orc_u2d((b & 0x000FFFFFFFFFFFFFull) | 0x3FF0000000000000ull);
+    const int j = (int)((b >> 45) & 127u);
+    const double ic = ORC_LOG_INVC[j];
+    const double r = fma(w, ic, -1.0);
+    double q = 1.0 / 7.0;
+    q = fma(q, r, -1.0 / 6.0);
+    q = fma(q, r, 1.0 / 5.0);
+    q = fma(q, r, -0.25);
+    q = fma(q, r, 1.0 / 3.0);
+    q = fma(q, r, -0.5);
+    const double l1 = fma(q * r, r, r);
+    double p = 1.0 - r;
+    for (int k = 0; k < 5; ++k) p = fma(-r, p, 1.0);
+    *rcp = ldexp(ic * p, -ei);
+    return fma(e, ln2_hi, ORC_LOG_LOGC[j]) + fma(e, ln2_lo, l1);
+}
+
 /* ---- Marsaglia–Tsang ziggurat (J. Stat. Softw. 5(8), 2000) ----
  * N(0,1): 8192 strips, Exp(1): 256 strips, 52-bit magnitudes.  r and v of the
  * 8192-strip normal table solve the M&T closure (top strip area = v) to double

@@ -233,6 +233,19 @@ def test_log_1_2_table_driven(oracle):
     assert oracle.log_1_2_vec(np.array([1.0]))[0] == 0.0 or abs(oracle.log_1_2_vec(np.array([1.0]))[0]) < 2 ** -60
 
 
+def test_rcp_1_2_table_driven(oracle):
+    """The MALA logistic terms' 1/u on [1, 2] (no division: the log reduction's
+    RN(1/c_j) times a degree-6 series in r): within 2 ulp of the exact quotient,
+    exact at u = 1 and u = 2."""
+    rng = np.random.default_rng(7)
+    u = np.concatenate([1.0 + rng.random(20000), 1.0 + np.exp(-rng.uniform(0, 40, 4000)),
+                        1.0 + np.arange(129) / 128.0, [np.nextafter(2.0, 0), np.nextafter(1.0, 2)]])
+    y = oracle.rcp_1_2_vec(u)
+    ref = 1.0 / u  # IEEE division: correctly rounded, within 0.5 ulp of the true quotient
+    assert np.all(np.abs(y - ref) <= 2.0 * np.spacing(ref))
+    assert oracle.rcp_1_2_vec(np.array([1.0, 2.0])).tolist() == [1.0, 0.5]
+
+
 def test_faithful_refactor_variant_has_the_same_bits(oracle):
     """The CPU baseline's "faithful" variant (a Cholesky per MvNormal construction,
     random_walk.jl:147,167, gsn_target.jl:20) gives the factor-once path's bits."""

@@ -16,7 +16,37 @@ namespace emcmc {
 #ifndef EMCMC_DIAG_BLOCK2
 #define EMCMC_DIAG_BLOCK2 256  // threads per block at ≤ 2 waves/SIMD (512: one table copy per CU)
 #endif
-constexpr int diag_block(int MINW) { return MINW >= 3 ? 256 * MINW : EMCMC_DIAG_BLOCK2; }
+// MINW = 2 with sibling pacing (below): one 512-thread block per CU, whose two
+// waves on each SIMD keep pace with each other
+#ifndef EMCMC_PACE
+#define EMCMC_PACE 1
+#endif
+constexpr int diag_block(int MINW) {
+    return MINW >= 3 ? 256 * MINW : (MINW == 2 && EMCMC_PACE) ? 512 : EMCMC_DIAG_BLOCK2;
+}
+
+// Sibling pacing.  Two waves share a SIMD at MINW = 2, and the SIMD issues for the
+// older one whenever it is ready (age order), so it runs ahead: on MI355X the older
+// wave of a pair finished its 100 steps at ≈ 0.78 of the pair's time and the younger
+// one ran the rest alone, at 0.21 steps/µs per SIMD instead of the pair's 0.33
+// (scripts/trace_diag.py, profiles/r4_pace/).  With both waves in one workgroup each
+// finds its sibling (the other wave on its SIMD, from HW_ID) and, at every step,
+// publishes its step count in LDS and lowers its issue priority when it is ahead of
+// the sibling, raises it when behind: the pair stays within a step of each other and
+// the SIMD keeps two waves' worth of overlap to the end.  No result depends on it.
+struct SiblingPace {
+    uint32_t *prog;  // [waves per block] steps done, in LDS
+    int me, sib;     // wave in block; sibling wave (−1: none)
+    __device__ __forceinline__ void publish(uint32_t steps_done) const {
+        if ((threadIdx.x & 63) == 0) __hip_atomic_store(prog + me, steps_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (sib < 0) return;
+        const uint32_t o = __hip_atomic_load(prog + sib, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t other = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
+        if (steps_done > other) __builtin_amdgcn_s_setprio(0);
+        else if (steps_done < other) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(1);
+    }
+};
 
 // Timing-only build (make trace → lib/libemcmc_trace.so, scripts/trace_diag.py):
 // every wave of rwm_gsn_diag_kernel records the 100 MHz real-time counter at its
@@ -33,12 +63,17 @@ __device__ __forceinline__ void trace_mark(uint32_t wave, int idx) {
     if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kTraceWaves && idx < kTraceSlots)
         emcmc_trace_buf[(size_t)wave * kTraceSlots + idx] = t;  // one lane: a vector store under exec
 }
+// where the wave runs: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID, in slots 124 / 125
+__device__ __forceinline__ void trace_where(uint32_t wave) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kTraceWaves) {
+        emcmc_trace_buf[(size_t)wave * kTraceSlots + 124] = hw;
+        emcmc_trace_buf[(size_t)wave * kTraceSlots + 125] = xcc;
+    }
+}
 #define EMCMC_TRACE_MARK(w, i) trace_mark((w), (i))
 #else
 #define EMCMC_TRACE_MARK(w, i) ((void)0)
-#endif
-#ifndef EMCMC_TILED_HIST
-#define EMCMC_TILED_HIST 0
 #endif
 #ifndef EMCMC_EARLY_STATE
 #define EMCMC_EARLY_STATE 0  // 1: the carried state's loads are issued before the table staging
@@ -56,9 +91,19 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 4 * D;
+    constexpr bool kPace = MINW == 2 && EMCMC_PACE;
+    constexpr int kWavesPerBlock = diag_block(MINW) / 64;
+    __shared__ uint32_t pace_prog[kWavesPerBlock], pace_simd[kWavesPerBlock];
+    if constexpr (kPace) {
+        if ((threadIdx.x & 63) == 0) {
+            pace_simd[threadIdx.x >> 6] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;  // HW_ID.simd_id
+            pace_prog[threadIdx.x >> 6] = 0u;
+        }
+    }  // (stage_lds's barrier orders these before the sibling search)
 #if EMCMC_TRACE
     const uint32_t twave = (uint32_t)((xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x) >> 6);
     EMCMC_TRACE_MARK(twave, 0);
+    trace_where(twave);
 #endif
 #if !EMCMC_EARLY_STATE
     const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
@@ -76,20 +121,17 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
 #endif
     const int sub = (int)(tid % LPC);
 #if !EMCMC_EARLY_STATE
-    if (chain >= a.C) return;
+    if (chain >= a.C) {
+        if (kPace && (threadIdx.x & 63) == 0) pace_prog[threadIdx.x >> 6] = ~0u;  // no steps to pace
+        return;
+    }
 #endif
     const int d0 = sub * DPL;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
 
     const uint64_t C = a.C;
     const SlotOffset<D> soff(C, chain, d0);
-#if EMCMC_TILED_HIST  // timing-only A/B: history slots in 32-chain tiles (readers not adapted)
-    SlotOffset<D> hoff = soff;
-    hoff.o = (uint32_t)(((((uint64_t)chain >> 5) * (D / 2) + (uint64_t)(d0 / 2)) * 32u + (chain & 31u)) * 16u);
-    hoff.stride = 512u;
-#else
     const SlotOffset<D> &hoff = soff;
-#endif
     const uint32_t c32 = (uint32_t)chain;  // C < 2^32 (emcmc_create)
     double th[DPL];
     load_slot<D>(a.theta, soff, th);
@@ -108,6 +150,12 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
                               (threadIdx.x >> 6) * (size_t)WaveScratch<DPL>::kBytes);
     const uint32_t wave_gid0 = a.chain0 + (uint32_t)((tid & ~(uint64_t)63) / LPC);
     if constexpr (kBatched) ws.fl[__lane_id()] = 0;
+    SiblingPace pace{pace_prog, (int)(threadIdx.x >> 6), -1};
+    if constexpr (kPace) {
+        const int nw = (int)(blockDim.x >> 6);
+        for (int w = 0; w < nw; ++w)
+            if (w != pace.me && pace.sib < 0 && pace_simd[w] == pace_simd[pace.me]) pace.sib = w;
+    }
     AcceptStream accs;
 #if EMCMC_VKEYS
     const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
@@ -222,7 +270,12 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         }
         // ---- update_stats! rolling acceptance (chain_statistics.jl:53-65)
         ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
+        if constexpr (kPace) pace.publish(s + 1);
         EMCMC_TRACE_MARK(twave, 3 + (int)s);
+    }
+    if constexpr (kPace) {
+        pace.publish(~0u);  // done: the sibling, alone now, stops lowering itself
+        __builtin_amdgcn_s_setprio(0);
     }
 
     if constexpr (kBatched) {

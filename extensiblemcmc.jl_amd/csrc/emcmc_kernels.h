@@ -82,12 +82,27 @@ struct StepParams {
 constexpr int LL_PER_OBS = 0;
 constexpr int LL_SUFFSTAT = 1;
 
-// HBM layout of θ state and θ/θ° histories (per history slot): pair-interleaved
-// SoA, element (d, c) at ((d/2)·C + c)·2 + d%2 when D is even, so lane c stores
-// the Box–Muller pair (2j, 2j+1) as one 16-byte word and a wave's store covers
-// contiguous 1 KiB (LPC = 1) or 4 × 256 B (LPC = 4).  Odd D: plain SoA d·C + c.
+// HBM layout of θ state and θ/θ° histories (per history slot), and of every
+// per-chain vector kept "in state_pos layout": tiled, pair-interleaved SoA.
+// The chains are cut into tiles of T = 32 (when C is a multiple of 32; else one
+// tile of all C chains).  A tile holds its chains' R "rows" one after another
+// (R = D/2 pairs (2j, 2j+1) as 16-byte words when D is even, R = D single
+// doubles when odd), each row T consecutive chains: row k of chain c is word
+// c0·R + k·T + (c − c0), c0 = c's tile start.  A wave of 32 chains (LPC = 2)
+// then writes one contiguous 8 KiB run per history and step (its tile), which
+// HBM takes at +3% over the untiled layout (T = C, where one wave's words lay
+// 16·C bytes apart; scripts/ubench/write_layout.hip, profiles/r4_store_ab/).
+__host__ __device__ __forceinline__ uint64_t soa_tile(uint64_t C) { return (C & 31u) == 0 ? 32u : C; }
+__host__ __device__ __forceinline__ uint64_t soa_tile0(uint64_t c, uint64_t C) {
+    return (C & 31u) == 0 ? (c & ~(uint64_t)31) : 0u;
+}
+// word index of row k of chain c, R rows per chain
+__host__ __device__ __forceinline__ uint64_t soa_row(uint64_t k, uint64_t c, uint64_t C, uint64_t R) {
+    const uint64_t c0 = soa_tile0(c, C);
+    return c0 * R + k * soa_tile(C) + (c - c0);
+}
 __host__ __device__ __forceinline__ uint64_t state_pos(uint64_t d, uint64_t c, uint64_t C, uint32_t D) {
-    return (D % 2 == 0) ? (((d >> 1) * C + c) << 1) + (d & 1) : d * C + c;
+    return (D % 2 == 0) ? (soa_row(d >> 1, c, C, D >> 1) << 1) + (d & 1) : soa_row(d, c, C, D);
 }
 
 typedef double d2v __attribute__((ext_vector_type(2)));
@@ -529,14 +544,14 @@ __device__ __forceinline__ void store_state(double *base, uint64_t C, uint64_t c
 #pragma unroll
         for (int j = 0; j < N / 2; ++j) {
             d2v x = {v[2 * j], v[2 * j + 1]};
-            d2v *p = reinterpret_cast<d2v *>(base) + ((uint64_t)(d0 / 2 + j) * C + c);
+            d2v *p = reinterpret_cast<d2v *>(base) + soa_row((uint64_t)(d0 / 2 + j), c, C, D / 2);
             if (nt) __builtin_nontemporal_store(x, p);
             else *p = x;
         }
     } else {
 #pragma unroll
         for (int i = 0; i < N; ++i) {
-            double *p = base + (uint64_t)(d0 + i) * C + c;
+            double *p = base + soa_row((uint64_t)(d0 + i), c, C, D);
             if (nt) __builtin_nontemporal_store(v[i], p);
             else *p = v[i];
         }
@@ -547,13 +562,13 @@ __device__ __forceinline__ void load_state(const double *base, uint64_t C, uint6
     if constexpr (D % 2 == 0) {
 #pragma unroll
         for (int j = 0; j < N / 2; ++j) {
-            const d2v x = reinterpret_cast<const d2v *>(base)[(uint64_t)(d0 / 2 + j) * C + c];
+            const d2v x = reinterpret_cast<const d2v *>(base)[soa_row((uint64_t)(d0 / 2 + j), c, C, D / 2)];
             v[2 * j] = x.x;
             v[2 * j + 1] = x.y;
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < N; ++i) v[i] = base[(uint64_t)(d0 + i) * C + c];
+        for (int i = 0; i < N; ++i) v[i] = base[soa_row((uint64_t)(d0 + i), c, C, D)];
     }
 }
 
@@ -564,14 +579,14 @@ __device__ __forceinline__ void load_state(const double *base, uint64_t C, uint6
 template <int D>
 struct SlotOffset {
     uint32_t o;       // lane's first word: pair d0/2 (even D) or coordinate d0 (odd D) of chain c
-    uint64_t stride;  // bytes between consecutive words of one chain (uniform)
+    uint64_t stride;  // bytes between consecutive words of one chain (uniform: the tile width)
     __device__ __forceinline__ SlotOffset(uint64_t C, uint64_t c, int d0) {
         if constexpr (D % 2 == 0) {
-            o = (uint32_t)((((uint64_t)(d0 / 2)) * C + c) * 16u);
-            stride = C * 16u;
+            o = (uint32_t)(soa_row((uint64_t)(d0 / 2), c, C, D / 2) * 16u);
+            stride = soa_tile(C) * 16u;
         } else {
-            o = (uint32_t)((((uint64_t)d0) * C + c) * 8u);
-            stride = C * 8u;
+            o = (uint32_t)(soa_row((uint64_t)d0, c, C, D) * 8u);
+            stride = soa_tile(C) * 8u;
         }
     }
 };
@@ -582,7 +597,11 @@ __device__ __forceinline__ void store_slot(double *slot_base, const SlotOffset<D
 #pragma unroll
         for (int j = 0; j < N / 2; ++j) {
             d2v x = {v[2 * j], v[2 * j + 1]};
+#if EMCMC_HIST_PLAIN  // timing-only A/B builds: plain instead of nontemporal history stores
+            *reinterpret_cast<d2v *>(b + (uint64_t)j * off.stride + off.o) = x;
+#else
             __builtin_nontemporal_store(x, reinterpret_cast<d2v *>(b + (uint64_t)j * off.stride + off.o));
+#endif
         }
     } else {
 #pragma unroll

@@ -89,13 +89,14 @@ struct SumSqAcc {
 // and stores use the global saddr form.
 struct LaneSoA {
     uint64_t stride;  // bytes between consecutive words of one chain (uniform)
-    uint32_t off;     // lane's byte offset within a word row
+    uint64_t off;     // lane's byte offset of its first word (tile start included)
 };
-// pair-interleaved layout (state_pos) of an n-element per-chain vector
+// tiled pair-interleaved layout (state_pos) of an n-element per-chain vector
 __device__ __forceinline__ LaneSoA lane_soa(uint64_t C, uint64_t chain, int n) {
-    uint64_t stride = (n % 2 == 0) ? C * 16u : C * 8u;
+    const uint64_t w = (n % 2 == 0) ? 16u : 8u;
+    uint64_t stride = soa_tile(C) * w;
     asm volatile("" : "+s"(stride));  // opaque: recomputed per step, never hoisted
-    return LaneSoA{stride, (uint32_t)((n % 2 == 0) ? chain * 16u : chain * 8u)};
+    return LaneSoA{stride, soa_row(0, chain, C, (uint64_t)((n % 2 == 0) ? n / 2 : n)) * w};
 }
 template <int NP>
 __device__ __forceinline__ double *soa_ptr(double *base, const LaneSoA &l, int q) {
@@ -664,7 +665,7 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
             const int e = (int)threadIdx.x + q * MT::BLOCK;
             const int k = e >> 6, l = e & 63;
             const uint64_t cc = (c0 + (uint64_t)l < C) ? c0 + (uint64_t)l : c0;
-            pf[q] = (e < PR * 64) ? __builtin_nontemporal_load(src + (uint64_t)k * C + cc) : rowv{};
+            pf[q] = (e < PR * 64) ? __builtin_nontemporal_load(src + soa_row((uint64_t)k, cc, C, (uint64_t)PR)) : rowv{};
         }
     };
     auto put = [&](double *st, const rowv (&pf)[NPF]) {

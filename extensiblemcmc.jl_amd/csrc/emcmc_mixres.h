@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
     const double iLBa = a.iLB[(uint64_t)fa * C + chain], iLBb = a.iLB[(uint64_t)fb * C + chain];
     const double c0B = a.c0B[chain];
 
-    const uint64_t po = ((uint64_t)r * C + chain) * 16u;  // the lane's pair word in a slot (64-bit: any C)
+    const uint64_t po = soa_row((uint64_t)r, chain, C, D / 2) * 16u;  // the lane's pair word in a slot (state_pos)
     double th0, th1;  // θ at coordinates 2r, 2r+1
     {
         const d2v t = *reinterpret_cast<const d2v *>(reinterpret_cast<const char *>(a.theta) + po);

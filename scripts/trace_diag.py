@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--settle-ms", type=float, default=150.0)
     ap.add_argument("--variant", type=int, default=0, help="kernel_variant (128: uncapped registers)")
+    ap.add_argument("--dump", default="", help="save the raw per-wave stamps to <dump>_rep<k>.npz")
     a = ap.parse_args()
     assert a.steps + 5 <= SLOTS
     lib = L.lib()
@@ -105,6 +106,28 @@ def main():
             "end_p10_p50_p90_us": [float(np.percentile(drained, q)) for q in (10, 50, 90)],
             "event_minus_trace_us": ms * 1e3 - float(drained.max()),
         }
+        # where the spread of end times comes from: per XCD (XCC_ID) and per SIMD slot
+        hw = buf[:nw, 124].astype(np.int64)
+        xcc = buf[:nw, 125].astype(np.int64) & 0xF
+        cu = (hw >> 8) & 0xF
+        se = (hw >> 13) & 0x7
+        simd = (hw >> 4) & 0x3
+        r["end_p50_by_xcc_us"] = [round(float(np.median(drained[xcc == x])), 1) for x in range(8)]
+        r["end_max_by_xcc_us"] = [round(float(drained[xcc == x].max()), 1) if (xcc == x).any() else None
+                                  for x in range(8)]
+        slot = (xcc * 8 + se) * 16 * 4 + cu * 4 + simd  # one id per SIMD
+        u, cnt = np.unique(slot, return_counts=True)
+        r["waves_per_simd_hist"] = {int(k): int(v) for k, v in zip(*np.unique(cnt, return_counts=True))}
+        r["cus_used"] = int(len(np.unique((xcc * 8 + se) * 16 + cu)))
+        # end-time spread within one SIMD's waves vs across SIMDs
+        per = {}
+        for sid, d in zip(slot, drained):
+            per.setdefault(int(sid), []).append(float(d))
+        simd_end = np.array([max(v) for v in per.values()])
+        r["simd_end_p10_p50_p90_max_us"] = [round(float(np.percentile(simd_end, q)), 1) for q in (10, 50, 90, 100)]
+        if a.dump:
+            np.savez_compressed(f"{a.dump}_rep{rep}.npz", t=buf[:nw, :3 + a.steps], end=buf[:nw, SLOTS - 2:],
+                                hw=hw, xcc=xcc)
         out.append(r)
         print(json.dumps(r), flush=True)
     eng.close()

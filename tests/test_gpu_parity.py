@@ -204,6 +204,21 @@ def test_scalar_obs_variant_bitwise(oracle, ll_mode, unit):
         assert_bitwise(e, o)
 
 
+@pytest.mark.parametrize("D,lpc", [(32, 2), (16, 1), (64, 4)])
+@pytest.mark.parametrize("variant", [0, L.VARIANT_UNCAPPED])
+def test_register_cap_variants_bitwise(oracle, D, lpc, variant):
+    """The diag kernel at D = 16 / 32 / 64 is built twice: capped at 256 registers
+    (MINW = 2, 512-thread blocks whose sibling waves pace each other — the default)
+    and uncapped (EMCMC_VARIANT_UNCAPPED, one wave per SIMD).  Same bits as the
+    oracle either way, with 1000 chains (a partial last block) and launch splits."""
+    w = W.cfg2(1000, D=D)
+    o = run_oracle(oracle, w, 1000, 60)
+    for spl in (0, 23):
+        e = run_engine(w, 1000, 60, lpc=lpc, spl=spl, variant=variant)
+        assert ("MINW=2" in e["kernel"]) == (variant == 0), e["kernel"]
+        assert_bitwise(e, o)
+
+
 def test_many_observations_beyond_lds(oracle):
     """Per-observation likelihood with more observations than the LDS holds
     (600 × 32 doubles = 150 KiB next to the 70 KiB ziggurat): the fused path

@@ -122,9 +122,11 @@ typedef enum emcmc_status {
 
 /* History selectors for emcmc_get_history / emcmc_history_device_ptr.
  * Host copies (emcmc_get_history*) use the layouts below.  In HBM the STATE and
- * PROPOSAL histories are pair-interleaved SoA per slot: element (d, c) of slot
- * s at s·D·C + ((d/2)·C + c)·2 + d%2 for even D (s·D·C + d·C + c for odd D),
- * which is what emcmc_history_device_ptr exposes. */
+ * PROPOSAL histories are tiled pair-interleaved SoA per slot, which is what
+ * emcmc_history_device_ptr exposes: with T = 32 when C is a multiple of 32 (else
+ * T = C, one tile), c0 = c − c mod T, element (d, c) of slot s is at
+ *   s·D·C + c0·D + ((d/2)·T + (c − c0))·2 + d%2   (even D)
+ *   s·D·C + c0·D + d·T + (c − c0)                 (odd D). */
 #define EMCMC_H_STATE 0u     /* state_history[iter][pidx]          : double [M][P][C][D] */
 #define EMCMC_H_PROPOSAL 1u  /* state_proposal_history[iter][pidx] : double [M][P][C][D] */
 #define EMCMC_H_LL 2u        /* local_wss[pidx].sub_ws.ll_history  : double [M][P][C]    */

@@ -92,9 +92,14 @@ constexpr int LL_SUFFSTAT = 1;
 // then writes one contiguous 8 KiB run per history and step (its tile), which
 // HBM takes at +3% over the untiled layout (T = C, where one wave's words lay
 // 16·C bytes apart; scripts/ubench/write_layout.hip, profiles/r4_store_ab/).
-__host__ __device__ __forceinline__ uint64_t soa_tile(uint64_t C) { return (C & 31u) == 0 ? 32u : C; }
+#ifndef EMCMC_SOA_TILE
+#define EMCMC_SOA_TILE 32  // chains per tile (a power of two); 0: the untiled round-3 layout (A/B builds)
+#endif
+__host__ __device__ __forceinline__ uint64_t soa_tile(uint64_t C) {
+    return (EMCMC_SOA_TILE && (C & (uint64_t)(EMCMC_SOA_TILE - 1)) == 0) ? (uint64_t)EMCMC_SOA_TILE : C;
+}
 __host__ __device__ __forceinline__ uint64_t soa_tile0(uint64_t c, uint64_t C) {
-    return (C & 31u) == 0 ? (c & ~(uint64_t)31) : 0u;
+    return (EMCMC_SOA_TILE && (C & (uint64_t)(EMCMC_SOA_TILE - 1)) == 0) ? (c & ~(uint64_t)(EMCMC_SOA_TILE - 1)) : 0u;
 }
 // word index of row k of chain c, R rows per chain
 __host__ __device__ __forceinline__ uint64_t soa_row(uint64_t k, uint64_t c, uint64_t C, uint64_t R) {

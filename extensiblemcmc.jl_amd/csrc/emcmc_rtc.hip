@@ -9,6 +9,12 @@
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+// the library's state_pos tile width (emcmc_kernels.h): run-time kernels must lay out
+// HBM as the ahead-of-time ones do, so it is passed to every compile (and digest)
+#ifndef EMCMC_SOA_TILE
+#define EMCMC_SOA_TILE 32
+#endif
+
 #include <dlfcn.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -211,6 +217,7 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
         d.add(std::string(file));
         d.add(ex);
         for (const auto &w : extra) d.add(w);
+        d.add("-DEMCMC_SOA_TILE=" + std::to_string(EMCMC_SOA_TILE));
         d.add("gfx950|-O3|-ffp-contract=off|-std=c++17|hiprtc " + std::to_string(vmaj) + "." + std::to_string(vmin) +
               "|HIP " + std::to_string(HIP_VERSION));
         dfile = dir + "/" + d.hex() + ".co";
@@ -232,7 +239,8 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
         HIPRTC_SUCCESS)
         return "hiprtcCreateProgram failed";
     hiprtcAddNameExpression(prog, ex.c_str());
-    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17"};
+    std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
+                                  "-DEMCMC_SOA_TILE=" + std::to_string(EMCMC_SOA_TILE)};
     o.insert(o.end(), extra.begin(), extra.end());
     std::vector<const char *> ov;
     for (const auto &w : o) ov.push_back(w.c_str());

@@ -513,6 +513,10 @@ __global__ void __launch_bounds__(64) moments_consts_kernel(uint64_t N0, uint32_
 
 #endif  // EMCMC_HOST_UNIT
 
+#ifndef EMCMC_MOMENTS_DIRECT
+#define EMCMC_MOMENTS_DIRECT 0
+#endif
+
 template <int D>
 struct MomentTiles {
     static constexpr int TB = D <= 8 ? D : 8;                 // block edge
@@ -682,6 +686,25 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
     MomentUnitState<D, UB> ub;
     ua.load(a, cl);
     if constexpr (TWO) ub.load(a, cl);
+#if EMCMC_MOMENTS_DIRECT
+    // every wave reads the θ coordinates of its own units straight from the history
+    // (L2-resident after the block's first reader): no block staging and no barrier,
+    // so the two waves of a SIMD overlap the whole launch instead of meeting at a
+    // barrier every step (the older one would otherwise wait there while the younger
+    // finishes alone)
+    (void)fetch;
+    (void)put;
+    (void)stage0;
+    (void)stage1;
+    for (uint32_t s = 0; s < a.nsteps; ++s) {
+        const double *th_s = a.theta + (uint64_t)s * D * C;
+        auto theta_at = [&](int d) -> double { return th_s[state_pos((uint64_t)d, cl, C, (uint32_t)D)]; };
+        const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
+        const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
+        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
+        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr);
+    }
+#else
     {
         rowv pf[NPF];
         fetch(0, pf);
@@ -704,6 +727,7 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
         if (s + 1 < a.nsteps) put((s & 1u) ? stage0 : stage1, pf);
         __syncthreads();
     }
+#endif
     if (!live) return;
     ua.store(a, chain);
     if constexpr (TWO) ub.store(a, chain);

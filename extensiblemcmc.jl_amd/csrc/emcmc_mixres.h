@@ -67,6 +67,24 @@ __device__ __forceinline__ uint32_t rbcast_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + L, 0xF, 0xF, true);
 }
 
+#ifndef EMCMC_MIXRES_DPPFMA
+#define EMCMC_MIXRES_DPPFMA 0
+#endif
+// acc = fma(v from lane L of the 16-lane row, m, acc) as ONE v_fmac_f64_dpp
+// (row_newbcast): the broadcast rides on the fma's first source instead of a
+// separate v_mov_b64_dpp (VOP3 fma has no DPP form; VOP2 fmac does).  NOP1: two wait
+// states first, for a v written by the instruction just before (VALU write → DPP
+// read); the callers pass it on the first read of each source.  fma is commutative
+// in its products, so the bits are those of fma(m, bcast(v), acc).
+template <int L, bool NOP1 = false>
+__device__ __forceinline__ void fmac_bcast(double &acc, double v, double m) {
+    if constexpr (NOP1)
+        asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+            : "+v"(acc) : "v"(v), "v"(m), "n"(L));
+    else
+        asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf" : "+v"(acc) : "v"(v), "v"(m), "n"(L));
+}
+
 // Σ y² over the chain's D = 32 coordinates in the canonical order (SumShape<32>:
 // blocks of 8 as s = y0·y0, s = fma(y, y, s), then ((b0 + b1) + (b2 + b3))),
 // lane r of the row holding coordinates 2r (y0) and 2r+1 (y1): block k is quad k
@@ -195,6 +213,18 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
         double lza = 0.0, lzb = 0.0;  // folded rows fa, fb of L_B z
         static_for<0, D>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
+#if EMCMC_MIXRES_DPPFMA
+            if constexpr (j == 0) {
+                const double zj = rbcast<0>(z0);
+                lza = La[0] * zj;
+                lzb = Lb[0] * zj;
+            } else {
+                // z0 / z1 were written long before the sweep; the first read of each
+                // still waits its two states in case a copy was scheduled right before
+                if constexpr (j < H) fmac_bcast<j / 2, j == 1 || j == 2>(lza, (j & 1) ? z1 : z0, La[j]);
+                fmac_bcast<j / 2, (j == 1 || j == 2) && j >= H>(lzb, (j & 1) ? z1 : z0, Lb[j]);
+            }
+#else
             const double zj = rbcast<j / 2>((j & 1) ? z1 : z0);
             if constexpr (j == 0) {
                 lza = La[0] * zj;
@@ -203,6 +233,7 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
                 if constexpr (j < H) lza = fma(La[j], zj, lza);
                 lzb = fma(Lb[j], zj, lzb);
             }
+#endif
         });
         if (__ballot(useB && (lza == 0.0 || lzb == 0.0)) != 0) {
             // an exact zero may carry the wrong sign after the padding columns: redo with masks
@@ -304,10 +335,19 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
                 // IEEE addition (x + (−0) = x for every x, ±0 and NaN included): the fold is
                 // 16 unconditional adds in k order instead of 16 scalar compare-and-branch
                 const double f = (k < nobs) ? fma(-0.5, tree_inplace(b), a.t_c0) : -0.0;
+#if EMCMC_MIXRES_DPPFMA
+                // llp + f_q as fma(f_q, 1, llp): f_q·1 is exact, so one rounding of the sum
+                const double one = 1.0;
+                static_for<0, kResLanes>([&](auto rc) {
+                    constexpr int q = decltype(rc)::value;
+                    fmac_bcast<q, q == 0>(llp, f, one);
+                });
+#else
                 static_for<0, kResLanes>([&](auto rc) {
                     constexpr int q = decltype(rc)::value;
                     llp = llp + rbcast<q>(f);
                 });
+#endif
             }
         } else {
             double y0 = xb0 - thp0, y1 = xb1 - thp1;

@@ -19,3 +19,4 @@ for L in libemcmc libemcmc_mboth; do
   EMCMC_LIB=$PWD/extensiblemcmc.jl_amd/lib/$L.so timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace/$L -o run -- python3 bench.py --workload cfg4 --no-cpu --no-parity > $OUT/trace/$L.json 2> $OUT/trace/$L.err || { echo "trace rc=$?"; exit 1; }
   find $OUT/trace/$L -name '*kernel_stats.csv' -exec head -4 {} \;
 done
+bash scripts/gpu_r4_s12.sh

@@ -68,7 +68,7 @@ __device__ __forceinline__ uint32_t rbcast_u32(uint32_t v) {
 }
 
 #ifndef EMCMC_MIXRES_DPPFMA
-#define EMCMC_MIXRES_DPPFMA 0
+#define EMCMC_MIXRES_DPPFMA 1
 #endif
 // acc = fma(v from lane L of the 16-lane row, m, acc) as ONE v_fmac_f64_dpp
 // (row_newbcast): the broadcast rides on the fma's first source instead of a

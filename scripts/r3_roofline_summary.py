@@ -41,7 +41,9 @@ def timed_slice(b, n_dispatch):
     nw = math.ceil(b["warmup"] / spl) if b["warmup"] else 0
     nw += (b["config"].get("clock_settle") or {}).get("launches", 0)
     per = b["roofline"]["launches"]
-    return nw, min(n_dispatch, nw + b["reps"] * per)
+    # round 4: each value rep is followed by a kernel-timing rep (bench.py kernel_timing_reps)
+    reps = b["reps"] + ((b.get("kernel_timing_reps") or {}).get("n") or 0)
+    return nw, min(n_dispatch, nw + reps * per)
 
 
 res = {}

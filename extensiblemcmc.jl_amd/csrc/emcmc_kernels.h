@@ -847,8 +847,12 @@ __device__ __forceinline__ void store_slot_late(double *slot_base, const SlotOff
     }
 }
 
+#ifndef EMCMC_CHOL_SHARED
+#define EMCMC_CHOL_SHARED 52  // D from which ltd and the likelihood share one sweep (0: never; A/B via EMCMC_RTC_EXTRA)
+#endif
 template <int D, bool FULL, int LLMODE>
 __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
+    constexpr bool kCholShared = EMCMC_CHOL_SHARED > 0 && D >= EMCMC_CHOL_SHARED;
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     constexpr int P = D * (D + 1) / 2;
 
@@ -882,6 +886,39 @@ __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
         }
         // ---- log_transition_density both ways (random_walk.jl:161-171): one evaluation
         double ltd;
+        double llp;
+        if constexpr (kCholShared) {
+        // One copy of the substitution sweep serves log_transition_density (k = −1:
+        // ‖L_rw⁻¹(θ° − θ)‖²) and compute_ll! (k ≥ 0: ‖L_t⁻¹(x_k − θ°)‖² per observation, or
+        // the x̄ term once): the sweep is the kernel's largest code, and with three unrolled
+        // copies (propose, ltd, ll) the kernel outgrew the instruction cache at D ≥ 48
+        // (66 KB of code at D = 48, 105 KB at D = 64).  Same operations, same order.
+        ltd = 0.0;
+        llp = 0.0;
+        {
+            const int kn = (LLMODE == LL_PER_OBS) ? (int)nobs : 1;
+            for (int k = -1; k < kn; ++k) {
+                cdouble *c = opaque_cptr(a.consts);
+                double acc[D];
+                if (k < 0) {
+#pragma unroll
+                    for (int i = 0; i < D; ++i) acc[i] = thp[i] - th[i];
+                } else {
+                    cdouble *x = (LLMODE == LL_PER_OBS) ? c + 3 * P + D + (size_t)k * D : c + 3 * P;
+#pragma unroll
+                    for (int i = 0; i < D; ++i) {
+                        acc[i] = x[i] - thp[i];
+                        vpin(acc[i]);
+                    }
+                }
+                cdouble *T = (k < 0) ? c + P : c + 2 * P;
+                const double q = chol_sqmahal<D, 0>(T, T, thp, acc);
+                if (k < 0) ltd = fma(-0.5, q, a.rw_c0);  // = c0 − q/2 (q/2 exact)
+                else if constexpr (LLMODE == LL_PER_OBS) llp = llp + fma(-0.5, q, a.t_c0);
+                else llp = a.n_tc0 - (a.S_c + a.nobs_d * q) * 0.5;
+            }
+        }
+        } else {
         {
             double acc[D];
 #pragma unroll
@@ -889,7 +926,6 @@ __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
             ltd = fma(-0.5, chol_sqmahal<D, 0>(cst, cst + P, thp, acc), a.rw_c0);
         }
         // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
-        double llp;
         if constexpr (LLMODE == LL_PER_OBS) {
             llp = 0.0;
             for (uint32_t k = 0; k < nobs; ++k) {
@@ -902,6 +938,7 @@ __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
             double acc[D];
             const double qv = chol_sqmahal<D, D>(c + 3 * P, c + 2 * P, thp, acc);
             llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
+        }
         }
         if (!(llp - llp == 0.0)) faults |= 1u;
         // ---- accept_reject! (run.jl:271-278), left-associative as written

@@ -189,6 +189,21 @@ void disk_put(const std::string &dir, const std::string &file, const RtcKernel &
     if (rename(tmp.c_str(), file.c_str()) != 0) (void)unlink(tmp.c_str());  // atomic: ranks may race
 }
 
+// EMCMC_RTC_EXTRA: extra options for every run-time compile (A/B builds of the run-time
+// kernels, e.g. "-DEMCMC_CHOL_SHARED=0"); part of the disk-cache digest and of the
+// process-cache key (rtc_env_extra is read once per process).
+const std::vector<std::string> &rtc_env_extra() {
+    static const std::vector<std::string> v = [] {
+        std::vector<std::string> out;
+        if (const char *e = getenv("EMCMC_RTC_EXTRA")) {
+            std::istringstream is(e);
+            for (std::string w; is >> w;) out.push_back(w);
+        }
+        return out;
+    }();
+    return v;
+}
+
 // Compile prog_src for gfx950 and fetch the code object of the kernel named by
 // the expression ex; cache it under key.  Returns "" or the compiler's log.
 // -ffp-contract=off: the parity contract with oracle/ (no implicit fma).
@@ -218,6 +233,7 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
         d.add(ex);
         for (const auto &w : extra) d.add(w);
         d.add("-DEMCMC_SOA_TILE=" + std::to_string(EMCMC_SOA_TILE));
+        for (const auto &w : rtc_env_extra()) d.add(w);
         d.add("gfx950|-O3|-ffp-contract=off|-std=c++17|hiprtc " + std::to_string(vmaj) + "." + std::to_string(vmin) +
               "|HIP " + std::to_string(HIP_VERSION));
         dfile = dir + "/" + d.hex() + ".co";
@@ -241,6 +257,7 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
     hiprtcAddNameExpression(prog, ex.c_str());
     std::vector<std::string> o = {"--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-std=c++17",
                                   "-DEMCMC_SOA_TILE=" + std::to_string(EMCMC_SOA_TILE)};
+    for (const auto &w : rtc_env_extra()) o.push_back(w);
     o.insert(o.end(), extra.begin(), extra.end());
     std::vector<const char *> ov;
     for (const auto &w : o) ov.push_back(w.c_str());

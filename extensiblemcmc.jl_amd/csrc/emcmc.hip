@@ -190,6 +190,7 @@ struct emcmc_handle {
     uint64_t row_bytes = 0;
     // general schedule path (mwg_gsn_kernel)
     double *d_mu_p = nullptr, *d_eps = nullptr, *d_tL = nullptr, *d_tiL = nullptr, *d_xbar = nullptr;
+    double *d_gcache = nullptr;  // MALA: ∇ℓ(θ) carried between the steps of a launch (emcmc_mwg.h mala_carry)
     uint32_t *d_aprop = nullptr, *d_aacc = nullptr, *d_steps = nullptr;
     MwgUpdate *d_mwg = nullptr;
     // user target (EMCMC_TARGET_USER): the loaded code object and the law's constants
@@ -1385,6 +1386,10 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.scov = h->d_scov;
     a.chain_moments = h->cfg.chain_moments ? 1u : 0u;
     a.nhaario = h->nhaario;
+    if (P == 1 && h->updates[0].kernel == EMCMC_MALA) {  // one MALA update: carry ∇ℓ(θ) between steps
+        if (!h->d_gcache) HIPCHK(h, hipMalloc(&h->d_gcache, C * (uint64_t)h->cfg.dim * sizeof(double)));
+        a.gcache = h->d_gcache;
+    }
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
     const uint64_t K = h->cfg.steps_per_launch;
     size_t ci = 0;  // next λ cut
@@ -2123,7 +2128,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
                     h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts,
-                    h->d_ll_prop,   h->d_uparams};
+                    h->d_ll_prop,   h->d_uparams,   h->d_gcache};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->umod) (void)hipModuleUnload(h->umod);

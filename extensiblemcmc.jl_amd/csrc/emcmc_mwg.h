@@ -135,6 +135,7 @@ struct MwgParams {
     const double *obs;         // [nobs][D]
     double *mixpool;           // GaussianRandomWalkMix / Haario per-chain state (MwgUpdate offsets)
     double *smean, *scov;      // GenericChainStats mean [D][C] and cov packed lower [D(D+1)/2][C]
+    double *gcache;            // [D][C] ∇ℓ at the current θ (state_pos layout), or null: the MALA carry below
     uint64_t C;
     uint64_t row_bytes;
     uint64_t N0;
@@ -142,6 +143,18 @@ struct MwgParams {
     uint32_t chain_moments, nhaario;  // update_stats! mean/cov on; number of Haario updates
     double t_c0, n_tc0, S_c, nobs_d;
 };
+
+// MALA gradient carry.  The reference calls compute_gradients_and_momenta! twice per
+// step: at P°.θ with coords ← θ (__PREVIOUS) and at P°.θ after set_parameters! (the
+// proposal, __PROPOSAL; run.jl:110, 259).  With ONE update over all D coordinates the
+// first point is θ itself, which is the previous step's proposal point when it was
+// accepted and the previous step's first point when it was rejected: the same doubles,
+// so the same gradient bits.  Within a launch the kernel therefore keeps ∇ℓ(θ) per chain
+// in gcache and evaluates the gradient once per step (the first step of a launch
+// computes it).  Anything else (P > 1, a partial update) evaluates both.
+__device__ __forceinline__ bool mala_carry(const MwgParams &a, uint32_t n, uint32_t D) {
+    return a.gcache != nullptr && a.P == 1u && n == D;
+}
 
 // log of any real: NaN below 0 (Julia's log throws DomainError there), −Inf at 0
 __device__ __forceinline__ double log_real(double x) { return (x < 0.0) ? __builtin_nan("") : log_any(x); }
@@ -1003,17 +1016,25 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         if constexpr (UPD::kMala) {
             if (mala) {  // compute_gradients_and_momenta!(__PREVIOUS) at P°.θ with coords ← θ
                 double x[D], g[D], gl[D];
+                if (mala_carry(a, n, (uint32_t)D) && s > 0) {  // ∇ℓ(θ) from the previous step
 #pragma unroll
-                for (int d = 0; d < D; ++d) x[d] = mp[d];
+                    for (int d = 0; d < D; ++d) g[d] = a.gcache[state_pos(d, chain, C, D)];
+                } else {
 #pragma unroll
-                for (int j = 0; j < D; ++j) {
-                    if ((uint32_t)j < n) {
-                        const uint32_t cj = u.coords[j];
+                    for (int d = 0; d < D; ++d) x[d] = mp[d];
 #pragma unroll
-                        for (int d = 0; d < D; ++d) x[d] = (cj == (uint32_t)d) ? tl[j] : x[d];
+                    for (int j = 0; j < D; ++j) {
+                        if ((uint32_t)j < n) {
+                            const uint32_t cj = u.coords[j];
+#pragma unroll
+                            for (int d = 0; d < D; ++d) x[d] = (cj == (uint32_t)d) ? tl[j] : x[d];
+                        }
                     }
+                    TGT::template grad<D, LLMODE>(a, x, g);
+                    if (mala_carry(a, n, (uint32_t)D))
+#pragma unroll
+                        for (int d = 0; d < D; ++d) a.gcache[state_pos(d, chain, C, D)] = g[d];
                 }
-                TGT::template grad<D, LLMODE>(a, x, g);
                 mwg_gather<D, D, false>(u, n, g, gl);
                 mwg_mala_forward<D, false>(a, zt, u, n, gid, iter, p, tl, gl, tp, ltd_fwd, faults);
 #pragma unroll
@@ -1050,11 +1071,12 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
         }
         // ---- compute_ll!: loglikelihood(P°, obs)
         const double llp = TGT::template loglik<D, LLMODE>(a, mp);
+        double gprop[UPD::kMala ? D : 1];  // ∇ℓ at the proposal: the next step's ∇ℓ(θ) if accepted
         if constexpr (UPD::kMala) {
             if (mala) {  // compute_gradients_and_momenta!(__PROPOSAL) at P°.θ
-                double g[D], gp[D];
-                TGT::template grad<D, LLMODE>(a, mp, g);
-                mwg_gather<D, D, false>(u, n, g, gp);
+                double gp[D];
+                TGT::template grad<D, LLMODE>(a, mp, gprop);
+                mwg_gather<D, D, false>(u, n, gprop, gp);
                 ltd_rev = mwg_mala_reverse<D, false>(u, n, tl, tp, gp);
             }
         }
@@ -1073,6 +1095,10 @@ __global__ void __launch_bounds__(256) mwg_gsn_kernel(const MwgParams a) {
 #pragma unroll
             for (int d = 0; d < D; ++d) th[d] = nst[d];
             ll = llp;
+            if constexpr (UPD::kMala)
+                if (mala && mala_carry(a, n, (uint32_t)D))
+#pragma unroll
+                    for (int d = 0; d < D; ++d) a.gcache[state_pos(d, chain, C, D)] = gprop[d];
         }
         if constexpr (FULL) {
 #pragma unroll
@@ -1142,9 +1168,17 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
                 for (int j = 0; j < NU; ++j)
                     if ((uint32_t)j < n) a.mu_p[state_pos(u.coords[j], chain, C, D)] = tl[j];
                 double x[D], g[D], gl[NU];
+                if (mala_carry(a, n, (uint32_t)D) && s > 0) {  // ∇ℓ(θ) from the previous step
 #pragma unroll
-                for (int d = 0; d < D; ++d) x[d] = a.mu_p[state_pos(d, chain, C, D)];
-                TGT::template grad<D, LLMODE, RT>(a, x, g);
+                    for (int d = 0; d < D; ++d) g[d] = a.gcache[state_pos(d, chain, C, D)];
+                } else {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) x[d] = a.mu_p[state_pos(d, chain, C, D)];
+                    TGT::template grad<D, LLMODE, RT>(a, x, g);
+                    if (mala_carry(a, n, (uint32_t)D))
+#pragma unroll
+                        for (int d = 0; d < D; ++d) a.gcache[state_pos(d, chain, C, D)] = g[d];
+                }
                 mwg_gather<D, NU, RU>(u, n, g, gl);
                 mwg_mala_forward<NU, RU>(a, zt, u, n, gid, iter, p, tl, gl, tp, ltd_fwd, faults);
                 for (int j = 0; j < NU; ++j) ta[j] = tp[j];
@@ -1168,11 +1202,12 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
         for (int d = 0; d < D; ++d) mp[d] = a.mu_p[state_pos(d, chain, C, D)];
         // ---- compute_ll!
         const double llp = TGT::template loglik<D, LLMODE, RT>(a, mp);
+        double gprop[UPD::kMala ? D : 1];  // ∇ℓ at the proposal: the next step's ∇ℓ(θ) if accepted
         if constexpr (UPD::kMala) {
             if (mala) {  // compute_gradients_and_momenta!(__PROPOSAL) at P°.θ
-                double g[D], gp[NU];
-                TGT::template grad<D, LLMODE, RT>(a, mp, g);
-                mwg_gather<D, NU, RU>(u, n, g, gp);
+                double gp[NU];
+                TGT::template grad<D, LLMODE, RT>(a, mp, gprop);
+                mwg_gather<D, NU, RU>(u, n, gprop, gp);
                 ltd_rev = mwg_mala_reverse<NU, RU>(u, n, tl, tp, gp);
             }
         }
@@ -1193,6 +1228,10 @@ __global__ void __launch_bounds__(256) mwg_wide_kernel(const MwgParams a) {
             for (int j = 0; j < NU; ++j)
                 if ((uint32_t)j < n) a.theta[state_pos(u.coords[j], chain, C, D)] = ta[j];
             ll = llp;
+            if constexpr (UPD::kMala)
+                if (mala && mala_carry(a, n, (uint32_t)D))
+#pragma unroll
+                    for (int d = 0; d < D; ++d) a.gcache[state_pos(d, chain, C, D)] = gprop[d];
         }
         if constexpr (FULL) {
             double *ht = a.hist_theta + slot * D * C;

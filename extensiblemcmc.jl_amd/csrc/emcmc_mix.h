@@ -30,6 +30,7 @@
 #pragma once
 
 #include "emcmc_kernels.h"
+#include "emcmc_fused.h"  // SiblingPace
 
 namespace emcmc {
 
@@ -516,6 +517,9 @@ __global__ void __launch_bounds__(64) moments_consts_kernel(uint64_t N0, uint32_
 #ifndef EMCMC_MOMENTS_DIRECT
 #define EMCMC_MOMENTS_DIRECT 0
 #endif
+#ifndef EMCMC_MOMENTS_PACE
+#define EMCMC_MOMENTS_PACE 0
+#endif
 
 template <int D>
 struct MomentTiles {
@@ -579,9 +583,9 @@ struct MomentUnitState {
     // ROWS_NEW: the new row means of another unit of the same wave with the same
     // row block, already advanced this step (the same formula, so the same bits):
     // taken instead of recomputed; nullptr: advance them here
-    template <typename TH>
+    template <typename TH, typename TICK>
     __device__ __forceinline__ void step(TH theta_at, double Nd, double N1d, double ca, double cb, double cc, double rN,
-                                         double rN1, const double *rows_new = nullptr) {
+                                         double rN1, const double *rows_new, TICK &&tick) {
         double ti[TB], tj[NJ];
 #pragma unroll
         for (int u = 0; u < TB; ++u) ti[u] = theta_at(I0 + u);
@@ -592,6 +596,7 @@ struct MomentUnitState {
 #pragma unroll
         for (int u = 0; u < TB; ++u) {
             __builtin_amdgcn_sched_barrier(0);  // one row at a time: bounded live temporaries
+            tick(u);
 #pragma unroll
             for (int v = DIAG ? u : 0; v < NJ; ++v) {
                 const double old_sq = ca * c[UT::slot(u, v)] + mi[u] * (DIAG ? mi[v] : mj[v]);
@@ -612,6 +617,7 @@ struct MomentUnitState {
 #pragma unroll
         for (int u = 0; u < TB; ++u) {
             __builtin_amdgcn_sched_barrier(0);
+            tick(u);
 #pragma unroll
             for (int v = DIAG ? u : 0; v < NJ; ++v)
                 c[UT::slot(u, v)] = c[UT::slot(u, v)] - cc * (mi[u] * (DIAG ? mi[v] : mj[v]));
@@ -651,7 +657,8 @@ struct MomentPairs {
 // The whole launch sweep of wave W (units a(W) and b(W)); every wave runs the
 // same number of block barriers.
 template <int D, int W>
-__device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *stage0, double *stage1) {
+__device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *stage0, double *stage1,
+                                             uint32_t *pace_prog, const uint32_t *pace_simd) {
     using MT = MomentTiles<D>;
     constexpr int PR = MT::PR, EW = MT::EW, NPF = MT::NPF;
     constexpr bool TWO = MT::UPW == 2;
@@ -680,6 +687,22 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
             if (e < PR * 64) dst[e] = pf[q];
         }
     };
+    // Sibling pacing (EMCMC_MOMENTS_PACE; SiblingPace, emcmc_fused.h): every fourth row of
+    // the unit sweeps publishes the wave's progress and sets its issue priority against the
+    // other wave on its SIMD, so the pair reaches the step's barrier together instead of the
+    // older one waiting there while the younger one finishes alone
+    SiblingPace pace{pace_prog, W, -1};
+    uint32_t ticks = 0;
+    if constexpr (EMCMC_MOMENTS_PACE) {
+        for (int w = 0; w < MT::WPB; ++w)
+            if (w != W && pace.sib < 0 && pace_simd[w] == pace_simd[W]) pace.sib = w;
+    }
+    auto tick = [&](int u) {
+        if constexpr (EMCMC_MOMENTS_PACE) {
+            ++ticks;
+            if ((u & 3) == 3) pace.publish(ticks);
+        }
+    };
     constexpr int UA = MomentPairs<D>::a(W), UB = TWO ? MomentPairs<D>::b(W) : UA;
     constexpr bool SHARE_ROWS = TWO && MomentUnit<D, UA>::I0 == MomentUnit<D, UB>::I0;
     MomentUnitState<D, UA> ua;
@@ -701,8 +724,8 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
         auto theta_at = [&](int d) -> double { return th_s[state_pos((uint64_t)d, cl, C, (uint32_t)D)]; };
         const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
         const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
-        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
-        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr);
+        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, nullptr, tick);
+        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr, tick);
     }
 #else
     {
@@ -722,8 +745,8 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
         };
         const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
         const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
-        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1);
-        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr);
+        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, nullptr, tick);
+        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr, tick);
         if (s + 1 < a.nsteps) put((s & 1u) ? stage0 : stage1, pf);
         __syncthreads();
     }
@@ -734,10 +757,11 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
 }
 
 template <int D, int W>
-__device__ __forceinline__ void moments_dispatch(int wave, const MixMomentsParams &a, double *stage0, double *stage1) {
+__device__ __forceinline__ void moments_dispatch(int wave, const MixMomentsParams &a, double *stage0, double *stage1,
+                                                 uint32_t *pace_prog, const uint32_t *pace_simd) {
     if constexpr (W < MomentTiles<D>::WPB) {
-        if (wave == W) moments_wave<D, W>(a, stage0, stage1);
-        else moments_dispatch<D, W + 1>(wave, a, stage0, stage1);
+        if (wave == W) moments_wave<D, W>(a, stage0, stage1, pace_prog, pace_simd);
+        else moments_dispatch<D, W + 1>(wave, a, stage0, stage1, pace_prog, pace_simd);
     }
 }
 
@@ -745,8 +769,16 @@ template <int D>
 __global__ void __launch_bounds__(MomentTiles<D>::BLOCK) mix_moments_kernel(const MixMomentsParams a) {
     using MT = MomentTiles<D>;
     __shared__ __attribute__((aligned(16))) double stage[2][MT::PR * 64 * MT::EW];
+    __shared__ uint32_t pace_prog[MT::WPB], pace_simd[MT::WPB];
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
-    moments_dispatch<D, 0>(wave, a, stage[0], stage[1]);
+    if constexpr (EMCMC_MOMENTS_PACE) {
+        if ((threadIdx.x & 63) == 0) {
+            pace_simd[wave] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;  // HW_ID.simd_id
+            pace_prog[wave] = 0u;
+        }
+        __syncthreads();
+    }
+    moments_dispatch<D, 0>(wave, a, stage[0], stage[1], pace_prog, pace_simd);
 }
 
 // ---- HaarioTypeAdaptation readjust! (adaptation.jl:422-426) -----------------

@@ -113,3 +113,36 @@ def test_state_beyond_32bit_offsets_rejected(hist):
     cfg.roll_window = 10
     h = C.c_void_p()
     assert L.lib().emcmc_create(C.byref(h), C.byref(cfg)) == L.INVALID_ARG
+
+
+def test_runtime_kernels_share_the_soa_tile_width():
+    """The state_pos tile width (emcmc_kernels.h EMCMC_SOA_TILE) is passed to every run-time
+    compile by emcmc_rtc.hip from its own default: the two defaults must agree, or the
+    run-time kernels would lay out θ and the histories differently from the ahead-of-time
+    ones (text-level)."""
+    csrc = ROOT / "extensiblemcmc.jl_amd" / "csrc"
+    pat = re.compile(r"#define\s+EMCMC_SOA_TILE\s+(\d+)")
+    k = pat.findall((csrc / "emcmc_kernels.h").read_text())
+    r = pat.findall((csrc / "emcmc_rtc.hip").read_text())
+    assert k and r and k == r, (k, r)
+    t = int(k[0])
+    assert t > 0 and t & (t - 1) == 0  # a power of two: tile starts are c & ~(T - 1)
+
+
+def test_state_pos_tiling_matches_the_documented_formula():
+    """state_pos as include/emcmc.h documents it for emcmc_history_device_ptr: tiles of
+    T = 32 chains when 32 | C (else one tile of C), pair-interleaved inside a tile; a
+    bijection of the D·C slot positions (restated here; the device gathers through the
+    same function, tests/test_gpu_* compare every history bitwise)."""
+    def pos(d, c, C, D):
+        T = 32 if C % 32 == 0 else C
+        c0 = c - c % T
+        return c0 * D + (((d // 2) * T + (c - c0)) * 2 + d % 2 if D % 2 == 0 else d * T + (c - c0))
+
+    for C, D in ((64, 32), (96, 5), (1000, 32), (37, 7), (32, 64)):
+        seen = {pos(d, c, C, D) for c in range(C) for d in range(D)}
+        assert seen == set(range(C * D)), (C, D)
+    # a wave's 32 chains (one tile at LPC = 2) write pair k of all its chains contiguously
+    C, D = 65536, 32
+    base = pos(0, 32 * 7, C, D)
+    assert [pos(2 * 3, 32 * 7 + c, C, D) for c in range(32)] == [base + 2 * (3 * 32 + c) for c in range(32)]

@@ -212,7 +212,9 @@ SIGNATURES = {
     "emcmc_check_user_target": (_ST, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_size_t]),
     "emcmc_check_user_update": (_ST, [C.c_char_p, C.c_uint32, C.c_char_p, C.c_char_p, C.c_size_t]),
     "emcmc_set_state": (_ST, [_H, C.POINTER(C.c_double), C.POINTER(C.c_double)]),
-    "emcmc_run": (_ST, [_H, C.POINTER(EmcmcStep), C.c_uint64]),
+    # const emcmc_step * passed as an address: the step list's numpy buffer, without a
+    # per-call ctypes pointer object (≈ 3 µs of the 20-step window's host path)
+    "emcmc_run": (_ST, [_H, C.c_void_p, C.c_uint64]),
     "emcmc_synchronize": (_ST, [_H]),
     "emcmc_destroy": (None, [_H]),
     "emcmc_last_error": (C.c_char_p, [_H]),

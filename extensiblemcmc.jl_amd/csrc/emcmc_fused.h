@@ -142,7 +142,10 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     uint32_t faults = chain_elem(a.faults, c32);
 #if EMCMC_EARLY_STATE
     const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
-    if (tid / LPC >= a.C) return;
+    if (tid / LPC >= a.C) {
+        if (kPace && (threadIdx.x & 63) == 0) pace_prog[threadIdx.x >> 6] = ~0u;  // no steps to pace
+        return;
+    }
 #endif
     constexpr bool kBatched = diag_batched(D, LPC);
     const size_t used = lds_align16(sizeof(double) * (size_t)(nconst + ((LLMODE == LL_PER_OBS) ? (int)nobs * D : 0)));

@@ -161,6 +161,32 @@ def test_fused_schedule_gap_restarts_rolling_rate(oracle):
     assert np.array_equal(ra[0], st.ra)
 
 
+def test_reused_step_array_is_read_at_every_run(oracle):
+    """Engine.run keeps the address of a step array it has seen (the driver's repeated
+    window): the same array object, refilled in place with the next iterations, and
+    then a reshaped one, must run the iterations it holds at each call."""
+    w = W.cfg2(320)
+    eng = Engine(EngineConfig(dim=w.D, num_chains=320, num_mcmc_steps=100, seed=w.seed))
+    eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    eng.set_state(np.zeros((320, w.D)))
+    steps = np.ones((20, 2), dtype=np.uint32)
+    for k in range(3):  # iterations 1..60 through one array
+        steps[:, 0] = np.arange(1 + 20 * k, 21 + 20 * k, dtype=np.uint32)
+        eng.run(steps)
+    steps[:, 0] = np.arange(61, 81, dtype=np.uint32)
+    steps.shape = (10, 4)  # the same object and buffer under another shape: the general path
+    eng.run(steps)
+    eng.run(np.stack([np.arange(81, 101, dtype=np.uint32), np.ones(20, np.uint32)], axis=1))
+    eng.synchronize()
+    st = oracle.OracleState(np.zeros((320, w.D)))
+    oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=100,
+                   nthreads=8, history=False)
+    th, ll = eng.get_state()
+    assert np.array_equal(th, st.theta) and np.array_equal(ll, st.ll)
+    eng.close()
+
+
 @pytest.mark.parametrize("C", [1, 63, 65, 257])
 def test_ragged_and_tiny_chain_counts(oracle, C):
     """One chain, and counts that leave partial waves / blocks at LPC = 2:

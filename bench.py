@@ -18,6 +18,13 @@ after the timed region: an all-gather of every rank's moments, Chan-merged.
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...
 
+`python bench.py --gpus N` with N > 1 and no WORLD_SIZE in the environment starts
+`torch.distributed.run --nproc-per-node N` on this same command line as a child
+process (before anything here imports torch or touches a GPU) and exits with its
+return code; rank 0 of the child prints the line.  Under a launcher, WORLD_SIZE
+must equal --gpus (when given): a mismatch exits non-zero instead of measuring a
+different N than the one asked for.
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -42,7 +49,9 @@ FP64_VALU_PEAK_TFS = 78.6  # MI355X FP64 vector peak: 1,024 SIMDs x 16 fma lanes
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (default: WORLD_SIZE under a launcher, else 1); N > 1 without a launcher "
+                         "runs N ranks through a torch.distributed.run child")
     ap.add_argument("--steps", type=int, default=1000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--workload", choices=["cfg2", "cfg3", "cfg4", "cfg5"], default="cfg2",
@@ -236,6 +245,26 @@ def reduce_over_ranks(x, dist, dev=None, op="max"):
     return float(t.item())
 
 
+STUB_ENV = "EMCMC_BENCH_STUB_ENGINE"
+
+
+def engine_classes():
+    """(Engine, EngineConfig) of the measured path: extensible_mcmc.engine over libemcmc.so.
+    EMCMC_BENCH_STUB_ENGINE=1 swaps in tests/bench_stub.py, a do-nothing engine with the
+    same methods, so CPU tests can drive the launcher and the rank plumbing of this file
+    with gloo; such a line says "stub_engine": true and measures nothing."""
+    if os.environ.get(STUB_ENV) == "1":
+        import importlib.util
+
+        spec = importlib.util.spec_from_file_location("bench_stub", ROOT / "tests" / "bench_stub.py")
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        return mod.Engine, mod.EngineConfig
+    from extensible_mcmc.engine import Engine, EngineConfig
+
+    return Engine, EngineConfig
+
+
 def settle_clock(w, Cg, device, a, first, cfg3, cfg4, ll_mode):
     """Bring the GPU to its steady-state clock right before the timed steps: the same step
     kernel (same workload shape, full histories into a ring of one launch) on a throwaway
@@ -243,8 +272,8 @@ def settle_clock(w, Cg, device, a, first, cfg3, cfg4, ll_mode):
     for ~10 ms, then settles; the measured handle's chains are untouched.
     Returns (handle, info); the caller closes the handle after the timed region."""
     from extensible_mcmc import _lib as L
-    from extensible_mcmc.engine import Engine, EngineConfig
 
+    Engine, EngineConfig = engine_classes()
     spl = 1 if cfg3 else a.steps_per_launch
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=1 << 20,
                               seed=w.seed ^ 0x5E77, first_chain_id=first, device=device,
@@ -276,14 +305,51 @@ def settle_clock(w, Cg, device, a, first, cfg3, cfg4, ll_mode):
                          "steps; not in the timed region"}
 
 
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """--gpus n > 1 with no launcher: run this command line as n ranks of a fresh
+    `torch.distributed.run` child (one rank per GPU, rendezvous on 127.0.0.1) and
+    return its exit code.  A child process, never an exec; nothing in this process
+    has imported torch or initialised a GPU.  The ranks inherit stdout, so the one
+    JSON line rank 0 prints is this command's output."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", str(Path(__file__).resolve()), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")  # dmabuf IPC only on this host driver (RCCL)
+    sys.stdout.flush()
+    return subprocess.run(cmd, env=env).returncode
+
+
+def world_size(a) -> int:
+    """The rank count this process belongs to; exits when --gpus and the launcher disagree."""
+    env = os.environ.get("WORLD_SIZE")
+    if env is None:
+        return 1
+    if a.gpus is not None and int(env) != a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={env}: the line would report "
+                 f"{env} GPU(s); launch {a.gpus} ranks or pass --gpus {env}")
+    return int(env)
+
+
 def main():
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if os.environ.get("WORLD_SIZE") is None and (a.gpus or 1) > 1:
+        sys.exit(launch_ranks(a.gpus))
+    world = world_size(a)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # EMCMC_BENCH_SHARED_DEVICE=1: every rank on device 0 with gloo (a rehearsal of
     # the torchrun path on a one-GPU box; RCCL needs one GPU per rank)
-    shared = os.environ.get("EMCMC_BENCH_SHARED_DEVICE") == "1"
+    stub = os.environ.get(STUB_ENV) == "1"
+    shared = os.environ.get("EMCMC_BENCH_SHARED_DEVICE") == "1" or stub
     # EMCMC_BENCH_FORCE_NCCL=1: the RCCL process group even at world size 1 (RCCL init, the
     # device all-gather of the diagnostics and libemcmc beside torch's HIP context in one process)
     force_nccl = os.environ.get("EMCMC_BENCH_FORCE_NCCL") == "1" and not shared
@@ -297,6 +363,8 @@ def main():
         if shared:
             dist.init_process_group("gloo")
         else:
+            if torch.cuda.device_count() < world:  # one GPU per rank: never two ranks silently on one device
+                sys.exit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPU(s)")
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
             dev = f"cuda:{local}"
@@ -304,8 +372,8 @@ def main():
     from extensible_mcmc import _lib as L
     from extensible_mcmc import diagnostics as DG
     from extensible_mcmc import workloads as W
-    from extensible_mcmc.engine import Engine, EngineConfig
 
+    Engine, EngineConfig = engine_classes()
     cfg4 = a.workload == "cfg4"
     cfg3 = a.workload == "cfg3"
     # cfg 5 (131,072 chains per GPU, 1,048,576 over 8, overdispersed θinit) only when asked for:
@@ -604,6 +672,9 @@ def main():
             out["cpu_baseline"] = {"error": repr(e)}
     if par is not None:
         out["parity"] = par
+    if stub:
+        out["stub_engine"] = True
+        out["data"] = "STUB ENGINE (tests/bench_stub.py): launcher and rank plumbing only, nothing measured"
     print(json.dumps(out))
     eng.close()
     if dist is not None:

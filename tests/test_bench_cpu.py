@@ -30,3 +30,43 @@ def test_cpu_baseline_leg_runs(name, monkeypatch):
     out = bench.cpu_baseline(w, 0.3, 0)
     assert out["value"] > 0 and out["cores"] == 2 and out["kind"] == "port"
     assert out["single_core"]["value"] > 0
+
+
+def _bench_line(args, env_extra, drop_world=True):
+    import json
+    import os
+    import subprocess
+
+    env = dict(os.environ, EMCMC_BENCH_STUB_ENGINE="1", **env_extra)
+    if drop_world:
+        for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+            env.pop(k, None)
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), *args], cwd=ROOT, env=env, capture_output=True,
+                       text=True, timeout=240)
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    return r, (json.loads(lines[-1]) if lines else None)
+
+
+STUB_ARGS = ["--steps", "20", "--warmup", "5", "--no-cpu", "--no-parity", "--settle-ms", "0", "--reps", "1"]
+
+
+def test_gpus_n_launches_n_ranks():
+    """`python bench.py --gpus 2` with no launcher runs 2 ranks (a torch.distributed.run
+    child, gloo under the stub engine) and rank 0's line reports them: the per-GPU shape
+    stays cfg 2's, the total doubles, and the diagnostics are merged over both shards."""
+    r, line = _bench_line(["--gpus", "2", *STUB_ARGS], {})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert line["stub_engine"] is True and line["n_gpus"] == 2
+    assert line["config"]["chains_per_gpu"] == 65536 and line["config"]["total_chains"] == 131072
+    assert line["config"]["process_group"] == "gloo"
+    assert line["config"]["first_chain_id"] == 0
+    one = _bench_line(["--gpus", "1", *STUB_ARGS], {})[1]
+    assert one["n_gpus"] == 1 and one["config"]["total_chains"] == 65536
+    assert line["diagnostics"]["max_split_rhat"] != one["diagnostics"]["max_split_rhat"]  # rank 1's shard merged
+
+
+def test_gpus_must_match_the_launchers_world_size():
+    r, line = _bench_line(["--gpus", "4", *STUB_ARGS], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"},
+                          drop_world=False)
+    assert r.returncode != 0 and line is None
+    assert "--gpus 4 but WORLD_SIZE=2" in r.stderr

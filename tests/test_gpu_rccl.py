@@ -48,14 +48,15 @@ def test_nccl_process_group_at_one_rank_matches_the_single_process_line():
 
 
 def test_two_ranks_on_one_device_carry_parity_and_the_same_per_gpu_shape():
-    """The N > 1 line at world size 2 (both ranks on device 0, gloo: one GPU on this
-    box): each rank replays 8 of its chains on the oracle, AND-reduced; the per-GPU
-    chain count is the N = 1 line's; the barriers sit outside the timed window."""
+    """`python bench.py --gpus 2` with no outer launcher (bench.py starts the
+    torch.distributed.run child itself) at world size 2, both ranks on device 0 with
+    gloo (one GPU on this box): each rank replays 8 of its chains on the oracle,
+    AND-reduced; the per-GPU chain count is the N = 1 line's; the barriers sit
+    outside the timed window."""
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", EMCMC_BENCH_SHARED_DEVICE="1")
-    env.pop("WORLD_SIZE", None)
-    two = _line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-                 "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
-                 *[x if x != "1" or i != 1 else "2" for i, x in enumerate(ARGS)]], env)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    two = _line([sys.executable, "bench.py", *[x if x != "1" or i != 1 else "2" for i, x in enumerate(ARGS)]], env)
     assert two["n_gpus"] == 2 and two["config"]["process_group"] == "gloo"
     assert two["config"]["chains_per_gpu"] == 65536 and two["config"]["total_chains"] == 131072
     assert two["parity"]["ranks"] == 2 and two["parity"]["all_ranks_bitwise"] is True

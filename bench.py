@@ -487,12 +487,20 @@ def main():
     korder = np.argsort([k[0] for k in kern])
     ms, launches, nbytes = kern[int(korder[len(korder) // 2])]  # the median kernel-timing rep
 
-    # diagnostics over the first timed window: one all-gather of 3·D+3 doubles per rank, Chan-merged
-    mom = eng.moments_window(a.warmup + 1, a.steps, split=True) if hist == L.HIST_FULL and not a.history_ring \
-        and a.steps >= 4 else None
-    if mom is not None and dist is not None:
-        mom = DG.allgather_moments(mom, w.D, device=dev)
-    diag = DG.rhat_from_moments(mom) if mom is not None else None
+    # diagnostics over the first timed window, through the C ABI (emcmc_diagnostics): one
+    # all-gather of 3·D+3 doubles per rank — ncclAllGather inside libemcmc on an RCCL comm
+    # (nccl process group), the host-callback comm over gloo — Chan-merged in rank order
+    diag, diag_via = None, None
+    if hist == L.HIST_FULL and not a.history_ring and a.steps >= 4:
+        comm = None
+        if dist is not None:
+            comm = DG.Comm.torch_host() if shared else DG.Comm.from_process_group(local)
+        diag = eng.diagnostics(a.warmup + 1, a.steps, split=True, comm=comm)
+        diag_via = ("emcmc_diagnostics, this rank alone" if comm is None else
+                    f"emcmc_diagnostics over {'a host all-gather (gloo)' if shared else 'RCCL (ncclAllGather)'}, "
+                    f"{diag['nranks']} ranks")
+        if comm is not None:
+            comm.close()
 
     # parity on every rank: 8 of its chains replayed on the oracle after the timed
     # region (global ids first + c), AND-reduced over the ranks
@@ -661,7 +669,8 @@ def main():
     if cfg4:
         out["posdef_faulted_chains"] = int(np.count_nonzero(eng.get_faults() & L.FAULT_POSDEF))
     if diag is not None:
-        out["diagnostics"] = {"accept_rate": diag["accept_rate"], "max_split_rhat": float(np.max(diag["rhat"]))}
+        out["diagnostics"] = {"accept_rate": diag["accept_rate"], "max_split_rhat": float(np.max(diag["rhat"])),
+                              "chains_merged": diag["num_chains"], "via": diag_via}
         if not cfg3:
             out["diagnostics"]["max_abs_mean_minus_xbar"] = float(np.max(np.abs(diag["mean"] - w.obs.mean(0))))
     if world == 1 and not a.no_cpu:

@@ -2550,6 +2550,15 @@ emcmc_status emcmc_host_free(void *ptr) {
     return EMCMC_OK;
 }
 
+}  // extern "C"
+
+// for emcmc_comm.hip (cross-rank diagnostics)
+int emcmc_internal_device(const emcmc_handle *h) { return h->cfg.device; }
+uint32_t emcmc_internal_dim(const emcmc_handle *h) { return h->cfg.dim; }
+void emcmc_internal_set_error(emcmc_handle *h, const std::string &msg) { h->err = msg; }
+
+extern "C" {
+
 emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t num_iters, int split,
                                   double *out3d, emcmc_moments *info) {
     if (!h || !out3d) return EMCMC_INVALID_ARG;

@@ -198,6 +198,29 @@ class EmcmcMoments(C.Structure):
     ]
 
 
+class EmcmcDiag(C.Structure):
+    _fields_ = [
+        ("num_chains", C.c_uint64),
+        ("num_draws", C.c_uint64),
+        ("accepted", C.c_uint64),
+        ("proposed", C.c_uint64),
+        ("accept_rate", C.c_double),
+        ("max_rhat", C.c_double),
+        ("dim", C.c_uint32),
+        ("nranks", C.c_uint32),
+        ("mean", C.POINTER(C.c_double)),
+        ("m2", C.POINTER(C.c_double)),
+        ("sum_var", C.POINTER(C.c_double)),
+        ("W", C.POINTER(C.c_double)),
+        ("B", C.POINTER(C.c_double)),
+        ("rhat", C.POINTER(C.c_double)),
+    ]
+
+
+COMM_ID_BYTES = 128
+# emcmc_allgather_fn: (send, recv, count, ctx) -> 0 on success
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.c_uint64, C.c_void_p)
+
 LAMBDA_FN = C.CFUNCTYPE(C.c_double, C.c_double, C.c_int64, C.c_int64, C.c_void_p)  # emcmc_lambda_fn
 
 # every symbol declared in include/emcmc.h, with its ctypes signature
@@ -243,6 +266,13 @@ SIGNATURES = {
         _ST,
         [_H, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(C.c_double), C.POINTER(EmcmcMoments)],
     ),
+    "emcmc_comm_unique_id": (_ST, [C.POINTER(C.c_uint8)]),
+    "emcmc_comm_init": (_ST, [C.POINTER(_H), C.c_int, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
+    "emcmc_comm_init_host": (_ST, [C.POINTER(_H), C.c_int, C.c_int, ALLGATHER_FN, C.c_void_p]),
+    "emcmc_comm_destroy": (None, [_H]),
+    "emcmc_comm_last_error": (C.c_char_p, [_H]),
+    "emcmc_diagnostics": (_ST, [_H, _H, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(EmcmcDiag)]),
+    "emcmc_diagnostics_merge": (_ST, [_H, C.POINTER(C.c_double), C.c_uint32, C.c_uint64, C.POINTER(EmcmcDiag)]),
     "emcmc_set_timing": (_ST, [_H, C.c_int]),
     "emcmc_get_timing": (
         _ST,

@@ -523,6 +523,20 @@ class Engine:
             "proposed": int(info.proposed),
         }
 
+    def diagnostics(self, iter_first: int, num_iters: int, split: bool = True, comm=None) -> dict:
+        """emcmc_diagnostics: this handle's moments over the window, all-gathered over comm
+        (an extensible_mcmc.diagnostics.Comm: RCCL or a host all-gather; None = this handle
+        alone), merged and turned into split-R̂ by the library.  Collective over comm."""
+        from .diagnostics import _diag_dict, _diag_out
+
+        d, arrs = _diag_out(self.cfg.dim)
+        st = self._lib.emcmc_diagnostics(self._h, comm.handle if comm else None, iter_first, num_iters, int(split),
+                                         C.byref(d))
+        if comm is not None and comm.callback_error is not None:
+            comm.check(st, "emcmc_diagnostics")
+        self._check(st, "emcmc_diagnostics")
+        return _diag_dict(d, arrs)
+
     # -- timing ------------------------------------------------------------------------
     def set_timing(self, enable: bool):
         self._check(self._lib.emcmc_set_timing(self._h, int(enable)), "emcmc_set_timing")

@@ -692,6 +692,121 @@ function moments_window(gws::MI355XGlobalWorkspace, iter_first::Integer, n::Inte
     out, info[]
 end
 
+# ---- cross-chain diagnostics over every rank (emcmc_comm_*, emcmc_diagnostics) ------------
+# One handle per GPU holds a shard of the chains; an HipComm joins the ranks of a job.
+# `HipComm(nranks, rank, device, id)` is RCCL over xGMI (rank 0 draws `rccl_unique_id()`,
+# the caller broadcasts the 128 bytes, e.g. MPI.Bcast!); `HipComm(nranks, rank, allgather!)`
+# wraps the caller's own all-gather of Float64 vectors (e.g. MPI.Allgather!), called by
+# the library through a @cfunction.  `diagnostics(gws, comm, iter_first, n)` all-gathers
+# the shards' moments and merges them in rank order (Chan), then split-R̂ — the same bits
+# on every rank and in extensible_mcmc/diagnostics.py.
+
+struct EmcmcDiag
+    num_chains::UInt64
+    num_draws::UInt64
+    accepted::UInt64
+    proposed::UInt64
+    accept_rate::Float64
+    max_rhat::Float64
+    dim::UInt32
+    nranks::UInt32
+    mean::Ptr{Float64}
+    m2::Ptr{Float64}
+    sum_var::Ptr{Float64}
+    W::Ptr{Float64}
+    B::Ptr{Float64}
+    rhat::Ptr{Float64}
+end
+
+mutable struct HipComm
+    ptr::Ptr{Cvoid}
+    allgather!::Any   # the host form's Julia all-gather (kept alive with the comm), else nothing
+    err::Any          # an exception the all-gather raised (a Julia exception cannot cross the C ABI)
+end
+
+function rccl_unique_id()
+    id = Vector{UInt8}(undef, 128)
+    check(ccall((:emcmc_comm_unique_id, LIB), Cint, (Ptr{UInt8},), id), C_NULL, "emcmc_comm_unique_id")
+    id
+end
+
+function _comm_check(st, c::HipComm, where)
+    if c.err !== nothing
+        e, c.err = c.err, nothing
+        throw(e)
+    end
+    st == 0 && return nothing
+    error("$where failed with emcmc_status $st: " *
+          unsafe_string(ccall((:emcmc_comm_last_error, LIB), Cstring, (Ptr{Cvoid},), c.ptr)))
+end
+
+function HipComm(nranks::Integer, rank::Integer, device::Integer, id::AbstractVector{UInt8})
+    length(id) == 128 || throw(ArgumentError("an RCCL unique id has 128 bytes"))
+    p = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:emcmc_comm_init, LIB), Cint, (Ref{Ptr{Cvoid}}, Cint, Cint, Cint, Ptr{UInt8}),
+                p, nranks, rank, device, Vector{UInt8}(id)), C_NULL, "emcmc_comm_init")
+    c = HipComm(p[], nothing, nothing)
+    finalizer(c -> (c.ptr != C_NULL && ccall((:emcmc_comm_destroy, LIB), Cvoid, (Ptr{Cvoid},), c.ptr);
+                    c.ptr = C_NULL), c)
+end
+
+# emcmc_allgather_fn: ctx is the HipComm; recv gets nranks·count doubles in rank order
+function _allgather_trampoline(send::Ptr{Float64}, recv::Ptr{Float64}, count::UInt64, ctx::Ptr{Cvoid})::Cint
+    c = unsafe_pointer_to_objref(ctx)::HipComm
+    try
+        s = copy(unsafe_wrap(Array, send, Int(count)))
+        r = c.allgather!(s)
+        dst = unsafe_wrap(Array, recv, length(r))
+        dst .= r
+        return Cint(0)
+    catch e
+        c.err = e
+        return Cint(1)
+    end
+end
+
+"""
+    HipComm(nranks, rank, allgather!)
+
+A host communicator: `allgather!(send::Vector{Float64}) -> Vector{Float64}` returns every
+rank's `send`, concatenated in rank order (e.g. `MPI.Allgather(send, comm)`).
+"""
+function HipComm(nranks::Integer, rank::Integer, allgather!::Function)
+    c = HipComm(C_NULL, allgather!, nothing)
+    p = Ref{Ptr{Cvoid}}(C_NULL)
+    fp = @cfunction(_allgather_trampoline, Cint, (Ptr{Float64}, Ptr{Float64}, UInt64, Ptr{Cvoid}))
+    check(ccall((:emcmc_comm_init_host, LIB), Cint, (Ref{Ptr{Cvoid}}, Cint, Cint, Ptr{Cvoid}, Ptr{Cvoid}),
+                p, nranks, rank, fp, pointer_from_objref(c)), C_NULL, "emcmc_comm_init_host")
+    c.ptr = p[]
+    finalizer(c -> (c.ptr != C_NULL && ccall((:emcmc_comm_destroy, LIB), Cvoid, (Ptr{Cvoid},), c.ptr);
+                    c.ptr = C_NULL), c)
+end
+
+"""
+    diagnostics(gws, comm, iter_first, n; split=true) -> NamedTuple
+
+Cross-chain diagnostics of θ over iterations iter_first … iter_first+n−1 over every rank
+of `comm` (`nothing`: this shard alone): `rhat` (split-R̂ per coordinate), `mean`, `W`,
+`B`, `m2`, `sum_var`, `max_rhat`, `accept_rate`, `num_chains`, `num_draws`.  Collective.
+"""
+function diagnostics(gws::MI355XGlobalWorkspace, comm::Union{HipComm,Nothing}, iter_first::Integer, n::Integer;
+                     split::Bool=true)
+    D = gws.dim
+    a = [Vector{Float64}(undef, D) for _ in 1:6]
+    d = Ref(EmcmcDiag(0, 0, 0, 0, 0.0, 0.0, 0, 0, pointer(a[1]), pointer(a[2]), pointer(a[3]), pointer(a[4]),
+                      pointer(a[5]), pointer(a[6])))
+    cp = comm === nothing ? C_NULL : comm.ptr
+    st = GC.@preserve a comm ccall((:emcmc_diagnostics, LIB), Cint,
+                                   (Ptr{Cvoid}, Ptr{Cvoid}, UInt64, UInt64, Cint, Ref{EmcmcDiag}),
+                                   gws.handle, cp, iter_first, n, Cint(split), d)
+    comm === nothing || comm.err === nothing || _comm_check(st, comm, "emcmc_diagnostics")
+    check(st, gws.handle, "emcmc_diagnostics")
+    r = d[]
+    (rhat=a[6], mean=a[1], W=a[4], B=a[5], m2=a[2], sum_var=a[3], max_rhat=r.max_rhat, accept_rate=r.accept_rate,
+     num_chains=Int(r.num_chains), num_draws=Int(r.num_draws), accepted=Int(r.accepted), proposed=Int(r.proposed),
+     nranks=Int(r.nranks))
+end
+
 """
     kernel_name(gws) -> String
 
@@ -861,6 +976,6 @@ eMCMC.name_of_update(lws::MI355XLocalWorkspace) = lws.updt_name
 
 export MI355XBackend, state_history, proposal_history, ll_history, acceptance_history, rolling_acceptance,
        adaptation_state, chain_moments, adaptation_moments, mix_state, faults, moments_window, kernel_name, device_count,
-       HipTargetLaw, HipUpdate, HipMALAUpdate
+       HipComm, rccl_unique_id, diagnostics, HipTargetLaw, HipUpdate, HipMALAUpdate
 
 end # module

@@ -46,7 +46,7 @@ typedef enum emcmc_status {
     EMCMC_OK = 0,
     EMCMC_INVALID_ARG = 1,        /* reference: @assert / error("…") in constructors */
     EMCMC_HIP_ERROR = 2,
-    EMCMC_RCCL_ERROR = 3,         /* reserved: collectives run in the host layer */
+    EMCMC_RCCL_ERROR = 3,         /* RCCL missing or a collective failed (emcmc_comm_*, emcmc_diagnostics) */
     EMCMC_UNSUPPORTED_PLUGIN = 4, /* update/target kind with no device plugin */
     EMCMC_CHAIN_FAULT = 5,        /* ≥1 chain raised a fault bit (see emcmc_get_faults) */
     EMCMC_OUT_OF_MEMORY = 6,
@@ -532,6 +532,60 @@ emcmc_status emcmc_history_device_ptr(emcmc_handle *h, uint32_t which, void **dp
  * split != 0 treats each chain as two halves (split-R̂). */
 emcmc_status emcmc_moments_window(emcmc_handle *h, uint64_t iter_first, uint64_t num_iters,
                                   int split, double *out3d, emcmc_moments *info);
+
+/* Cross-chain diagnostics over every rank (SURVEY.md §8(b) `emcmc_diagnostics`; new: the
+ * reference's GenericChainStats, src/chain_statistics.jl:16-66, is single-chain).  Chains are
+ * sharded one handle per GPU; a communicator joins the handles of one job:
+ *   - RCCL (emcmc_comm_init): rank 0 draws an id with emcmc_comm_unique_id, the caller
+ *     broadcasts its 128 bytes (MPI, torch.distributed, a file), every rank calls
+ *     emcmc_comm_init on its own GPU; the all-gather runs over xGMI (ncclAllGather).
+ *     librccl.so.1 is opened at the first call (the copy already loaded, e.g. by torch, or
+ *     the system's); without it these calls return EMCMC_RCCL_ERROR.
+ *   - host callback (emcmc_comm_init_host): the caller's own all-gather of doubles
+ *     (MPI.Allgather!, gloo), for callers that already hold a process group.
+ * The per-rank record is the 3·D + 3 doubles [num_chains | m̄ (D) | M2 (D) | Σvar (D) |
+ * accepted | proposed] (emcmc_moments_window's moments); every rank merges the gathered
+ * records in rank order with Chan's pairwise update and forms split-R̂ (BDA3 §11.4):
+ *   B = n/(m−1)·M2, W = Σvar/m, var⁺ = (n−1)/n·W + B/n, R̂ = √(var⁺/W),
+ * m (half-)chains of n draws: the arithmetic of extensible_mcmc/diagnostics.py, bit for bit. */
+typedef struct emcmc_comm emcmc_comm;
+#define EMCMC_COMM_ID_BYTES 128
+/* all-gather of `count` doubles per rank: recv = nranks·count doubles in rank order; 0 = ok */
+typedef int (*emcmc_allgather_fn)(const double *send, double *recv, uint64_t count, void *ctx);
+
+emcmc_status emcmc_comm_unique_id(uint8_t id[EMCMC_COMM_ID_BYTES]);
+emcmc_status emcmc_comm_init(emcmc_comm **comm, int nranks, int rank, int device,
+                             const uint8_t id[EMCMC_COMM_ID_BYTES]);
+emcmc_status emcmc_comm_init_host(emcmc_comm **comm, int nranks, int rank, emcmc_allgather_fn fn, void *ctx);
+void emcmc_comm_destroy(emcmc_comm *comm);
+const char *emcmc_comm_last_error(const emcmc_comm *comm);
+
+typedef struct emcmc_diag {
+    uint64_t num_chains;  /* (half-)chains merged over every rank */
+    uint64_t num_draws;   /* draws per (half-)chain */
+    uint64_t accepted;    /* accepted proposals in the window, every rank */
+    uint64_t proposed;
+    double accept_rate;   /* accepted / max(1, proposed) */
+    double max_rhat;      /* max over the dimensions of R̂ (NaN if any is) */
+    uint32_t dim;         /* out: D */
+    uint32_t nranks;      /* out: records merged */
+    double *mean;         /* caller-owned [D] arrays, each may be NULL: m̄ (the chain-mean mean) */
+    double *m2;           /*   M2 = Σ_c (m_c − m̄)² */
+    double *sum_var;      /*   Σ_c var_c */
+    double *W;            /*   within-chain variance */
+    double *B;            /*   between-chain variance */
+    double *rhat;         /*   split-R̂ */
+} emcmc_diag;
+
+/* emcmc_moments_window of this handle's chains, all-gathered over `comm` (NULL: this
+ * handle alone) and merged; every rank gets the same result.  Collective: every rank of
+ * comm calls it with the same window.  An RCCL comm must be on the handle's device. */
+emcmc_status emcmc_diagnostics(emcmc_handle *h, emcmc_comm *comm, uint64_t iter_first, uint64_t num_iters,
+                               int split, emcmc_diag *out);
+/* The same from a caller-made record (3·dim + 3 doubles as above) and draws per
+ * (half-)chain; no handle, and no device with a host comm or comm = NULL. */
+emcmc_status emcmc_diagnostics_merge(emcmc_comm *comm, const double *record, uint32_t dim, uint64_t num_draws,
+                                     emcmc_diag *out);
 
 /* ---- timing (bench / roofline) ----------------------------------------- */
 

@@ -56,6 +56,12 @@ class Engine:
                 "sum_var": np.full(D, 1.5 * C * halves), "num_chains": C * halves,
                 "num_draws": num_iters // halves, "accepted": C * num_iters // 4, "proposed": C * num_iters}
 
+    def diagnostics(self, iter_first, num_iters, split=True, comm=None):
+        from extensible_mcmc import diagnostics as DG  # the library's merge (emcmc_diagnostics_merge)
+
+        m = self.moments_window(iter_first, num_iters, split)
+        return DG.merge_c(DG.pack(m), self.cfg.dim, m["num_draws"], comm)
+
     def get_faults(self):
         return np.zeros(self.cfg.num_chains, dtype=np.uint32)
 

@@ -63,6 +63,8 @@ def test_gpus_n_launches_n_ranks():
     one = _bench_line(["--gpus", "1", *STUB_ARGS], {})[1]
     assert one["n_gpus"] == 1 and one["config"]["total_chains"] == 65536
     assert line["diagnostics"]["max_split_rhat"] != one["diagnostics"]["max_split_rhat"]  # rank 1's shard merged
+    assert line["diagnostics"]["chains_merged"] == 2 * 131072  # split halves of both shards
+    assert "host all-gather (gloo), 2 ranks" in line["diagnostics"]["via"]
 
 
 def test_gpus_must_match_the_launchers_world_size():

@@ -165,3 +165,61 @@ def test_bench_scaling_line_two_ranks(tmp_path):
     assert r0["dmax"] == r1["dmax"] == max(r0["dt"], r1["dt"])
     assert r0["all_ok"] is False and r1["all_ok"] is False
     assert r0["cg"] == r1["cg"] == [65536, 32768, 131072, 131072]
+
+
+def _diag_c_worker(rank, world, port, out_dir):
+    """Each rank: its shard's record through the library's host-callback comm
+    (emcmc_comm_init_host + emcmc_diagnostics_merge, over gloo) and through the
+    Python all-gather + merge; both results saved for the parent to compare."""
+    sys.path[:0] = [str(ROOT), str(ROOT / "extensiblemcmc.jl_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+
+    from extensible_mcmc import diagnostics as DG
+    from extensible_mcmc import workloads as W
+    from oracle import oracle as O
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    w = W.cfg5(192, D=6)
+    per = 192 // world
+    lo = rank * per
+    st = O.OracleState(w.theta_init[lo:lo + per])
+    h = O.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=80, chain0=lo)
+    m = shard_moments(h["theta"][16:])
+    m["accepted"] = int(h["acc"][16:].sum())
+    m["proposed"] = int(h["acc"][16:].size)
+    comm = DG.Comm.torch_host()
+    c = DG.merge_c(DG.pack(m), w.D, m["num_draws"], comm)
+    py = DG.rhat_from_moments(DG.allgather_moments(m, w.D))
+    # an all-gather that raises: the exception comes back through the C ABI, not a crash
+    bad = DG.Comm.host(world, rank, lambda s: (_ for _ in ()).throw(KeyError("boom")))
+    try:
+        DG.merge_c(DG.pack(m), w.D, m["num_draws"], bad)
+        raised = None
+    except KeyError as e:
+        raised = str(e)
+    np.savez(os.path.join(out_dir, f"diag_{rank}.npz"), c_rhat=c["rhat"], c_mean=c["mean"], c_W=c["W"], c_B=c["B"],
+             py_rhat=py["rhat"], py_mean=py["mean"], py_W=py["W"], py_B=py["B"],
+             scal=np.array([c["accept_rate"], py["accept_rate"], c["num_chains"], c["nranks"], c["max_rhat"]]),
+             raised=np.array([raised or ""]))
+    comm.close()
+    bad.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_diagnostics_through_the_c_abi(tmp_path, oracle):
+    """emcmc_diagnostics_merge over a host all-gather (the callback form an MPI or gloo
+    caller passes through the C ABI): every rank gets the Python reduction's bits."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_diag_c_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    r0, r1 = (np.load(tmp_path / f"diag_{r}.npz") for r in (0, 1))
+    for r in (r0, r1):
+        for k in ("rhat", "mean", "W", "B"):
+            assert np.array_equal(r[f"c_{k}"], r[f"py_{k}"]), k
+        acc_c, acc_py, nch, nranks, mx = r["scal"]
+        assert acc_c == acc_py and nch == 2 * 192 and nranks == 2 and mx == np.max(r["py_rhat"])
+        assert "boom" in str(r["raised"][0])
+    for k in ("c_rhat", "c_mean"):
+        assert np.array_equal(r0[k], r1[k])

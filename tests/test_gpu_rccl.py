@@ -43,8 +43,43 @@ def test_nccl_process_group_at_one_rank_matches_the_single_process_line():
     assert single["config"]["process_group"] is None
     assert rccl["config"]["process_group"] == "nccl" and rccl["n_gpus"] == 1
     assert rccl["config"]["workload"] == single["config"]["workload"]
+    via = rccl["diagnostics"].pop("via")
+    assert "RCCL (ncclAllGather), 1 ranks" in via and single["diagnostics"].pop("via").endswith("this rank alone")
     assert rccl["diagnostics"] == single["diagnostics"]
     assert rccl["parity"]["all_ranks_bitwise"] is True and single["parity"]["accept_stream_bitwise"] is True
+
+
+def test_emcmc_diagnostics_on_an_rccl_comm_equals_the_python_reduction():
+    """emcmc_diagnostics at world size 1 on a real RCCL communicator:
+    the library's all-gather (ncclAllGather on the comm's stream), Chan merge and
+    split-R̂ give the bits of extensible_mcmc.diagnostics on the same moments, as do
+    the no-comm call and emcmc_diagnostics_merge over the RCCL comm."""
+    import numpy as np
+
+    from extensible_mcmc import diagnostics as DG
+    from extensible_mcmc import workloads as W
+    from extensible_mcmc.engine import Engine, EngineConfig
+
+    w = W.cfg2(4096)
+    eng = Engine(EngineConfig(dim=w.D, num_chains=4096, num_mcmc_steps=40, seed=w.seed, device=0))
+    eng.add_gaussian_rw_update(np.arange(w.D), w.rw_sigma)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    eng.set_state(np.zeros((4096, w.D)))
+    eng.run_iters(1, 40)
+    eng.synchronize()
+    mom = eng.moments_window(9, 32, split=True)
+    py = DG.rhat_from_moments(mom)
+    comm = DG.Comm.rccl(1, 0, 0, DG.Comm.unique_id())
+    try:
+        for got in (eng.diagnostics(9, 32, comm=comm), eng.diagnostics(9, 32),
+                    DG.merge_c(DG.pack(mom), w.D, mom["num_draws"], comm)):
+            for k in ("rhat", "mean", "W", "B"):
+                assert np.array_equal(got[k], py[k]), k
+            assert got["accept_rate"] == py["accept_rate"] and got["num_chains"] == 2 * 4096
+            assert got["max_rhat"] == float(np.max(py["rhat"]))
+    finally:
+        comm.close()
+        eng.close()
 
 
 def test_two_ranks_on_one_device_carry_parity_and_the_same_per_gpu_shape():

@@ -22,7 +22,8 @@ C_NAME = {"EmcmcConfig": "emcmc_config", "EmcmcUpdateDesc": "emcmc_update_desc",
           "EmcmcUnifRWAdaptationVec": "emcmc_unifrw_adaptation_vec",
           "EmcmcTargetDesc": "emcmc_target_desc", "EmcmcStep": "emcmc_step", "EmcmcMoments": "emcmc_moments",
           "EmcmcPriorFactor": "emcmc_prior_factor", "EmcmcPriorDesc": "emcmc_prior_desc",
-          "EmcmcUserTargetDesc": "emcmc_user_target_desc", "EmcmcUserUpdateDesc": "emcmc_user_update_desc"}
+          "EmcmcUserTargetDesc": "emcmc_user_target_desc", "EmcmcUserUpdateDesc": "emcmc_user_update_desc",
+          "EmcmcDiag": "emcmc_diag"}
 
 JL_SCALAR = {"UInt8": 1, "Int8": 1, "UInt16": 2, "Int16": 2, "UInt32": 4, "Int32": 4, "Cint": 4, "Float32": 4,
              "UInt64": 8, "Int64": 8, "Float64": 8, "Csize_t": 8, "Cstring": 8}
@@ -181,3 +182,14 @@ def test_plugin_updates_reach_emcmc_add_update():
         assert re.search(rf"^function _update_desc\(updt::{t}, keep\)", src, flags=re.M), t
     loop = src[src.index("for (i, u) in enumerate(updates)"):src.index(":emcmc_add_update")]
     assert not _RW_ONLY.search(loop), loop
+
+
+def test_diagnostics_collective_is_bound():
+    """The cross-rank diagnostics (SURVEY §8(b) emcmc_diagnostics) reach the Julia caller:
+    the RCCL and host-callback communicators and the diagnostics call itself."""
+    src = SHIM.read_text()
+    for fn in ("emcmc_comm_unique_id", "emcmc_comm_init", "emcmc_comm_init_host", "emcmc_comm_destroy",
+               "emcmc_comm_last_error", "emcmc_diagnostics"):
+        assert f"ccall((:{fn}, LIB)" in src, fn
+    assert re.search(r"@cfunction\(_allgather_trampoline, Cint, \(Ptr\{Float64\}, Ptr\{Float64\}, UInt64, "
+                     r"Ptr\{Cvoid\}\)\)", src)

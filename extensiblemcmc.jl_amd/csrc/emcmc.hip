@@ -153,6 +153,7 @@ struct Variant {
     bool mix = false;
     bool xres = false;  // xfn is mix_res_kernel (16 lanes per chain, L_B in registers)
     bool xchol = false;  // xfn is mix_chol_kernel (dense Σ_A / Σ_t through the scalar cache)
+    bool block = false;  // mfn / ufn is mwg_block_kernel (one MALA or user update over all D coordinates)
     int lpc = 1;
     int dense = 0;  // 0 rwm_gsn_diag_kernel, 1 rwm_gsn_dense_kernel, 2 rwm_gsn_chol_kernel
     bool unit = false;
@@ -191,6 +192,7 @@ struct emcmc_handle {
     // general schedule path (mwg_gsn_kernel)
     double *d_mu_p = nullptr, *d_eps = nullptr, *d_tL = nullptr, *d_tiL = nullptr, *d_xbar = nullptr;
     double *d_gcache = nullptr;  // MALA: ∇ℓ(θ) carried between the steps of a launch (emcmc_mwg.h mala_carry)
+    double *d_bconsts = nullptr;  // mwg_block_kernel's constant table (emcmc_block.h BlockConsts)
     uint32_t *d_aprop = nullptr, *d_aacc = nullptr, *d_steps = nullptr;
     MwgUpdate *d_mwg = nullptr;
     // user target (EMCMC_TARGET_USER): the loaded code object and the law's constants
@@ -479,6 +481,48 @@ emcmc_status load_rtc_module(emcmc_handle *h, const RtcKernel &k) {
     return EMCMC_OK;
 }
 
+// mwg_block_kernel's shapes: one MALA or user update (kinds 4, 5) over coords 1:D in order,
+// ImproperPrior, no chain moments / mixture state, 17 ≤ D ≤ 64, the built-in GsnTargetLaw
+// over μ (d = D) or a user law
+bool block_eligible(const emcmc_handle *h, bool xt) {
+    const int D = (int)h->cfg.dim;
+    if (xt || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_BLOCK) || h->updates.size() != 1 || D < kBlockMinD || D > kMwgMaxD) return false;
+    const UpdateHost &u = h->updates[0];
+    if ((u.kernel != EMCMC_MALA && u.kernel != EMCMC_USER_UPDATE) || u.prior != EMCMC_PRIOR_IMPROPER ||
+        u.adaptation != EMCMC_ADPT_NONE || u.coords.size() != (size_t)D)
+        return false;
+    for (int j = 0; j < D; ++j)
+        if (u.coords[j] != (uint32_t)j) return false;
+    const TargetHost &t = h->target;
+    return t.kind == EMCMC_TARGET_USER || (t.kind == EMCMC_TARGET_GSN && (int)t.dim == D);
+}
+
+// BlockConsts (emcmc_block.h): L_t forward table (packed column-major, 1/L_jj on the
+// diagonal) | backward table (rows D−1 … 0: 1/L_jj, L_j0 … L_j,j−1) | x̄ | 1/L_ii | observations
+emcmc_status upload_block_consts(emcmc_handle *h) {
+    const TargetHost &t = h->target;
+    const int D = (int)h->cfg.dim;
+    const size_t P = (size_t)D * (D + 1) / 2;
+    std::vector<double> c(2 * P + 2 * (size_t)D + t.nobs * (size_t)D, 0.0);
+    for (int j = 0; j < D; ++j)
+        for (int i = j; i < D; ++i)
+            c[(size_t)chol_col(D, j) + (size_t)(i - j)] = (i == j) ? t.invdiag[j] : t.L[(size_t)i * D + j];
+    for (int tt = 0; tt < D; ++tt) {
+        const int j = D - 1 - tt;
+        double *r = c.data() + P + (size_t)chol_col(D, tt);
+        r[0] = t.invdiag[j];
+        for (int i = 0; i < j; ++i) r[1 + i] = t.L[(size_t)j * D + i];
+    }
+    std::copy(t.xbar.begin(), t.xbar.end(), c.begin() + 2 * P);
+    std::copy(t.invdiag.begin(), t.invdiag.end(), c.begin() + 2 * P + D);
+    std::copy(t.obs.begin(), t.obs.end(), c.begin() + 2 * P + 2 * D);
+    if (h->d_bconsts) (void)hipFree(h->d_bconsts);
+    h->d_bconsts = nullptr;
+    HIPCHK(h, hipMalloc(&h->d_bconsts, c.size() * sizeof(double)));
+    HIPCHK(h, hipMemcpy(h->d_bconsts, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));
+    return EMCMC_OK;
+}
+
 emcmc_status select_mwg(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
     if (h->allocated) {
@@ -510,8 +554,39 @@ emcmc_status select_mwg(emcmc_handle *h) {
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "MALA needs the target's gradient (compute_gradients_and_momenta!): the user law defines none "
                     "(EMCMC_USER_GRAD { … })");
+    // one MALA or user update over all 17 ≤ D ≤ 64 coordinates: mwg_block_kernel (emcmc_block.h),
+    // every per-chain vector in registers (the wide kernel's NU = D loops live in scratch)
+    if (block_eligible(h, xt)) {
+        const bool tdense = !h->target.diag;
+        if (!user && usrc.empty())
+            for (const auto &e : block_table())
+                if (e.D == D && e.tdense == (int)tdense && e.full == (int)full && e.ll == ll) v.mfn = e.fn;
+        if (!v.mfn) {
+            RtcKernel k;
+            const std::string log = rtc_compile_block(D, full, user ? 0 : ll, tdense, user ? h->target.src : "",
+                                                      user ? h->target.opts : "", usrc, uopts, k);
+            if (!log.empty()) {
+                h->err = std::string(user || !usrc.empty() ? "user target / update does not compile:\n"
+                                                            : "run-time kernel build failed:\n") +
+                         log;
+                return (user || !usrc.empty()) ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
+            }
+            if (emcmc_status st = load_rtc_module(h, k)) return st;
+            HIPCHK(h, hipModuleGetFunction(&v.ufn, h->umod, k.lowered.c_str()));
+            v.name = k.name;
+        } else {
+            char bn[160];
+            snprintf(bn, sizeof bn, "mwg_block_kernel<D=%d,%s,%s,%s,MALA>", D, full ? "FULL" : "ACCEPT_ONLY",
+                     ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", tdense ? "DENSE_T" : "DIAG_T");
+            v.name = bn;
+        }
+        v.block = true;
+        if (!user) {
+            if (emcmc_status st = upload_block_consts(h)) return st;
+        }
+    }
     for (const auto &e : mwg_table()) {
-        if (user || !usrc.empty() || xt || mala) break;
+        if (user || !usrc.empty() || xt || mala || v.block) break;
         if (e.D != D) continue;
         if (e.nu != 0 && ((size_t)e.nu < nmax || e.nu >= best_nu)) continue;  // smallest NU that fits
         if (e.nu != 0) best_nu = e.nu;
@@ -520,7 +595,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
     }
     // a user law, or a dimension without an ahead-of-time instantiation: the
     // same kernel compiled at run time (emcmc_rtc.hip, cached per process)
-    if (user || !usrc.empty() || xt || mala || (!v.mfn && D <= kMwgMaxD)) {
+    if (!v.block && (user || !usrc.empty() || xt || mala || (!v.mfn && D <= kMwgMaxD))) {
         RtcKernel k;
         const int nu = rtc_wide_nu(D, (int)nmax);
         const std::string log = user ? rtc_compile_user(h->target.src, h->target.opts, D, full, nu, k, usrc, uopts, xt,
@@ -625,7 +700,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
         (st = upload(h->d_obs, t.obs)) || (st = upload(h->d_uparams, t.params)))
         return st;
     char nm[160];
-    if (v.ufn)
+    if (v.ufn || v.block)
         snprintf(nm, sizeof nm, "%s", v.name.c_str());
     else if (best_nu < (1 << 30))
         snprintf(nm, sizeof nm, "mwg_wide_kernel<D=%d,NU=%d,P=%zu,%s,%s>", D, best_nu, h->updates.size(),
@@ -844,10 +919,7 @@ emcmc_status select_variant(emcmc_handle *h) {
         for (int i = 0; i < D; ++i) unit = unit && h->target.invdiag[i] == 1.0;
         v.unit = unit;
         // default: the 2-waves-per-SIMD register cap where instantiated (inst_diag2.hip)
-        const int occ = (h->cfg.kernel_variant & EMCMC_VARIANT_HIGH_OCCUPANCY) ? 4
-                        : (h->cfg.kernel_variant & EMCMC_VARIANT_OCCUPANCY3)   ? 3
-                        : (h->cfg.kernel_variant & EMCMC_VARIANT_UNCAPPED)     ? 0
-                                                                               : 2;
+        const int occ = (h->cfg.kernel_variant & EMCMC_VARIANT_UNCAPPED) ? 0 : 2;
         v.fn = lookup(D, lpc, full, ll, false, unit, occ);
         v.occ = occ;
         if (!v.fn && occ) {
@@ -889,7 +961,7 @@ emcmc_status select_variant(emcmc_handle *h) {
     snprintf(nm, sizeof nm, "rwm_gsn_%s_kernel<D=%d,LPC=%d,%s,%s%s%s>%s",
              v.dense == 3 ? "diag_s" : v.dense == 2 ? "chol" : v.dense ? "dense" : "diag", D, v.lpc,
              full ? "FULL" : "ACCEPT_ONLY", ll == LL_PER_OBS ? "PER_OBS" : "SUFFSTAT", v.unit ? ",UNIT_T" : "",
-             v.occ == 4 ? ",MINW=4" : v.occ == 3 ? ",MINW=3" : v.occ == 2 ? ",MINW=2" : "", v.ffn ? "[hiprtc]" : "");
+             v.occ == 2 ? ",MINW=2" : "", v.ffn ? "[hiprtc]" : "");
     v.name = nm;
     // constants for this variant
     std::vector<double> c;
@@ -1386,6 +1458,7 @@ emcmc_status run_mwg(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     a.scov = h->d_scov;
     a.chain_moments = h->cfg.chain_moments ? 1u : 0u;
     a.nhaario = h->nhaario;
+    a.consts = h->d_bconsts;
     if (P == 1 && h->updates[0].kernel == EMCMC_MALA) {  // one MALA update: carry ∇ℓ(θ) between steps
         if (!h->d_gcache) HIPCHK(h, hipMalloc(&h->d_gcache, C * (uint64_t)h->cfg.dim * sizeof(double)));
         a.gcache = h->d_gcache;
@@ -1919,17 +1992,47 @@ emcmc_status emcmc_check_user_update(const char *source, uint32_t dim, const cha
     return log.empty() ? EMCMC_OK : EMCMC_INVALID_ARG;
 }
 
-emcmc_status emcmc_prebuild_chol_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, char *log_out,
-                                        size_t log_len) {
-    if (dim < 2 || dim > (uint32_t)kCholRtcMaxD || history_mode > 1 || ll_mode > 1) return EMCMC_INVALID_ARG;
-    RtcKernel k;
-    const std::string log = rtc_compile_chol((int)dim, history_mode == EMCMC_HIST_FULL, (int)ll_mode, k);
+namespace {
+void copy_log(const std::string &log, char *log_out, size_t log_len) {
     if (log_out && log_len) {
         const size_t n = std::min(log.size(), log_len - 1);
         std::memcpy(log_out, log.data(), n);
         log_out[n] = '\0';
     }
+}
+}  // namespace
+
+emcmc_status emcmc_prebuild_chol_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, char *log_out,
+                                        size_t log_len) {
+    if (dim < 2 || dim > (uint32_t)kCholRtcMaxD || history_mode > 1 || ll_mode > 1) return EMCMC_INVALID_ARG;
+    copy_log("", log_out, log_len);
+    if (lookup((int)dim, 1, history_mode == EMCMC_HIST_FULL, (int)ll_mode, 2, false)) return EMCMC_OK;  // ahead of time
+    RtcKernel k;
+    const std::string log = rtc_compile_chol((int)dim, history_mode == EMCMC_HIST_FULL, (int)ll_mode, k);
+    copy_log(log, log_out, log_len);
     return log.empty() ? EMCMC_OK : EMCMC_HIP_ERROR;
+}
+
+emcmc_status emcmc_prebuild_block_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, int dense_target,
+                                         const char *target_source, const char *target_options,
+                                         const char *update_source, const char *update_options, char *log_out,
+                                         size_t log_len) {
+    if (dim < (uint32_t)kBlockMinD || dim > (uint32_t)kMwgMaxD || history_mode > 1 || ll_mode > 1)
+        return EMCMC_INVALID_ARG;
+    copy_log("", log_out, log_len);
+    const bool full = history_mode == EMCMC_HIST_FULL, user = target_source && *target_source;
+    const bool upd = update_source && *update_source;
+    if (!user && !upd)
+        for (const auto &e : block_table())
+            if (e.D == (int)dim && e.tdense == (dense_target ? 1 : 0) && e.full == (int)full && e.ll == (int)ll_mode)
+                return EMCMC_OK;  // ahead of time
+    RtcKernel k;
+    const std::string log =
+        rtc_compile_block((int)dim, full, user ? 0 : (int)ll_mode, dense_target != 0, user ? target_source : "",
+                          target_options ? target_options : "", upd ? update_source : "",
+                          update_options ? update_options : "", k);
+    copy_log(log, log_out, log_len);
+    return log.empty() ? EMCMC_OK : (user || upd) ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
 }
 
 emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {
@@ -2128,7 +2231,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_tiL,       h->d_xbar,      h->d_aprop,   h->d_aacc,     h->d_steps, h->d_mwg,
                     h->d_mean,      h->d_cov,       h->d_LB,      h->d_iLB,      h->d_c0B,   h->d_Lnew,
                     h->d_grad,      h->d_X,         h->d_y,       h->d_mom_scratch, h->d_mean_alt, h->d_mom_consts,
-                    h->d_ll_prop,   h->d_uparams,   h->d_gcache};
+                    h->d_ll_prop,   h->d_uparams,   h->d_gcache,  h->d_bconsts};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     if (h->umod) (void)hipModuleUnload(h->umod);

@@ -12,6 +12,7 @@
 #include "emcmc_mala.h"
 #include "emcmc_mix.h"
 #include "emcmc_mwg.h"
+#include "emcmc_block.h"
 
 namespace emcmc {
 
@@ -41,6 +42,15 @@ struct MwgEntry {
     MwgFn full_perobs, full_suff, acc_perobs, acc_suff;
 };
 const std::vector<MwgEntry> &mwg_table();
+
+// one MALA update over all D coordinates on the built-in GsnTargetLaw (mwg_block_kernel,
+// emcmc_block.h), ahead of time at the D listed in inst_block.hip; other 17 ≤ D ≤ 64,
+// user updates and user laws compile at run time
+struct BlockEntry {
+    int D, tdense, full, ll;
+    MwgFn fn;
+};
+const std::vector<BlockEntry> &block_table();
 
 // GaussianRandomWalkMix / chain moments (mix_gsn_kernel, mix_moments_kernel, mix_readjust_kernel)
 struct MixEntry {

@@ -136,6 +136,7 @@ struct MwgParams {
     double *mixpool;           // GaussianRandomWalkMix / Haario per-chain state (MwgUpdate offsets)
     double *smean, *scov;      // GenericChainStats mean [D][C] and cov packed lower [D(D+1)/2][C]
     double *gcache;            // [D][C] ∇ℓ at the current θ (state_pos layout), or null: the MALA carry below
+    const double *consts;      // mwg_block_kernel's constant table (emcmc_block.h BlockConsts), else null
     uint64_t C;
     uint64_t row_bytes;
     uint64_t N0;

@@ -111,4 +111,13 @@ constexpr int kCholRtcMaxChunks = 400;
 inline int chol_rtc_chunks(int D) { return (D + 15) / 16 + (D * (D + 1) / 2 + 15) / 16; }
 std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out);
 
+// mwg_block_kernel<D, FULL, LL, TGT, UPD> (emcmc_block.h): one MALA or user update over
+// all 17 ≤ D ≤ 64 coordinates with the per-chain vectors in registers.  src: a user
+// law (TGT = its loglik / grad), else the built-in GsnTargetLaw through the scalar
+// cache (TGT = GsnSweep<tdense>); usrc: a user update (UPD = its proposal! /
+// log_transition_density), else MALA.
+std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const std::string &src,
+                              const std::string &opts, const std::string &usrc, const std::string &uopts,
+                              RtcKernel &out);
+
 }  // namespace emcmc

@@ -152,9 +152,37 @@ struct Digest {
     }
 };
 
-const char kDiskMagic[8] = {'E', 'M', 'C', 'R', 'T', 'C', '1', '\n'};
+// Entry file: magic | lowered-name length, name | code length, code | 128-bit digest of
+// (name, code).  A reader checks the digest, so a torn, truncated or zero-filled file is a
+// miss (recompiled), never a code object that runs.
+const char kDiskMagic[8] = {'E', 'M', 'C', 'R', 'T', 'C', '2', '\n'};
 
-bool disk_get(const std::string &file, RtcKernel &k) {
+std::string payload_digest(const RtcKernel &k) {
+    Digest d;
+    d.add(k.lowered);
+    d.add(k.code.data(), k.code.size());
+    return d.hex();
+}
+
+// The cache directory is used only when it is private to this user: owned by the
+// effective uid and neither group- nor world-writable (else anyone who can write it could
+// plant a code object every later handle would execute).  Created 0700 when absent.
+bool private_dir(const std::string &dir, bool create) {
+    struct stat st;
+    if (stat(dir.c_str(), &st) != 0) {
+        if (!create || mkdir(dir.c_str(), 0700) != 0 || stat(dir.c_str(), &st) != 0) return false;
+    }
+    if (!S_ISDIR(st.st_mode) || st.st_uid != geteuid() || (st.st_mode & (S_IWGRP | S_IWOTH))) {
+        if (getenv("EMCMC_RTC_LOG"))
+            fprintf(stderr, "[emcmc rtc] %s is not a private directory of this user: on-disk cache not used\n",
+                    dir.c_str());
+        return false;
+    }
+    return true;
+}
+
+bool disk_get(const std::string &dir, const std::string &file, RtcKernel &k) {
+    if (!private_dir(dir, false)) return false;
     std::ifstream f(file, std::ios::binary);
     if (!f) return false;
     char m[8];
@@ -166,27 +194,29 @@ bool disk_get(const std::string &file, RtcKernel &k) {
     if (!f.read(reinterpret_cast<char *>(&nc), 8) || nc == 0 || nc > (1ull << 30)) return false;
     k.code.resize(nc);
     if (!f.read(k.code.data(), (std::streamsize)nc)) return false;
+    char dg[32];
+    if (!f.read(dg, 32) || std::string(dg, 32) != payload_digest(k)) return false;
     return f.peek() == std::char_traits<char>::eof();  // a truncated or padded file is not an entry
 }
 
 void disk_put(const std::string &dir, const std::string &file, const RtcKernel &k) {
-    (void)mkdir(dir.c_str(), 0775);
-    const std::string tmp = file + ".tmp." + std::to_string((long)getpid());
-    {
-        std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
-        if (!f) return;  // read-only location: the process cache still holds it
-        const uint64_t nl = k.lowered.size(), nc = k.code.size();
-        f.write(kDiskMagic, 8);
-        f.write(reinterpret_cast<const char *>(&nl), 8);
-        f.write(k.lowered.data(), (std::streamsize)nl);
-        f.write(reinterpret_cast<const char *>(&nc), 8);
-        f.write(k.code.data(), (std::streamsize)nc);
-        if (!f) {
-            (void)unlink(tmp.c_str());
-            return;
-        }
+    if (!private_dir(dir, true)) return;
+    std::string tmp = file + ".tmp.XXXXXX";  // unique per writer (threads of one process included)
+    const int fd = mkstemp(&tmp[0]);
+    if (fd < 0) return;  // read-only location: the process cache still holds it
+    FILE *f = fdopen(fd, "wb");
+    if (!f) {
+        close(fd);
+        (void)unlink(tmp.c_str());
+        return;
     }
-    if (rename(tmp.c_str(), file.c_str()) != 0) (void)unlink(tmp.c_str());  // atomic: ranks may race
+    const uint64_t nl = k.lowered.size(), nc = k.code.size();
+    const std::string dg = payload_digest(k);
+    bool ok = fwrite(kDiskMagic, 1, 8, f) == 8 && fwrite(&nl, 8, 1, f) == 1 &&
+              fwrite(k.lowered.data(), 1, nl, f) == nl && fwrite(&nc, 8, 1, f) == 1 &&
+              fwrite(k.code.data(), 1, nc, f) == nc && fwrite(dg.data(), 1, 32, f) == 32;
+    ok = (fclose(f) == 0) && ok;
+    if (!ok || rename(tmp.c_str(), file.c_str()) != 0) (void)unlink(tmp.c_str());  // atomic: ranks may race
 }
 
 // EMCMC_RTC_EXTRA: extra options for every run-time compile (A/B builds of the run-time
@@ -238,7 +268,7 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
               "|HIP " + std::to_string(HIP_VERSION));
         dfile = dir + "/" + d.hex() + ".co";
         RtcKernel k;
-        if (disk_get(dfile, k)) {
+        if (disk_get(dir, dfile, k)) {
             k.name = name;
             k.origin = kRtcFromDisk;
             k.seconds = since();
@@ -366,6 +396,35 @@ std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
          << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
     return compile_kernel(key.str(), "#include \"emcmc_kernels.h\"\n", "chol_kernel.hip", expr.str(), name.str(),
                           {"-ftemplate-depth=2048"}, out);
+}
+
+std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const std::string &src,
+                              const std::string &opts, const std::string &usrc, const std::string &uopts,
+                              RtcKernel &out) {
+    if (D < 17 || D > 64) return "mwg_block_kernel runs 17 ≤ D ≤ 64";
+    const bool user = !src.empty(), upd = !usrc.empty();
+    std::ostringstream key, expr, name;
+    key << "block|" << D << '|' << full << '|' << ll_mode << '|' << tdense << '|' << opts << '|' << src << '|'
+        << uopts << '|' << usrc;
+    if (cache_get(key.str(), out)) return "";
+    const char *tgt = user ? "emcmc::UserTarget" : tdense ? "emcmc::GsnSweep<true>" : "emcmc::GsnSweep<false>";
+    expr << "emcmc::mwg_block_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ", " << tgt
+         << ", " << (upd ? "emcmc::UserUpdate" : "emcmc::MalaOnly") << ">";
+    name << "mwg_block_kernel<D=" << D << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (user ? "UserTarget" : ll_mode == 0 ? "PER_OBS" : "SUFFSTAT")
+         << (user ? "" : tdense ? ",DENSE_T" : ",DIAG_T") << (upd ? ",UserUpdate" : ",MALA") << "[hiprtc]>";
+    std::string prog_src = std::string(kPrelude) + "#include \"emcmc_block.h\"\n";
+    if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
+    if (upd) prog_src += std::string("#line 1 \"user_update\"\n") + usrc + "\n" + kUpdEpilogue;
+    std::vector<std::string> extra = {"-ftemplate-depth=2048"};
+    if (!upd) extra.push_back("-DEMCMC_RTC_MALA=1");
+    if (user && rtc_defines_user_grad(src)) extra.push_back("-DEMCMC_HAS_USER_GRAD=1");
+    for (const std::string *op : {&opts, &uopts}) {
+        std::istringstream is(*op);
+        for (std::string w; is >> w;) extra.push_back(w);
+    }
+    return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : upd ? "user_update.hip" : "block_kernel.hip",
+                          expr.str(), name.str(), extra, out);
 }
 
 const char *rtc_builtin_law(const char *name) {

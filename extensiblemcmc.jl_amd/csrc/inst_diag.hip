@@ -19,16 +19,6 @@ KernelFn dense_fn() {
         {{D, LPC, 0, 0, 0, U, 0}, diag_fn<D, LPC, false, 0, U>()},                                   \
         {{D, LPC, 0, 1, 0, U, 0}, diag_fn<D, LPC, false, 1, U>()}
 #define DIAG4(D, LPC) DIAGU(D, LPC, false), DIAGU(D, LPC, true)
-#define DIAGO(D, LPC, U)                                                                          \
-    {{D, LPC, 1, 0, 0, U, 4}, diag_fn<D, LPC, true, 0, U, 4>()},                                     \
-        {{D, LPC, 1, 1, 0, U, 4}, diag_fn<D, LPC, true, 1, U, 4>()},                                 \
-        {{D, LPC, 0, 0, 0, U, 4}, diag_fn<D, LPC, false, 0, U, 4>()},                                \
-        {{D, LPC, 0, 1, 0, U, 4}, diag_fn<D, LPC, false, 1, U, 4>()}
-#define DIAGO3(D, LPC, U)                                                                         \
-    {{D, LPC, 1, 0, 0, U, 3}, diag_fn<D, LPC, true, 0, U, 3>()},                                     \
-        {{D, LPC, 1, 1, 0, U, 3}, diag_fn<D, LPC, true, 1, U, 3>()},                                 \
-        {{D, LPC, 0, 0, 0, U, 3}, diag_fn<D, LPC, false, 0, U, 3>()},                                \
-        {{D, LPC, 0, 1, 0, U, 3}, diag_fn<D, LPC, false, 1, U, 3>()}
 #define DENSE4(D)                                                                                    \
     {{D, 1, 1, 0, 1, 0, 0}, dense_fn<D, true, 0>()}, {{D, 1, 1, 1, 1, 0, 0}, dense_fn<D, true, 1>()},   \
         {{D, 1, 0, 0, 1, 0, 0}, dense_fn<D, false, 0>()}, {{D, 1, 0, 1, 1, 0, 0}, dense_fn<D, false, 1>()}
@@ -36,8 +26,7 @@ const std::vector<Entry> &diag_table() {
     static const std::vector<Entry> t = {
         DIAG4(1, 1),  DIAG4(2, 1),  DIAG4(3, 1),  DIAG4(4, 1),  DIAG4(8, 1),
         DIAG4(16, 1), DIAG4(16, 2), DIAG4(32, 1), DIAG4(32, 2), DIAG4(32, 4),
-        DIAG4(64, 2), DIAG4(64, 4), DIAGO(32, 4, true), DIAGO(32, 4, false), DIAGO(32, 2, true),
-        DIAGO3(32, 2, true), DIAGO3(32, 4, true), DIAGO3(32, 1, true),
+        DIAG4(64, 2), DIAG4(64, 4),
         DENSE4(1),    DENSE4(2),    DENSE4(3),
         DENSE4(4),    DENSE4(8),
     };

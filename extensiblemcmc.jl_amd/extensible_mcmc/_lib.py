@@ -51,14 +51,13 @@ FAULT_NONFINITE_LL = 1
 FAULT_RNG_RETRIES = 2
 FAULT_POSDEF = 4
 FAULT_PRIOR_RESAMPLES = 8
-VARIANT_HIGH_OCCUPANCY = 1
-VARIANT_OCCUPANCY3 = 2
 VARIANT_SCALAR_OBS = 4
 VARIANT_MIX_STREAM = 8
 VARIANT_NO_XCD_ORDER = 16
 VARIANT_NO_RTC_CHOL = 32
 VARIANT_NO_MIX_CHOL = 64
 VARIANT_UNCAPPED = 128  # diag kernel without the 2-waves-per-SIMD register cap
+VARIANT_NO_BLOCK = 256  # one MALA / user update over all D > 16 coordinates: the wide kernel, not mwg_block_kernel
 
 
 class EmcmcConfig(C.Structure):
@@ -281,6 +280,9 @@ SIGNATURES = {
     "emcmc_kernel_name": (_ST, [_H, C.c_char_p, C.c_size_t]),
     "emcmc_rtc_info": (_ST, [_H, C.POINTER(C.c_uint32), C.POINTER(C.c_double)]),
     "emcmc_prebuild_chol_kernel": (_ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t]),
+    "emcmc_prebuild_block_kernel": (
+        _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+              C.c_size_t]),
     "emcmc_probe_variates": (
         _ST,
         [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -388,6 +390,19 @@ def prebuild_chol_kernel(dim: int, history_mode: int = 0, ll_mode: int = 0) -> N
     st = lib().emcmc_prebuild_chol_kernel(dim, history_mode, ll_mode, buf, len(buf))
     if st != OK:
         raise EMCMCError(st, "emcmc_prebuild_chol_kernel", buf.value.decode(errors="replace"))
+
+
+def prebuild_block_kernel(dim: int, history_mode: int = 0, ll_mode: int = 0, dense_target: bool = True,
+                          target_source: str = "", target_options: str = "", update_source: str = "",
+                          update_options: str = "") -> None:
+    """Compile mwg_block_kernel (one MALA or user update over all 17 ≤ dim ≤ 64 coordinates)
+    into the on-disk code-object cache (no device needed)."""
+    buf = C.create_string_buffer(1 << 16)
+    enc = lambda x: x.encode() if x else None  # noqa: E731
+    st = lib().emcmc_prebuild_block_kernel(dim, history_mode, ll_mode, int(bool(dense_target)), enc(target_source),
+                                           enc(target_options), enc(update_source), enc(update_options), buf, len(buf))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_prebuild_block_kernel", buf.value.decode(errors="replace"))
 
 
 def device_count() -> int:

@@ -168,19 +168,21 @@ typedef struct emcmc_config {
     uint32_t reserved[4];
 } emcmc_config;
 
-/* kernel_variant flags: performance-only choices, bit-identical results */
-#define EMCMC_VARIANT_HIGH_OCCUPANCY 1u  /* cap registers for 4 waves/SIMD where instantiated */
-#define EMCMC_VARIANT_OCCUPANCY3 2u      /* cap registers for 3 waves/SIMD where instantiated */
+/* kernel_variant flags: performance-only choices among kernels the library keeps for other
+ * shapes, bit-identical results (A/B timing).  Bits 1 and 2 selected register-capped builds of
+ * the diagonal kernel that lost their A/B; they are retired and ignored. */
 #define EMCMC_VARIANT_SCALAR_OBS 4u      /* diagonal Σ: one lane per chain, observations as SGPR operands */
 #define EMCMC_VARIANT_MIX_STREAM 8u      /* GaussianRandomWalkMix: stream L_B from HBM every step (mix_gsn_kernel)
                                             instead of keeping it in registers (mix_res_kernel) */
 #define EMCMC_VARIANT_NO_XCD_ORDER 16u   /* blocks in blockIdx order instead of one contiguous chain range per XCD */
 #define EMCMC_VARIANT_NO_RTC_CHOL 32u    /* a correlated Σ at a D without an ahead-of-time rwm_gsn_chol_kernel runs on
                                             the general kernel instead of the chol kernel compiled at run time */
-#define EMCMC_VARIANT_NO_MIX_CHOL 64u    /* GaussianRandomWalkMix / chain moments with a dense Σ_A or Σ_t at D = 16,
-                                            24, 32: the general kernel instead of mix_chol_kernel */
+#define EMCMC_VARIANT_NO_MIX_CHOL 64u    /* GaussianRandomWalkMix / chain moments with a dense Σ_A or Σ_t at D = 16 or
+                                            32: the general kernel instead of mix_chol_kernel */
 #define EMCMC_VARIANT_UNCAPPED 128u      /* diagonal fused kernel without the 2-waves-per-SIMD register cap
                                             (D = 16, 32, 64 build it at MINW = 2 by default) */
+#define EMCMC_VARIANT_NO_BLOCK 256u      /* one MALA / user update over all 17 ≤ D ≤ 64 coordinates: the general
+                                            wide kernel instead of mwg_block_kernel */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,
@@ -403,12 +405,23 @@ emcmc_status emcmc_check_user_target(const char *source, uint32_t dim, const cha
 emcmc_status emcmc_check_user_update(const char *source, uint32_t dim, const char *options, char *log_out,
                                      size_t log_len);
 
-/* Compile (no device needed) the run-time rwm_gsn_chol_kernel for a correlated
- * Σ at dimension dim (9 ≤ dim ≤ 64 without an ahead-of-time instantiation) into
- * the on-disk code-object cache (emcmc_rtc_info), so the first handle of a
- * deployment loads it instead of compiling it (≈ 1 minute at dim ≥ 40). */
+/* Compile (no device needed) the run-time rwm_gsn_chol_kernel for a correlated Σ at a
+ * dimension 2 ≤ dim ≤ 64 the library has no ahead-of-time instantiation of (it has 16, 24
+ * and 32: those return EMCMC_OK without compiling) into the on-disk code-object cache
+ * (emcmc_rtc_info), so the first handle of a deployment loads it instead of compiling it
+ * (≈ 1 minute at dim ≥ 40). */
 emcmc_status emcmc_prebuild_chol_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, char *log_out,
                                         size_t log_len);
+/* The same for mwg_block_kernel, the kernel a handle with ONE MALA update (update_source =
+ * NULL) or ONE user update (its EMCMC_USER_PROPOSAL/EMCMC_USER_LTD source) over coordinates
+ * 1:dim, ImproperPrior, selects at 17 ≤ dim ≤ 64: on the built-in GsnTargetLaw
+ * (target_source = NULL; dense_target != 0 for a non-diagonal Σ) or on a user law
+ * (target_source, its options).  MALA on GsnTargetLaw at dim = 32 is ahead of time (EMCMC_OK,
+ * nothing compiled). */
+emcmc_status emcmc_prebuild_block_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, int dense_target,
+                                         const char *target_source, const char *target_options,
+                                         const char *update_source, const char *update_options, char *log_out,
+                                         size_t log_len);
 
 /* θinit for every chain (row-major [C][D]); ll = NULL means the reference's
  * initial ll = -Inf (workspaces.jl:425), i.e. the first step always accepts.

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--haario-chains", type=int, default=131072)
     ap.add_argument("--haario-iters", type=int, default=400)
     ap.add_argument("--only", default="", help="comma-separated workload names (default: all)")
+    ap.add_argument("--variant", type=int, default=0, help="emcmc_config.kernel_variant (EMCMC_VARIANT_* A/B flags)")
     a = ap.parse_args()
     C, M = a.chains, a.iters
     w = W.cfg2(8)
@@ -68,9 +69,9 @@ def main():
         if want(name):
             haario_dense(name, variant, a.haario_chains, a.haario_iters, report)
     if want("mala_gsn_d32"):
-        mala_gsn(C, M, report)
+        mala_gsn(C, M, report, a.variant)
     if want("pcn_user_d32"):
-        pcn_user(C, M, report)
+        pcn_user(C, M, report, a.variant)
 
 
 def corr_d32(seed=32, D=32, nobs=10):
@@ -106,12 +107,12 @@ def haario_dense(name, variant, C, M, report):
     eng.close()
 
 
-def mala_gsn(C, M, report):
+def mala_gsn(C, M, report, variant=0):
     """MALA (ϵ = 0.05) on GsnTargetLaw(μ, BBᵀ/32 + I) at D = 32 (general kernel, the target's
     built-in gradient)."""
     D = 32
     mu, ts, obs = corr_d32(7)
-    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=5))
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=5, kernel_variant=variant))
     eng.add_mala_update(np.arange(D), 0.05)
     eng.set_gsn_target(mu, ts, obs)
     eng.set_state(np.tile(obs.mean(0), (C, 1)))
@@ -120,13 +121,13 @@ def mala_gsn(C, M, report):
     eng.close()
 
 
-def pcn_user(C, M, report):
+def pcn_user(C, M, report, variant=0):
     """The pCN user update (tests/user_updates/pcn.c, ρ = 0.9, σ = 0.3, centred at x̄) at D = 32
     on the correlated GsnTargetLaw (general kernel, run-time compiled)."""
     D = 32
     mu, ts, obs = corr_d32(9)
     src = (ROOT / "tests" / "user_updates" / "pcn.c").read_text()
-    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=6))
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=6, kernel_variant=variant))
     eng.add_user_update(np.arange(D), src, params=np.concatenate([[0.9, 0.3], obs.mean(0)]))
     eng.set_gsn_target(mu, ts, obs)
     eng.set_state(np.tile(obs.mean(0), (C, 1)))

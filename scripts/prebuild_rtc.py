@@ -20,6 +20,12 @@ DEFAULT = [(9, 0, 0), (12, 0, 1), (20, 0, 0), (20, 1, 0), (27, 0, 0), (33, 0, 0)
            (49, 0, 0), (64, 0, 0)]
 
 
+# mwg_block_kernel (one MALA / user update over all coordinates) of tests/test_gpu_block.py and
+# scripts/bench_general.py: (D, history mode, ll mode, dense target, user law, user update)
+BLOCK = [(20, 0, 0, True, None, None), (40, 0, 0, True, None, None), (32, 0, 0, True, None, "pcn"),
+         (20, 0, 0, True, "logistic_regression", None)]
+
+
 def one(job):
     D, hist, ll = job
     t = time.time()
@@ -27,8 +33,20 @@ def one(job):
     return f"D={D} hist={hist} ll={ll}: {time.time() - t:.1f} s"
 
 
+def one_block(job):
+    D, hist, ll, dense, law, upd = job
+    t = time.time()
+    tsrc = (ROOT / "tests" / "user_targets" / f"{law}.c").read_text() if law else ""
+    usrc = (ROOT / "tests" / "user_updates" / f"{upd}.c").read_text() if upd else ""
+    L.prebuild_block_kernel(D, hist, ll, dense, target_source=tsrc, update_source=usrc)
+    return f"block D={D} hist={hist} ll={ll} law={law} update={upd or 'MALA'}: {time.time() - t:.1f} s"
+
+
 if __name__ == "__main__":
     jobs = [(int(d), 0, 0) for d in sys.argv[1:]] or DEFAULT
     with ThreadPoolExecutor(4) as ex:
-        for line in ex.map(one, jobs):
-            print(line, flush=True)
+        futs = [ex.submit(one, j) for j in jobs]
+        if not sys.argv[1:]:
+            futs += [ex.submit(one_block, j) for j in BLOCK]
+        for f in futs:
+            print(f.result(), flush=True)

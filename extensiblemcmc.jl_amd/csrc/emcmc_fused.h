@@ -13,17 +13,9 @@ namespace emcmc {
 // threads when MINW ≥ 3, so a single copy of the 70 KiB of tables serves
 // MINW waves per SIMD (two 256-thread blocks, each with its own copy, are
 // all the LDS allows)
-#ifndef EMCMC_DIAG_BLOCK2
-#define EMCMC_DIAG_BLOCK2 256  // threads per block at ≤ 2 waves/SIMD (512: one table copy per CU)
-#endif
 // MINW = 2 with sibling pacing (below): one 512-thread block per CU, whose two
-// waves on each SIMD keep pace with each other
-#ifndef EMCMC_PACE
-#define EMCMC_PACE 1
-#endif
-constexpr int diag_block(int MINW) {
-    return MINW >= 3 ? 256 * MINW : (MINW == 2 && EMCMC_PACE) ? 512 : EMCMC_DIAG_BLOCK2;
-}
+// waves on each SIMD keep pace with each other; 256 threads otherwise
+constexpr int diag_block(int MINW) { return MINW >= 3 ? 256 * MINW : MINW == 2 ? 512 : 256; }
 
 // Sibling pacing.  Two waves share a SIMD at MINW = 2, and the SIMD issues for the
 // older one whenever it is ready (age order), so it runs ahead: on MI355X the older
@@ -48,37 +40,6 @@ struct SiblingPace {
     }
 };
 
-// Timing-only build (make trace → lib/libemcmc_trace.so, scripts/trace_diag.py):
-// every wave of rwm_gsn_diag_kernel records the 100 MHz real-time counter at its
-// start, after the table staging, after its carried state arrived, at the end of
-// every step and after its last stores drained.  Not a product path.
-#ifndef EMCMC_TRACE
-#define EMCMC_TRACE 0
-#endif
-#if EMCMC_TRACE
-constexpr int kTraceSlots = 128, kTraceWaves = 16384;
-static __device__ uint64_t emcmc_trace_buf[kTraceSlots * kTraceWaves];
-__device__ __forceinline__ void trace_mark(uint32_t wave, int idx) {
-    const uint64_t t = __builtin_amdgcn_s_memrealtime();
-    if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kTraceWaves && idx < kTraceSlots)
-        emcmc_trace_buf[(size_t)wave * kTraceSlots + idx] = t;  // one lane: a vector store under exec
-}
-// where the wave runs: HW_ID (wave, SIMD, CU, SH, SE fields) and XCC_ID, in slots 124 / 125
-__device__ __forceinline__ void trace_where(uint32_t wave) {
-    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4), xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);
-    if ((threadIdx.x & 63) == 0 && wave < (uint32_t)kTraceWaves) {
-        emcmc_trace_buf[(size_t)wave * kTraceSlots + 124] = hw;
-        emcmc_trace_buf[(size_t)wave * kTraceSlots + 125] = xcc;
-    }
-}
-#define EMCMC_TRACE_MARK(w, i) trace_mark((w), (i))
-#else
-#define EMCMC_TRACE_MARK(w, i) ((void)0)
-#endif
-#ifndef EMCMC_EARLY_STATE
-#define EMCMC_EARLY_STATE 0  // 1: the carried state's loads are issued before the table staging
-#endif
-
 // MINW = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
 template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1>
@@ -91,7 +52,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
     const int nconst = 4 * D;
-    constexpr bool kPace = MINW == 2 && EMCMC_PACE;
+    constexpr bool kPace = MINW == 2;
     constexpr int kWavesPerBlock = diag_block(MINW) / 64;
     __shared__ uint32_t pace_prog[kWavesPerBlock], pace_simd[kWavesPerBlock];
     if constexpr (kPace) {
@@ -100,32 +61,16 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
             pace_prog[threadIdx.x >> 6] = 0u;
         }
     }  // (stage_lds's barrier orders these before the sibling search)
-#if EMCMC_TRACE
-    const uint32_t twave = (uint32_t)((xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x) >> 6);
-    EMCMC_TRACE_MARK(twave, 0);
-    trace_where(twave);
-#endif
-#if !EMCMC_EARLY_STATE
     const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
-#endif
     const double *cst0 = lds;
-    EMCMC_TRACE_MARK(twave, 1);
 
     const uint64_t tid = (uint64_t)xcd_block(blockIdx.x, gridDim.x, a.xcd) * blockDim.x + threadIdx.x;
-#if EMCMC_EARLY_STATE
-    // the carried state's loads go out first and stay in flight during the
-    // table staging (lanes past C read chain 0 and leave after the barrier)
-    const uint64_t chain = (tid / LPC < a.C) ? tid / LPC : 0;
-#else
     const uint64_t chain = tid / LPC;
-#endif
     const int sub = (int)(tid % LPC);
-#if !EMCMC_EARLY_STATE
     if (chain >= a.C) {
         if (kPace && (threadIdx.x & 63) == 0) pace_prog[threadIdx.x >> 6] = ~0u;  // no steps to pace
         return;
     }
-#endif
     const int d0 = sub * DPL;
     const uint32_t gid = a.chain0 + (uint32_t)chain;
 
@@ -140,19 +85,6 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     uint64_t r0 = chain_elem(a.ring, 2 * c32), r1 = chain_elem(a.ring, 2 * c32 + 1);
     uint32_t nacc = chain_elem(a.nacc, c32);
     uint32_t faults = chain_elem(a.faults, c32);
-#if EMCMC_EARLY_STATE
-    const ZigTabs zt = stage_lds(lds, a.zig, a.consts, nconst, a.obs, (LLMODE == LL_PER_OBS) ? (int)nobs * D : 0);
-    if (tid / LPC >= a.C) {
-        if (kPace && (threadIdx.x & 63) == 0) pace_prog[threadIdx.x >> 6] = ~0u;  // no steps to pace
-        return;
-    }
-#endif
-    constexpr bool kBatched = diag_batched(D, LPC);
-    const size_t used = lds_align16(sizeof(double) * (size_t)(nconst + ((LLMODE == LL_PER_OBS) ? (int)nobs * D : 0)));
-    const WaveScratch<DPL> ws(reinterpret_cast<char *>(lds) + used +
-                              (threadIdx.x >> 6) * (size_t)WaveScratch<DPL>::kBytes);
-    const uint32_t wave_gid0 = a.chain0 + (uint32_t)((tid & ~(uint64_t)63) / LPC);
-    if constexpr (kBatched) ws.fl[__lane_id()] = 0;
     SiblingPace pace{pace_prog, (int)(threadIdx.x >> 6), -1};
     if constexpr (kPace) {
         const int nw = (int)(blockDim.x >> 6);
@@ -160,15 +92,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
             if (w != pace.me && pace.sib < 0 && pace_simd[w] == pace_simd[pace.me]) pace.sib = w;
     }
     AcceptStream accs;
-#if EMCMC_VKEYS
     const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
-#else
-    const PhiloxVKeys vkeys{};
-#endif
-#if EMCMC_TRACE
-    __builtin_amdgcn_s_waitcnt(0);  // the carried state has arrived
-    EMCMC_TRACE_MARK(twave, 2);
-#endif
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
@@ -181,12 +105,8 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         const double *X = cst + 4 * D;
         // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151)
         double thp[DPL];
-        if constexpr (kBatched)
-            propose_diag_batched<DPL, LPC>(zt, ws, a.key0, a.key1, gid, wave_gid0, iter, a.pidx0, (uint32_t)d0, th,
-                                           Lrw + d0, thp);
-        else
-            propose_diag<DPL, EMCMC_VKEYS != 0>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0,
-                                                thp, faults, vkeys);
+        propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults,
+                                vkeys);
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
         const double ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
@@ -252,7 +172,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
         // ---- accept_reject! (run.jl:271-278), left-associative as written
         const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
-        const double E = accs.next<EMCMC_VKEYS != 0>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
+        const double E = accs.next<true>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
         const bool acc = E > -llr;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
         if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
@@ -274,20 +194,15 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         // ---- update_stats! rolling acceptance (chain_statistics.jl:53-65)
         ra = rolling_update(ra, r0, r1, iter, a.W, a.N0 + s, a.rcp_W, acc);
         if constexpr (kPace) pace.publish(s + 1);
-        EMCMC_TRACE_MARK(twave, 3 + (int)s);
     }
     if constexpr (kPace) {
         pace.publish(~0u);  // done: the sibling, alone now, stops lowering itself
         __builtin_amdgcn_s_setprio(0);
     }
 
-    if constexpr (kBatched) {
-        wave_lds_sync();
-        faults |= ws.fl[__lane_id()];
-        // the chain's lanes may hold different resolver fault bits
-        if constexpr (LPC >= 2) faults |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)faults, 0xB1, 0xF, 0xF, false);
-        if constexpr (LPC >= 4) faults |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)faults, 0x4E, 0xF, 0xF, false);
-    }
+    // the chain's lanes may hold different rare-path fault bits (each draws its own normals)
+    if constexpr (LPC >= 2) faults |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)faults, 0xB1, 0xF, 0xF, false);
+    if constexpr (LPC >= 4) faults |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)faults, 0x4E, 0xF, 0xF, false);
     if (sub == 0) {
         chain_elem(a.ll, c32) = ll;
         chain_elem(a.ra, c32) = ra;
@@ -298,11 +213,6 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         if (faults) *a.fault_flag = 1u;
     }
     store_slot_cached<D>(a.theta, soff, th);
-#if EMCMC_TRACE
-    EMCMC_TRACE_MARK(twave, kTraceSlots - 2);
-    __builtin_amdgcn_s_waitcnt(0);  // this wave's stores acknowledged
-    EMCMC_TRACE_MARK(twave, kTraceSlots - 1);
-#endif
 }
 
 // ---------------------------------------------------------------------------

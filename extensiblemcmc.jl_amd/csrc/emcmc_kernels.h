@@ -134,12 +134,6 @@ __device__ __forceinline__ ZigTabs stage_lds(double *lds, const Ziggurat *zig, c
     return ZigTabs{tabs.n, zig->nf, tabs.e, tabs.ef};
 }
 
-#ifndef EMCMC_SERIAL_PAIRS
-#define EMCMC_SERIAL_PAIRS 1
-#endif
-// 1: keep the scheduler from interleaving the Philox blocks of different
-// pairs (register pressure → occupancy; the waves of a SIMD supply the ILP)
-constexpr bool kSerialPairs = EMCMC_SERIAL_PAIRS != 0;
 
 // N normals of (chain, iter, pidx0) with lane-local index i ↔ global normal
 // index g0 + i, written as out[i] = base[i] + scale[i]·z (the diagonal
@@ -156,7 +150,9 @@ __device__ __forceinline__ void propose_diag(const ZigTabs &zt, uint32_t key0, u
     uint32_t pend = 0;
 #pragma unroll
     for (int j = 0; j < NP; ++j) {
-        if constexpr (kSerialPairs) __builtin_amdgcn_sched_barrier(0);
+        // one Philox block at a time: interleaving the pairs' blocks costs registers
+        // (occupancy), and the waves of a SIMD supply the ILP
+        __builtin_amdgcn_sched_barrier(0);
         u32x4 r;
         if constexpr (VK) r = draw_vk(vk, chain, iter, (g0 >> 1) + j, pidx0);
         else r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
@@ -164,7 +160,6 @@ __device__ __forceinline__ void propose_diag(const ZigTabs &zt, uint32_t key0, u
         if (2 * j + 1 < N)
             if (!zig_normal_fast(zig_split_n(r.z, r.w), zt.n, out[2 * j + 1])) pend |= 1u << (2 * j + 1);
     }
-    if constexpr ((EMCMC_ABLATE & 2) != 0) pend = 0;  // timing-only build: no rare paths
     // wave-uniform loop, one pending draw per lane per trip (with 8192 normal
     // layers a wave of 1024 draws has ≈ 0.6 pending, usually on one lane); the
     // result is written with selects OUTSIDE the divergent region, so the
@@ -182,46 +177,6 @@ __device__ __forceinline__ void propose_diag(const ZigTabs &zt, uint32_t key0, u
     for (int i = 0; i < N; ++i) out[i] = base[i] + scale[i] * out[i];
 }
 
-// ---------------------------------------------------------------------------
-// Wave-batched rare paths (diag kernels).  Per wave the LDS holds
-//   zs[64][N]  this step's normals, lane-major (N = coordinates per lane)
-//   q[64]      rare-path work queue: (owner lane << 8) | lane-local index
-//   fl[64]     fault bits raised by resolvers on behalf of each owner lane
-// Every lane writes its fast-path normals to zs; a draw that fails the fast
-// test is queued; then the wave's active lanes resolve up to 64 queued draws
-// at once (one rare-path pass per wave-step, however the failures spread over
-// lanes) and write the values into the owner's zs slots; each lane reads its
-// N normals back.  No lane-dynamic register indexing, no per-lane retry loop.
-#ifndef EMCMC_BATCH_MODE
-#define EMCMC_BATCH_MODE 2  // 1: all normals round-trip through LDS; 2: compact results + selects
-#endif
-template <int N>
-struct WaveScratch {
-    static constexpr int kZs = (EMCMC_BATCH_MODE == 1) ? 64 * N * 8 : 64 * 8;
-    static constexpr int kBytes = kZs + 64 * 4 + 64 * 4;
-    double *zs;  // mode 1: [64][N] normals; mode 2: [64] resolved values by queue position
-    uint32_t *q;
-    uint32_t *fl;
-    __device__ __forceinline__ explicit WaveScratch(char *base) {
-        zs = reinterpret_cast<double *>(base);
-        q = reinterpret_cast<uint32_t *>(base + kZs);
-        fl = q + 64;
-    }
-};
-
-// LDS bytes of the per-wave scratch of a diag kernel (4 waves per block); the
-// scratch starts 16-byte aligned after the tables, constants and observations.
-// (batched only for ≤ 16 coordinates per lane: 4 waves × 64 lanes × 16 × 8 B
-// = 32 KiB of normals per block keeps the block within 64 KiB of LDS)
-#ifndef EMCMC_BATCHED
-#define EMCMC_BATCHED 0  // 1: wave-batched rare paths (the better choice with 256 normal layers)
-#endif
-constexpr bool diag_batched(int D, int LPC) { return EMCMC_BATCHED && (D / LPC) % 2 == 0 && D / LPC <= 16; }
-// (diag_block, the diag kernel's threads per block: emcmc_fused.h)
-constexpr size_t diag_scratch_bytes(int D, int LPC, int waves = 4) {
-    return diag_batched(D, LPC) ? waves * (size_t)(((EMCMC_BATCH_MODE == 1) ? 64 * (D / LPC) * 8 : 64 * 8) + 64 * 4 + 64 * 4)
-                                : 0;
-}
 __host__ __device__ constexpr size_t lds_align16(size_t b) { return (b + 15) & ~(size_t)15; }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -230,118 +185,6 @@ __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ uint32_t lane_rank(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
-
-// θ° = base + scale·z for the lane's N coordinates (lane-local index i ↔
-// normal g0 + i of chain `chain`); LPC lanes per chain, so lane L of the wave
-// owns chain gid0 + L/LPC and normals (L % LPC)·N + i.
-template <int N, int LPC>
-__device__ __forceinline__ void propose_diag_batched(const ZigTabs &zt, const WaveScratch<N> &ws, uint32_t key0,
-                                                     uint32_t key1, uint32_t chain, uint32_t wave_gid0,
-                                                     uint32_t iter, uint32_t pidx0, uint32_t g0,
-                                                     const double (&base)[N], const double *scale,
-                                                     double (&out)[N]) {
-    static_assert(N % 2 == 0, "pairs");
-    const uint32_t lane = __lane_id();
-    uint32_t pend = 0;
-    // software-pipelined fast pass: pair j's Philox block and table reads are
-    // issued before pair j−1 is consumed, so the LDS latency of the lookups
-    // hides behind the next block's integer work
-    ZigDraw pa, pb;
-    ZigNPair ta, tb;
-#pragma unroll
-    for (int j = 0; j <= N / 2; ++j) {
-        ZigDraw na, nb;
-        ZigNPair sa, sb;
-        if (j < N / 2) {
-            __builtin_amdgcn_sched_barrier(0);
-            const u32x4 r = draw(key0, key1, chain, iter, (g0 >> 1) + j, pidx0, 0);
-            na = zig_split_n(r.x, r.y);
-            nb = zig_split_n(r.z, r.w);
-            sa = zig_npair(zt.n, na);
-            sb = zig_npair(zt.n, nb);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        if (j > 0) {
-            const int k = j - 1;
-            out[2 * k] = zig_scale(pa.v, with_sign(ta.w, pa.sbit));
-            out[2 * k + 1] = zig_scale(pb.v, with_sign(tb.w, pb.sbit));
-            if (!(fabs(out[2 * k]) < ta.b)) pend |= 1u << (2 * k);
-            if (!(fabs(out[2 * k + 1]) < tb.b)) pend |= 1u << (2 * k + 1);
-            if constexpr (EMCMC_BATCH_MODE == 1)
-                reinterpret_cast<d2v *>(ws.zs + lane * N)[k] = d2v{out[2 * k], out[2 * k + 1]};
-        }
-        if (j < N / 2) {
-            pa = na;
-            pb = nb;
-            ta = sa;
-            tb = sb;
-        }
-    }
-    if constexpr ((EMCMC_ABLATE & 2) != 0) pend = 0;  // timing-only build: no rare paths
-    if (__ballot(pend != 0) != 0) {
-        const uint32_t rank = lane_rank(__ballot(true));  // resolver slot among active lanes
-        uint32_t rem = pend;
-        while (__ballot(rem != 0) != 0) {
-            const uint32_t rem0 = rem;
-            uint32_t qn = 0;  // wave-uniform queue fill
-            for (;;) {
-                const uint64_t m = __ballot(rem != 0);
-                if (m == 0 || qn >= 64) break;
-                const uint32_t pos = qn + lane_rank(m);
-                if (rem != 0 && pos < 64) {
-                    ws.q[pos] = (lane << 8) | (uint32_t)__builtin_ctz(rem);
-                    rem &= rem - 1;
-                }
-                const uint32_t c = (uint32_t)__popcll(m);
-                qn = (qn + c > 64) ? 64 : qn + c;
-            }
-            wave_lds_sync();
-            if (rank < qn) {
-                const uint32_t e = ws.q[rank];
-                const uint32_t ol = e >> 8, i = e & 0xFFu;
-                uint32_t f = 0;
-                const double z = normal_draw(zt, key0, key1, wave_gid0 + ol / LPC, iter, pidx0,
-                                             (ol % LPC) * N + i, f);
-                if constexpr (EMCMC_BATCH_MODE == 1) ws.zs[ol * N + i] = z;
-                else ws.zs[rank] = z;
-                if (f) atomicOr(ws.fl + ol, f);
-            }
-            wave_lds_sync();
-            if constexpr (EMCMC_BATCH_MODE == 2) {
-                // replay the queue order to find this lane's results
-                uint32_t rr = rem0, qb = 0;
-                for (;;) {
-                    const uint64_t m = __ballot(rr != 0);
-                    if (m == 0 || qb >= 64) break;
-                    const uint32_t pos = qb + lane_rank(m);
-                    const bool take = rr != 0 && pos < 64;
-                    const uint32_t i = take ? (uint32_t)__builtin_ctz(rr) : 0xFFu;
-                    const double z = ws.zs[take ? pos : 0];
-#pragma unroll
-                    for (int qq = 0; qq < N; ++qq) out[qq] = (i == (uint32_t)qq) ? z : out[qq];
-                    if (take) rr &= rr - 1;
-                    const uint32_t c = (uint32_t)__popcll(m);
-                    qb = (qb + c > 64) ? 64 : qb + c;
-                }
-                wave_lds_sync();
-            }
-        }
-    }
-    if constexpr (EMCMC_BATCH_MODE == 1) {
-#pragma unroll
-        for (int j = 0; j < N / 2; ++j) {
-            const d2v z = reinterpret_cast<const d2v *>(ws.zs + lane * N)[j];
-            out[2 * j] = z.x;
-            out[2 * j + 1] = z.y;
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = base[i] + scale[i] * out[i];
 }
 
 // The N standard normals themselves (dense-L proposals).
@@ -388,7 +231,7 @@ struct AcceptStream {
         }
         const ZigDraw d = accept_split(r, iter);
         double e;
-        if (!zig_exp_fast(d, zt.e, e) && (EMCMC_ABLATE & 2) == 0) e = zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
+        if (!zig_exp_fast(d, zt.e, e)) e = zig_exp_slow(d, zt.e, zt.ef, key0, key1, chain, iter, kBlockAccept, pidx0, faults);
         return e;
     }
 };
@@ -434,12 +277,6 @@ __device__ __forceinline__ double tree_inplace(double (&b)[N]) {
     return b[0];
 }
 
-#ifndef EMCMC_VKEYS
-#define EMCMC_VKEYS 1  // Philox round keys precomputed once into VGPRs (diag kernel); 0: derived per call (SALU)
-#endif
-#ifndef EMCMC_SUMSQ_BARRIER
-#define EMCMC_SUMSQ_BARRIER 1
-#endif
 // Σ y_i² in the canonical order with y_i = yf(i) produced on the fly, one
 // block at a time (sched barriers keep the scheduler from materialising all
 // NV values — e.g. a whole observation row — at once).
@@ -450,7 +287,7 @@ __device__ __forceinline__ double canon_sumsq_f(YF yf) {
     double b[BPL];
 #pragma unroll
     for (int k = 0; k < BPL; ++k) {
-        if constexpr (BPL > 1 && EMCMC_SUMSQ_BARRIER) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (BPL > 1) __builtin_amdgcn_sched_barrier(0);
         const double y0 = yf(k * BLK);
         double s = y0 * y0;
 #pragma unroll
@@ -602,11 +439,7 @@ __device__ __forceinline__ void store_slot(double *slot_base, const SlotOffset<D
 #pragma unroll
         for (int j = 0; j < N / 2; ++j) {
             d2v x = {v[2 * j], v[2 * j + 1]};
-#if EMCMC_HIST_PLAIN  // timing-only A/B builds: plain instead of nontemporal history stores
-            *reinterpret_cast<d2v *>(b + (uint64_t)j * off.stride + off.o) = x;
-#else
             __builtin_nontemporal_store(x, reinterpret_cast<d2v *>(b + (uint64_t)j * off.stride + off.o));
-#endif
         }
     } else {
 #pragma unroll
@@ -847,12 +680,10 @@ __device__ __forceinline__ void store_slot_late(double *slot_base, const SlotOff
     }
 }
 
-#ifndef EMCMC_CHOL_SHARED
-#define EMCMC_CHOL_SHARED 52  // D from which ltd and the likelihood share one sweep (0: never; A/B via EMCMC_RTC_EXTRA)
-#endif
+constexpr int kCholSharedD = 52;  // D from which ltd and the likelihood share one sweep
 template <int D, bool FULL, int LLMODE>
 __global__ void __launch_bounds__(256) rwm_gsn_chol_kernel(const StepParams a) {
-    constexpr bool kCholShared = EMCMC_CHOL_SHARED > 0 && D >= EMCMC_CHOL_SHARED;
+    constexpr bool kCholShared = D >= kCholSharedD;
     const ZigTabs zt = stage_lds(nullptr, a.zig, nullptr, 0, nullptr, 0);
     constexpr int P = D * (D + 1) / 2;
 

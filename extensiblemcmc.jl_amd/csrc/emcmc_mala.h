@@ -27,12 +27,6 @@ namespace emcmc {
 
 typedef double mala_d4 __attribute__((ext_vector_type(4)));
 
-#ifndef EMCMC_MALA_IEEE_DIV
-#define EMCMC_MALA_IEEE_DIV 0
-#endif
-#ifndef EMCMC_MALA_ABLATE
-#define EMCMC_MALA_ABLATE 0
-#endif
 constexpr int kMalaTileRows = 64;     // rows of X per LDS tile (33.8 KB at D = 64)
 constexpr int kMalaChainsPerWG = 64;  // 4 waves × 16 chains
 
@@ -78,9 +72,6 @@ __device__ __forceinline__ void logistic_terms(double eta, double y, double &ell
     const double u = 1.0 + t;
     double v;
     const double lu = log_rcp_1_2(u, mt.invc, mt.logc, v);
-#if EMCMC_MALA_IEEE_DIV  // timing-only A/B build: the round-3 quotient (not the oracle's bits)
-    v = 1.0 / u;
-#endif
     const double lp1 = (u == 1.0) ? t : lu - ((u - 1.0) - t) * v;
     const double sp = (eta > 0.0 ? eta : 0.0) + lp1;
     const double sig = (eta >= 0.0 ? 1.0 : t) * v;
@@ -154,7 +145,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
     for (uint32_t t = 0; t < a.ntiles; ++t) {
         const uint64_t n0 = (uint64_t)t * kMalaTileRows;
         __syncthreads();  // previous tile consumed
-        if (!(EMCMC_MALA_ABLATE & 2) || t == 0) {  // timing-only ablation 2: reuse the first tile
+        {
             const double2 *src = reinterpret_cast<const double2 *>(a.X + n0 * D);
             constexpr int PAIRS = kMalaTileRows * D / 2;
 #pragma unroll
@@ -196,12 +187,7 @@ __global__ void __launch_bounds__(256, 2) mala_logistic_kernel(const MalaParams 
             for (int q = 0; q < 4; ++q) {
                 const int row = 4 * q + g;
                 double ell, rr;
-#if EMCMC_MALA_ABLATE & 1  // timing-only: no elementwise terms
-                ell = eta[q];
-                rr = eta[q] * ys[rb + row];
-#else
                 logistic_terms(eta[q], ys[rb + row], ell, rr, mt);
-#endif
                 // rows past N are zero rows of X, so their r only meets zeros in the
                 // ∇ℓ MFMA (fma(0, r, G) = G for finite r); only ℓ is masked
                 if ((uint32_t)(rb + row) < rem) S = S + ell;

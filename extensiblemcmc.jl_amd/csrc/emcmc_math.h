@@ -54,10 +54,6 @@ struct u32x4 {
     uint32_t x, y, z, w;
 };
 
-#ifndef EMCMC_ABLATE
-#define EMCMC_ABLATE 0  // timing-only builds (make ablate): 1 = Philox replaced by a cheap hash
-#endif
-
 #if defined(__HIP_DEVICE_COMPILE__)
 // a ^ b ^ k in one VALU op (gfx950 v_bitop3_b32, truth table 0x96); k is a
 // round key derived from the seed, wave-uniform, so it sits in an SGPR
@@ -85,19 +81,9 @@ __device__ __forceinline__ uint32_t key_local(uint32_t k) {
 static inline uint32_t key_local(uint32_t k) { return k; }
 #endif
 
-#ifndef EMCMC_KEY_LOCAL
-#define EMCMC_KEY_LOCAL 1
-#endif
-
 EMCMC_HD u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
-    if (EMCMC_KEY_LOCAL) {
-        k0 = key_local(k0);
-        k1 = key_local(k1);
-    }
-#if EMCMC_ABLATE & 1
-    u32x4 o = {c.x * 0x9E3779B9u ^ k0, c.y * 0x85EBCA6Bu ^ c.x, c.z * 0xC2B2AE35u ^ k1, c.w ^ c.y * 0x27D4EB2Fu};
-    return o;
-#endif
+    k0 = key_local(k0);
+    k1 = key_local(k1);
     const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u;
     const uint32_t W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll

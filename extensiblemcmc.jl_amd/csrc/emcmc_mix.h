@@ -514,13 +514,6 @@ __global__ void __launch_bounds__(64) moments_consts_kernel(uint64_t N0, uint32_
 
 #endif  // EMCMC_HOST_UNIT
 
-#ifndef EMCMC_MOMENTS_DIRECT
-#define EMCMC_MOMENTS_DIRECT 0
-#endif
-#ifndef EMCMC_MOMENTS_PACE
-#define EMCMC_MOMENTS_PACE 0
-#endif
-
 template <int D>
 struct MomentTiles {
     static constexpr int TB = D <= 8 ? D : 8;                 // block edge
@@ -583,9 +576,9 @@ struct MomentUnitState {
     // ROWS_NEW: the new row means of another unit of the same wave with the same
     // row block, already advanced this step (the same formula, so the same bits):
     // taken instead of recomputed; nullptr: advance them here
-    template <typename TH, typename TICK>
+    template <typename TH>
     __device__ __forceinline__ void step(TH theta_at, double Nd, double N1d, double ca, double cb, double cc, double rN,
-                                         double rN1, const double *rows_new, TICK &&tick) {
+                                         double rN1, const double *rows_new) {
         double ti[TB], tj[NJ];
 #pragma unroll
         for (int u = 0; u < TB; ++u) ti[u] = theta_at(I0 + u);
@@ -596,7 +589,6 @@ struct MomentUnitState {
 #pragma unroll
         for (int u = 0; u < TB; ++u) {
             __builtin_amdgcn_sched_barrier(0);  // one row at a time: bounded live temporaries
-            tick(u);
 #pragma unroll
             for (int v = DIAG ? u : 0; v < NJ; ++v) {
                 const double old_sq = ca * c[UT::slot(u, v)] + mi[u] * (DIAG ? mi[v] : mj[v]);
@@ -617,7 +609,6 @@ struct MomentUnitState {
 #pragma unroll
         for (int u = 0; u < TB; ++u) {
             __builtin_amdgcn_sched_barrier(0);
-            tick(u);
 #pragma unroll
             for (int v = DIAG ? u : 0; v < NJ; ++v)
                 c[UT::slot(u, v)] = c[UT::slot(u, v)] - cc * (mi[u] * (DIAG ? mi[v] : mj[v]));
@@ -657,8 +648,7 @@ struct MomentPairs {
 // The whole launch sweep of wave W (units a(W) and b(W)); every wave runs the
 // same number of block barriers.
 template <int D, int W>
-__device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *stage0, double *stage1,
-                                             uint32_t *pace_prog, const uint32_t *pace_simd) {
+__device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *stage0, double *stage1) {
     using MT = MomentTiles<D>;
     constexpr int PR = MT::PR, EW = MT::EW, NPF = MT::NPF;
     constexpr bool TWO = MT::UPW == 2;
@@ -687,47 +677,12 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
             if (e < PR * 64) dst[e] = pf[q];
         }
     };
-    // Sibling pacing (EMCMC_MOMENTS_PACE; SiblingPace, emcmc_fused.h): every fourth row of
-    // the unit sweeps publishes the wave's progress and sets its issue priority against the
-    // other wave on its SIMD, so the pair reaches the step's barrier together instead of the
-    // older one waiting there while the younger one finishes alone
-    SiblingPace pace{pace_prog, W, -1};
-    uint32_t ticks = 0;
-    if constexpr (EMCMC_MOMENTS_PACE) {
-        for (int w = 0; w < MT::WPB; ++w)
-            if (w != W && pace.sib < 0 && pace_simd[w] == pace_simd[W]) pace.sib = w;
-    }
-    auto tick = [&](int u) {
-        if constexpr (EMCMC_MOMENTS_PACE) {
-            ++ticks;
-            if ((u & 3) == 3) pace.publish(ticks);
-        }
-    };
     constexpr int UA = MomentPairs<D>::a(W), UB = TWO ? MomentPairs<D>::b(W) : UA;
     constexpr bool SHARE_ROWS = TWO && MomentUnit<D, UA>::I0 == MomentUnit<D, UB>::I0;
     MomentUnitState<D, UA> ua;
     MomentUnitState<D, UB> ub;
     ua.load(a, cl);
     if constexpr (TWO) ub.load(a, cl);
-#if EMCMC_MOMENTS_DIRECT
-    // every wave reads the θ coordinates of its own units straight from the history
-    // (L2-resident after the block's first reader): no block staging and no barrier,
-    // so the two waves of a SIMD overlap the whole launch instead of meeting at a
-    // barrier every step (the older one would otherwise wait there while the younger
-    // finishes alone)
-    (void)fetch;
-    (void)put;
-    (void)stage0;
-    (void)stage1;
-    for (uint32_t s = 0; s < a.nsteps; ++s) {
-        const double *th_s = a.theta + (uint64_t)s * D * C;
-        auto theta_at = [&](int d) -> double { return th_s[state_pos((uint64_t)d, cl, C, (uint32_t)D)]; };
-        const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
-        const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
-        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, nullptr, tick);
-        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr, tick);
-    }
-#else
     {
         rowv pf[NPF];
         fetch(0, pf);
@@ -745,23 +700,21 @@ __device__ __forceinline__ void moments_wave(const MixMomentsParams &a, double *
         };
         const double *k = a.kst + 8 * (uint64_t)s;  // wave-uniform: scalar loads
         const double Nd = k[0], N1d = k[1], ca = k[2], cb = k[3], cc = k[4], rN = k[5], rN1 = k[6];
-        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, nullptr, tick);
-        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr, tick);
+        ua.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, nullptr);
+        if constexpr (TWO) ub.step(theta_at, Nd, N1d, ca, cb, cc, rN, rN1, SHARE_ROWS ? ua.mi : nullptr);
         if (s + 1 < a.nsteps) put((s & 1u) ? stage0 : stage1, pf);
         __syncthreads();
     }
-#endif
     if (!live) return;
     ua.store(a, chain);
     if constexpr (TWO) ub.store(a, chain);
 }
 
 template <int D, int W>
-__device__ __forceinline__ void moments_dispatch(int wave, const MixMomentsParams &a, double *stage0, double *stage1,
-                                                 uint32_t *pace_prog, const uint32_t *pace_simd) {
+__device__ __forceinline__ void moments_dispatch(int wave, const MixMomentsParams &a, double *stage0, double *stage1) {
     if constexpr (W < MomentTiles<D>::WPB) {
-        if (wave == W) moments_wave<D, W>(a, stage0, stage1, pace_prog, pace_simd);
-        else moments_dispatch<D, W + 1>(wave, a, stage0, stage1, pace_prog, pace_simd);
+        if (wave == W) moments_wave<D, W>(a, stage0, stage1);
+        else moments_dispatch<D, W + 1>(wave, a, stage0, stage1);
     }
 }
 
@@ -769,16 +722,8 @@ template <int D>
 __global__ void __launch_bounds__(MomentTiles<D>::BLOCK) mix_moments_kernel(const MixMomentsParams a) {
     using MT = MomentTiles<D>;
     __shared__ __attribute__((aligned(16))) double stage[2][MT::PR * 64 * MT::EW];
-    __shared__ uint32_t pace_prog[MT::WPB], pace_simd[MT::WPB];
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform
-    if constexpr (EMCMC_MOMENTS_PACE) {
-        if ((threadIdx.x & 63) == 0) {
-            pace_simd[wave] = (__builtin_amdgcn_s_getreg((31 << 11) | 4) >> 4) & 3u;  // HW_ID.simd_id
-            pace_prog[wave] = 0u;
-        }
-        __syncthreads();
-    }
-    moments_dispatch<D, 0>(wave, a, stage[0], stage[1], pace_prog, pace_simd);
+    moments_dispatch<D, 0>(wave, a, stage[0], stage[1]);
 }
 
 // ---- HaarioTypeAdaptation readjust! (adaptation.jl:422-426) -----------------

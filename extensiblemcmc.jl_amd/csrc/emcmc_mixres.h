@@ -67,9 +67,6 @@ __device__ __forceinline__ uint32_t rbcast_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150 + L, 0xF, 0xF, true);
 }
 
-#ifndef EMCMC_MIXRES_DPPFMA
-#define EMCMC_MIXRES_DPPFMA 1
-#endif
 // acc = fma(v from lane L of the 16-lane row, m, acc) as ONE v_fmac_f64_dpp
 // (row_newbcast): the broadcast rides on the fma's first source instead of a
 // separate v_mov_b64_dpp (VOP3 fma has no DPP form; VOP2 fmac does).  NOP1: two wait
@@ -104,11 +101,9 @@ __device__ __forceinline__ double row_sumsq32(double y0, double y1, bool quad_le
     return rbcast<15>(t);
 }
 
-#ifndef EMCMC_MIXRES_MINB
-#define EMCMC_MIXRES_MINB 2  // blocks per CU the register budget is sized for (2: 256 VGPRs, 2 waves/SIMD)
-#endif
+constexpr int kMixResMinBlocks = 2;  // blocks per CU the register budget is sized for (256 VGPRs, 2 waves/SIMD)
 template <int D, bool FULL, int LLMODE, bool UNIT_T>
-__global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const MixParams a) {
+__global__ void __launch_bounds__(256, kMixResMinBlocks) mix_res_kernel(const MixParams a) {
     static_assert(D == 2 * kResLanes, "two rows of L_B per lane");
     constexpr int DP = packed_n(D), DD = D * D, XS = D + 2;
     extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -213,7 +208,6 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
         double lza = 0.0, lzb = 0.0;  // folded rows fa, fb of L_B z
         static_for<0, D>([&](auto jc) {
             constexpr int j = decltype(jc)::value;
-#if EMCMC_MIXRES_DPPFMA
             if constexpr (j == 0) {
                 const double zj = rbcast<0>(z0);
                 lza = La[0] * zj;
@@ -224,16 +218,6 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
                 if constexpr (j < H) fmac_bcast<j / 2, j == 1 || j == 2>(lza, (j & 1) ? z1 : z0, La[j]);
                 fmac_bcast<j / 2, (j == 1 || j == 2) && j >= H>(lzb, (j & 1) ? z1 : z0, Lb[j]);
             }
-#else
-            const double zj = rbcast<j / 2>((j & 1) ? z1 : z0);
-            if constexpr (j == 0) {
-                lza = La[0] * zj;
-                lzb = Lb[0] * zj;
-            } else {
-                if constexpr (j < H) lza = fma(La[j], zj, lza);
-                lzb = fma(Lb[j], zj, lzb);
-            }
-#endif
         });
         if (__ballot(useB && (lza == 0.0 || lzb == 0.0)) != 0) {
             // an exact zero may carry the wrong sign after the padding columns: redo with masks
@@ -335,19 +319,12 @@ __global__ void __launch_bounds__(256, EMCMC_MIXRES_MINB) mix_res_kernel(const M
                 // IEEE addition (x + (−0) = x for every x, ±0 and NaN included): the fold is
                 // 16 unconditional adds in k order instead of 16 scalar compare-and-branch
                 const double f = (k < nobs) ? fma(-0.5, tree_inplace(b), a.t_c0) : -0.0;
-#if EMCMC_MIXRES_DPPFMA
                 // llp + f_q as fma(f_q, 1, llp): f_q·1 is exact, so one rounding of the sum
                 const double one = 1.0;
                 static_for<0, kResLanes>([&](auto rc) {
                     constexpr int q = decltype(rc)::value;
                     fmac_bcast<q, q == 0>(llp, f, one);
                 });
-#else
-                static_for<0, kResLanes>([&](auto rc) {
-                    constexpr int q = decltype(rc)::value;
-                    llp = llp + rbcast<q>(f);
-                });
-#endif
             }
         } else {
             double y0 = xb0 - thp0, y1 = xb1 - thp1;

@@ -237,9 +237,16 @@ const std::vector<std::string> &rtc_env_extra() {
 // Compile prog_src for gfx950 and fetch the code object of the kernel named by
 // the expression ex; cache it under key.  Returns "" or the compiler's log.
 // -ffp-contract=off: the parity contract with oracle/ (no implicit fma).
+// Embedded headers a program includes (directly or not): its disk-cache digest covers these
+// only, so editing the block kernel's header leaves the cached chol kernels valid.
+const std::vector<std::string> kCholDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h"};
+const std::vector<std::string> kMwgDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_mwg.h"};
+const std::vector<std::string> kBlockDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_mwg.h",
+                                             "emcmc_block.h"};
+
 std::string compile_kernel(const std::string &key, const std::string &prog_src, const char *file,
                            const std::string &ex, const std::string &name, const std::vector<std::string> &extra,
-                           RtcKernel &out) {
+                           RtcKernel &out, const std::vector<std::string> &deps) {
     const auto t0 = std::chrono::steady_clock::now();
     const auto since = [&] { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
     // disk cache: the digest covers every input of the compile
@@ -247,17 +254,14 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
     std::string dfile;
     if (!dir.empty()) {
         Digest d;
-        static const std::string hdr_digest = [] {
-            Digest h;
-            for (int i = 0; i < kRtcHeaderCount; ++i) {
-                h.add(std::string(kRtcHeaderNames[i]));
-                h.add(std::string(kRtcHeaderSrc[i]));
-            }
-            return h.hex();
-        }();
+        for (const auto &dep : deps)
+            for (int i = 0; i < kRtcHeaderCount; ++i)
+                if (dep == kRtcHeaderNames[i]) {
+                    d.add(dep);
+                    d.add(std::string(kRtcHeaderSrc[i]));
+                }
         int vmaj = 0, vmin = 0;
         (void)hiprtcVersion(&vmaj, &vmin);
-        d.add(hdr_digest);
         d.add(prog_src);
         d.add(std::string(file));
         d.add(ex);
@@ -377,7 +381,7 @@ std::string rtc_compile(const std::string &src, const std::string &opts, int D, 
         for (std::string w; is >> w;) extra.push_back(w);
     }
     return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : upd ? "user_update.hip" : "gsn_target.hip",
-                          expr.str(), name.str(), extra, out);
+                          expr.str(), name.str(), extra, out, kMwgDeps);
 }
 
 std::string rtc_compile_user(const std::string &src, const std::string &opts, int D, bool full, int nu,
@@ -395,7 +399,7 @@ std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
     name << "rwm_gsn_chol_kernel<D=" << D << ",LPC=1," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
     return compile_kernel(key.str(), "#include \"emcmc_kernels.h\"\n", "chol_kernel.hip", expr.str(), name.str(),
-                          {"-ftemplate-depth=2048"}, out);
+                          {"-ftemplate-depth=2048"}, out, kCholDeps);
 }
 
 std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const std::string &src,
@@ -424,7 +428,7 @@ std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const 
         for (std::string w; is >> w;) extra.push_back(w);
     }
     return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : upd ? "user_update.hip" : "block_kernel.hip",
-                          expr.str(), name.str(), extra, out);
+                          expr.str(), name.str(), extra, out, kBlockDeps);
 }
 
 const char *rtc_builtin_law(const char *name) {

@@ -28,19 +28,3 @@ const std::vector<Entry> &diag2_table() {
 }
 
 }  // namespace emcmc
-
-#if EMCMC_TRACE
-// timing-only build: the MINW = 2 kernels' trace buffer (a static of this unit)
-extern "C" int emcmc_trace_fetch2(void *dst, size_t bytes, int clear) {
-    const size_t n = sizeof(uint64_t) * emcmc::kTraceSlots * emcmc::kTraceWaves;
-    if (bytes < n) return -1;
-    if (hipMemcpyFromSymbol(dst, HIP_SYMBOL(emcmc::emcmc_trace_buf), n, 0, hipMemcpyDeviceToHost) != hipSuccess)
-        return -2;
-    if (clear) {
-        void *p = nullptr;
-        if (hipGetSymbolAddress(&p, HIP_SYMBOL(emcmc::emcmc_trace_buf)) != hipSuccess || hipMemset(p, 0, n) != hipSuccess)
-            return -3;
-    }
-    return 0;
-}
-#endif

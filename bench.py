@@ -397,10 +397,12 @@ def main():
     ll_mode = L.LL_PER_OBS if a.ll_mode == "per_obs" else L.LL_SUFFSTAT
     hist = L.HIST_FULL if a.history == "full" else L.HIST_ACCEPT_ONLY
     reps = a.reps
-    if reps <= 0:  # median of 5 timed repetitions when their full histories fit in 96 GB of HBM
+    # every value rep is followed by a kernel-timing rep of the same launches (below), and
+    # every timed step keeps its history slot: the repetitions' histories must fit in HBM
+    rep_factor = 1 if a.no_kernel_timing else 2
+    if reps <= 0:  # median of 5 value repetitions when all the histories fit in 96 GB of HBM
         per_iter = Cg * (16 * w.D + 8.125) if (hist == L.HIST_FULL and not a.history_ring) else 0
-        reps = 5 if (a.warmup + 5 * a.steps) * per_iter <= 96e9 else 1
-    # every value rep is followed by a kernel-timing rep of the same launches (below)
+        reps = 5 if (a.warmup + rep_factor * 5 * a.steps) * per_iter <= 96e9 else 1
     timing_reps = 0 if a.no_kernel_timing else reps
     M = a.warmup + a.steps * (reps + timing_reps)
     eng = Engine(EngineConfig(dim=w.D, num_chains=Cg, num_mcmc_steps=M, seed=w.seed, first_chain_id=first,

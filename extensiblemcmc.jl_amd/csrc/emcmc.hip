@@ -233,11 +233,6 @@ struct emcmc_handle {
     uint64_t ring = 0;     // iterations held per history buffer
     uint64_t hi_iter = 0;  // highest iteration launched
     hipStream_t cstream = nullptr;
-    // GaussianRandomWalkMix + Haario (run_mix): the batched mean/cov kernel of a launch runs on
-    // mstream, beside the next launch's step kernel (cfg 4 overlap)
-    hipStream_t mstream = nullptr;
-    hipEvent_t ev_step = nullptr, ev_mom = nullptr;
-    bool mix_overlap = true;  // EMCMC_MIX_OVERLAP=0: everything on one stream (A/B)
     struct Copy {
         uint64_t lo, hi;  // iterations read
         hipEvent_t ev;
@@ -258,9 +253,10 @@ struct emcmc_handle {
     bool host_timing = false;
     double ht_run_us = 0.0, ht_sync_us = 0.0;
     uint64_t ht_runs = 0, ht_syncs = 0;
-    // EMCMC_SYNC: how emcmc_synchronize waits: 0 hipStreamSynchronize, 1 an event recorded
-    // behind the queued work and hipEventSynchronize, 2 the same event polled with hipEventQuery
-    int sync_mode = 0;
+    // how emcmc_synchronize waits: 1 (default) an event recorded behind the queued work and
+    // hipEventSynchronize, ≈ 6 µs less than 0 = hipStreamSynchronize on a 150 µs window
+    // (scripts/host_gap.py); EMCMC_SYNC=0 selects the latter for A/B
+    int sync_mode = 1;
     hipEvent_t sync_ev = nullptr;
 };
 
@@ -1233,27 +1229,12 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
     const dim3 block(256), grid((unsigned)((C + 255) / 256));
     const dim3 rgrid_res((unsigned)(C / kMixResChainsPerBlock));  // mix_res_kernel: 16 chains per block (C % 16 == 0)
     const uint64_t K = h->cfg.steps_per_launch;
-    // Overlap (HaarioTypeAdaptation, full histories, no ring): the mean/cov recurrence of a
-    // launch reads only that launch's θ history slots and the running moments, and nothing
-    // but readjust! reads the moments (adaptation.jl:416-426), so it runs on mstream while the
-    // step kernel of the next launch of the same readjust period runs on h->stream; a period
-    // is cut into two launches for that, and readjust waits for both moments.  Same kernels,
-    // same order of every recurrence: same bits.
-    const bool overlap = h->mix_overlap && haario && h->d_hist_theta && h->ring == h->cfg.num_mcmc_steps;
-    if (overlap && !h->mstream) {
-        HIPCHK(h, hipStreamCreateWithFlags(&h->mstream, hipStreamNonBlocking));
-        HIPCHK(h, hipEventCreateWithFlags(&h->ev_step, hipEventDisableTiming));
-        HIPCHK(h, hipEventCreateWithFlags(&h->ev_mom, hipEventDisableTiming));
-    }
-    hipStream_t ms = overlap ? h->mstream : h->stream;  // the moments' stream
-    bool mom_pending = false;  // moments enqueued on mstream that h->stream has not waited for
-    hipEvent_t te0 = nullptr;  // an open timing interval (overlap: one per readjust period)
-    double tbytes = 0.0;
+    // (running the mean/cov kernel of a launch on a second stream beside the next launch's
+    // step kernel was measured 18% slower at cfg 4: DESIGN.md §6, scripts/ab/mix_overlap.patch)
     uint64_t i = 0;
     while (i < num_steps) {
         uint64_t cap = K;
         if (haario) cap = std::min<uint64_t>(cap, k - h->mix_M);
-        if (overlap && cap == k - h->mix_M && cap >= 2) cap -= cap / 2;  // the period's first half
         uint64_t j = i + 1;
         while (j < num_steps && j - i < cap && steps[j].mcmciter == steps[j - 1].mcmciter + 1 &&
                ring_epoch(h, steps[j].mcmciter) == ring_epoch(h, steps[i].mcmciter))
@@ -1274,17 +1255,15 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
         if (p.iter0 > 1 && h->last_iter[0] != p.iter0 - 1)  // rolling_ar[iter−1] never written → 0.0
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[0] = steps[j - 1].mcmciter;
-        if (h->timing && !te0) {
-            te0 = get_event(h);
-            HIPCHK(h, hipEventRecord(te0, h->stream));
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (h->timing) {
+            e0 = get_event(h);
+            e1 = get_event(h);
+            HIPCHK(h, hipEventRecord(e0, h->stream));
         }
         void *args[] = {&p};
         HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.xfn), h->var.xres ? rgrid_res : grid, block,
                                   args, h->lds_bytes, h->stream));
-        if (overlap) {  // the moments wait for this launch's θ history only
-            HIPCHK(h, hipEventRecord(h->ev_step, h->stream));
-            HIPCHK(h, hipStreamWaitEvent(ms, h->ev_step, 0));
-        }
         {  // the launch's mean/cov recurrence, from its θ history
             MixMomentsParams mp{};
             mp.theta = p.hist_theta ? p.hist_theta + (uint64_t)(p.iter0 - 1) * h->cfg.dim * C : h->d_mom_scratch;
@@ -1301,27 +1280,19 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
                 double *kst = h->d_mom_consts;
                 void *kargs[] = {&n0, &ns, &kst};
                 HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(&moments_consts_kernel),
-                                          dim3((ns + 63) / 64), dim3(64), kargs, 0, ms));
+                                          dim3((ns + 63) / 64), dim3(64), kargs, 0, h->stream));
             }
             void *margs[] = {&mp};
             // one block per 64 chains, one wave per unit of the packed triangle
             const dim3 mgrid((unsigned)((C + 63) / 64)), mblock((unsigned)(64 * h->var.mo_tiles));
-            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mofn), mgrid, mblock, margs, 0, ms));
+            HIPCHK(h, hipLaunchKernel(reinterpret_cast<const void *>(h->var.mofn), mgrid, mblock, margs, 0, h->stream));
             std::swap(h->d_mean, h->d_mean_alt);
-            if (overlap) {
-                HIPCHK(h, hipEventRecord(h->ev_mom, ms));
-                mom_pending = true;
-            }
         }
         h->stats_N += n;
         bool readjusted = false;
         if (haario) {
             h->mix_M += (uint32_t)n;
             if (h->mix_M >= k) {  // time_to_update: readjust!, M = 0
-                if (mom_pending) {  // readjust! reads the cov both halves' moments produced
-                    HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_mom, 0));
-                    mom_pending = false;
-                }
                 void *rargs[] = {&r};
                 const int cpb = readjust_chains_per_block((int)h->cfg.dim);
                 const dim3 rgrid((unsigned)((C + cpb - 1) / cpb));
@@ -1336,25 +1307,13 @@ emcmc_status run_mix(emcmc_handle *h, const emcmc_step *steps, uint64_t num_step
                 }
             }
         }
-        tbytes += bytes_per_launch(h, n, readjusted);
-        i = j;
-        // the group (step kernel, mean/cov kernel, readjust) closes a timing interval; with the
-        // overlap the interval is the readjust period, whose moments end before its readjust
-        if (h->timing && (!overlap || readjusted || i == num_steps)) {
-            if (mom_pending) {
-                HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_mom, 0));
-                mom_pending = false;
-            }
-            hipEvent_t te1 = get_event(h);
-            HIPCHK(h, hipEventRecord(te1, h->stream));
-            h->ev.emplace_back(te0, te1);
-            h->pending_bytes += tbytes;
-            te0 = nullptr;
-            tbytes = 0.0;
+        if (h->timing) {  // the whole group: step kernel, mean/cov kernel, readjust
+            HIPCHK(h, hipEventRecord(e1, h->stream));
+            h->ev.emplace_back(e0, e1);
+            h->pending_bytes += bytes_per_launch(h, n, readjusted);
         }
+        i = j;
     }
-    if (mom_pending)  // later work on h->stream (synchronize, read-backs, the next run) follows the moments
-        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_mom, 0));
     return EMCMC_OK;
 }
 
@@ -1609,8 +1568,7 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
         return EMCMC_HIP_ERROR;
     }
     if (const char *e = getenv("EMCMC_HOST_TIMING")) h->host_timing = *e && *e != '0';
-    if (const char *e = getenv("EMCMC_MIX_OVERLAP")) h->mix_overlap = !(*e == '0');
-    if (const char *e = getenv("EMCMC_SYNC")) h->sync_mode = atoi(e);
+    if (const char *e = getenv("EMCMC_SYNC")) h->sync_mode = atoi(e) ? 1 : 0;
     if (h->sync_mode && hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming) != hipSuccess) h->sync_mode = 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
@@ -2283,14 +2241,7 @@ emcmc_status emcmc_synchronize(emcmc_handle *h) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
     } else {
         HIPCHK(h, hipEventRecord(h->sync_ev, h->stream));
-        if (h->sync_mode == 1) {
-            HIPCHK(h, hipEventSynchronize(h->sync_ev));
-        } else {
-            hipError_t q;
-            while ((q = hipEventQuery(h->sync_ev)) == hipErrorNotReady) {
-            }
-            HIPCHK(h, q);
-        }
+        HIPCHK(h, hipEventSynchronize(h->sync_ev));
     }
     if (h->host_timing) {
         h->ht_sync_us += host_us() - t0;
@@ -2313,10 +2264,6 @@ void emcmc_destroy(emcmc_handle *h) {
                 h->ht_runs ? h->ht_run_us / h->ht_runs : 0.0, (unsigned long long)h->ht_runs,
                 h->ht_syncs ? h->ht_sync_us / h->ht_syncs : 0.0, (unsigned long long)h->ht_syncs, h->sync_mode);
     if (h->sync_ev) (void)hipEventDestroy(h->sync_ev);
-    if (h->mstream) (void)hipStreamSynchronize(h->mstream);
-    if (h->mstream) (void)hipStreamDestroy(h->mstream);
-    if (h->ev_step) (void)hipEventDestroy(h->ev_step);
-    if (h->ev_mom) (void)hipEventDestroy(h->ev_mom);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->cstream) (void)hipStreamSynchronize(h->cstream);
     for (auto &c : h->copies) (void)hipEventDestroy(c.ev);

@@ -48,9 +48,22 @@ const Rccl &rccl() {
     static Rccl r;
     static std::once_flag once;
     std::call_once(once, [] {
+        // The RCCL beside the HIP runtime this library is bound to: a process can hold two
+        // HIP runtimes (torch's wheel bundles one, SONAME libamdhip64.so.7 like the system's,
+        // and its libraries load it by another name when libemcmc.so came first), and an RCCL
+        // of the other runtime cannot use this library's streams.
+        std::string dir;
+        Dl_info info;
+        if (dladdr(reinterpret_cast<void *>(&hipGetDeviceCount), &info) && info.dli_fname) {
+            dir = info.dli_fname;
+            const size_t sl = dir.rfind('/');
+            dir = (sl == std::string::npos) ? std::string() : dir.substr(0, sl + 1);
+        }
         void *so = nullptr;
-        for (const char *name : {"librccl.so.1", "/opt/rocm/lib/librccl.so.1", "librccl.so"})
-            if ((so = dlopen(name, RTLD_NOW | RTLD_GLOBAL))) break;
+        const std::string cands[] = {dir.empty() ? "" : dir + "librccl.so.1", dir.empty() ? "" : dir + "librccl.so",
+                                     "librccl.so.1", "/opt/rocm/lib/librccl.so.1"};
+        for (const auto &name : cands)
+            if (!name.empty() && (so = dlopen(name.c_str(), RTLD_NOW | RTLD_GLOBAL))) break;
         if (!so) {
             const char *e = dlerror();
             r.err = std::string("cannot open librccl.so.1: ") + (e ? e : "?");
@@ -68,6 +81,9 @@ const Rccl &rccl() {
 }
 
 }  // namespace
+
+// why the last emcmc_comm_init / emcmc_comm_unique_id failed (no comm exists to hold it)
+thread_local std::string g_comm_err;
 
 struct emcmc_comm {
     int nranks = 1, rank = 0, device = -1;
@@ -185,9 +201,15 @@ emcmc_status emcmc_comm_unique_id(uint8_t id[EMCMC_COMM_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == EMCMC_COMM_ID_BYTES, "ncclUniqueId size");
     int nd = 0;  // RCCL aborts the process when no device is visible: refuse first
     if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMCMC_NO_DEVICE;
-    if (!rccl().ok) return EMCMC_RCCL_ERROR;
+    if (!rccl().ok) {
+        g_comm_err = rccl().err;
+        return EMCMC_RCCL_ERROR;
+    }
     ncclUniqueId u;
-    if (rccl().get_unique_id(&u) != ncclSuccess) return EMCMC_RCCL_ERROR;
+    if (const ncclResult_t r = rccl().get_unique_id(&u); r != ncclSuccess) {
+        g_comm_err = std::string("ncclGetUniqueId: ") + rccl().error_string(r);
+        return EMCMC_RCCL_ERROR;
+    }
     std::memcpy(id, &u, sizeof u);
     return EMCMC_OK;
 }
@@ -196,7 +218,10 @@ emcmc_status emcmc_comm_init(emcmc_comm **out, int nranks, int rank, int device,
                              const uint8_t id[EMCMC_COMM_ID_BYTES]) {
     if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0) return EMCMC_INVALID_ARG;
     *out = nullptr;
-    if (!rccl().ok) return EMCMC_RCCL_ERROR;
+    if (!rccl().ok) {
+        g_comm_err = rccl().err;
+        return EMCMC_RCCL_ERROR;
+    }
     int nd = 0;
     if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMCMC_NO_DEVICE;
     if (device >= nd) return EMCMC_INVALID_ARG;
@@ -211,7 +236,8 @@ emcmc_status emcmc_comm_init(emcmc_comm **out, int nranks, int rank, int device,
         delete c;
         return EMCMC_HIP_ERROR;
     }
-    if (rccl().init_rank(&c->nccl, nranks, u, rank) != ncclSuccess) {
+    if (const ncclResult_t r = rccl().init_rank(&c->nccl, nranks, u, rank); r != ncclSuccess) {
+        g_comm_err = std::string("ncclCommInitRank: ") + rccl().error_string(r);
         (void)hipStreamDestroy(c->stream);
         delete c;
         return EMCMC_RCCL_ERROR;
@@ -244,7 +270,7 @@ void emcmc_comm_destroy(emcmc_comm *c) {
 }
 
 const char *emcmc_comm_last_error(const emcmc_comm *c) {
-    if (!c) return rccl().ok ? "" : rccl().err.c_str();
+    if (!c) return g_comm_err.c_str();  // the calling thread's last failed init / unique id
     return c->err.c_str();
 }
 

@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "emcmc_kernels.h"
+#include "emcmc_chol.h"
 #include "emcmc_fused.h"
 #include "emcmc_mala.h"
 #include "emcmc_mix.h"

@@ -170,8 +170,8 @@ __device__ __forceinline__ double log_real(double x) { return (x < 0.0) ? __buil
 //   LogNormal(μ=a, σ=b), c = log σ:   x ≤ 0 ? −Inf : (−(z² + log2π)/2 − c) − log x, z = (log x − μ)/σ
 //   Beta(α=a, β=b), c = logbeta(α, β): x ∉ [0, 1] ? −Inf : (xlogy(α−1, x) + xlog1py(β−1, −x)) − c
 //   InverseGamma(α=a, θ=b), c = α·log θ − lgamma(α): x ≤ 0 ? −Inf : (c − (α + 1)·log x) − θ/x
-//   Cauchy(μ=a, σ=b), c = log σ:  −((log1p(z²) + log π) + c), z = (x − μ)/σ (Distributions.jl's
-//     −(log1psq(z) + logπ + log(σ)), left to right)
+//   Cauchy(μ=a, σ=b), c = log σ:  −((log1psq(z) + log π) + c), z = (x − μ)/σ (Distributions.jl's
+//     −(log1psq(z) + logπ + log(σ)), left to right; log1psq(z) = |z| < 2^53 ? log1p(z²) : 2·log|z|)
 //   Laplace(μ=a, θ=b), c = log(2θ):   −(|x − μ|/θ + c)
 //   TDist(ν=a), b = (ν + 1)/2, c = (lgamma((ν+1)/2) − lgamma(ν/2)) − log(νπ)/2:  c − b·log1p(x²/ν)
 __device__ __forceinline__ double univariate_logpdf(uint32_t fam, double a, double b, double c, double x) {
@@ -199,9 +199,10 @@ __device__ __forceinline__ double univariate_logpdf(uint32_t fam, double a, doub
     case kDistInverseGamma:
         if (!(x > 0.0)) return (x != x) ? x : ninf;
         return (c - (a + 1.0) * log_any(x)) - b / x;
-    case kDistCauchy: {
-        const double z = (x - a) / b;
-        return -((log1p_any(z * z) + 1.1447298858494002) + c);  // log π
+    case kDistCauchy: {  // log1psq(z): log1p(z²) below maxintfloat = 2^53, else 2·log|z|
+        const double z = (x - a) / b, az = fabs(z);
+        const double l = (az < 0x1p53) ? log1p_any(az * az) : 2.0 * log_any(az);
+        return -((l + 1.1447298858494002) + c);  // log π
     }
     case kDistLaplace: return -(fabs(x - a) / b + c);
     default:  // kDistTDist

@@ -239,7 +239,7 @@ const std::vector<std::string> &rtc_env_extra() {
 // -ffp-contract=off: the parity contract with oracle/ (no implicit fma).
 // Embedded headers a program includes (directly or not): its disk-cache digest covers these
 // only, so editing the block kernel's header leaves the cached chol kernels valid.
-const std::vector<std::string> kCholDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h"};
+const std::vector<std::string> kCholDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_chol.h"};
 const std::vector<std::string> kMwgDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_mwg.h"};
 const std::vector<std::string> kBlockDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_mwg.h",
                                              "emcmc_block.h"};
@@ -398,7 +398,7 @@ std::string rtc_compile_chol(int D, bool full, int ll_mode, RtcKernel &out) {
     expr << "emcmc::rwm_gsn_chol_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ">";
     name << "rwm_gsn_chol_kernel<D=" << D << ",LPC=1," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << ">[hiprtc]";
-    return compile_kernel(key.str(), "#include \"emcmc_kernels.h\"\n", "chol_kernel.hip", expr.str(), name.str(),
+    return compile_kernel(key.str(), "#include \"emcmc_chol.h\"\n", "chol_kernel.hip", expr.str(), name.str(),
                           {"-ftemplate-depth=2048"}, out, kCholDeps);
 }
 

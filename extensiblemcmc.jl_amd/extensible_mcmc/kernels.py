@@ -230,8 +230,10 @@ class Cauchy(UnivariateDistribution):
         self.a, self.b = float(mu), float(sigma)
 
     def logpdf(self, x):
-        z = (np.asarray(x, dtype=float) - self.a) / self.b
-        return -(np.log(np.pi) + np.log(self.b) + np.log1p(z * z))
+        z = np.abs((np.asarray(x, dtype=float) - self.a) / self.b)
+        with np.errstate(over="ignore"):  # log1psq: z² overflows long before log(1 + z²) does
+            l = np.where(z < 2.0 ** 53, np.log1p(z * z), 2.0 * np.log(z))
+        return -(np.log(np.pi) + np.log(self.b) + l)
 
 
 class Laplace(UnivariateDistribution):

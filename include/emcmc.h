@@ -571,7 +571,8 @@ emcmc_status emcmc_comm_init(emcmc_comm **comm, int nranks, int rank, int device
                              const uint8_t id[EMCMC_COMM_ID_BYTES]);
 emcmc_status emcmc_comm_init_host(emcmc_comm **comm, int nranks, int rank, emcmc_allgather_fn fn, void *ctx);
 void emcmc_comm_destroy(emcmc_comm *comm);
-const char *emcmc_comm_last_error(const emcmc_comm *comm);
+const char *emcmc_comm_last_error(const emcmc_comm *comm);  /* comm = NULL: why this thread's last
+                                                              emcmc_comm_init / _unique_id failed */
 
 typedef struct emcmc_diag {
     uint64_t num_chains;  /* (half-)chains merged over every rank */

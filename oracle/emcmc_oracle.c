@@ -595,7 +595,8 @@ static double orc_log_real(double x) { return (x < 0.0) ? NAN : orc_log_any(x); 
  *   LogNormal(μ, σ): x ≤ 0 ? −Inf : normlogpdf(μ, σ, log x) − log x
  *   Beta(α, β): x ∉ [0, 1] ? −Inf : xlogy(α − 1, x) + xlog1py(β − 1, −x) − logbeta(α, β)
  *   InverseGamma(α, θ): x ≤ 0 ? −Inf : α log θ − loggamma(α) − (α + 1) log x − θ/x
- *   Cauchy(μ, σ): −((log1p(z²) + log π) + log σ)  (Distributions.jl: −(log1psq(z) + logπ + log(σ)))
+ *   Cauchy(μ, σ): −((log1psq(z) + log π) + log σ)  (Distributions.jl: −(log1psq(z) + logπ + log(σ))),
+ *     log1psq(z) = |z| < 2^53 ? log1p(z²) : 2·log|z|  (StatsFuns / LogExpFunctions)
  *   Laplace(μ, θ): −(|x − μ|/θ + log(2θ))
  *   TDist(ν): loggamma((ν+1)/2) − loggamma(ν/2) − log(νπ)/2 − (ν+1)/2 · log1p(x²/ν)
  * (a, b) are the parameters as the device holds them (Exponential: b = 1/θ,
@@ -627,8 +628,11 @@ static double orc_univariate_logpdf(uint32_t fam, double a, double b, double c, 
         if (x <= 0.0) return -INFINITY;
         return (c - (a + 1.0) * orc_log_any(x)) - b / x;
     case ORC_DIST_CAUCHY: {
-        const double z = (x - a) / b;
-        return -((orc_log1p_any(z * z) + ORC_LOGPI) + c);
+        /* StatsFuns log1psq: log1p(z²) below maxintfloat = 2^53, else 2·log|z| (z² would
+           lose z or overflow) */
+        const double z = (x - a) / b, az = fabs(z);
+        const double l = (az < 0x1p53) ? orc_log1p_any(az * az) : 2.0 * orc_log_any(az);
+        return -((l + ORC_LOGPI) + c);
     }
     case ORC_DIST_LAPLACE: return -(fabs(x - a) / b + c);
     default: /* TDist */

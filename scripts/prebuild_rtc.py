@@ -8,7 +8,7 @@ where a handle then loads instead of compiling (run-time compilat
 """
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import ProcessPoolExecutor
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
@@ -17,7 +17,7 @@ from extensible_mcmc import _lib as L  # noqa: E402
 
 # (D, history mode, ll mode) of tests/test_gpu_chol.py, tests/test_gpu_api.py and scripts/bench_dense.py
 DEFAULT = [(9, 0, 0), (12, 0, 1), (20, 0, 0), (20, 1, 0), (27, 0, 0), (33, 0, 0), (40, 0, 1), (48, 0, 0),
-           (49, 0, 0), (64, 0, 0)]
+           (49, 0, 0), (53, 0, 0), (56, 0, 1), (64, 0, 0)]
 
 
 # mwg_block_kernel (one MALA / user update over all coordinates) of tests/test_gpu_block.py and
@@ -44,7 +44,8 @@ def one_block(job):
 
 if __name__ == "__main__":
     jobs = [(int(d), 0, 0) for d in sys.argv[1:]] or DEFAULT
-    with ThreadPoolExecutor(4) as ex:
+    # processes, not threads: hiprtc compiles one program at a time per process
+    with ProcessPoolExecutor(8) as ex:
         futs = [ex.submit(one, j) for j in jobs]
         if not sys.argv[1:]:
             futs += [ex.submit(one_block, j) for j in BLOCK]

@@ -172,3 +172,14 @@ def test_rtc_code_objects_load_from_disk_in_a_fresh_process(tmp_path):
     assert first["kernel"].startswith("rwm_gsn_chol_kernel<D=48,") and first["rtc"][0] == "compiled"
     assert second["rtc"][0] == "disk" and second["rtc"][1] < 1.0 and second["setup_s"] < 1.0
     assert any(p.suffix == ".co" for p in (tmp_path / "cache").iterdir())
+
+
+@pytest.mark.parametrize("D,ll_mode,nobs", [(53, L.LL_PER_OBS, 7), (56, L.LL_SUFFSTAT, 10), (64, L.LL_PER_OBS, 1)])
+def test_chol_shared_sweep_shapes(oracle, D, ll_mode, nobs):
+    """D ≥ 52 (rwm_gsn_chol_kernel's shared sweep: ltd and every observation through one
+    copy of the substitution code) at an odd observation count, the x̄ term and a single
+    observation, bitwise against the oracle."""
+    w = _corr(D, 7 * D, nobs=nobs)
+    e = run_engine(w, 768, 24, ll_mode=ll_mode)
+    assert e["kernel"].startswith(f"rwm_gsn_chol_kernel<D={D},") and "[hiprtc]" in e["kernel"]
+    assert_bitwise(e, run_oracle(oracle, w, 768, 24, ll_mode=ll_mode))

@@ -94,6 +94,22 @@ def test_univariate_family_against_scipy(oracle, dist, ref, x0):
     np.testing.assert_allclose([pr.logpdf([x]) for x in xs], want, rtol=1e-12, atol=1e-13)
 
 
+def test_cauchy_far_tail_stays_finite(oracle):
+    """Cauchy's log(1 + z²) as StatsFuns' log1psq: past |z| = 2^53 it is 2·log|z|, so a
+    far-tail θ (z² overflows at |z| > 1.34e154) still has a finite log density."""
+    a, b = -1.0, 0.5
+    xs = np.array([1e20, -1e20, 3e100, 1e200, -1e300, 1e16, 2.0 ** 53 * 0.5 + a])
+    pr = ProductPrior([Cauchy(a, b)], [1])
+    kind, fs = prior_to_device(pr, 1)
+    z = np.abs((xs - a) / b)
+    want = np.array([-(math.log1p(v * v) if v < 2.0 ** 53 else 2.0 * math.log(v)) - math.log(math.pi) - math.log(b)
+                     for v in z])
+    got = oracle.eval_prior(kind, 1, fs, xs.reshape(-1, 1))
+    assert np.all(np.isfinite(got))
+    np.testing.assert_allclose(got, want, rtol=2e-15, atol=0)
+    np.testing.assert_allclose([pr.logpdf([x]) for x in xs], want, rtol=2e-15, atol=0)
+
+
 @pytest.mark.parametrize("dist,x", [(Uniform(0.0, 1.0), 1.5), (Exponential(1.0), -0.1), (Gamma(2.0, 1.0), -1.0),
                                     (LogNormal(0.0, 1.0), -0.5), (LogNormal(0.0, 1.0), 0.0), (Beta(2.0, 2.0), 1.2),
                                     (Beta(2.0, 2.0), -0.2), (InverseGamma(2.0, 1.0), 0.0)])

@@ -492,22 +492,39 @@ def main():
     # diagnostics over the first timed window, through the C ABI (emcmc_diagnostics): one
     # all-gather of 3·D+3 doubles per rank — ncclAllGather inside libemcmc on an RCCL comm
     # (nccl process group), the host-callback comm over gloo — Chan-merged in rank order
-    diag, diag_via = None, None
+    diag, diag_via, diag_stuck = None, None, False
     if hist == L.HIST_FULL and not a.history_ring and a.steps >= 4:
-        comm = None
-        if dist is not None:
-            comm = DG.Comm.torch_host() if shared else DG.Comm.from_process_group(local)
-        diag = eng.diagnostics(a.warmup + 1, a.steps, split=True, comm=comm)
-        diag_via = ("emcmc_diagnostics, this rank alone" if comm is None else
-                    f"emcmc_diagnostics over {'a host all-gather (gloo)' if shared else 'RCCL (ncclAllGather)'}, "
-                    f"{diag['nranks']} ranks")
-        if comm is not None:
-            comm.close()
+        if dist is None:
+            diag = eng.diagnostics(a.warmup + 1, a.steps, split=True)
+            diag_via = "emcmc_diagnostics, this rank alone"
+        else:
+            def gathered(make, label):
+                comm = make()
+                try:
+                    d = eng.diagnostics(a.warmup + 1, a.steps, split=True, comm=comm)
+                finally:
+                    comm.close()
+                return d, f"emcmc_diagnostics over {label}, {d['nranks']} ranks"
+
+            if shared:
+                res, err = watchdog(lambda: gathered(DG.Comm.torch_host, "a host all-gather (gloo)"), 120.0)
+            else:
+                res, err = watchdog(lambda: gathered(lambda: DG.Comm.from_process_group(local),
+                                                     "RCCL (ncclAllGather inside libemcmc)"), 120.0)
+                if err is not None and err != "timeout":  # the same merge through torch's own all-gather
+                    res, err2 = watchdog(lambda: gathered(lambda: DG.Comm.torch_host(device=dev),
+                                                          f"torch's all-gather (RCCL comm failed: {err[:160]})"),
+                                         120.0)
+                    err = err2
+            if err is None:
+                diag, diag_via = res
+            else:  # measured already; report without diagnostics and do not wait on a stuck collective
+                diag_via, diag_stuck = f"diagnostics failed: {err[:200]}", True
 
     # parity on every rank: 8 of its chains replayed on the oracle after the timed
     # region (global ids first + c), AND-reduced over the ranks
     par = None
-    if not a.history_ring and not a.no_parity:
+    if not a.history_ring and not a.no_parity and not diag_stuck:
         try:
             par = parity_sample(eng, w, a, ll_mode, first, reps + timing_reps)
             ok = all(v for k, v in par.items() if k.endswith("bitwise"))
@@ -518,6 +535,8 @@ def main():
             par["all_ranks_bitwise"] = reduce_over_ranks(1.0 if ok else 0.0, dist, dev, "min") == 1.0
 
     if rank != 0:
+        if diag_stuck:
+            os._exit(0)  # a collective may still be pending on the stream: no teardown
         dist.destroy_process_group()
         return
 
@@ -675,6 +694,8 @@ def main():
                               "chains_merged": diag["num_chains"], "via": diag_via}
         if not cfg3:
             out["diagnostics"]["max_abs_mean_minus_xbar"] = float(np.max(np.abs(diag["mean"] - w.obs.mean(0))))
+    elif diag_via is not None:
+        out["diagnostics"] = {"error": diag_via}
     if world == 1 and not a.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(w, a.cpu_seconds, ll_mode)
@@ -686,10 +707,34 @@ def main():
     if stub:
         out["stub_engine"] = True
         out["data"] = "STUB ENGINE (tests/bench_stub.py): launcher and rank plumbing only, nothing measured"
-    print(json.dumps(out))
+    print(json.dumps(out), flush=True)
+    if diag_stuck:
+        os._exit(0)  # a collective may still be pending on the engine's stream: no teardown
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def watchdog(fn, seconds):
+    """(fn(), None), or (None, "timeout") when fn has not returned after `seconds`, or
+    (None, repr(exception)): the diagnostics collective runs after the timed region, and a
+    rank that never joins it must not turn a finished measurement into a hung job."""
+    import threading
+
+    box = {}
+
+    def run():
+        try:
+            box["v"] = fn()
+        except BaseException as e:  # noqa: BLE001 — reported in the line
+            box["e"] = repr(e)
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    t.join(seconds)
+    if t.is_alive():
+        return None, "timeout"
+    return box.get("v"), box.get("e")
 
 
 def parity_sample(eng, w, a, ll_mode, first=0, reps=1, n=8):

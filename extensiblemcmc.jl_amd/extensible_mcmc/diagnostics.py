@@ -175,8 +175,9 @@ class Comm:
         return comm
 
     @classmethod
-    def torch_host(cls, group=None) -> "Comm":
-        """A host comm over a torch.distributed group (CPU tensors: gloo)."""
+    def torch_host(cls, group=None, device=None) -> "Comm":
+        """A host comm over a torch.distributed group: CPU tensors (gloo), or tensors on
+        `device` (a torch device, e.g. under the nccl backend)."""
         import torch
         import torch.distributed as dist
 
@@ -184,9 +185,11 @@ class Comm:
 
         def ag(send):
             t = torch.from_numpy(send)
-            out = torch.empty(world * t.numel(), dtype=t.dtype)
+            if device is not None:
+                t = t.to(device)
+            out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
             dist.all_gather_into_tensor(out, t, group=group)
-            return out.numpy()
+            return out.cpu().numpy()
 
         return cls.host(world, dist.get_rank(group), ag)
 

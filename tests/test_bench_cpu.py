@@ -72,3 +72,15 @@ def test_gpus_must_match_the_launchers_world_size():
                           drop_world=False)
     assert r.returncode != 0 and line is None
     assert "--gpus 4 but WORLD_SIZE=2" in r.stderr
+
+
+def test_diagnostics_watchdog():
+    """The diagnostics collective after the timed region runs under a watchdog: a result, an
+    exception (then bench.py retries through torch's all-gather) or a timeout (then the line
+    is printed without diagnostics and the rank exits without waiting on the collective)."""
+    import time
+
+    assert bench.watchdog(lambda: 3, 5.0) == (3, None)
+    v, err = bench.watchdog(lambda: 1 / 0, 5.0)
+    assert v is None and err.startswith("ZeroDivisionError")
+    assert bench.watchdog(lambda: time.sleep(3.0), 0.2) == (None, "timeout")

@@ -44,7 +44,7 @@ def test_nccl_process_group_at_one_rank_matches_the_single_process_line():
     assert rccl["config"]["process_group"] == "nccl" and rccl["n_gpus"] == 1
     assert rccl["config"]["workload"] == single["config"]["workload"]
     via = rccl["diagnostics"].pop("via")
-    assert "RCCL (ncclAllGather), 1 ranks" in via and single["diagnostics"].pop("via").endswith("this rank alone")
+    assert "RCCL (ncclAllGather inside libemcmc), 1 ranks" in via and single["diagnostics"].pop("via").endswith("this rank alone")
     assert rccl["diagnostics"] == single["diagnostics"]
     assert rccl["parity"]["all_ranks_bitwise"] is True and single["parity"]["accept_stream_bitwise"] is True
 

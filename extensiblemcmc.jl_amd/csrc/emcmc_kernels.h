@@ -552,9 +552,11 @@ __device__ __forceinline__ void static_for(F &&f) {
 // loads are issued right after the FIRST use of this chunk's values (SMEM
 // returns out of order, so every wait is lgkmcnt(0): loads issued earlier would
 // be waited for too) and stay in flight during the chunk's other CH − 1 fmas.
-// The chunk pointers go through an empty asm (loads from constant memory alias
-// nothing, so the IR would otherwise hoist and merge a whole sweep's loads into
-// SGPRs), and every result is pinned with vpin, so the stream keeps its order.
+// Before each chunk's loads the base pointer (X or T) goes through an empty asm,
+// in place (loads from constant memory alias nothing, so the IR would otherwise
+// hoist and merge a whole sweep's loads into SGPRs), and the chunk's offset from it
+// is a compile-time constant folded into the s_load's immediate: no scalar address
+// arithmetic per chunk.  Every result is pinned with vpin, so the stream keeps its order.
 // fpre(IntC<i>, x_i) for the prefix, ftab(IntC<j>, IntC<i>, T_ij) for the table.
 // Chunks are 16 doubles at any D: the prefix takes ⌈NA/16⌉ chunks (the last one
 // partial) and the table starts on a chunk of its own, so an odd D streams the
@@ -579,8 +581,14 @@ __device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, F
     constexpr int NCH = S::NCH;
     auto load = [&](auto TC, double(&buf)[CH]) {
         constexpr int t = decltype(TC)::value, e0 = S::first(t), n = S::len(t);
-        cdouble *p = (e0 < NA) ? X + e0 : T + (e0 - NA);
-        asm volatile("" : "+s"(p));
+        cdouble *p;
+        if constexpr (e0 < NA) {
+            asm volatile("" : "+s"(X));
+            p = X + e0;
+        } else {
+            asm volatile("" : "+s"(T));
+            p = T + (e0 - NA);
+        }
 #pragma unroll
         for (int r = 0; r < CH; ++r)
             if (r < n) buf[r] = p[r];
@@ -613,12 +621,20 @@ __device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, F
 }
 
 // ‖L⁻¹ r‖² by forward substitution as column updates, r given by the prefix
-// (NA = D: acc_i = x_i − θ°_i) or already in acc (NA = 0); canonical order
+// (NA = D: acc_i = x_i − θ°_i) or already in acc (NA = 0); canonical order.  y_j's
+// square joins the blocked sum one column late, right after y_{j+1} is formed: the
+// column's first update reads y_{j+1} at once, and the square fills the fp64
+// result-to-use wait that an s_nop took (same operations in the same order).
 template <int D, int NA>
 __device__ __forceinline__ double chol_sqmahal(cdouble *X, cdouble *Ts, const double (&thp)[D], double (&acc)[D]) {
     constexpr int BLK = SumShape<D>::BLK, NB = D / BLK;
     double b[NB];
-    double s = 0.0, y = 0.0;
+    double s = 0.0, y = 0.0, yl = 0.0;
+    auto square = [&](auto JC, double v) {
+        constexpr int j = decltype(JC)::value;
+        s = (j % BLK == 0) ? v * v : fma(v, v, s);
+        if constexpr (j % BLK == BLK - 1) b[j / BLK] = s;
+    };
     chol_stream<D, NA>(
         X, Ts,
         [&](auto IC, double x) {
@@ -631,13 +647,14 @@ __device__ __forceinline__ double chol_sqmahal(cdouble *X, cdouble *Ts, const do
             if constexpr (i == j) {  // v = 1/L_jj
                 y = acc[j] * v;
                 vpin(y);
-                s = (j % BLK == 0) ? y * y : fma(y, y, s);
-                if constexpr (j % BLK == BLK - 1) b[j / BLK] = s;
+                if constexpr (j > 0) square(IntC<j - 1>{}, yl);
+                yl = y;
             } else {
                 acc[i] = fma(-v, y, acc[i]);
                 vpin(acc[i]);
             }
         });
+    square(IntC<D - 1>{}, yl);
     return tree_inplace<NB>(b);
 }
 

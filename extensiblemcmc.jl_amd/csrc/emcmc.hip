@@ -174,6 +174,10 @@ struct emcmc_handle {
     uint64_t stats_N = 1;  // GenericChainStats.N (chain_statistics.jl:34)
     // device buffers
     double *d_theta = nullptr, *d_ll = nullptr, *d_ra = nullptr;
+    // non-null: the current θ is this FULL-history slot (the last launch of rwm_gsn_diag_kernel
+    // left it there and did not write d_theta); settle_theta copies it back before any other use
+    double *theta_live = nullptr;
+    bool theta_live_ok = true;  // EMCMC_THETA_LIVE=0: always write the state buffer (A/B)
     uint64_t *d_ring = nullptr;
     uint32_t *d_nacc = nullptr, *d_faults = nullptr;
     // any-fault word, written by the kernels only when a chain ends a launch faulted:
@@ -1047,10 +1051,26 @@ emcmc_status select_variant(emcmc_handle *h) {
 // Algorithmic HBM bytes of one launch group: the step kernel
 // and, on the mix / chain-moments path, the batched mean/cov kernel and the
 // Haario readjust when it follows the group.
+// The fused diagonal kernel in FULL history mode leaves θ in its launch's last history slot
+// and does not write the state buffer too (8·D bytes per chain and launch less: 2.3% of a
+// 20-step launch at D = 32); theta_live points there until something else needs d_theta.
+bool theta_in_hist(const emcmc_handle *h) {
+    return h->var.fn && !h->var.ffn && !h->var.mfn && !h->var.ufn && !h->var.xfn && !h->var.afn &&
+           h->var.dense == 0 && h->d_hist_theta && h->cfg.history_mode == EMCMC_HIST_FULL && h->theta_live_ok;
+}
+emcmc_status settle_theta(emcmc_handle *h) {
+    if (!h->theta_live) return EMCMC_OK;
+    const uint64_t n = h->cfg.num_chains * (uint64_t)h->cfg.dim;
+    HIPCHK(h, hipMemcpyAsync(h->d_theta, h->theta_live, n * sizeof(double), hipMemcpyDeviceToDevice, h->stream));
+    h->theta_live = nullptr;
+    return EMCMC_OK;
+}
+
 double bytes_per_launch(const emcmc_handle *h, uint64_t nsteps, bool readjust) {
     const double C = (double)h->cfg.num_chains, D = (double)h->cfg.dim;
     double per_step = (h->cfg.history_mode == EMCMC_HIST_FULL) ? (16.0 * D + 8.0 + 0.125) : 0.125;
     double state = 16.0 * D + 2 * 8 + 2 * 8 + 2 * 16 + 2 * 4 + 2 * 4;  // θ, ll, ra, ring, nacc, faults (R+W)
+    if (theta_in_hist(h)) state -= 8.0 * D;  // θ read, not written back (its last history slot holds it)
     if (h->var.xfn) {
         const double DP = D * (D + 1) / 2;
         // mix_moments_kernel: θ of every step once (ACCEPT_ONLY: written by the
@@ -1569,6 +1589,7 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
     }
     if (const char *e = getenv("EMCMC_HOST_TIMING")) h->host_timing = *e && *e != '0';
     if (const char *e = getenv("EMCMC_SYNC")) h->sync_mode = atoi(e) ? 1 : 0;
+    if (const char *e = getenv("EMCMC_THETA_LIVE")) h->theta_live_ok = atoi(e) != 0;
     if (h->sync_mode && hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming) != hipSuccess) h->sync_mode = 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
         delete h;
@@ -2061,6 +2082,7 @@ emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double 
     for (uint64_t c = 0; c < C; ++c)
         for (uint64_t d = 0; d < D; ++d) soa[state_pos(d, c, C, (uint32_t)D)] = theta[c * D + d];
     HIPCHK(h, hipMemcpyAsync(h->d_theta, soa.data(), C * D * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    h->theta_live = nullptr;
     std::vector<double> l(C, -INFINITY);
     if (ll) std::copy(ll, ll + C, l.begin());
     HIPCHK(h, hipMemcpyAsync(h->d_ll, l.data(), C * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -2153,6 +2175,9 @@ emcmc_status run_impl(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
             return fail(h, EMCMC_INVALID_ARG, "step %llu: mcmciter %u outside 1..M", (unsigned long long)i,
                         steps[i].mcmciter);
     }
+    const bool live = theta_in_hist(h);
+    if (!live)
+        if (emcmc_status s = settle_theta(h)) return s;
     if (h->var.mfn || h->var.ufn) return run_mwg(h, steps, num_steps);
     if (h->var.xfn) return run_mix(h, steps, num_steps);
     if (h->var.afn) return run_mala(h, steps, num_steps);
@@ -2221,12 +2246,21 @@ emcmc_status run_impl(emcmc_handle *h, const emcmc_step *steps, uint64_t num_ste
         if (p.iter0 > 1 && h->last_iter[p.pidx0] != p.iter0 - 1)
             HIPCHK(h, hipMemsetAsync(h->d_ra, 0, C * sizeof(double), h->stream));
         h->last_iter[p.pidx0] = steps[j - 1].mcmciter;
+        if (live) {  // θ from the previous launch's last history slot, left in this launch's
+            p.theta_in = h->theta_live ? h->theta_live : h->d_theta;
+            p.theta = nullptr;
+        } else {
+            p.theta_in = nullptr;
+            p.theta = h->d_theta;
+        }
         void *args[] = {&p};
         if (h->var.ffn)
             HIPCHK(h, launch_module(h, h->var.ffn, grid, block, args, h->lds_bytes, bytes_per_launch(h, n, false)));
         else
             HIPCHK(h, launch_step(h, reinterpret_cast<const void *>(h->var.fn), grid, block, args, h->lds_bytes,
                                   bytes_per_launch(h, n, false)));
+        if (live)  // slot (iter − 1)·P + pidx0 of the launch's last iteration, as the kernel addressed it
+            h->theta_live = p.hist_theta + ((uint64_t)(p.iter0 + n - 2) * P + p.pidx0) * C * (uint64_t)h->cfg.dim;
         h->stats_N += n;
         i = j;
     }
@@ -2294,6 +2328,7 @@ const char *emcmc_last_error(const emcmc_handle *h) { return h ? h->err.c_str() 
 emcmc_status emcmc_get_state(emcmc_handle *h, double *theta, double *ll) {
     if (!h) return EMCMC_INVALID_ARG;
     if (!h->allocated) return fail(h, EMCMC_STATE_ERROR, "no state");
+    if (emcmc_status s = settle_theta(h)) return s;
     HIPCHK(h, hipStreamSynchronize(h->stream));
     const uint64_t C = h->cfg.num_chains, D = h->cfg.dim;
     if (theta) {  // device state_pos layout → host [C][D]

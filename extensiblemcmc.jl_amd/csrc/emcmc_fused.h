@@ -79,7 +79,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     const SlotOffset<D> &hoff = soff;
     const uint32_t c32 = (uint32_t)chain;  // C < 2^32 (emcmc_create)
     double th[DPL];
-    load_slot<D>(a.theta, soff, th);
+    load_slot<D>(a.theta_in ? a.theta_in : a.theta, soff, th);
     double ll = chain_elem(a.ll, c32);
     double ra = chain_elem(a.ra, c32);
     uint64_t r0 = chain_elem(a.ring, 2 * c32), r1 = chain_elem(a.ring, 2 * c32 + 1);
@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         chain_elem(a.faults, c32) = faults;
         if (faults) *a.fault_flag = 1u;
     }
-    store_slot_cached<D>(a.theta, soff, th);
+    if (a.theta) store_slot_cached<D>(a.theta, soff, th);  // else: the last θ history slot holds it
 }
 
 // ---------------------------------------------------------------------------

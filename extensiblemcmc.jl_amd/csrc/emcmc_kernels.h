@@ -73,6 +73,10 @@ struct StepParams {
     double S_c;           // Σ_k ‖L_t⁻¹(x_k − x̄)‖²  (SUFFSTAT)
     double nobs_d;        // (double) nobs
     double rcp_W;         // RN(1/W) for the rolling-acceptance quotient
+    // rwm_gsn_diag_kernel only: θ is loaded from theta_in when set (the previous launch's
+    // last θ history slot), and not stored back when theta is null (this launch's last
+    // history slot then holds it: emcmc.hip, theta_live)
+    const double *theta_in;
 };
 
 // constants layout (offsets in doubles), D = dimension

@@ -79,4 +79,6 @@ def test_timing_reports_launches(full_run):
     eng.synchronize()
     ms, n, b = eng.get_timing()
     assert n == 2 and ms > 0
-    assert b == pytest.approx(65536 * (128 * (16 * 32 + 8.125) + 2 * (16 * 32 + 80)))
+    # per launch: θ, ll, ra, ring, nacc, faults read and written, except θ's write-back: the
+    # fused kernel leaves θ in its last history slot in FULL mode (emcmc.hip theta_live)
+    assert b == pytest.approx(65536 * (128 * (16 * 32 + 8.125) + 2 * (8 * 32 + 80)))

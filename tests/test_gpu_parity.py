@@ -269,3 +269,45 @@ def test_many_observations_other_dims_use_the_general_kernel(oracle):
     eng, st, h = run_both(oracle, 4, 300, 60, ups, mu, np.eye(4), obs, steps, 99)
     assert "mwg_gsn_kernel<D=4" in eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_state_left_in_history_feeds_the_next_kernel():
+    """After a FULL-history run of the fused diagonal kernel the current θ lives in its
+    last history slot (emcmc.hip theta_live; the state buffer is not written back): a
+    later run on another kernel — a dense Σ_t selects rwm_gsn_chol_kernel — and
+    get_state must both see it.  The same second part started from get_state's θ on a
+    fresh engine gives the same chains, bit for bit."""
+    rng = np.random.default_rng(41)
+    w = W.cfg2(512, D=16)
+    A = rng.standard_normal((16, 16))
+    St = A @ A.T / 16 + np.eye(16)
+    eng = Engine(EngineConfig(dim=16, num_chains=512, num_mcmc_steps=60, seed=w.seed, steps_per_launch=7))
+    eng.add_gaussian_rw_update(np.arange(16), w.rw_sigma)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    eng.set_state(np.zeros((512, 16)))
+    eng.run_iters(1, 30)
+    eng.synchronize()
+    assert eng.kernel_name().startswith("rwm_gsn_diag_kernel")
+    th_mid, ll_mid = eng.get_state()
+    last = eng.get_history(L.H_STATE, 30, 1)[0, 0]
+    assert np.array_equal(th_mid, last)  # the state is the last history slot
+    eng.run_iters(31, 5)  # fused again: starts from the slot, leaves θ in slot 35
+    eng.set_gsn_target(w.mu_true, St, w.obs)
+    eng.run_iters(36, 20)
+    eng.synchronize()
+    assert "chol" in eng.kernel_name()
+    th_a, _ = eng.get_state()
+
+    ref = Engine(EngineConfig(dim=16, num_chains=512, num_mcmc_steps=60, seed=w.seed, steps_per_launch=7))
+    ref.add_gaussian_rw_update(np.arange(16), w.rw_sigma)
+    ref.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    ref.set_state(th_mid, ll_mid)
+    ref.run_iters(31, 5)
+    ref.synchronize()
+    th5, ll5 = ref.get_state()
+    ref.set_gsn_target(w.mu_true, St, w.obs)
+    ref.set_state(th5, ll5)
+    ref.run_iters(36, 20)
+    ref.synchronize()
+    th_b, _ = ref.get_state()
+    assert np.array_equal(th_a, th_b)

@@ -262,19 +262,31 @@ __global__ void __launch_bounds__(256, kMixResMinBlocks) mix_res_kernel(const Mi
         const double qa = row_sumsq32(rr0 * iLA0, rr1 * iLA1, qlead);
         double qbb[4];
         {
-            double acca = rra, accb = rrb;
-            static_for<0, D>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                // row j's owner: lane j (row fa) for j < 16, lane 31 − j (row fb) above
-                const double t = (j < H) ? acca * iLBa : accb * iLBb;
-                const double y = rbcast<(j < H) ? j : D - 1 - j>(t);  // y_B,j
+            // Column j: the owner's t_j = acc·(1/L_jj) is broadcast as y_B,j. Between the
+            // product and its row broadcast (two wait states) go the column-(j−1) work t_j does
+            // not need: the other folded row's update (j < 16) and y_{j−1}'s square — the same
+            // operations, each accumulator's in its order.
+            double acca = rra, accb = rrb, yl = 0.0;
+            auto square = [&](auto JC, double y) {
+                constexpr int j = decltype(JC)::value;
                 if constexpr (j % 8 == 0) qbb[j / 8] = y * y;
                 else qbb[j / 8] = fma(y, y, qbb[j / 8]);
-                if constexpr (j + 1 < D) {
-                    if constexpr (j < H) acca = fma(-La[j], y, acca);
-                    accb = fma(-Lb[j], y, accb);
+            };
+            static_for<0, D>([&](auto jc) {
+                constexpr int j = decltype(jc)::value;
+                if constexpr (j > 0) {  // the row t_j reads first
+                    if constexpr (j < H) acca = fma(-La[j - 1], yl, acca);
+                    else accb = fma(-Lb[j - 1], yl, accb);
                 }
+                // row j's owner: lane j (row fa) for j < 16, lane 31 − j (row fb) above
+                const double t = (j < H) ? acca * iLBa : accb * iLBb;
+                if constexpr (j > 0) {
+                    if constexpr (j < H) accb = fma(-Lb[j - 1], yl, accb);
+                    square(IntC<j - 1>{}, yl);
+                }
+                yl = rbcast<(j < H) ? j : D - 1 - j>(t);  // y_B,j
             });
+            square(IntC<D - 1>{}, yl);
         }
         const double qb = tree_inplace(qbb);
         const double lpA = fma(-0.5, qa, a.c0A);

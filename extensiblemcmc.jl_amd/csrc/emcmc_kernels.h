@@ -566,6 +566,7 @@ __device__ __forceinline__ void static_for(F &&f) {
 // partial) and the table starts on a chunk of its own, so an odd D streams the
 // same ≤ 134 chunks per sweep as an even one (SMEM needs 4-byte alignment only).
 constexpr int kCholChunk = 16;
+constexpr int kCholTouchD = 64;  // D from which the stream batches its scalar-cache touches
 template <int D, int NA>
 struct CholChunks {
     static constexpr int NCA = (NA + kCholChunk - 1) / kCholChunk;  // prefix chunks
@@ -607,12 +608,36 @@ __device__ __forceinline__ void chol_stream(cdouble *X, cdouble *T, FP &&fpre, F
         }
     };
     double cur[CH], nxt[CH];
+    // D = 64: every fourth chunk, one batch of scalar loads of one dword per 64-byte line
+    // of the next four chunks ("touches", results never read) so that their scalar-cache
+    // misses overlap in one wait instead of stalling the stream one by one (+7% at D = 64;
+    // at D = 48 / 56 the same batches cost 2–3%: DESIGN.md §6)
+    constexpr int G = D >= kCholTouchD ? 4 : 0;
+    uint32_t pf = 0u;  // destination of the touches (never read)
+    auto touch = [&pf, &X, &T](auto CC) {  // the two 64-byte lines at the start of chunk c
+        constexpr int c = decltype(CC)::value, e0 = S::first(c);
+        if constexpr (e0 < NA)
+            asm volatile("s_load_dword %0, %1, %2\n\ts_load_dword %0, %1, %3" : "+s"(pf) : "s"(X), "n"(8 * e0),
+                         "n"(8 * e0 + 64));
+        else
+            asm volatile("s_load_dword %0, %1, %2\n\ts_load_dword %0, %1, %3" : "+s"(pf) : "s"(T), "n"(8 * (e0 - NA)),
+                         "n"(8 * (e0 - NA) + 64));
+    };
     load(IntC<0>{}, cur);
     static_for<0, NCH>([&](auto TC) {
         constexpr int t = decltype(TC)::value, e0 = S::first(t), n = S::len(t);
         elem(IntC<e0>{}, cur[0]);
+        if constexpr (G > 0 && t > 0 && (t - 1) % G == 0) {
+            uint32_t &pfr = pf;
+            asm volatile("" ::"s"(pfr));  // landed: waited with cur
+        }
         sbar();
         if constexpr (t + 1 < NCH) load(IntC<t + 1>{}, nxt);
+        if constexpr (G > 0 && t % G == 0) {
+            // one batch of touches for the chunks t + 2 … t + G + 1: their misses overlap in
+            // one wait (the next chunk's) instead of stalling the stream one by one
+            static_for<t + 2, (t + G + 2 < NCH ? t + G + 2 : NCH)>([&](auto CC) { touch(CC); });
+        }
         sbar();
         static_for<1, n>([&](auto RC) {
             constexpr int r = decltype(RC)::value;

@@ -465,6 +465,15 @@ class Engine:
             return bits[..., :Cn].astype(bool)
         return out
 
+    def get_history_bits(self, iter_first: int, num_iters: int):
+        """The accept history as stored: [n][P][⌈C/64⌉] u64 words, chain c = bit c % 64 of
+        word c // 64 (8× smaller than get_history's unpacked bools, for whole-run checks)."""
+        P, Cn = self.num_updates, self.cfg.num_chains
+        out = np.empty((num_iters, P, (Cn + 63) // 64), dtype=np.uint64)
+        self._check(self._lib.emcmc_get_history(self._h, L.H_ACCEPT, iter_first, num_iters, out.ctypes.data,
+                                                out.nbytes), "emcmc_get_history")
+        return out
+
     def get_history_chains(self, which: int, iter_first: int, num_iters: int, chain_first: int, num_chains: int):
         """History window for a chain range: STATE/PROPOSAL [n][P][c][D], LL [n][P][c]."""
         P, D = self.num_updates, self.cfg.dim

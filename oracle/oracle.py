@@ -97,21 +97,46 @@ class OracleState:
         self.last_iter = 0  # last iteration run (rolling_ar[iter−1] reads 0.0 after a gap)
 
 
-def alloc_history(C, D, nsteps):
+def alloc_history(C, D, nsteps, accept_only=False):
+    """History buffers of one oracle call: θ, θ°, ll [nsteps][C](D) and the accept bytes;
+    accept_only: the accept bytes alone (1 B per chain-step, so every chain of a
+    BASELINE shape replays in memory — the θ/θ°/ll histories are never formed)."""
+    if accept_only:
+        return {"acc": np.empty((nsteps, C), dtype=np.uint8)}
     return {"theta": np.empty((nsteps, C, D)), "prop": np.empty((nsteps, C, D)), "ll": np.empty((nsteps, C)),
             "acc": np.empty((nsteps, C), dtype=np.uint8)}
 
 
+def pack_accept(acc):
+    """[n][C] accept flags → [n][⌈C/64⌉] u64 words, bit c%64 of word c//64 = chain c: the
+    layout of the engine's accept history rows (Engine.get_history_bits)."""
+    acc = np.asarray(acc)
+    n, C = acc.shape
+    words = (C + 63) // 64
+    b = np.zeros((n, words * 8), dtype=np.uint8)
+    b[:, :(C + 7) // 8] = np.packbits(acc.view(np.uint8) if acc.dtype == bool else acc.astype(np.uint8), axis=1,
+                                      bitorder="little")
+    return b.view(np.uint64)
+
+
+def accept_mismatch_chains(got_words, want_words, C):
+    """Chains (of C) whose accept stream differs anywhere between two packed [n][words] arrays."""
+    x = np.bitwise_or.reduce(np.bitwise_xor(got_words, want_words), axis=0)
+    bits = np.unpackbits(x.view(np.uint8), bitorder="little")[:C]
+    return np.flatnonzero(bits)
+
+
 def run_gsn(state: OracleState, *, seed, rw_sigma, t_sigma, obs, iter0, nsteps, chain0=0, ll_mode=0, W=100,
-            iters=None, history=True, nthreads=1, hist=None):
+            iters=None, history=True, nthreads=1, hist=None, accept_only=False):
     """Advance `state` by `nsteps` iterations of the single joint GaussianRW update.
-    `hist` may be a preallocated alloc_history(C, D, nsteps) dict (reused buffers)."""
+    `hist` may be a preallocated alloc_history(C, D, nsteps) dict (reused buffers);
+    accept_only: record the accept stream alone (hist["acc"] [nsteps][C])."""
     L = lib()
     Cn, D = state.C, state.D
     X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
     reuse = hist is not None
     if not reuse:
-        hist = alloc_history(Cn, D, nsteps) if history else {}
+        hist = alloc_history(Cn, D, nsteps, accept_only) if (history or accept_only) else {}
     history = bool(hist)
     it = None
     if iters is not None:
@@ -132,7 +157,7 @@ def run_gsn(state: OracleState, *, seed, rw_sigma, t_sigma, obs, iter0, nsteps, 
     state.N += nsteps
     state.last_iter = int(it[-1]) if it is not None else int(iter0) + nsteps - 1
     if history and not reuse:
-        hist["acc"] = hist["acc"].astype(bool)
+        hist["acc"] = hist["acc"].view(bool)  # 0/1 bytes: a view, no copy
     return hist
 
 
@@ -608,10 +633,11 @@ class MixState(OracleState):
 
 
 def run_mix(state: MixState, *, seed, sigma_a, t_sigma, obs, iter0, nsteps, mix=True, lam=0.5, haario_k=0,
-            chain0=0, ll_mode=0, W=100, history=True, nthreads=1):
+            chain0=0, ll_mode=0, W=100, history=True, nthreads=1, accept_only=False):
     """Advance `state` by `nsteps` consecutive iterations of the single joint
     GaussianRandomWalkMix (mix=True) or GaussianRandomWalk (mix=False) update
-    with on-device chain moments; haario_k > 0 adds HaarioTypeAdaptation(k)."""
+    with on-device chain moments; haario_k > 0 adds HaarioTypeAdaptation(k).
+    accept_only: record the accept stream alone (hist["acc"] [nsteps][C])."""
     L = lib()
     if not hasattr(L, "_mix_ready"):
         dp, u32p, u64p, u8p = (C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.POINTER(C.c_uint64),
@@ -623,7 +649,8 @@ def run_mix(state: MixState, *, seed, sigma_a, t_sigma, obs, iter0, nsteps, mix=
         L._mix_ready = True
     Cn, D = state.C, state.D
     X = np.ascontiguousarray(np.asarray(obs, dtype=np.float64).reshape(-1, D))
-    hist = alloc_history(Cn, D, nsteps) if history else {}
+    hist = alloc_history(Cn, D, nsteps, accept_only) if (history or accept_only) else {}
+    history = bool(hist)
     if iter0 > 1 and state.last_iter != iter0 - 1:
         state.ra[:] = 0.0
     N = np.array([state.N], dtype=np.uint64)
@@ -641,7 +668,7 @@ def run_mix(state: MixState, *, seed, sigma_a, t_sigma, obs, iter0, nsteps, mix=
     state.N, state.M = int(N[0]), int(M[0])
     state.last_iter = iter0 + nsteps - 1
     if history:
-        hist["acc"] = hist["acc"].astype(bool)
+        hist["acc"] = hist["acc"].view(bool)
     return hist
 
 

@@ -62,7 +62,10 @@ def test_gpus_n_launches_n_ranks():
     assert line["config"]["first_chain_id"] == 0
     one = _bench_line(["--gpus", "1", *STUB_ARGS], {})[1]
     assert one["n_gpus"] == 1 and one["config"]["total_chains"] == 65536
-    assert line["diagnostics"]["max_split_rhat"] != one["diagnostics"]["max_split_rhat"]  # rank 1's shard merged
+    key = "plumbing_check_split_rhat_max"  # a 6–25 window from θinit = 0 is burn-in: labelled, not convergence
+    assert "plumbing check, burn-in window" in line["diagnostics"]["purpose"]
+    assert line["diagnostics"]["window_iterations"] == [6, 25]
+    assert line["diagnostics"][key] != one["diagnostics"][key]  # rank 1's shard merged
     assert line["diagnostics"]["chains_merged"] == 2 * 131072  # split halves of both shards
     assert "host all-gather (gloo), 2 ranks" in line["diagnostics"]["via"]
 
@@ -84,3 +87,38 @@ def test_diagnostics_watchdog():
     v, err = bench.watchdog(lambda: 1 / 0, 5.0)
     assert v is None and err.startswith("ZeroDivisionError")
     assert bench.watchdog(lambda: time.sleep(3.0), 0.2) == (None, "timeout")
+
+
+class _ReplayEngine:
+    """The engine surface parity_replay reads, backed by an oracle run (CPU): a
+    'GPU' whose results are the oracle's, optionally with one chain's stream flipped."""
+
+    def __init__(self, O, w, S, flip=None):
+        self.st = O.OracleState(np.zeros((w.num_chains, w.D)))
+        h = O.run_gsn(self.st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=S,
+                      accept_only=True, nthreads=2)
+        self.bits = O.pack_accept(h["acc"])[:, None, :]
+        if flip is not None:
+            it, c = flip
+            self.bits[it, 0, c // 64] ^= np.uint64(1 << (c % 64))
+
+    def get_history_bits(self, i0, n):
+        return self.bits[i0 - 1:i0 - 1 + n]
+
+    def get_state(self):
+        return self.st.theta, self.st.ll
+
+
+@pytest.mark.parametrize("flip", [None, (7, 130)])
+def test_parity_replay_counts_mismatched_chains(oracle, flip):
+    """bench.py's replay: every chain within the budget, mismatches counted."""
+    import types
+
+    w = W.cfg2(256)
+    a = types.SimpleNamespace(warmup=5, steps=10)
+    eng = _ReplayEngine(oracle, w, 5 + 10 * 2, flip)
+    par = bench.parity_replay(eng, w, a, 0, first=0, reps=2)
+    assert par["chains_replayed"] == 256 and par["iterations"] == 25
+    assert par["mismatched_chains"] == (0 if flip is None else 1)
+    assert par["accept_stream_bitwise"] == (flip is None)
+    assert par["final_theta_ll_bitwise"]

@@ -1,8 +1,11 @@
 """Headline workload at full size (BASELINE cfg 2: 65,536 chains × 1,000
-iterations, D = 32, full histories in HBM).  The oracle is too slow to replay
-every chain here, so full size is checked through size-independent properties
-plus a bitwise replay of a random sample of chains (each chain is independent
-and keyed by its global id, so the oracle replays it alone)."""
+iterations, D = 32, full histories in HBM).  Every chain's accept stream and
+final state are replayed on the oracle in its accept-only mode (6.6e7
+chain-steps, a few seconds on the box's 16 cores); a random sample of chains is
+also compared on the full θ / ll histories; size-independent properties
+(first-step auto-accept, acceptance band, analytic posterior) on top."""
+import os
+
 import numpy as np
 import pytest
 
@@ -38,6 +41,29 @@ def test_sampled_chains_bitwise(oracle, full_run):
         ll = eng.get_history_chains(L.H_LL, 1, 1000, int(c), 1)[:, 0, 0]
         assert np.array_equal(ll, h["ll"][:, 0])
         assert np.array_equal(e["theta"][c], st.theta[0])
+
+
+def _threads():
+    return max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+
+
+def test_every_chain_accept_stream_and_state_bitwise(oracle, full_run):
+    """north_star's claim at the BASELINE cfg 2 shape: all 65,536 accept/reject streams
+    over 1,000 iterations (run.jl:268-281) plus each chain's final θ, ll, rolling
+    acceptance and accept count, bit for bit."""
+    w, e = full_run
+    eng = e["engine"]
+    st = oracle.OracleState(np.zeros((65536, 32)))
+    h = oracle.run_gsn(st, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=1000,
+                       accept_only=True, nthreads=_threads())
+    got = eng.get_history_bits(1, 1000)[:, 0]
+    bad = oracle.accept_mismatch_chains(got, oracle.pack_accept(h["acc"]), 65536)
+    assert bad.size == 0, f"{bad.size} of 65536 chains' accept streams differ (first: {bad[:8]})"
+    bad_th = np.flatnonzero((e["theta"] != st.theta).any(axis=1) | (e["ll"] != st.ll))
+    assert bad_th.size == 0, f"{bad_th.size} chains' final θ/ll differ (first: {bad_th[:8]})"
+    assert np.array_equal(e["ra"], st.ra)
+    assert np.array_equal(e["nacc"], st.nacc.astype(e["nacc"].dtype))
+    assert np.array_equal(e["faults"], st.faults)
 
 
 def test_acceptance_and_first_step(full_run):

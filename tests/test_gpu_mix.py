@@ -247,6 +247,42 @@ def test_cfg4_shape_moments_match_oracle_on_sampled_chains(oracle, hist):
         assert faults[c] == st.faults[0], c
 
 
+def test_cfg4_every_chain_through_two_readjusts(oracle):
+    """The BASELINE cfg 4 shape as bench.py runs it (131,072 chains, D = 32, k = 200,
+    one launch group per readjust period, full histories) over 400 iterations — two
+    Haario readjusts — with EVERY chain compared bit for bit against orc_run_mix in its
+    accept-only mode: the accept stream (run.jl:268-281), θ, ll, rolling acceptance,
+    accept count, GenericChainStats mean/cov (chain_statistics.jl:41-66), each chain's
+    Σ_B factor L_B after the readjusts (adaptation.jl:406-426) and the PosDef fault bits."""
+    import os
+
+    D, C, M, k = 32, 131072, 400, 200
+    w = W.cfg4(C, k=k)
+    eng = _engine(D, C, M, w.seed, w.mu_true, w.t_sigma, w.obs, w.rw_sigma, w.sigma_b, w.lam, k, L.LL_PER_OBS,
+                  L.HIST_FULL, spl=k)
+    eng.run_iters(1, M)
+    eng.synchronize(allow_faults=True)
+    kname = eng.kernel_name()
+    st = oracle.MixState(np.zeros((C, D)), sigma_b=w.sigma_b)
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)))
+    h = oracle.run_mix(st, seed=w.seed, sigma_a=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=M,
+                       lam=w.lam, haario_k=k, accept_only=True, nthreads=threads)
+    bad = oracle.accept_mismatch_chains(eng.get_history_bits(1, M)[:, 0], oracle.pack_accept(h["acc"]), C)
+    assert bad.size == 0, f"{kname}: {bad.size} of {C} accept streams differ (first: {bad[:8]})"
+    th, ll = eng.get_state()
+    assert np.array_equal(th, st.theta) and np.array_equal(ll, st.ll)
+    ra, nacc = eng.get_chain_stats()
+    assert np.array_equal(ra[0], st.ra) and np.array_equal(nacc[0], st.nacc)
+    assert np.array_equal(eng.get_faults(), st.faults)
+    mean, cov = eng.get_chain_moments()
+    assert np.array_equal(mean, st.mean)
+    assert np.array_equal(cov, st.cov)
+    Lb, Mr = eng.get_mix_state(1)
+    assert Mr == st.M == M % k  # Haario M counts steps since the last readjust
+    assert np.array_equal(Lb, st.LB)
+    eng.close()
+
+
 def _flam(lam, N, it):
     """A custom HaarioTypeAdaptation fλ(λ, N, mcmc_iter) (adaptation.jl:425)."""
     return 0.5 + 0.4 * np.sin(it / 37.0) * (N % 5) / 4.0

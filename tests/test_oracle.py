@@ -262,3 +262,35 @@ def test_faithful_refactor_variant_has_the_same_bits(oracle):
     assert np.array_equal(a.theta, b.theta) and np.array_equal(a.ll, b.ll) and np.array_equal(a.ra, b.ra)
     for k in ("theta", "prop", "ll", "acc"):
         assert np.array_equal(ha[k], hb[k]), k
+
+
+def test_accept_only_mode_matches_full_history(oracle):
+    """run_gsn / run_mix accept_only=True: the same accept stream and final state as a
+    full-history call (the θ/θ°/ll buffers are optional outputs of the same loop), and
+    pack_accept / accept_mismatch_chains agree with the unpacked comparison."""
+    from extensible_mcmc import workloads as W
+
+    w = W.cfg2(200)
+    a = oracle.OracleState(np.zeros((200, 32)))
+    b = oracle.OracleState(np.zeros((200, 32)))
+    ha = oracle.run_gsn(a, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=30)
+    hb = oracle.run_gsn(b, seed=w.seed, rw_sigma=w.rw_sigma, t_sigma=w.t_sigma, obs=w.obs, iter0=1, nsteps=30,
+                        accept_only=True)
+    assert set(hb) == {"acc"} and np.array_equal(ha["acc"], hb["acc"])
+    assert np.array_equal(a.theta, b.theta) and np.array_equal(a.ll, b.ll) and np.array_equal(a.ra, b.ra)
+    pa = oracle.pack_accept(ha["acc"])
+    assert pa.shape == (30, 4) and pa.dtype == np.uint64
+    assert oracle.accept_mismatch_chains(pa, oracle.pack_accept(hb["acc"]), 200).size == 0
+    flipped = ha["acc"].copy()
+    flipped[3, 77] ^= True
+    flipped[29, 199] ^= True
+    assert list(oracle.accept_mismatch_chains(oracle.pack_accept(flipped), pa, 200)) == [77, 199]
+    w4 = W.cfg4(64, k=10)
+    m1 = oracle.MixState(np.zeros((64, 32)), sigma_b=w4.sigma_b)
+    m2 = oracle.MixState(np.zeros((64, 32)), sigma_b=w4.sigma_b)
+    kw = dict(seed=w4.seed, sigma_a=w4.rw_sigma, t_sigma=w4.t_sigma, obs=w4.obs, iter0=1, nsteps=25, lam=w4.lam,
+              haario_k=10)
+    h1 = oracle.run_mix(m1, **kw)
+    h2 = oracle.run_mix(m2, accept_only=True, **kw)
+    assert set(h2) == {"acc"} and np.array_equal(h1["acc"], h2["acc"])
+    assert np.array_equal(m1.LB, m2.LB) and np.array_equal(m1.cov, m2.cov) and m1.M == m2.M == 25 % 10

@@ -508,23 +508,35 @@ def main():
                     comm.close()
                 return d, f"emcmc_diagnostics over {label}, {d['nranks']} ranks"
 
+            def agree(ok):
+                """every rank's verdict on its last diagnostics collective (MIN over the ranks), so
+                that no rank takes the fallback collective while another moves on to the parity
+                reduction; None when the agreement itself does not complete"""
+                v, e = watchdog(lambda: reduce_over_ranks(1.0 if ok else 0.0, dist, dev, "min"), 60.0)
+                return None if e is not None else v == 1.0
+
             if shared:
                 res, err = watchdog(lambda: gathered(DG.Comm.torch_host, "a host all-gather (gloo)"), 120.0)
             else:
                 res, err = watchdog(lambda: gathered(lambda: DG.Comm.from_process_group(local),
                                                      "RCCL (ncclAllGather inside libemcmc)"), 120.0)
-                if err is not None and err != "timeout":  # the same merge through torch's own all-gather
-                    res, err2 = watchdog(lambda: gathered(lambda: DG.Comm.torch_host(device=dev),
-                                                          f"torch's all-gather (RCCL comm failed: {err[:160]})"),
-                                         120.0)
-                    err = err2
+                if err != "timeout":
+                    all_ok = agree(err is None)
+                    if all_ok is None:
+                        err = "timeout"
+                    elif not all_ok:  # a rank's RCCL comm failed: every rank merges through torch's all-gather
+                        why = (err or "on another rank")[:160]
+                        res, err = watchdog(lambda: gathered(lambda: DG.Comm.torch_host(device=dev),
+                                                             f"torch's all-gather (RCCL comm failed: {why})"), 120.0)
+                        if err != "timeout" and not agree(err is None):
+                            err = err or "the fallback all-gather failed on another rank"
             if err is None:
                 diag, diag_via = res
             else:  # measured already; report without diagnostics and do not wait on a stuck collective
                 diag_via, diag_stuck = f"diagnostics failed: {err[:200]}", True
 
     # parity on every rank: its first 4,096 chains (all of them within the replay budget)
-    # replayed on the oracle after the timed region, mismatches summed over the ranks
+    # replayed on the oracle after the timed region, AND-reduced over the ranks
     par = None
     if not a.history_ring and not a.no_parity and not diag_stuck:
         try:
@@ -675,6 +687,16 @@ def main():
                     "source": "profiles/r3_valu_f64_ubench.txt (scripts/ubench/valu_f64_rate.hip: v_fma_f64, 8 "
                               "independent chains per lane, 2 waves/SIMD as these kernels run; 59.5 at 4)"},
                 "source": ent["source"]}
+            # the binding limit is VALU issue (both kernels; the HBM fraction is ≈ 0.17): the
+            # compute roofline is the line's primary figure, the HBM one its secondary
+            hbm = out["roofline"]
+            comp = hbm.pop("compute")
+            out["roofline"] = {"bound": "valu", "achieved": comp["achieved"], "peak": comp["peak"],
+                               "unit": comp["unit"], "frac": comp["frac"], "traffic": hbm["traffic"],
+                               "kernel": kname, "valu_busy": comp["valu_busy"],
+                               "fp64_share_of_valu": comp["fp64_share_of_valu"],
+                               "measured_valu_ceiling": comp["measured_valu_ceiling"], "note": comp["note"],
+                               "source": comp["source"], "secondary_hbm": hbm}
     if cfg3:  # MFMA-bound: the two contractions, 4·N·D flop per chain-step
         flops = 4.0 * w.nobs * w.D * Cg * (a.steps / launches)
         tfs = flops / avg_launch_s / 1e12

@@ -538,6 +538,71 @@ emcmc_status upload_block_consts(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
+// mwg_rw_block_kernel's shapes (emcmc_rwblock.h): ONE UniformRandomWalk or GaussianRandomWalk
+// update over coords 1:D in order, 17 ≤ D ≤ 64, any prior, positivity flags, AdaptationUnifRW
+// on a UniformRandomWalk; no chain moments / mixture state; the built-in GsnTargetLaw over μ
+// (d = D) or a user law.  (A GaussianRandomWalk with ImproperPrior and no flags on the built-in
+// target never reaches select_mwg: the fused kernels take it.)
+bool rwblock_eligible(const UpdateHost &u, uint32_t D) {
+    if (D < (uint32_t)kBlockMinD || D > (uint32_t)kMwgMaxD) return false;
+    if (u.kernel != EMCMC_RW_UNIFORM && u.kernel != EMCMC_RW_GAUSSIAN) return false;
+    if (u.adaptation != EMCMC_ADPT_NONE && !(u.kernel == EMCMC_RW_UNIFORM && u.adaptation == EMCMC_ADPT_UNIF_RW))
+        return false;
+    if (u.coords.size() != D) return false;
+    for (uint32_t j = 0; j < D; ++j)
+        if (u.coords[j] != j) return false;
+    return true;
+}
+bool rwblock_eligible(const emcmc_handle *h, bool xt) {
+    if (xt || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_BLOCK) || h->updates.size() != 1) return false;
+    const TargetHost &t = h->target;
+    if (!(t.kind == EMCMC_TARGET_USER || (t.kind == EMCMC_TARGET_GSN && t.dim == h->cfg.dim))) return false;
+    return rwblock_eligible(h->updates[0], h->cfg.dim);
+}
+
+// The compile-time shape of an eligible update (emcmc_rwblock.h RwShape): its kind, diagonal
+// Σ, positivity mask, adaptation and the prior's slot structure; label: the kernel-name tag.
+std::string rw_shape_source(const UpdateHost &u, std::string &label) {
+    uint64_t pos = 0;
+    for (size_t j = 0; j < u.pos.size(); ++j)
+        if (u.pos[j]) pos |= 1ull << j;
+    const bool uni = u.kernel == EMCMC_RW_UNIFORM;
+    const bool adapt = uni && u.adaptation == EMCMC_ADPT_UNIF_RW;
+    const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
+    char buf[64];
+    std::string src = "namespace emcmc {\nstruct RwShape {\n";
+    src += "    static constexpr uint32_t kind = " + std::to_string(u.kernel) + "u;\n";
+    src += std::string("    static constexpr bool diag = ") + ((uni || u.diag) ? "true" : "false") + ";\n";
+    snprintf(buf, sizeof buf, "0x%016llxull", (unsigned long long)pos);
+    src += std::string("    static constexpr uint64_t pos = ") + buf + ";\n";
+    src += std::string("    static constexpr bool adapt = ") + (adapt ? "true" : "false") + ";\n";
+    src += "    static constexpr uint32_t prior = " + std::to_string(u.prior) + "u;\n";
+    src += "    static constexpr int nslot = " + std::to_string(slots ? u.nslot : 0u) + ";\n";
+    const uint64_t masks[4] = {u.psrc0, u.pstart, u.pend, u.pmvn};
+    const char *mnames[4] = {"psrc0", "pstart", "pend", "pmvn"};
+    for (int k = 0; k < 4; ++k) {
+        snprintf(buf, sizeof buf, "0x%016llxull", (unsigned long long)(slots ? masks[k] : 0ull));
+        src += std::string("    static constexpr uint64_t ") + mnames[k] + " = " + buf + ";\n";
+    }
+    std::string fam = "    static constexpr uint32_t fam[64] = {", mvs = "    static constexpr int mvs[64] = {";
+    for (int j = 0; j < 64; ++j) {
+        const bool in = slots && (uint32_t)j < u.nslot;
+        fam += std::to_string(in ? u.pfam[j] : 0u) + (j < 63 ? "," : "};\n");
+        mvs += std::to_string(in ? u.pmvs[j] : 0u) + (j < 63 ? "," : "};\n");
+    }
+    src += fam + mvs + "};\n}  // namespace emcmc\n";
+    static const char *kPriorName[4] = {"ImproperPrior", "ImproperPosPrior", "ProductPrior", "StandardPrior"};
+    label = std::string(uni ? "UniformRandomWalk" : "GaussianRandomWalk") + (uni || u.diag ? "" : ",DENSE_SIGMA");
+    if (pos) {
+        snprintf(buf, sizeof buf, ",pos=0x%llx", (unsigned long long)pos);
+        label += buf;
+    }
+    if (adapt) label += ",AdaptationUnifRW";
+    label += std::string(",") + (u.prior < 4 ? kPriorName[u.prior] : "?");
+    if (slots && u.pmvn) label += "(MvNormal)";
+    return src;
+}
+
 emcmc_status select_mwg(emcmc_handle *h) {
     const int D = (int)h->cfg.dim;
     if (h->allocated) {
@@ -569,9 +634,31 @@ emcmc_status select_mwg(emcmc_handle *h) {
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "MALA needs the target's gradient (compute_gradients_and_momenta!): the user law defines none "
                     "(EMCMC_USER_GRAD { … })");
+    // one UniformRandomWalk / GaussianRandomWalk update over all 17 ≤ D ≤ 64 coordinates with a
+    // prior, positivity flags or AdaptationUnifRW: mwg_rw_block_kernel (emcmc_rwblock.h), the
+    // update's structure compiled in, every per-chain vector in registers
+    if (usrc.empty() && !mala && rwblock_eligible(h, xt)) {
+        const bool tdense = !h->target.diag;
+        std::string label;
+        const std::string shape = rw_shape_source(h->updates[0], label);
+        RtcKernel k;
+        const std::string log = rtc_compile_rwblock(D, full, user ? 0 : ll, tdense, shape, label,
+                                                    user ? h->target.src : "", user ? h->target.opts : "", k);
+        if (!log.empty()) {
+            h->err = std::string(user ? "user target does not compile:\n" : "run-time kernel build failed:\n") + log;
+            return user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
+        }
+        if (emcmc_status st = load_rtc_module(h, k)) return st;
+        HIPCHK(h, hipModuleGetFunction(&v.ufn, h->umod, k.lowered.c_str()));
+        v.name = k.name;
+        v.block = true;
+        if (!user) {
+            if (emcmc_status st = upload_block_consts(h)) return st;
+        }
+    }
     // one MALA or user update over all 17 ≤ D ≤ 64 coordinates: mwg_block_kernel (emcmc_block.h),
     // every per-chain vector in registers (the wide kernel's NU = D loops live in scratch)
-    if (block_eligible(h, xt)) {
+    if (!v.block && block_eligible(h, xt)) {
         const bool tdense = !h->target.diag;
         if (!user && usrc.empty())
             for (const auto &e : block_table())
@@ -660,6 +747,7 @@ emcmc_status select_mwg(emcmc_handle *h) {
             m.diag = 1u;
         } else if (u.kernel == EMCMC_RW_UNIFORM) {
             for (uint32_t j = 0; j < m.nc; ++j) m.eps0[j] = u.eps[j];
+            for (uint32_t j = 0; j < m.nc; ++j) m.uc[j] = -log_any(2.0 * u.eps[j]);
             for (uint32_t j = 0; j < m.nc; ++j) m.posmask |= (u.pos.size() > j && u.pos[j]) ? (1ull << j) : 0ull;
             if (u.adaptation == EMCMC_ADPT_UNIF_RW) {
                 m.k = u.adpt.adapt_every_k_steps;
@@ -1736,9 +1824,11 @@ emcmc_status build_prior_slots(emcmc_handle *h, const emcmc_update_desc *u, Upda
 }
 }  // namespace
 
-emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
-    if (!h || !u) return EMCMC_INVALID_ARG;
-    if (h->allocated) return fail(h, EMCMC_STATE_ERROR, "updates must be added before set_state/run");
+namespace {
+// emcmc_update_desc → UpdateHost: every check and host-side factorisation of
+// emcmc_add_update (h supplies D, the error text and the handle's other updates; a
+// device-less handle serves emcmc_prebuild_rw_block_kernel)
+emcmc_status build_update(emcmc_handle *h, const emcmc_update_desc *u, UpdateHost &uh) {
     const uint32_t D = h->cfg.dim;
     if (u->num_coords == 0 || !u->coords) return fail(h, EMCMC_INVALID_ARG, "update needs coords");
     if (u->num_coords > D) return fail(h, EMCMC_INVALID_ARG, "more coords than D");
@@ -1784,7 +1874,6 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
                             "positivity-restricted coordinates are on device for the random walks only");
         }
     if (h->updates.size() >= 64) return fail(h, EMCMC_INVALID_ARG, "at most 64 updates");
-    UpdateHost uh;
     uh.kernel = u->kernel;
     uh.prior = u->prior;
     uh.adaptation = u->adaptation;
@@ -1864,6 +1953,15 @@ emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
             uh.aoff.assign(ad->offset, ad->offset + n);
         }
     }
+    return EMCMC_OK;
+}
+}  // namespace
+
+emcmc_status emcmc_add_update(emcmc_handle *h, const emcmc_update_desc *u) {
+    if (!h || !u) return EMCMC_INVALID_ARG;
+    if (h->allocated) return fail(h, EMCMC_STATE_ERROR, "updates must be added before set_state/run");
+    UpdateHost uh;
+    if (emcmc_status st = build_update(h, u, uh)) return st;
     h->updates.push_back(std::move(uh));
     return select_variant(h);
 }
@@ -2070,6 +2168,36 @@ emcmc_status emcmc_prebuild_block_kernel(uint32_t dim, uint32_t history_mode, ui
                           update_options ? update_options : "", k);
     copy_log(log, log_out, log_len);
     return log.empty() ? EMCMC_OK : (user || upd) ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
+}
+
+emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, int dense_target,
+                                            const emcmc_update_desc *update, const char *target_source,
+                                            const char *target_options, char *log_out, size_t log_len) {
+    copy_log("", log_out, log_len);
+    if (!update || dim < (uint32_t)kBlockMinD || dim > (uint32_t)kMwgMaxD || history_mode > 1 || ll_mode > 1)
+        return EMCMC_INVALID_ARG;
+    emcmc_handle tmp;  // no device: build_update only reads cfg.dim and the (empty) update list
+    tmp.cfg.dim = dim;
+    UpdateHost uh;
+    if (emcmc_status st = build_update(&tmp, update, uh)) {
+        copy_log(tmp.err, log_out, log_len);
+        return st;
+    }
+    if (!rwblock_eligible(uh, dim)) {
+        copy_log("not a mwg_rw_block_kernel shape: one UniformRandomWalk / GaussianRandomWalk update over coords "
+                 "0..dim-1 (AdaptationUnifRW on a UniformRandomWalk only)",
+                 log_out, log_len);
+        return EMCMC_INVALID_ARG;
+    }
+    const bool user = target_source && *target_source;
+    std::string label;
+    const std::string shape = rw_shape_source(uh, label);
+    RtcKernel k;
+    const std::string log = rtc_compile_rwblock((int)dim, history_mode == EMCMC_HIST_FULL, user ? 0 : (int)ll_mode,
+                                                dense_target != 0, shape, label, user ? target_source : "",
+                                                target_options ? target_options : "", k);
+    copy_log(log, log_out, log_len);
+    return log.empty() ? EMCMC_OK : user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
 }
 
 emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {

@@ -15,11 +15,13 @@
 // librccl.so.1 (torch's copy) shares it, others get the system's; a host without it
 // still loads libemcmc.so and gets EMCMC_RCCL_ERROR from the RCCL calls only.
 #include <dlfcn.h>
+#include <link.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -80,10 +82,49 @@ const Rccl &rccl() {
     return r;
 }
 
+// Every HIP runtime image mapped into this process (dl_iterate_phdr): objects whose file
+// name starts with "libamdhip64.so", one per load address.  torch's wheel bundles its own
+// runtime; when libemcmc.so is loaded first, torch's libraries load theirs beside it, and
+// streams, events and device pointers of one runtime mean nothing to the other (an RCCL of
+// the other runtime then fails in ncclCommInitRank).
+std::vector<std::string> hip_runtime_images() {
+    std::vector<std::pair<uintptr_t, std::string>> seen;
+    dl_iterate_phdr(
+        [](struct dl_phdr_info *info, size_t, void *p) -> int {
+            auto *v = static_cast<std::vector<std::pair<uintptr_t, std::string>> *>(p);
+            const char *path = info->dlpi_name ? info->dlpi_name : "";
+            const char *base = std::strrchr(path, '/');
+            base = base ? base + 1 : path;
+            if (std::strncmp(base, "libamdhip64.so", 14) != 0) return 0;
+            for (const auto &e : *v)
+                if (e.first == (uintptr_t)info->dlpi_addr) return 0;
+            v->push_back({(uintptr_t)info->dlpi_addr, path});
+            return 0;
+        },
+        &seen);
+    std::vector<std::string> out;
+    for (const auto &e : seen) out.push_back(e.second);
+    return out;
+}
+
 }  // namespace
 
-// why the last emcmc_comm_init / emcmc_comm_unique_id failed (no comm exists to hold it)
+// why the last emcmc_comm_init / emcmc_comm_unique_id / handle-less merge failed (no comm
+// exists to hold it)
 thread_local std::string g_comm_err;
+
+namespace {
+// the refusal of a process that holds two HIP runtimes (emcmc_comm_init, emcmc_comm_unique_id)
+bool two_runtimes(std::string &msg) {
+    const std::vector<std::string> imgs = hip_runtime_images();
+    if (imgs.size() < 2) return false;
+    msg = "this process holds " + std::to_string(imgs.size()) + " HIP runtimes (";
+    for (size_t i = 0; i < imgs.size(); ++i) msg += (i ? ", " : "") + imgs[i];
+    msg += "): RCCL and the library's streams must share one — import torch (or the caller's HIP "
+           "runtime) before libemcmc.so is loaded, or point LD_LIBRARY_PATH at one ROCm";
+    return true;
+}
+}  // namespace
 
 struct emcmc_comm {
     int nranks = 1, rank = 0, device = -1;
@@ -105,7 +146,8 @@ emcmc_status comm_fail(emcmc_comm *c, emcmc_status st, const std::string &msg) {
 
 // The gathered records [nranks][3D+3] merged in rank order: diagnostics.merge, then
 // diagnostics.rhat_from_moments.
-void merge_records(const double *rows, int nranks, uint32_t D, uint64_t num_draws, emcmc_diag *out) {
+emcmc_status merge_records(const double *rows, int nranks, uint32_t D, uint64_t num_draws, emcmc_diag *out,
+                           std::string &err) {
     const size_t rec = 3 * (size_t)D + 3;
     std::vector<double> mean(rows + 1, rows + 1 + D), m2(rows + 1 + D, rows + 1 + 2 * D),
         sv(rows + 1 + 2 * D, rows + 1 + 3 * D);
@@ -128,8 +170,12 @@ void merge_records(const double *rows, int nranks, uint32_t D, uint64_t num_draw
         acc += (uint64_t)std::llround(b[1 + 3 * D]);
         prop += (uint64_t)std::llround(b[2 + 3 * D]);
     }
+    if (nch < 2) {  // B = n·M2/(m − 1): split-R̂ needs two (half-)chains over all ranks
+        err = "split-R̂ needs at least 2 (half-)chains over all ranks, got " + std::to_string(nch);
+        return EMCMC_INVALID_ARG;
+    }
     const double mch = (double)nch, n = (double)num_draws;
-    const double fB = n / (double)(nch - 1), fW = (double)(num_draws - 1) / n;
+    const double fB = n / ((double)nch - 1.0), fW = (double)(num_draws - 1) / n;
     double mx = -INFINITY;
     bool nan = false;
     for (uint32_t d = 0; d < D; ++d) {
@@ -154,6 +200,7 @@ void merge_records(const double *rows, int nranks, uint32_t D, uint64_t num_draw
     out->max_rhat = nan ? NAN : mx;
     out->dim = D;
     out->nranks = (uint32_t)nranks;
+    return EMCMC_OK;
 }
 
 #define RCCLCHK(c, expr)                                                                         \
@@ -197,10 +244,17 @@ emcmc_status gather(emcmc_comm *c, const double *send, double *rows, size_t coun
 extern "C" {
 
 emcmc_status emcmc_comm_unique_id(uint8_t id[EMCMC_COMM_ID_BYTES]) {
-    if (!id) return EMCMC_INVALID_ARG;
+    if (!id) {
+        g_comm_err = "emcmc_comm_unique_id: null id";
+        return EMCMC_INVALID_ARG;
+    }
     static_assert(sizeof(ncclUniqueId) == EMCMC_COMM_ID_BYTES, "ncclUniqueId size");
+    if (two_runtimes(g_comm_err)) return EMCMC_HIP_ERROR;
     int nd = 0;  // RCCL aborts the process when no device is visible: refuse first
-    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMCMC_NO_DEVICE;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) {
+        g_comm_err = "emcmc_comm_unique_id: no HIP device visible";
+        return EMCMC_NO_DEVICE;
+    }
     if (!rccl().ok) {
         g_comm_err = rccl().err;
         return EMCMC_RCCL_ERROR;
@@ -216,15 +270,25 @@ emcmc_status emcmc_comm_unique_id(uint8_t id[EMCMC_COMM_ID_BYTES]) {
 
 emcmc_status emcmc_comm_init(emcmc_comm **out, int nranks, int rank, int device,
                              const uint8_t id[EMCMC_COMM_ID_BYTES]) {
-    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0) return EMCMC_INVALID_ARG;
+    if (!out || !id || nranks < 1 || rank < 0 || rank >= nranks || device < 0) {
+        g_comm_err = "emcmc_comm_init: invalid argument (null out/id, or rank/nranks/device out of range)";
+        return EMCMC_INVALID_ARG;
+    }
     *out = nullptr;
+    if (two_runtimes(g_comm_err)) return EMCMC_HIP_ERROR;
     if (!rccl().ok) {
         g_comm_err = rccl().err;
         return EMCMC_RCCL_ERROR;
     }
     int nd = 0;
-    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return EMCMC_NO_DEVICE;
-    if (device >= nd) return EMCMC_INVALID_ARG;
+    if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) {
+        g_comm_err = "emcmc_comm_init: no HIP device visible";
+        return EMCMC_NO_DEVICE;
+    }
+    if (device >= nd) {
+        g_comm_err = "emcmc_comm_init: device " + std::to_string(device) + " of " + std::to_string(nd);
+        return EMCMC_INVALID_ARG;
+    }
     auto *c = new emcmc_comm;
     c->nranks = nranks;
     c->rank = rank;
@@ -233,6 +297,8 @@ emcmc_status emcmc_comm_init(emcmc_comm **out, int nranks, int rank, int device,
     std::memcpy(&u, id, sizeof u);
     if (hipSetDevice(device) != hipSuccess ||
         hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        g_comm_err = std::string("emcmc_comm_init: hipSetDevice / hipStreamCreateWithFlags: ") +
+                     hipGetErrorString(hipGetLastError());
         delete c;
         return EMCMC_HIP_ERROR;
     }
@@ -247,7 +313,10 @@ emcmc_status emcmc_comm_init(emcmc_comm **out, int nranks, int rank, int device,
 }
 
 emcmc_status emcmc_comm_init_host(emcmc_comm **out, int nranks, int rank, emcmc_allgather_fn fn, void *ctx) {
-    if (!out || !fn || nranks < 1 || rank < 0 || rank >= nranks) return EMCMC_INVALID_ARG;
+    if (!out || !fn || nranks < 1 || rank < 0 || rank >= nranks) {
+        g_comm_err = "emcmc_comm_init_host: invalid argument (null out/fn, or rank/nranks out of range)";
+        return EMCMC_INVALID_ARG;
+    }
     auto *c = new emcmc_comm;
     c->nranks = nranks;
     c->rank = rank;
@@ -286,8 +355,25 @@ emcmc_status emcmc_diagnostics_merge(emcmc_comm *c, const double *record, uint32
     } else {
         std::memcpy(rows.data(), record, rec * sizeof(double));
     }
-    merge_records(rows.data(), nranks, dim, num_draws, out);
-    return EMCMC_OK;
+    std::string err;
+    const emcmc_status st = merge_records(rows.data(), nranks, dim, num_draws, out, err);
+    if (st) {
+        if (c) c->err = err;
+        else g_comm_err = err;
+    }
+    return st;
+}
+
+int emcmc_hip_runtime_images(char *paths_out, size_t len) {
+    const std::vector<std::string> imgs = hip_runtime_images();
+    std::string all;
+    for (size_t i = 0; i < imgs.size(); ++i) all += (i ? "\n" : "") + imgs[i];
+    if (paths_out && len) {
+        const size_t n = std::min(all.size(), len - 1);
+        std::memcpy(paths_out, all.data(), n);
+        paths_out[n] = '\0';
+    }
+    return (int)imgs.size();
 }
 
 emcmc_status emcmc_diagnostics(emcmc_handle *h, emcmc_comm *c, uint64_t iter_first, uint64_t num_iters, int split,
@@ -306,7 +392,7 @@ emcmc_status emcmc_diagnostics(emcmc_handle *h, emcmc_comm *c, uint64_t iter_fir
     record[1 + 3 * D] = (double)info.accepted;
     record[2 + 3 * D] = (double)info.proposed;
     st = emcmc_diagnostics_merge(c, record.data(), D, info.num_draws, out);
-    if (st && c) emcmc_internal_set_error(h, std::string("emcmc_diagnostics: ") + c->err);
+    if (st) emcmc_internal_set_error(h, std::string("emcmc_diagnostics: ") + (c ? c->err : g_comm_err));
     return st;
 }
 

@@ -73,6 +73,8 @@ struct MwgUpdate {
     uint32_t k;       // adapt_every_k_steps
     uint32_t coords[kMwgMaxD];
     double eps0[kMwgMaxD];          // UniformRandomWalk ϵ (initial for adaptive updates)
+    double uc[kMwgMaxD];            // UniformRandomWalk: −log(2ϵ_j) of eps0 by the device's log_any
+                                    // (mwg_rw_block_kernel's logpdf constant; host-computed)
     double L[kMwgMaxD * kMwgMaxD];  // GaussianRandomWalk: lower Cholesky factor, row-major, local indices;
                                     // a user update: its parameters (≤ 4096 doubles)
     double iL[kMwgMaxD];            // 1 / L_ii

@@ -243,6 +243,8 @@ const std::vector<std::string> kCholDeps = {"emcmc_tables.h", "emcmc_math.h", "e
 const std::vector<std::string> kMwgDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_mwg.h"};
 const std::vector<std::string> kBlockDeps = {"emcmc_tables.h", "emcmc_math.h", "emcmc_kernels.h", "emcmc_mwg.h",
                                              "emcmc_block.h"};
+const std::vector<std::string> kRwBlockDeps = {"emcmc_tables.h", "emcmc_math.h",  "emcmc_kernels.h",
+                                               "emcmc_mwg.h",    "emcmc_block.h", "emcmc_rwblock.h"};
 
 std::string compile_kernel(const std::string &key, const std::string &prog_src, const char *file,
                            const std::string &ex, const std::string &name, const std::vector<std::string> &extra,
@@ -429,6 +431,31 @@ std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const 
     }
     return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : upd ? "user_update.hip" : "block_kernel.hip",
                           expr.str(), name.str(), extra, out, kBlockDeps);
+}
+
+std::string rtc_compile_rwblock(int D, bool full, int ll_mode, bool tdense, const std::string &shape,
+                                const std::string &shape_name, const std::string &src, const std::string &opts,
+                                RtcKernel &out) {
+    if (D < 17 || D > 64) return "mwg_rw_block_kernel runs 17 ≤ D ≤ 64";
+    const bool user = !src.empty();
+    std::ostringstream key, expr, name;
+    key << "rwblock|" << D << '|' << full << '|' << ll_mode << '|' << tdense << '|' << shape << '|' << opts << '|'
+        << src;
+    if (cache_get(key.str(), out)) return "";
+    const char *tgt = user ? "emcmc::UserTarget" : tdense ? "emcmc::GsnSweep<true>" : "emcmc::GsnSweep<false>";
+    expr << "emcmc::mwg_rw_block_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ", " << tgt
+         << ", emcmc::RwShape>";
+    name << "mwg_rw_block_kernel<D=" << D << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (user ? "UserTarget" : ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << (user ? "" : tdense ? ",DENSE_T" : ",DIAG_T")
+         << "," << shape_name << "[hiprtc]>";
+    std::string prog_src = std::string(kPrelude) + "#include \"emcmc_rwblock.h\"\n" + shape;
+    if (user) prog_src += std::string("#line 1 \"user_target\"\n") + src + "\n" + kEpilogue;
+    std::vector<std::string> extra = {"-ftemplate-depth=2048"};
+    if (user && rtc_defines_user_grad(src)) extra.push_back("-DEMCMC_HAS_USER_GRAD=1");
+    std::istringstream is(opts);
+    for (std::string w; is >> w;) extra.push_back(w);
+    return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : "rw_block_kernel.hip", expr.str(),
+                          name.str(), extra, out, kRwBlockDeps);
 }
 
 const char *rtc_builtin_law(const char *name) {

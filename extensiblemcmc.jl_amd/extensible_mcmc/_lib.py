@@ -270,6 +270,7 @@ SIGNATURES = {
     "emcmc_comm_init_host": (_ST, [C.POINTER(_H), C.c_int, C.c_int, ALLGATHER_FN, C.c_void_p]),
     "emcmc_comm_destroy": (None, [_H]),
     "emcmc_comm_last_error": (C.c_char_p, [_H]),
+    "emcmc_hip_runtime_images": (C.c_int, [C.c_char_p, C.c_size_t]),
     "emcmc_diagnostics": (_ST, [_H, _H, C.c_uint64, C.c_uint64, C.c_int, C.POINTER(EmcmcDiag)]),
     "emcmc_diagnostics_merge": (_ST, [_H, C.POINTER(C.c_double), C.c_uint32, C.c_uint64, C.POINTER(EmcmcDiag)]),
     "emcmc_set_timing": (_ST, [_H, C.c_int]),
@@ -282,6 +283,9 @@ SIGNATURES = {
     "emcmc_prebuild_chol_kernel": (_ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_char_p, C.c_size_t]),
     "emcmc_prebuild_block_kernel": (
         _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
+              C.c_size_t]),
+    "emcmc_prebuild_rw_block_kernel": (
+        _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p,
               C.c_size_t]),
     "emcmc_probe_variates": (
         _ST,
@@ -332,6 +336,34 @@ def lib() -> C.CDLL:
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+def hip_runtime_images() -> list[str]:
+    """Paths of the HIP runtime images (libamdhip64.so*) mapped into this process."""
+    buf = C.create_string_buffer(1 << 14)
+    n = lib().emcmc_hip_runtime_images(buf, len(buf))
+    paths = [p for p in buf.value.decode(errors="replace").split("\n") if p]
+    return paths if len(paths) == n else paths + ["?"] * (n - len(paths))
+
+
+_warned_runtimes = False
+
+
+def check_single_hip_runtime() -> bool:
+    """Warn (once per process) when more than one HIP runtime is mapped: torch's wheel bundles
+    its own, and when libemcmc.so is loaded before torch both end up in the process — the
+    library's streams and device pointers then mean nothing to torch's runtime (and RCCL
+    refuses, emcmc_comm_init).  Returns True when one runtime (or none) is mapped."""
+    global _warned_runtimes
+    imgs = hip_runtime_images()
+    if len(imgs) > 1 and not _warned_runtimes:
+        import warnings
+
+        _warned_runtimes = True
+        warnings.warn("this process holds %d HIP runtimes (%s): import torch before extensible_mcmc (or run "
+                      "without torch) so that one runtime serves both; RCCL communicators refuse to start"
+                      % (len(imgs), ", ".join(imgs)), RuntimeWarning, stacklevel=2)
+    return len(imgs) <= 1
 
 
 def dptr(a: np.ndarray):
@@ -403,6 +435,20 @@ def prebuild_block_kernel(dim: int, history_mode: int = 0, ll_mode: int = 0, den
                                            enc(target_options), enc(update_source), enc(update_options), buf, len(buf))
     if st != OK:
         raise EMCMCError(st, "emcmc_prebuild_block_kernel", buf.value.decode(errors="replace"))
+
+
+def prebuild_rw_block_kernel(dim: int, update_desc, history_mode: int = 0, ll_mode: int = 0,
+                             dense_target: bool = False, target_source: str = "", target_options: str = "") -> None:
+    """Compile mwg_rw_block_kernel for the structure of `update_desc` (an EmcmcUpdateDesc, e.g.
+    Engine.uniform_rw_desc(...)[0]: one random-walk update over coords 0..dim-1) into the on-disk
+    code-object cache (no device needed)."""
+    buf = C.create_string_buffer(1 << 16)
+    enc = lambda x: x.encode() if x else None  # noqa: E731
+    st = lib().emcmc_prebuild_rw_block_kernel(dim, history_mode, ll_mode, int(bool(dense_target)),
+                                              C.cast(C.pointer(update_desc), C.c_void_p), enc(target_source),
+                                              enc(target_options), buf, len(buf))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_prebuild_rw_block_kernel", buf.value.decode(errors="replace"))
 
 
 def device_count() -> int:

@@ -57,8 +57,11 @@ def merge(parts: list[dict]) -> dict:
 
 
 def rhat_from_moments(m: dict) -> dict:
-    """Split-R̂ (Gelman et al., BDA3 §11.4): B = n·M2/(m−1), W = Σvar/m."""
+    """Split-R̂ (Gelman et al., BDA3 §11.4): B = n·M2/(m−1), W = Σvar/m.  Fewer than two
+    (half-)chains: ValueError (the library's emcmc_diagnostics_merge returns INVALID_ARG)."""
     mch = m["num_chains"]
+    if mch < 2:
+        raise ValueError(f"split-R̂ needs at least 2 (half-)chains over all ranks, got {mch}")
     n = m["num_draws"]
     mean = np.asarray(m["mean"], dtype=np.float64)
     B = n / (mch - 1) * np.asarray(m["m2"], dtype=np.float64)
@@ -233,5 +236,5 @@ def merge_c(record: np.ndarray, D: int, num_draws: int, comm: Comm | None = None
     if comm is not None:
         comm.check(st, "emcmc_diagnostics_merge")
     elif st != L.OK:
-        raise L.EMCMCError(st, "emcmc_diagnostics_merge")
+        raise L.EMCMCError(st, "emcmc_diagnostics_merge", L.lib().emcmc_comm_last_error(None).decode())
     return _diag_dict(d, arrs)

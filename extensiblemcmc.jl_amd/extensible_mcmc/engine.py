@@ -66,6 +66,7 @@ class Engine:
     def __init__(self, cfg: EngineConfig):
         self.cfg = cfg
         self._lib = L.lib()
+        L.check_single_hip_runtime()  # warns once if torch's runtime was mapped beside the library's
         self._run_memo = None
         c = L.EmcmcConfig()
         c.abi_version = L.ABI_VERSION
@@ -143,35 +144,44 @@ class Engine:
             keep += [arr, pd]
             u.prior_params = C.cast(C.pointer(pd), C.c_void_p)
 
-    def add_gaussian_rw_update(self, coords0, sigma, prior=L.PRIOR_IMPROPER, adaptation=L.ADPT_NONE, pos=None,
-                               prior_factors=None):
+    @classmethod
+    def gaussian_rw_desc(cls, coords0, sigma, prior=L.PRIOR_IMPROPER, adaptation=L.ADPT_NONE, pos=None,
+                         prior_factors=None):
+        """(emcmc_update_desc, keepalive) of GaussianRandomWalk(Σ) on coords0 (0-based)."""
         keep = []
         coords = np.ascontiguousarray(coords0, dtype=np.uint32)
         S = np.asfortranarray(np.asarray(sigma, dtype=np.float64).reshape(len(coords), len(coords)))
         Sf = np.ascontiguousarray(S.ravel(order="F"))
+        keep += [coords, Sf]
         u = L.EmcmcUpdateDesc()
         u.kernel = L.RW_GAUSSIAN
-        self._prior_desc(u, prior, prior_factors, keep)
+        cls._prior_desc(u, prior, prior_factors, keep)
         u.adaptation = adaptation
         u.num_coords = len(coords)
         u.coords = L.u32ptr(coords)
         u.sigma = L.dptr(Sf)
         if pos is not None:
             p = np.ascontiguousarray(pos, dtype=np.uint8)
+            keep.append(p)
             u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
-        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
-        self.num_updates += 1
-        self._update_n.append(int(len(coords)))
+        return u, keep
 
-    def add_uniform_rw_update(self, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):
-        """UniformRandomWalk(ϵ) on coords0 (0-based); adapt: None or a dict with
-        AdaptationUnifRW's k, target, scale, min, max, offset."""
+    def add_gaussian_rw_update(self, coords0, sigma, prior=L.PRIOR_IMPROPER, adaptation=L.ADPT_NONE, pos=None,
+                               prior_factors=None):
+        u, keep = self.gaussian_rw_desc(coords0, sigma, prior, adaptation, pos, prior_factors)
+        self.add_update_desc(u, keep)
+
+    @classmethod
+    def uniform_rw_desc(cls, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):
+        """(emcmc_update_desc, keepalive) of UniformRandomWalk(ϵ) on coords0 (0-based); adapt: None
+        or a dict with AdaptationUnifRW's k, target, scale, min, max, offset."""
         keep = []
         coords = np.ascontiguousarray(coords0, dtype=np.uint32)
         e = np.ascontiguousarray(np.broadcast_to(np.asarray(eps, dtype=np.float64), (len(coords),)))
+        keep += [coords, e]
         u = L.EmcmcUpdateDesc()
         u.kernel = L.RW_UNIFORM
-        self._prior_desc(u, prior, prior_factors, keep)
+        cls._prior_desc(u, prior, prior_factors, keep)
         u.num_coords = len(coords)
         u.coords = L.u32ptr(coords)
         u.epsilon = L.dptr(e)
@@ -189,13 +199,19 @@ class Engine:
                 ad = L.EmcmcUnifRWAdaptationVec(int(adapt["k"]), 0, float(adapt["target"]),
                                                 *[L.dptr(a) for a in arrs])
                 u.adaptation = L.ADPT_UNIF_RW_VEC
+            keep.append(ad)
             u.adaptation_params = C.cast(C.pointer(ad), C.c_void_p)
         if pos is not None:
             p = np.ascontiguousarray(pos, dtype=np.uint8)
+            keep.append(p)
             u.pos = p.ctypes.data_as(C.POINTER(C.c_uint8))
-        self._check(self._lib.emcmc_add_update(self._h, C.byref(u)), "emcmc_add_update")
-        self.num_updates += 1
-        self._update_n.append(int(len(coords)))
+        return u, keep
+
+    def add_uniform_rw_update(self, coords0, eps, adapt=None, prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):
+        """UniformRandomWalk(ϵ) on coords0 (0-based); adapt: None or a dict with
+        AdaptationUnifRW's k, target, scale, min, max, offset."""
+        u, keep = self.uniform_rw_desc(coords0, eps, adapt, prior, pos, prior_factors)
+        self.add_update_desc(u, keep)
 
     def add_gaussian_rw_mix_update(self, coords0, sigma_a, sigma_b, lam=0.5, haario_k=None, haario_scale=2.38 ** 2,
                                    prior=L.PRIOR_IMPROPER, pos=None, prior_factors=None):

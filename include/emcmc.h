@@ -181,8 +181,9 @@ typedef struct emcmc_config {
                                             32: the general kernel instead of mix_chol_kernel */
 #define EMCMC_VARIANT_UNCAPPED 128u      /* diagonal fused kernel without the 2-waves-per-SIMD register cap
                                             (D = 16, 32, 64 build it at MINW = 2 by default) */
-#define EMCMC_VARIANT_NO_BLOCK 256u      /* one MALA / user update over all 17 ≤ D ≤ 64 coordinates: the general
-                                            wide kernel instead of mwg_block_kernel */
+#define EMCMC_VARIANT_NO_BLOCK 256u      /* one MALA / user / random-walk update over all 17 ≤ D ≤ 64 coordinates:
+                                            the general wide kernel instead of mwg_block_kernel /
+                                            mwg_rw_block_kernel */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,
@@ -423,6 +424,17 @@ emcmc_status emcmc_prebuild_block_kernel(uint32_t dim, uint32_t history_mode, ui
                                          const char *update_source, const char *update_options, char *log_out,
                                          size_t log_len);
 
+/* The same for mwg_rw_block_kernel, the kernel a handle with ONE UniformRandomWalk or
+ * GaussianRandomWalk update over coordinates 0..dim-1 selects at 17 ≤ dim ≤ 64 when it has a
+ * prior, positivity flags or AdaptationUnifRW (or a user law): the kernel is compiled for the
+ * update's structure (kind, diagonal Σ, pos flags, adaptation, prior families), so `update` is
+ * the emcmc_update_desc the handle will be given (its values may differ: they are read at run
+ * time).  The built-in GsnTargetLaw (target_source = NULL; dense_target != 0 for a non-diagonal
+ * Σ) or a user law (target_source, its options). */
+emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, int dense_target,
+                                            const emcmc_update_desc *update, const char *target_source,
+                                            const char *target_options, char *log_out, size_t log_len);
+
 /* θinit for every chain (row-major [C][D]); ll = NULL means the reference's
  * initial ll = -Inf (workspaces.jl:425), i.e. the first step always accepts.
  * Also resets the rolling-acceptance statistics (chain_statistics.jl:23-36). */
@@ -572,7 +584,14 @@ emcmc_status emcmc_comm_init(emcmc_comm **comm, int nranks, int rank, int device
 emcmc_status emcmc_comm_init_host(emcmc_comm **comm, int nranks, int rank, emcmc_allgather_fn fn, void *ctx);
 void emcmc_comm_destroy(emcmc_comm *comm);
 const char *emcmc_comm_last_error(const emcmc_comm *comm);  /* comm = NULL: why this thread's last
-                                                              emcmc_comm_init / _unique_id failed */
+                                                              emcmc_comm_init / _unique_id / comm-less
+                                                              emcmc_diagnostics_merge failed */
+/* HIP runtime images (libamdhip64.so*) mapped into this process; their paths, newline-separated,
+ * in paths_out (truncated to len bytes, NUL-terminated; may be NULL).  More than one means a
+ * second runtime was loaded beside the one libemcmc.so is bound to (e.g. torch's bundled copy
+ * when libemcmc.so was loaded first): emcmc_comm_init / emcmc_comm_unique_id then refuse with
+ * EMCMC_HIP_ERROR and say so in emcmc_comm_last_error(NULL), and the Python layer warns. */
+int emcmc_hip_runtime_images(char *paths_out, size_t len);
 
 typedef struct emcmc_diag {
     uint64_t num_chains;  /* (half-)chains merged over every rank */
@@ -597,7 +616,8 @@ typedef struct emcmc_diag {
 emcmc_status emcmc_diagnostics(emcmc_handle *h, emcmc_comm *comm, uint64_t iter_first, uint64_t num_iters,
                                int split, emcmc_diag *out);
 /* The same from a caller-made record (3·dim + 3 doubles as above) and draws per
- * (half-)chain; no handle, and no device with a host comm or comm = NULL. */
+ * (half-)chain; no handle, and no device with a host comm or comm = NULL.  Fewer than 2
+ * (half-)chains over all ranks: EMCMC_INVALID_ARG (B = n·M2/(m − 1) is undefined). */
 emcmc_status emcmc_diagnostics_merge(emcmc_comm *comm, const double *record, uint32_t dim, uint64_t num_draws,
                                      emcmc_diag *out);
 

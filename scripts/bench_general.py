@@ -72,6 +72,12 @@ def main():
         mala_gsn(C, M, report, a.variant)
     if want("pcn_user_d32"):
         pcn_user(C, M, report, a.variant)
+    # (5) one random-walk update over all 32 coordinates with a prior / positivity flags
+    # (mwg_rw_block_kernel; the "_wide" twins run the same schedule on mwg_wide_kernel)
+    for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32"):
+        for suffix, variant in (("", a.variant), ("_wide", L.VARIANT_NO_BLOCK)):
+            if want(name + suffix) or (not only and suffix == ""):
+                rw_prior(name, suffix, C, M, report, variant)
 
 
 def corr_d32(seed=32, D=32, nobs=10):
@@ -133,6 +139,35 @@ def pcn_user(C, M, report, variant=0):
     eng.set_state(np.tile(obs.mean(0), (C, 1)))
     ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
     report("pcn_user_d32", eng, 1, ms, b)
+    eng.close()
+
+
+def rw_prior(name, suffix, C, M, report, variant=0):
+    """One joint update over D = 32 coordinates on cfg 2's target (10 observations, per
+    observation likelihood, full histories), VERDICT r5 next-step 2's shapes:
+      rw_product_normal_d32     GaussianRandomWalk(σ²I) + ProductPrior([Product(32 × Normal)])
+      rw_standard_mvnormal_d32  GaussianRandomWalk(σ²I) + StandardPrior(MvNormal(μ0, Σ0)), Σ0 dense
+      unif_pos_d32              UniformRandomWalk(ϵ) with positivity flags on every coordinate"""
+    D = 32
+    w = W.cfg2(8)
+    shift = 4.0 if name == "unif_pos_d32" else 0.0
+    mu = np.asarray(w.mu_true) + shift
+    obs = np.asarray(w.obs) - np.asarray(w.mu_true) + mu
+    s2 = (2.38 / np.sqrt(D * 10)) ** 2
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed, kernel_variant=variant))
+    if name == "rw_product_normal_d32":
+        eng.add_gaussian_rw_update(np.arange(D), s2 * np.eye(D), prior=L.PRIOR_PRODUCT,
+                                   prior_factors=[(L.DIST_PRODUCT, D, [(L.DIST_NORMAL, 0.0, 3.0)] * D)])
+    elif name == "rw_standard_mvnormal_d32":
+        B = np.random.default_rng(9).standard_normal((D, D))
+        eng.add_gaussian_rw_update(np.arange(D), s2 * np.eye(D), prior=L.PRIOR_STANDARD,
+                                   prior_factors=[(L.DIST_MVNORMAL, D, np.zeros(D), B @ B.T / D + np.eye(D))])
+    else:
+        eng.add_uniform_rw_update(np.arange(D), 0.06, pos=np.ones(D))
+    eng.set_gsn_target(mu, np.eye(D), obs)
+    eng.set_state(np.tile(mu, (C, 1)))
+    ms, b = timed(eng, [(i, 1) for i in range(1, M + 1)], reps=3)
+    report(name + suffix, eng, 1, ms, b)
     eng.close()
 
 

@@ -1,0 +1,240 @@
+"""mwg_rw_block_kernel on the GPU: one UniformRandomWalk or
+GaussianRandomWalk update over all 17 ≤ D ≤ 64 coordinates with a prior
+(priors.jl:11-88), positivity flags (random_walk.jl:45-94, 136-171), the proposal!
+redraw loop (updates.jl:191-196) and AdaptationUnifRW (adaptation.jl:273-329), the
+update's structure compiled in at run time, against the oracle (orc_run_mwg kinds 1
+and 2 — the restatement the general kernels are checked against), bit for bit:
+accept streams, θ / θ° / ll histories, sub_ws°.ll, rolling acceptance, fault bits,
+the adaptive ϵ.  The same schedules on the wide general kernel
+(EMCMC_VARIANT_NO_BLOCK) give the same bits."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc import workloads as W
+from extensible_mcmc.engine import Engine, EngineConfig
+from extensible_mcmc.schedule import MCMCSchedule
+from test_gpu_mwg import ADAPT, check, full_steps
+
+pytestmark = pytest.mark.gpu
+
+N_, U_, E_, G_, LN_ = L.DIST_NORMAL, L.DIST_UNIFORM, L.DIST_EXPONENTIAL, L.DIST_GAMMA, L.DIST_LOGNORMAL
+IG_, C_, LA_, T_ = L.DIST_INVERSE_GAMMA, L.DIST_CAUCHY, L.DIST_LAPLACE, L.DIST_TDIST
+P_, MV_ = L.DIST_PRODUCT, L.DIST_MVNORMAL
+
+
+@pytest.fixture(autouse=True)
+def _gpu(require_gpu):
+    pass
+
+
+def problem(D, shift=0.0, dense_t=False, seed=5):
+    """cfg 2's Gaussian target at dimension D, μ* shifted (a positive target for pos flags)."""
+    w = W.cfg2(8, D=D)
+    mu = np.asarray(w.mu_true) + shift
+    obs = np.asarray(w.obs) - np.asarray(w.mu_true) + mu
+    ts = np.eye(D)
+    if dense_t:
+        B = np.random.default_rng(seed).standard_normal((D, D))
+        ts = B @ B.T / D + np.eye(D)
+    return w.seed, mu, ts, obs
+
+
+def engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL, spl=0, variant=0,
+               theta0=None, user=None):
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
+                              steps_per_launch=spl, kernel_variant=variant))
+    for u in ups:
+        pr = dict(prior=u.get("prior", 0), prior_factors=u.get("factors") or None)
+        if u["kind"] == 1:
+            eng.add_uniform_rw_update(u["coords"], u["eps"], adapt=u["adapt"], pos=u.get("pos"), **pr)
+        else:
+            eng.add_gaussian_rw_update(u["coords"], u["sigma"], pos=u.get("pos"), **pr)
+    if user is None:
+        eng.set_gsn_target(mu, ts, obs, ll_mode=ll_mode)
+    else:
+        eng.set_user_target(user, obs=obs, theta0=np.zeros(D))
+    eng.set_state(np.zeros((C, D)) if theta0 is None else theta0)
+    return eng
+
+
+def run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, theta0, steps=None, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL,
+             spl=0, user=None, calls=None):
+    steps = steps or full_steps(M, 1)
+    eng = engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode, hist, spl, theta0=theta0,
+                     user=None if user is None else user[1])
+    for a, b in (calls or [(0, len(steps))]):
+        eng.run(steps[a:b])
+    st = oracle.MWGState(np.array(theta0, dtype=np.float64), mu if user is None else np.zeros(D), ups)
+    kw = {} if user is None else {"user_ll": user[0]}
+    h = oracle.run_mwg(st, ups, seed=seed, t_sigma=ts, obs=obs, steps=steps, ll_mode=ll_mode, nthreads=8, **kw)
+    return eng, st, h, steps
+
+
+def assert_block(eng, D):
+    assert eng.kernel_name().startswith(f"mwg_rw_block_kernel<D={D}"), eng.kernel_name()
+
+
+def s2(D, n=10, f=1.0):
+    return f * (2.38 / np.sqrt(D * n)) ** 2
+
+
+@pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
+@pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
+def test_d32_gaussian_rw_product_prior_normal(oracle, ll_mode, hist):
+    """VERDICT shape 1: D = 32 joint GaussianRandomWalk + ProductPrior of Normal factors
+    (one Product of 32 Normals: the logpdf folded left over the components)."""
+    D, C, M = 32, 2048, 160
+    seed, mu, ts, obs = problem(D)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, D, [(N_, 0.1 * j, 1.0 + 0.05 * j) for j in range(D)])])]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, ll_mode=ll_mode, hist=hist)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1, full=(hist == L.HIST_FULL))
+    assert 0.1 < h["acc"].mean() < 0.6
+
+
+def test_d32_gaussian_rw_standard_prior_mvnormal(oracle):
+    """VERDICT shape 2: D = 32 joint GaussianRandomWalk + StandardPrior(MvNormal(μ0, Σ0)),
+    Σ0 dense (the forward substitution over the prior's factor, squares folded left)."""
+    D, C, M = 32, 2048, 160
+    seed, mu, ts, obs = problem(D)
+    B = np.random.default_rng(9).standard_normal((D, D))
+    S0 = B @ B.T / D + 0.5 * np.eye(D)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_STANDARD,
+                             factors=[(MV_, D, 0.3 * np.ones(D), S0)])]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+@pytest.mark.parametrize("prior", [L.PRIOR_IMPROPER, L.PRIOR_IMPROPER_POS])
+def test_d32_uniform_rw_with_pos_flags(oracle, prior):
+    """VERDICT shape 3: D = 32 joint UniformRandomWalk with positivity flags (θ° = θ·e^U on
+    24 of 32 coordinates, the −log(2ϵ) − log θ° density terms folded left), ImproperPrior
+    and ImproperPosPrior."""
+    D, C, M = 32, 2048, 200
+    seed, mu, ts, obs = problem(D, shift=4.0)
+    pos = [j % 4 != 3 for j in range(D)]
+    eps = [0.05 + 0.002 * j for j in range(D)]
+    ups = [oracle.mwg_update(1, range(D), eps=eps, pos=pos, prior=prior)]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+    assert 0.05 < h["acc"].mean() < 0.9
+
+
+def test_d32_adaptive_uniform_rw_with_pos(oracle):
+    """AdaptationUnifRW (per-chain ϵ, readjusted every k = 25 proposals) on a D = 32
+    UniformRandomWalk with positivity flags, split into launches of 7 steps."""
+    D, C, M = 32, 1024, 150
+    seed, mu, ts, obs = problem(D, shift=4.0)
+    pos = [j % 2 == 0 for j in range(D)]
+    ups = [oracle.mwg_update(1, range(D), eps=[0.08] * D, pos=pos, adapt=dict(ADAPT, k=25, scale=0.02))]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, spl=7,
+                                 calls=[(0, 40), (40, 41), (41, 150)])
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_d24_dense_sigma_all_families_and_redraws(oracle):
+    """D = 24, a dense Σ (column sweep of L z, row substitutions of the densities), a
+    ProductPrior over the univariate families (dims-1 factors reading θ[1]), a Product factor
+    and an MvNormal factor, and Uniform(1.6, 3.4) factors the target pushes the chains
+    against: the proposal! redraw loop runs (normal indices (r << 17) | j) and the carried
+    log-prior follows each accept."""
+    D, C, M = 24, 1536, 120
+    seed, mu, ts, obs = problem(D, shift=2.5, dense_t=True)
+    A = np.random.default_rng(3).standard_normal((D, D))
+    sig = s2(D, f=0.6) * (A @ A.T / D + np.eye(D))
+    fam1 = [(N_, 1, 2.0, 1.5), (LN_, 1, 0.5, 1.0), (G_, 1, 2.0, 1.5), (E_, 1, 2.0, 0.0)]  # dims-1: read θ[1]
+    fam_prod = (P_, 6, [(IG_, 3.0, 2.0), (C_, 1.0, 2.0), (LA_, 2.0, 1.0),
+                        (T_, 5.0, 0.0), (N_, 2.5, 3.0), (G_, 3.0, 1.0)])
+    mvn = (MV_, 8, 2.5 * np.ones(8), np.eye(8) + 0.2 * np.ones((8, 8)))
+    unif = (P_, 6, [(U_, 1.6, 3.4)] * 6)
+    ups = [oracle.mwg_update(2, range(D), sigma=sig, prior=L.PRIOR_PRODUCT, factors=fam1 + [fam_prod, mvn, unif])]
+    th0 = np.tile(np.where(np.arange(D) >= 18, 2.5, mu), (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+    prop = h["prop"][..., 18:]
+    assert np.all((prop >= 1.6) & (prop <= 3.4))  # every stored θ° inside the Uniform support
+
+
+@pytest.mark.parametrize("D", [20, 33])
+def test_gaussian_rw_with_pos_round_trips(oracle, D):
+    """GaussianRandomWalk with positivity flags on half the coordinates: the reference's
+    in-place exp/log round trips (θ°₃, θ₃), ImproperPosPrior (no log-prior carry), odd and
+    even D."""
+    C, M = 1024, 120
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    pos = [j % 2 == 1 for j in range(D)]
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=0.05) * np.eye(D), pos=pos, prior=L.PRIOR_IMPROPER_POS)]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_schedule_gap_and_launch_cuts(oracle):
+    """The update excluded on iterations 31:50 (rolling_ar restarts from 0.0) and launches
+    of 9 steps across three run calls: the log-prior is re-evaluated at each launch's
+    first step and carried inside it."""
+    D, C, M = 32, 1024, 110
+    seed, mu, ts, obs = problem(D)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, D, [(C_, 0.0, 3.0)] * D)])]
+    steps = [(s.mcmciter, s.pidx) for s in MCMCSchedule(M, 1, [(1, range(31, 51))])]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, steps=steps, spl=9,
+                                 calls=[(0, 25), (25, 26), (26, len(steps))])
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_user_law_with_prior(oracle):
+    """A user law (logistic regression, EMCMC_USER_LOGLIK) under a D = 20 UniformRandomWalk
+    with a ProductPrior of Normals: the block kernel with TGT = the user's law."""
+    D, C, M, n = 20, 512, 80, 60
+    rng = np.random.default_rng(12)
+    X = rng.standard_normal((n, D)) / np.sqrt(D)
+    beta = rng.normal(scale=0.3, size=D)
+    y = (rng.uniform(size=n) < 1.0 / (1.0 + np.exp(-(X @ beta)))).astype(float)
+    obs = np.column_stack([X, y])
+    fn, src = oracle.user_loglik("logistic_regression")
+    ups = [oracle.mwg_update(1, range(D), eps=[0.2] * D, prior=L.PRIOR_PRODUCT, factors=[(P_, D, [(N_, 0.0, 1.0)] * D)])]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, None, None, obs, 41, np.zeros((C, D)), user=(fn, src))
+    assert_block(eng, D)
+    assert "UserTarget" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_wide_kernel_gives_the_same_bits():
+    """EMCMC_VARIANT_NO_BLOCK runs the same update on mwg_wide_kernel<D=32,NU=32>: every
+    history and the final state equal the block kernel's."""
+    D, C, M = 32, 1024, 60
+    seed, mu, ts, obs = problem(D, shift=4.0)
+    pos = [j % 3 == 0 for j in range(D)]
+    fac = [(P_, D, [(G_, 4.0, 1.0)] * D)]
+    out = []
+    for variant in (0, L.VARIANT_NO_BLOCK):
+        eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, kernel_variant=variant))
+        eng.add_uniform_rw_update(range(D), [0.07] * D, pos=pos, prior=L.PRIOR_PRODUCT, prior_factors=fac)
+        eng.set_gsn_target(mu, ts, obs)
+        eng.set_state(np.tile(mu, (C, 1)))
+        eng.run_iters(1, M)
+        eng.synchronize(allow_faults=True)
+        out.append((eng.kernel_name(), eng.get_state(), eng.get_history(L.H_ACCEPT, 1, M),
+                    eng.get_history(L.H_PROPOSAL, 1, M), eng.get_faults()))
+        eng.close()
+    assert out[0][0].startswith("mwg_rw_block_kernel") and out[1][0].startswith("mwg_wide_kernel<D=32")
+    for a, b in zip(out[0][1:], out[1][1:]):
+        if isinstance(a, tuple):
+            for x, y in zip(a, b):
+                assert np.array_equal(x, y)
+        else:
+            assert np.array_equal(a, b)

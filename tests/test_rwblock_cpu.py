@@ -1,0 +1,42 @@
+"""mwg_rw_block_kernel's host side on CPU (no device): emcmc_prebuild_rw_block_kernel
+compiles the kernel for an update's structure (emcmc.hip rw_shape_source → hiprtc)
+into an on-disk cache, and refuses a shape the kernel does not serve."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc.engine import Engine
+
+
+@pytest.fixture
+def cache(tmp_path, monkeypatch):
+    d = tmp_path / "rtc"
+    monkeypatch.setenv("EMCMC_RTC_CACHE", str(d))
+    return d
+
+
+def test_prebuild_compiles_a_shape_into_the_cache(cache):
+    D = 17
+    u, keep = Engine.uniform_rw_desc(range(D), 0.1, pos=[j % 2 for j in range(D)], prior=L.PRIOR_PRODUCT,
+                                     prior_factors=[(L.DIST_PRODUCT, D, [(L.DIST_GAMMA, 2.0, 1.0)] * D)])
+    L.prebuild_rw_block_kernel(D, u, history_mode=L.HIST_ACCEPT_ONLY)
+    assert len(list(cache.glob("*.co"))) == 1
+
+
+@pytest.mark.parametrize("case", ["coords", "mix", "small_d"])
+def test_prebuild_refuses_other_shapes(cache, case):
+    D = 20 if case != "small_d" else 8
+    coords = list(range(D))[::-1] if case == "coords" else range(D)
+    if case == "mix":
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.RW_GAUSSIAN_MIX
+        c = np.arange(D, dtype=np.uint32)
+        S = np.ascontiguousarray(np.eye(D).ravel())
+        u.num_coords, u.coords, u.sigma, u.sigma_b, u.mix_lambda = D, L.u32ptr(c), L.dptr(S), L.dptr(S), 0.5
+        keep = [c, S]
+    else:
+        u, keep = Engine.gaussian_rw_desc(coords, 0.01 * np.eye(D), prior=L.PRIOR_IMPROPER_POS)
+    with pytest.raises(L.EMCMCError) as e:
+        L.prebuild_rw_block_kernel(D, u)
+    assert e.value.status == L.INVALID_ARG
+    assert not list(cache.glob("*.co"))

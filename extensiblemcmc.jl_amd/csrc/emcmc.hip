@@ -561,8 +561,9 @@ bool rwblock_eligible(const emcmc_handle *h, bool xt) {
 }
 
 // The compile-time shape of an eligible update (emcmc_rwblock.h RwShape): its kind, diagonal
-// Σ, positivity mask, adaptation and the prior's slot structure; label: the kernel-name tag.
-std::string rw_shape_source(const UpdateHost &u, std::string &label) {
+// Σ, positivity mask, adaptation and the prior's slot structure; label: the kernel-name tag;
+// shape_name: the generated struct's name (RwShape_<digest of the shape>).
+std::string rw_shape_source(const UpdateHost &u, std::string &label, std::string &shape_name) {
     uint64_t pos = 0;
     for (size_t j = 0; j < u.pos.size(); ++j)
         if (u.pos[j]) pos |= 1ull << j;
@@ -591,6 +592,14 @@ std::string rw_shape_source(const UpdateHost &u, std::string &label) {
         mvs += std::to_string(in ? u.pmvs[j] : 0u) + (j < 63 ? "," : "};\n");
     }
     src += fam + mvs + "};\n}  // namespace emcmc\n";
+    // the struct's name carries a digest of the shape, so kernels of different shapes have
+    // different symbol names in a profile (rocprofv3 merges dispatches by name)
+    uint64_t hsh = 0xcbf29ce484222325ull;
+    for (unsigned char ch : src) hsh = (hsh ^ ch) * 0x100000001b3ull;
+    snprintf(buf, sizeof buf, "RwShape_%016llx", (unsigned long long)hsh);
+    for (size_t at = src.find("RwShape"); at != std::string::npos; at = src.find("RwShape", at + 1))
+        src.replace(at, 7, buf), at += std::strlen(buf) - 1;
+    shape_name = buf;
     static const char *kPriorName[4] = {"ImproperPrior", "ImproperPosPrior", "ProductPrior", "StandardPrior"};
     label = std::string(uni ? "UniformRandomWalk" : "GaussianRandomWalk") + (uni || u.diag ? "" : ",DENSE_SIGMA");
     if (pos) {
@@ -639,10 +648,10 @@ emcmc_status select_mwg(emcmc_handle *h) {
     // update's structure compiled in, every per-chain vector in registers
     if (usrc.empty() && !mala && rwblock_eligible(h, xt)) {
         const bool tdense = !h->target.diag;
-        std::string label;
-        const std::string shape = rw_shape_source(h->updates[0], label);
+        std::string label, sname;
+        const std::string shape = rw_shape_source(h->updates[0], label, sname);
         RtcKernel k;
-        const std::string log = rtc_compile_rwblock(D, full, user ? 0 : ll, tdense, shape, label,
+        const std::string log = rtc_compile_rwblock(D, full, user ? 0 : ll, tdense, shape, sname, label,
                                                     user ? h->target.src : "", user ? h->target.opts : "", k);
         if (!log.empty()) {
             h->err = std::string(user ? "user target does not compile:\n" : "run-time kernel build failed:\n") + log;
@@ -2190,11 +2199,11 @@ emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode,
         return EMCMC_INVALID_ARG;
     }
     const bool user = target_source && *target_source;
-    std::string label;
-    const std::string shape = rw_shape_source(uh, label);
+    std::string label, sname;
+    const std::string shape = rw_shape_source(uh, label, sname);
     RtcKernel k;
     const std::string log = rtc_compile_rwblock((int)dim, history_mode == EMCMC_HIST_FULL, user ? 0 : (int)ll_mode,
-                                                dense_target != 0, shape, label, user ? target_source : "",
+                                                dense_target != 0, shape, sname, label, user ? target_source : "",
                                                 target_options ? target_options : "", k);
     copy_log(log, log_out, log_len);
     return log.empty() ? EMCMC_OK : user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;

@@ -122,11 +122,11 @@ std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const 
 
 // mwg_rw_block_kernel<D, FULL, LL, TGT, RwShape> (emcmc_rwblock.h): one UniformRandomWalk or
 // GaussianRandomWalk update over all 17 ≤ D ≤ 64 coordinates with any prior, positivity flags
-// and AdaptationUnifRW.  shape: the source of `namespace emcmc { struct RwShape { … }; }`, the
-// update's compile-time structure (emcmc.hip rw_shape_source); shape_name: its label in the
+// and AdaptationUnifRW.  shape: the source of `namespace emcmc { struct <shape_struct> { … }; }`,
+// the update's compile-time structure (emcmc.hip rw_shape_source); shape_name: its label in the
 // kernel name; src / opts: a user law, else the built-in GsnTargetLaw (GsnSweep<tdense>).
 std::string rtc_compile_rwblock(int D, bool full, int ll_mode, bool tdense, const std::string &shape,
-                                const std::string &shape_name, const std::string &src, const std::string &opts,
-                                RtcKernel &out);
+                                const std::string &shape_struct, const std::string &shape_name,
+                                const std::string &src, const std::string &opts, RtcKernel &out);
 
 }  // namespace emcmc

@@ -434,8 +434,8 @@ std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const 
 }
 
 std::string rtc_compile_rwblock(int D, bool full, int ll_mode, bool tdense, const std::string &shape,
-                                const std::string &shape_name, const std::string &src, const std::string &opts,
-                                RtcKernel &out) {
+                                const std::string &shape_struct, const std::string &shape_name,
+                                const std::string &src, const std::string &opts, RtcKernel &out) {
     if (D < 17 || D > 64) return "mwg_rw_block_kernel runs 17 ≤ D ≤ 64";
     const bool user = !src.empty();
     std::ostringstream key, expr, name;
@@ -444,7 +444,7 @@ std::string rtc_compile_rwblock(int D, bool full, int ll_mode, bool tdense, cons
     if (cache_get(key.str(), out)) return "";
     const char *tgt = user ? "emcmc::UserTarget" : tdense ? "emcmc::GsnSweep<true>" : "emcmc::GsnSweep<false>";
     expr << "emcmc::mwg_rw_block_kernel<" << D << ", " << (full ? "true" : "false") << ", " << ll_mode << ", " << tgt
-         << ", emcmc::RwShape>";
+         << ", emcmc::" << shape_struct << ">";
     name << "mwg_rw_block_kernel<D=" << D << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (user ? "UserTarget" : ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << (user ? "" : tdense ? ",DENSE_T" : ",DIAG_T")
          << "," << shape_name << "[hiprtc]>";

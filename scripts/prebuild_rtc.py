@@ -26,6 +26,34 @@ BLOCK = [(20, 0, 0, True, None, None), (40, 0, 0, True, None, None), (32, 0, 0, 
          (20, 0, 0, True, "logistic_regression", None)]
 
 
+# mwg_rw_block_kernel shapes of scripts/bench_general.py rw_prior (D = 32, FULL, per observation,
+# diagonal target): (name, update-desc factory)
+def rw_shapes():
+    import numpy as np
+    from extensible_mcmc.engine import Engine
+
+    D = 32
+    s2 = (2.38 / np.sqrt(D * 10)) ** 2
+    B = np.random.default_rng(9).standard_normal((D, D))
+    return [
+        ("rw_product_normal_d32", lambda: Engine.gaussian_rw_desc(
+            np.arange(D), s2 * np.eye(D), prior=L.PRIOR_PRODUCT,
+            prior_factors=[(L.DIST_PRODUCT, D, [(L.DIST_NORMAL, 0.0, 3.0)] * D)])),
+        ("rw_standard_mvnormal_d32", lambda: Engine.gaussian_rw_desc(
+            np.arange(D), s2 * np.eye(D), prior=L.PRIOR_STANDARD,
+            prior_factors=[(L.DIST_MVNORMAL, D, np.zeros(D), B @ B.T / D + np.eye(D))])),
+        ("unif_pos_d32", lambda: Engine.uniform_rw_desc(np.arange(D), 0.06, pos=np.ones(D))),
+    ]
+
+
+def one_rw(i):
+    name, make = rw_shapes()[i]
+    t = time.time()
+    u, keep = make()
+    L.prebuild_rw_block_kernel(32, u, 0, 0, False)
+    return f"rw block {name}: {time.time() - t:.1f} s"
+
+
 def one(job):
     D, hist, ll = job
     t = time.time()
@@ -49,5 +77,6 @@ if __name__ == "__main__":
         futs = [ex.submit(one, j) for j in jobs]
         if not sys.argv[1:]:
             futs += [ex.submit(one_block, j) for j in BLOCK]
+            futs += [ex.submit(one_rw, i) for i in range(3)]
         for f in futs:
             print(f.result(), flush=True)

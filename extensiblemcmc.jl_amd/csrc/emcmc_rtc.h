@@ -34,7 +34,9 @@ struct RtcKernel {
     uint32_t origin = 0;
     double seconds = 0.0;
 };
-enum : uint32_t { kRtcFromProcess = 0, kRtcFromDisk = 1, kRtcCompiled = 2 };
+// kRtcCompiledCacheRefused: compiled because the on-disk cache directory exists but is not
+// private to this user (emcmc_rtc.hip private_dir; a one-time stderr warning says so)
+enum : uint32_t { kRtcFromProcess = 0, kRtcFromDisk = 1, kRtcCompiled = 2, kRtcCompiledCacheRefused = 3 };
 
 // The on-disk code-object cache: EMCMC_RTC_CACHE (a directory; "off" disables
 // it), else rtc_cache/ beside libemcmc.so.  Entries are keyed by a 128-bit

@@ -167,22 +167,30 @@ std::string payload_digest(const RtcKernel &k) {
 // The cache directory is used only when it is private to this user: owned by the
 // effective uid and neither group- nor world-writable (else anyone who can write it could
 // plant a code object every later handle would execute).  Created 0700 when absent.
-bool private_dir(const std::string &dir, bool create) {
+bool private_dir(const std::string &dir, bool create, bool *refused = nullptr) {
     struct stat st;
     if (stat(dir.c_str(), &st) != 0) {
         if (!create || mkdir(dir.c_str(), 0700) != 0 || stat(dir.c_str(), &st) != 0) return false;
     }
     if (!S_ISDIR(st.st_mode) || st.st_uid != geteuid() || (st.st_mode & (S_IWGRP | S_IWOTH))) {
-        if (getenv("EMCMC_RTC_LOG"))
-            fprintf(stderr, "[emcmc rtc] %s is not a private directory of this user: on-disk cache not used\n",
-                    dir.c_str());
+        if (refused) *refused = true;
+        // said once per process whatever EMCMC_RTC_LOG says: every run-time kernel now compiles in
+        // every process (≈ 1 minute each at D ≥ 40) and the cause is the directory's owner or mode
+        static std::once_flag once;
+        std::call_once(once, [&] {
+            fprintf(stderr,
+                    "[emcmc rtc] warning: %s is not a private directory of this user (owner uid %u, euid %u, "
+                    "mode %03o): the on-disk code-object cache is not used, run-time kernels compile in every "
+                    "process; make it owned by the running user with mode 0700 (INTEGRATION.md)\n",
+                    dir.c_str(), (unsigned)st.st_uid, (unsigned)geteuid(), (unsigned)(st.st_mode & 0777));
+        });
         return false;
     }
     return true;
 }
 
-bool disk_get(const std::string &dir, const std::string &file, RtcKernel &k) {
-    if (!private_dir(dir, false)) return false;
+bool disk_get(const std::string &dir, const std::string &file, RtcKernel &k, bool *refused) {
+    if (!private_dir(dir, false, refused)) return false;
     std::ifstream f(file, std::ios::binary);
     if (!f) return false;
     char m[8];
@@ -254,6 +262,7 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
     // disk cache: the digest covers every input of the compile
     const std::string dir = rtc_cache_dir();
     std::string dfile;
+    bool refused = false;  // the cache directory exists but is not private: not read, not written
     if (!dir.empty()) {
         Digest d;
         for (const auto &dep : deps)
@@ -274,7 +283,7 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
               "|HIP " + std::to_string(HIP_VERSION));
         dfile = dir + "/" + d.hex() + ".co";
         RtcKernel k;
-        if (disk_get(dir, dfile, k)) {
+        if (disk_get(dir, dfile, k, &refused)) {
             k.name = name;
             k.origin = kRtcFromDisk;
             k.seconds = since();
@@ -319,9 +328,9 @@ std::string compile_kernel(const std::string &key, const std::string &prog_src, 
     }
     hiprtcDestroyProgram(&prog);
     k.name = name;
-    k.origin = kRtcCompiled;
+    k.origin = refused ? kRtcCompiledCacheRefused : kRtcCompiled;
     k.seconds = since();
-    if (!dfile.empty()) disk_put(dir, dfile, k);
+    if (!dfile.empty() && !refused) disk_put(dir, dfile, k);
     if (getenv("EMCMC_RTC_LOG"))
         fprintf(stderr, "[emcmc rtc] compiled %s in %.1f s%s%s\n", name.c_str(), k.seconds,
                 dfile.empty() ? "" : ", cached as ", dfile.c_str());

@@ -581,11 +581,12 @@ class Engine:
         self._check(self._lib.emcmc_kernel_name(self._h, buf, 256), "emcmc_kernel_name")
         return buf.value.decode()
 
-    RTC_ORIGIN = {0: "process", 1: "disk", 2: "compiled"}
+    RTC_ORIGIN = {0: "process", 1: "disk", 2: "compiled", 3: "compiled (cache directory not private: not used)"}
 
     def rtc_info(self):
         """(origin, seconds) of the handle's run-time compiled kernel: "process"
-        (this process's cache), "disk" (the code-object cache) or "compiled"."""
+        (this process's cache), "disk" (the code-object cache), "compiled", or "compiled (cache
+        directory not private: not used)" when the cache directory's owner or mode refused it."""
         o, s = C.c_uint32(), C.c_double()
         self._check(self._lib.emcmc_rtc_info(self._h, C.byref(o), C.byref(s)), "emcmc_rtc_info")
         return self.RTC_ORIGIN.get(o.value, str(o.value)), float(s.value)

@@ -636,8 +636,10 @@ emcmc_status emcmc_kernel_name(emcmc_handle *h, char *buf, size_t buflen);
 /* How the handle's run-time compiled kernel (hiprtc: user laws and updates, the
  * general kernel at other D, the chol kernel at other D) was obtained: origin
  * 0 = this process's cache, 1 = the on-disk code-object cache (EMCMC_RTC_CACHE,
- * else rtc_cache/ beside libemcmc.so), 2 = compiled now; seconds = the time it
- * took.  EMCMC_STATE_ERROR when the selected kernel is compiled ahead of time. */
+ * else rtc_cache/ beside libemcmc.so), 2 = compiled now, 3 = compiled now because the cache
+ * directory exists but is not private to this user (owned by the effective uid, not group- or
+ * world-writable; the library also says so once on stderr); seconds = the time it took.
+ * EMCMC_STATE_ERROR when the selected kernel is compiled ahead of time. */
 emcmc_status emcmc_rtc_info(emcmc_handle *h, uint32_t *origin, double *seconds);
 
 /* ---- self-test probes (run the device's own math on given inputs) ------- */

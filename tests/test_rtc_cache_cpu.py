@@ -83,6 +83,8 @@ def test_a_group_writable_directory_is_not_used(tmp_path):
     cache.mkdir()
     os.chmod(cache, 0o775)
     log = prebuild(cache)
-    assert "not a private directory" in log and "compiled" in log
+    # said without EMCMC_RTC_LOG too: the refusal costs a compile in every process
+    assert "warning" in log and "not a private directory" in log and "mode 775" in log and "compiled" in log
+    assert log.count("not a private directory") == 1  # once per process
     assert entries(cache) == []
     assert "compiled" in prebuild(cache)  # and nothing was loaded from it either

@@ -779,16 +779,21 @@ def watchdog(fn, seconds):
 
 
 BURN_IN_ITERS = 2000  # diagnostics windows starting at or before this iteration are labelled burn-in
-REPLAY_BUDGET = 6.0e7  # chain-steps the oracle replays after the timed region (~3 s at 16 threads on cfg 2)
+# the oracle's accept-only replay after the timed region: ~REPLAY_SECONDS of its measured rate on
+# 16 threads (profiles/r6_bench: 2.3e7 chain-steps/s on cfg 2 / 5, 1.0e7 on cfg 4), so the
+# driver's 20-step line and the 1000-step default replay every chain, cfg 4 / cfg 5 ≥ 4,096
+REPLAY_SECONDS = 10.0
+REPLAY_RATE_16T = {"gsn": 2.0e7, "mix": 0.9e7}
 
 
 def parity_replay(eng, w, a, ll_mode, first=0, reps=1, n=4096):
-    """the accept bitstream of the first n local chains (global ids first + c)
+    """the accept bitstream of the rank's first chains (global ids first + c)
     over EVERY iteration this handle ran (warm-up and all timed repetitions), replayed on the
     oracle in its accept-only mode, plus each chain's final θ and ll; the count of chains
-    whose stream or state differs is reported.  All of the rank's chains when they fit the
-    replay budget (the driver's 20-step line: 65,536 × 205).  cfg 3 (MALA: 4·N·D flop per
-    oracle chain-step) replays the first 20 iterations of 2 chains."""
+    whose stream or state differs is reported.  As many chains as the replay budget holds
+    (REPLAY_SECONDS at the oracle's rate; all of them for the driver's 20-step line and the
+    1000-step default), at least n.  cfg 3 (MALA: 4·N·D flop per oracle chain-step) replays
+    the first 20 iterations of 2 chains."""
     from extensible_mcmc import _lib as L
     from oracle import oracle as O
 
@@ -809,7 +814,9 @@ def parity_replay(eng, w, a, ll_mode, first=0, reps=1, n=4096):
         return {"chains_replayed": 2, "iterations": int(S), "mismatched_chains": bad,
                 "accept_stream_bitwise": bad == 0, "theta_at_last_replayed_iteration_bitwise": bad == 0,
                 "replay_s": time.perf_counter() - t0, "oracle_threads": threads}
-    C = w.num_chains if w.num_chains * S <= REPLAY_BUDGET else min(n, w.num_chains)
+    rate = REPLAY_RATE_16T["mix" if w.haario_k is not None else "gsn"] * threads / 16.0
+    fit = int(rate * REPLAY_SECONDS / S) // 64 * 64  # chains whose whole run fits the replay budget
+    C = min(w.num_chains, max(n, fit))
     C -= C % 64 if C > 64 else 0  # whole accept words
     init = np.ascontiguousarray(np.broadcast_to(np.asarray(w.theta_init, dtype=np.float64), (w.num_chains, w.D))[:C])
     if w.haario_k is not None:

@@ -29,6 +29,7 @@
 #include "emcmc_mix.h"
 #include "emcmc_mwg.h"
 #include "emcmc_dispatch.h"
+#include "emcmc_rwblock.h"
 #include "emcmc_rtc.h"
 
 using namespace emcmc;
@@ -538,77 +539,102 @@ emcmc_status upload_block_consts(emcmc_handle *h) {
     return EMCMC_OK;
 }
 
-// mwg_rw_block_kernel's shapes (emcmc_rwblock.h): ONE UniformRandomWalk or GaussianRandomWalk
-// update over coords 1:D in order, 17 ≤ D ≤ 64, any prior, positivity flags, AdaptationUnifRW
-// on a UniformRandomWalk; no chain moments / mixture state; the built-in GsnTargetLaw over μ
-// (d = D) or a user law.  (A GaussianRandomWalk with ImproperPrior and no flags on the built-in
-// target never reaches select_mwg: the fused kernels take it.)
-bool rwblock_eligible(const UpdateHost &u, uint32_t D) {
-    if (D < (uint32_t)kBlockMinD || D > (uint32_t)kMwgMaxD) return false;
+// mwg_rw_block_kernel's schedules (emcmc_rwblock.h): 1 ≤ P ≤ 8 UniformRandomWalk /
+// GaussianRandomWalk updates over any coordinate subsets at 17 ≤ D ≤ 64, any prior, positivity
+// flags, AdaptationUnifRW on a UniformRandomWalk; no chain moments / mixture state, no MALA or user
+// updates; the built-in GsnTargetLaw over μ (d = D) or a user law.  (A single GaussianRandomWalk
+// over coords 1:D with ImproperPrior and no flags on the built-in target never reaches select_mwg:
+// the fused kernels take it.)
+bool rwblock_update_ok(const UpdateHost &u) {
     if (u.kernel != EMCMC_RW_UNIFORM && u.kernel != EMCMC_RW_GAUSSIAN) return false;
-    if (u.adaptation != EMCMC_ADPT_NONE && !(u.kernel == EMCMC_RW_UNIFORM && u.adaptation == EMCMC_ADPT_UNIF_RW))
+    return u.adaptation == EMCMC_ADPT_NONE || (u.kernel == EMCMC_RW_UNIFORM && u.adaptation == EMCMC_ADPT_UNIF_RW);
+}
+bool rwblock_eligible(const std::vector<UpdateHost> &ups, uint32_t D) {
+    if (D < (uint32_t)kBlockMinD || D > (uint32_t)kMwgMaxD || ups.empty() || ups.size() > (size_t)kRwMaxP)
         return false;
-    if (u.coords.size() != D) return false;
-    for (uint32_t j = 0; j < D; ++j)
-        if (u.coords[j] != j) return false;
+    for (const auto &u : ups)
+        if (!rwblock_update_ok(u)) return false;
     return true;
 }
 bool rwblock_eligible(const emcmc_handle *h, bool xt) {
-    if (xt || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_BLOCK) || h->updates.size() != 1) return false;
+    if (xt || (h->cfg.kernel_variant & EMCMC_VARIANT_NO_BLOCK)) return false;
     const TargetHost &t = h->target;
     if (!(t.kind == EMCMC_TARGET_USER || (t.kind == EMCMC_TARGET_GSN && t.dim == h->cfg.dim))) return false;
-    return rwblock_eligible(h->updates[0], h->cfg.dim);
+    return rwblock_eligible(h->updates, h->cfg.dim);
 }
 
-// The compile-time shape of an eligible update (emcmc_rwblock.h RwShape): its kind, diagonal
-// Σ, positivity mask, adaptation and the prior's slot structure; label: the kernel-name tag;
-// shape_name: the generated struct's name (RwShape_<digest of the shape>).
-std::string rw_shape_source(const UpdateHost &u, std::string &label, std::string &shape_name) {
-    uint64_t pos = 0;
-    for (size_t j = 0; j < u.pos.size(); ++j)
-        if (u.pos[j]) pos |= 1ull << j;
-    const bool uni = u.kernel == EMCMC_RW_UNIFORM;
-    const bool adapt = uni && u.adaptation == EMCMC_ADPT_UNIF_RW;
-    const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
+// The compile-time schedule of eligible updates (emcmc_rwblock.h): per update its coordinates,
+// kind, diagonal Σ, positivity mask, adaptation, the prior's slot structure and whether it shares
+// no coordinate with another update; label: the kernel-name tag; sched_name: the generated
+// struct's name (RwSched_<digest of the schedule>, so kernels of different schedules have
+// different symbol names in a profile).
+std::string rw_sched_source(const std::vector<UpdateHost> &ups, std::string &label, std::string &sched_name) {
+    const size_t P = ups.size();
     char buf[64];
-    std::string src = "namespace emcmc {\nstruct RwShape {\n";
-    src += "    static constexpr uint32_t kind = " + std::to_string(u.kernel) + "u;\n";
-    src += std::string("    static constexpr bool diag = ") + ((uni || u.diag) ? "true" : "false") + ";\n";
-    snprintf(buf, sizeof buf, "0x%016llxull", (unsigned long long)pos);
-    src += std::string("    static constexpr uint64_t pos = ") + buf + ";\n";
-    src += std::string("    static constexpr bool adapt = ") + (adapt ? "true" : "false") + ";\n";
-    src += "    static constexpr uint32_t prior = " + std::to_string(u.prior) + "u;\n";
-    src += "    static constexpr int nslot = " + std::to_string(slots ? u.nslot : 0u) + ";\n";
-    const uint64_t masks[4] = {u.psrc0, u.pstart, u.pend, u.pmvn};
-    const char *mnames[4] = {"psrc0", "pstart", "pend", "pmvn"};
-    for (int k = 0; k < 4; ++k) {
-        snprintf(buf, sizeof buf, "0x%016llxull", (unsigned long long)(slots ? masks[k] : 0ull));
-        src += std::string("    static constexpr uint64_t ") + mnames[k] + " = " + buf + ";\n";
+    std::string body;
+    static const char *kPriorName[4] = {"ImproperPrior", "ImproperPosPrior", "ProductPrior", "StandardPrior"};
+    label.clear();
+    for (size_t p = 0; p < P; ++p) {
+        const UpdateHost &u = ups[p];
+        uint64_t pos = 0;
+        for (size_t j = 0; j < u.pos.size(); ++j)
+            if (u.pos[j]) pos |= 1ull << j;
+        const bool uni = u.kernel == EMCMC_RW_UNIFORM;
+        const bool adapt = uni && u.adaptation == EMCMC_ADPT_UNIF_RW;
+        const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
+        bool disjoint = true;
+        for (size_t q = 0; q < P && disjoint; ++q)
+            if (q != p)
+                for (uint32_t c : ups[q].coords)
+                    if (std::find(u.coords.begin(), u.coords.end(), c) != u.coords.end()) disjoint = false;
+        std::string b = "template <> struct RWSCHED::U<" + std::to_string(p) + "> {\n";
+        b += "    static constexpr int n = " + std::to_string(u.coords.size()) + ";\n";
+        b += "    static constexpr int coords[64] = {";
+        for (size_t j = 0; j < 64; ++j) b += std::to_string(j < u.coords.size() ? u.coords[j] : 0u) + (j < 63 ? "," : "};\n");
+        b += "    static constexpr uint32_t kind = " + std::to_string(u.kernel) + "u;\n";
+        b += std::string("    static constexpr bool diag = ") + ((uni || u.diag) ? "true" : "false") + ";\n";
+        snprintf(buf, sizeof buf, "0x%016llxull", (unsigned long long)pos);
+        b += std::string("    static constexpr uint64_t pos = ") + buf + ";\n";
+        b += std::string("    static constexpr bool adapt = ") + (adapt ? "true" : "false") + ";\n";
+        b += std::string("    static constexpr bool disjoint = ") + (disjoint ? "true" : "false") + ";\n";
+        b += "    static constexpr uint32_t prior = " + std::to_string(u.prior) + "u;\n";
+        b += "    static constexpr int nslot = " + std::to_string(slots ? u.nslot : 0u) + ";\n";
+        const uint64_t masks[4] = {u.psrc0, u.pstart, u.pend, u.pmvn};
+        const char *mnames[4] = {"psrc0", "pstart", "pend", "pmvn"};
+        for (int k = 0; k < 4; ++k) {
+            snprintf(buf, sizeof buf, "0x%016llxull", (unsigned long long)(slots ? masks[k] : 0ull));
+            b += std::string("    static constexpr uint64_t ") + mnames[k] + " = " + buf + ";\n";
+        }
+        std::string fam = "    static constexpr uint32_t fam[64] = {", mvs = "    static constexpr int mvs[64] = {";
+        for (int j = 0; j < 64; ++j) {
+            const bool in = slots && (uint32_t)j < u.nslot;
+            fam += std::to_string(in ? u.pfam[j] : 0u) + (j < 63 ? "," : "};\n");
+            mvs += std::to_string(in ? u.pmvs[j] : 0u) + (j < 63 ? "," : "};\n");
+        }
+        body += b + fam + mvs + "};\n";
+        // kernel-name tag
+        std::string l = std::string(uni ? "UniformRandomWalk" : "GaussianRandomWalk") + (uni || u.diag ? "" : "(dense)");
+        bool ident = true;
+        for (size_t j = 0; j < u.coords.size(); ++j) ident = ident && u.coords[j] == j;
+        if (P > 1 || !ident) l += "[" + std::to_string(u.coords.size()) + "]";
+        if (pos) {
+            snprintf(buf, sizeof buf, ",pos=0x%llx", (unsigned long long)pos);
+            l += buf;
+        }
+        if (adapt) l += ",AdaptationUnifRW";
+        l += std::string(",") + (u.prior < 4 ? kPriorName[u.prior] : "?");
+        if (slots && u.pmvn) l += "(MvNormal)";
+        label += (p ? ";" : "") + l;
     }
-    std::string fam = "    static constexpr uint32_t fam[64] = {", mvs = "    static constexpr int mvs[64] = {";
-    for (int j = 0; j < 64; ++j) {
-        const bool in = slots && (uint32_t)j < u.nslot;
-        fam += std::to_string(in ? u.pfam[j] : 0u) + (j < 63 ? "," : "};\n");
-        mvs += std::to_string(in ? u.pmvs[j] : 0u) + (j < 63 ? "," : "};\n");
-    }
-    src += fam + mvs + "};\n}  // namespace emcmc\n";
-    // the struct's name carries a digest of the shape, so kernels of different shapes have
-    // different symbol names in a profile (rocprofv3 merges dispatches by name)
+    std::string src = "namespace emcmc {\nstruct RWSCHED {\n    static constexpr int P = " + std::to_string(P) +
+                      ";\n    template <int p> struct U;\n};\n" + body + "}  // namespace emcmc\n";
     uint64_t hsh = 0xcbf29ce484222325ull;
     for (unsigned char ch : src) hsh = (hsh ^ ch) * 0x100000001b3ull;
-    snprintf(buf, sizeof buf, "RwShape_%016llx", (unsigned long long)hsh);
-    for (size_t at = src.find("RwShape"); at != std::string::npos; at = src.find("RwShape", at + 1))
-        src.replace(at, 7, buf), at += std::strlen(buf) - 1;
-    shape_name = buf;
-    static const char *kPriorName[4] = {"ImproperPrior", "ImproperPosPrior", "ProductPrior", "StandardPrior"};
-    label = std::string(uni ? "UniformRandomWalk" : "GaussianRandomWalk") + (uni || u.diag ? "" : ",DENSE_SIGMA");
-    if (pos) {
-        snprintf(buf, sizeof buf, ",pos=0x%llx", (unsigned long long)pos);
-        label += buf;
-    }
-    if (adapt) label += ",AdaptationUnifRW";
-    label += std::string(",") + (u.prior < 4 ? kPriorName[u.prior] : "?");
-    if (slots && u.pmvn) label += "(MvNormal)";
+    snprintf(buf, sizeof buf, "RwSched_%016llx", (unsigned long long)hsh);
+    sched_name = buf;
+    for (size_t at = src.find("RWSCHED"); at != std::string::npos; at = src.find("RWSCHED", at + 1))
+        src.replace(at, 7, sched_name);
+    if (P > 1) label = "P=" + std::to_string(P) + "," + label;
     return src;
 }
 
@@ -643,13 +669,13 @@ emcmc_status select_mwg(emcmc_handle *h) {
         return fail(h, EMCMC_UNSUPPORTED_PLUGIN,
                     "MALA needs the target's gradient (compute_gradients_and_momenta!): the user law defines none "
                     "(EMCMC_USER_GRAD { … })");
-    // one UniformRandomWalk / GaussianRandomWalk update over all 17 ≤ D ≤ 64 coordinates with a
-    // prior, positivity flags or AdaptationUnifRW: mwg_rw_block_kernel (emcmc_rwblock.h), the
-    // update's structure compiled in, every per-chain vector in registers
+    // a schedule of 1 ≤ P ≤ 8 UniformRandomWalk / GaussianRandomWalk updates at 17 ≤ D ≤ 64 (priors,
+    // positivity flags, AdaptationUnifRW, any coordinate subsets): mwg_rw_block_kernel
+    // (emcmc_rwblock.h), the schedule's structure compiled in, every per-chain vector in registers
     if (usrc.empty() && !mala && rwblock_eligible(h, xt)) {
         const bool tdense = !h->target.diag;
         std::string label, sname;
-        const std::string shape = rw_shape_source(h->updates[0], label, sname);
+        const std::string shape = rw_sched_source(h->updates, label, sname);
         RtcKernel k;
         const std::string log = rtc_compile_rwblock(D, full, user ? 0 : ll, tdense, shape, sname, label,
                                                     user ? h->target.src : "", user ? h->target.opts : "", k);
@@ -2180,27 +2206,32 @@ emcmc_status emcmc_prebuild_block_kernel(uint32_t dim, uint32_t history_mode, ui
 }
 
 emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, int dense_target,
-                                            const emcmc_update_desc *update, const char *target_source,
-                                            const char *target_options, char *log_out, size_t log_len) {
+                                            const emcmc_update_desc *updates, uint32_t num_updates,
+                                            const char *target_source, const char *target_options, char *log_out,
+                                            size_t log_len) {
     copy_log("", log_out, log_len);
-    if (!update || dim < (uint32_t)kBlockMinD || dim > (uint32_t)kMwgMaxD || history_mode > 1 || ll_mode > 1)
+    if (!updates || num_updates == 0 || dim < (uint32_t)kBlockMinD || dim > (uint32_t)kMwgMaxD || history_mode > 1 ||
+        ll_mode > 1)
         return EMCMC_INVALID_ARG;
-    emcmc_handle tmp;  // no device: build_update only reads cfg.dim and the (empty) update list
+    emcmc_handle tmp;  // no device: build_update only reads cfg.dim and the updates already built
     tmp.cfg.dim = dim;
-    UpdateHost uh;
-    if (emcmc_status st = build_update(&tmp, update, uh)) {
-        copy_log(tmp.err, log_out, log_len);
-        return st;
+    for (uint32_t p = 0; p < num_updates; ++p) {
+        UpdateHost uh;
+        if (emcmc_status st = build_update(&tmp, updates + p, uh)) {
+            copy_log(tmp.err, log_out, log_len);
+            return st;
+        }
+        tmp.updates.push_back(std::move(uh));
     }
-    if (!rwblock_eligible(uh, dim)) {
-        copy_log("not a mwg_rw_block_kernel shape: one UniformRandomWalk / GaussianRandomWalk update over coords "
-                 "0..dim-1 (AdaptationUnifRW on a UniformRandomWalk only)",
+    if (!rwblock_eligible(tmp.updates, dim)) {
+        copy_log("not a mwg_rw_block_kernel schedule: 1..8 UniformRandomWalk / GaussianRandomWalk updates "
+                 "(AdaptationUnifRW on a UniformRandomWalk only) at 17 <= dim <= 64",
                  log_out, log_len);
         return EMCMC_INVALID_ARG;
     }
     const bool user = target_source && *target_source;
     std::string label, sname;
-    const std::string shape = rw_shape_source(uh, label, sname);
+    const std::string shape = rw_sched_source(tmp.updates, label, sname);
     RtcKernel k;
     const std::string log = rtc_compile_rwblock((int)dim, history_mode == EMCMC_HIST_FULL, user ? 0 : (int)ll_mode,
                                                 dense_target != 0, shape, sname, label, user ? target_source : "",

@@ -285,8 +285,8 @@ SIGNATURES = {
         _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p, C.c_char_p,
               C.c_size_t]),
     "emcmc_prebuild_rw_block_kernel": (
-        _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_char_p, C.c_char_p, C.c_char_p,
-              C.c_size_t]),
+        _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p,
+              C.c_char_p, C.c_size_t]),
     "emcmc_probe_variates": (
         _ST,
         [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -437,15 +437,18 @@ def prebuild_block_kernel(dim: int, history_mode: int = 0, ll_mode: int = 0, den
         raise EMCMCError(st, "emcmc_prebuild_block_kernel", buf.value.decode(errors="replace"))
 
 
-def prebuild_rw_block_kernel(dim: int, update_desc, history_mode: int = 0, ll_mode: int = 0,
+def prebuild_rw_block_kernel(dim: int, update_descs, history_mode: int = 0, ll_mode: int = 0,
                              dense_target: bool = False, target_source: str = "", target_options: str = "") -> None:
-    """Compile mwg_rw_block_kernel for the structure of `update_desc` (an EmcmcUpdateDesc, e.g.
-    Engine.uniform_rw_desc(...)[0]: one random-walk update over coords 0..dim-1) into the on-disk
-    code-object cache (no device needed)."""
+    """Compile mwg_rw_block_kernel for the schedule of `update_descs` (EmcmcUpdateDesc objects, in
+    update order, e.g. [Engine.uniform_rw_desc(...)[0]]; a single desc is accepted too) into the
+    on-disk code-object cache (no device needed)."""
+    if isinstance(update_descs, EmcmcUpdateDesc):
+        update_descs = [update_descs]
+    arr = (EmcmcUpdateDesc * len(update_descs))(*update_descs)
     buf = C.create_string_buffer(1 << 16)
     enc = lambda x: x.encode() if x else None  # noqa: E731
     st = lib().emcmc_prebuild_rw_block_kernel(dim, history_mode, ll_mode, int(bool(dense_target)),
-                                              C.cast(C.pointer(update_desc), C.c_void_p), enc(target_source),
+                                              C.cast(arr, C.c_void_p), len(update_descs), enc(target_source),
                                               enc(target_options), buf, len(buf))
     if st != OK:
         raise EMCMCError(st, "emcmc_prebuild_rw_block_kernel", buf.value.decode(errors="replace"))

@@ -424,16 +424,19 @@ emcmc_status emcmc_prebuild_block_kernel(uint32_t dim, uint32_t history_mode, ui
                                          const char *update_source, const char *update_options, char *log_out,
                                          size_t log_len);
 
-/* The same for mwg_rw_block_kernel, the kernel a handle with ONE UniformRandomWalk or
- * GaussianRandomWalk update over coordinates 0..dim-1 selects at 17 ≤ dim ≤ 64 when it has a
- * prior, positivity flags or AdaptationUnifRW (or a user law): the kernel is compiled for the
- * update's structure (kind, diagonal Σ, pos flags, adaptation, prior families), so `update` is
- * the emcmc_update_desc the handle will be given (its values may differ: they are read at run
- * time).  The built-in GsnTargetLaw (target_source = NULL; dense_target != 0 for a non-diagonal
- * Σ) or a user law (target_source, its options). */
+/* The same for mwg_rw_block_kernel, the kernel a handle whose schedule is 1 ≤ P ≤ 8
+ * UniformRandomWalk / GaussianRandomWalk updates (any coordinate subsets, priors, positivity
+ * flags, AdaptationUnifRW on a UniformRandomWalk) selects at 17 ≤ dim ≤ 64 — unless it is one
+ * GaussianRandomWalk over 0..dim-1 with ImproperPrior and no flags on the built-in target, which
+ * the fused kernels take.  The kernel is compiled for the schedule's structure (kinds, coordinates,
+ * diagonal Σ, pos flags, adaptation, prior families), so `updates` are the num_updates
+ * emcmc_update_desc the handle will be given, in order (their values may differ: they are read at
+ * run time).  The built-in GsnTargetLaw (target_source = NULL; dense_target != 0 for a
+ * non-diagonal Σ) or a user law (target_source, its options). */
 emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode, uint32_t ll_mode, int dense_target,
-                                            const emcmc_update_desc *update, const char *target_source,
-                                            const char *target_options, char *log_out, size_t log_len);
+                                            const emcmc_update_desc *updates, uint32_t num_updates,
+                                            const char *target_source, const char *target_options, char *log_out,
+                                            size_t log_len);
 
 /* θinit for every chain (row-major [C][D]); ll = NULL means the reference's
  * initial ll = -Inf (workspaces.jl:425), i.e. the first step always accepts.

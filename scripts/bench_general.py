@@ -60,6 +60,11 @@ def main():
     # (1) D = 32, two GaussianRandomWalk blocks of 16 coordinates (Metropolis-within-Gibbs)
     if want("mwg_d32_two_blocks"):
         mwg_two_blocks(C, M, w, report)
+    if want("mwg_d32_two_blocks_wide"):
+        mwg_two_blocks(C, M, w, report, L.VARIANT_NO_BLOCK, "_wide")
+    for nm, variant in (("mwg_d64_two_blocks", a.variant), ("mwg_d64_two_blocks_wide", L.VARIANT_NO_BLOCK)):
+        if want(nm):
+            mwg_d64(nm, C, M, report, variant)
     if want("dense_d32_joint"):
         dense_joint(C, M, w, report)
     if want("user_student_t_d4"):
@@ -171,15 +176,33 @@ def rw_prior(name, suffix, C, M, report, variant=0):
     eng.close()
 
 
-def mwg_two_blocks(C, M, w, report):
-    eng = Engine(EngineConfig(dim=32, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed))
+def mwg_d64(name, C, M, report, variant=0):
+    """D = 64 as two GaussianRandomWalk blocks of 32 coordinates (P = 2), the first with a
+    ProductPrior of Normals, on a 64-dimensional Gaussian target (10 observations)."""
+    D = 64
+    w = W.cfg2(8, D=D)
+    s2 = (2.38 / np.sqrt(32 * 10)) ** 2
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed, kernel_variant=variant))
+    eng.add_gaussian_rw_update(np.arange(32), s2 * np.eye(32), prior=L.PRIOR_PRODUCT,
+                               prior_factors=[(L.DIST_PRODUCT, 32, [(L.DIST_NORMAL, 0.0, 4.0)] * 32)])
+    eng.add_gaussian_rw_update(np.arange(32, 64), s2 * np.eye(32))
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    eng.set_state(np.tile(w.mu_true, (C, 1)))
+    steps = [(i, p) for i in range(1, M + 1) for p in (1, 2)]
+    ms, b = timed(eng, steps, reps=3)
+    report(name, eng, 2, ms, b)
+    eng.close()
+
+
+def mwg_two_blocks(C, M, w, report, variant=0, suffix=""):
+    eng = Engine(EngineConfig(dim=32, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed, kernel_variant=variant))
     for blk in (range(0, 16), range(16, 32)):
         eng.add_gaussian_rw_update(np.array(blk), np.asarray(w.rw_sigma)[:16, :16] * 2.0)
     eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
     eng.set_state(np.zeros((C, 32)))
     steps = [(i, p) for i in range(1, 2 * M + 1) for p in (1, 2)]
     ms, b = timed(eng, steps[: 2 * M], reps=3)
-    report("mwg_d32_two_blocks", eng, 2, ms, b)
+    report("mwg_d32_two_blocks" + suffix, eng, 2, ms, b)
     eng.close()
 
 

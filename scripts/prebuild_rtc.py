@@ -50,7 +50,7 @@ def one_rw(i):
     name, make = rw_shapes()[i]
     t = time.time()
     u, keep = make()
-    L.prebuild_rw_block_kernel(32, u, 0, 0, False)
+    L.prebuild_rw_block_kernel(32, [u], 0, 0, False)
     return f"rw block {name}: {time.time() - t:.1f} s"
 
 

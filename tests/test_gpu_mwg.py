@@ -24,9 +24,10 @@ def full_steps(M, P, first=1):
     return [(i, p) for i in range(first, M + 1) for p in range(1, P + 1)]
 
 
-def make_engine(D, C, M, ups, mu, t_sigma, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL, spl=0, theta0=None):
+def make_engine(D, C, M, ups, mu, t_sigma, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL, spl=0, theta0=None,
+                variant=0):
     eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
-                              steps_per_launch=spl))
+                              steps_per_launch=spl, kernel_variant=variant))
     for u in ups:
         pr = dict(prior=u.get("prior", 0), prior_factors=u.get("factors") or None)
         if u["kind"] == 1:

@@ -57,11 +57,13 @@ def test_resampling_outside_the_support(oracle):
     assert not np.any(st.faults & L.FAULT_PRIOR_RESAMPLES)
 
 
+@pytest.mark.parametrize("variant", [0, L.VARIANT_NO_BLOCK])
 @pytest.mark.parametrize("ll_mode", [0, 1])
-def test_d32_two_blocks_with_priors_on_the_wide_kernel(oracle, ll_mode):
+def test_d32_two_blocks_with_priors(oracle, ll_mode, variant):
     """Metropolis-within-Gibbs at the headline D = 32: two GaussianRandomWalk blocks of
     16 coordinates, a ProductPrior of Product(Normal)/Product(Gamma) factors on one and a
-    StandardPrior(Product(Exponential)) on the other (so a Gaussian target at μ* > 0 keeps mass in the support)."""
+    StandardPrior(Product(Exponential)) on the other (so a Gaussian target at μ* > 0 keeps mass
+    in the support) — on the compiled-schedule block kernel (round 6) and on the wide kernel."""
     w = W.cfg2(2048)
     mu = np.abs(w.mu_true) + 0.5
     obs = w.obs - w.mu_true + mu
@@ -73,8 +75,8 @@ def test_d32_two_blocks_with_priors_on_the_wide_kernel(oracle, ll_mode):
     steps = full_steps(120, 2)
     th0 = np.tile(mu, (2048, 1))
     eng, st, h = run_both(oracle, 32, 2048, 120, ups, mu, np.eye(32), obs, steps, w.seed, ll_mode=ll_mode,
-                          theta0=th0)
-    assert "mwg_wide_kernel<D=32" in eng.kernel_name()
+                          theta0=th0, variant=variant)
+    assert ("mwg_wide_kernel<D=32" if variant else "mwg_rw_block_kernel<D=32") in eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 2)
 
 

@@ -238,3 +238,105 @@ def test_wide_kernel_gives_the_same_bits():
                 assert np.array_equal(x, y)
         else:
             assert np.array_equal(a, b)
+
+
+# ---- compiled schedules of several updates (Metropolis-within-Gibbs, round 6) ----------------
+def sched_problem(D, shift=0.0):
+    seed, mu, ts, obs = problem(D, shift=shift)
+    return seed, mu, ts, obs, np.tile(mu, (1, 1))
+
+
+@pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
+@pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
+def test_d32_two_blocks_of_16(oracle, ll_mode, hist):
+    """Two GaussianRandomWalk blocks of 16 coordinates (run.jl:64-83 over P = 2): the compiled
+    schedule keeps θ, P°.θ and both blocks' vectors in registers; slots (iter−1)·2 + p."""
+    D, C, M = 32, 2048, 100
+    seed, mu, ts, obs, _ = sched_problem(D)
+    ups = [oracle.mwg_update(2, range(0, 16), sigma=s2(16) * np.eye(16)),
+           oracle.mwg_update(2, range(16, 32), sigma=s2(16) * np.eye(16))]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, steps=full_steps(M, 2),
+                                 ll_mode=ll_mode, hist=hist)
+    assert_block(eng, D)
+    assert "P=2" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 2, full=(hist == L.HIST_FULL))
+
+
+def test_three_interleaved_updates_of_every_kind(oracle):
+    """D = 33: a UniformRandomWalk with pos flags and AdaptationUnifRW on coords 0, 3, 6, …, a
+    dense GaussianRandomWalk on 1, 4, 7, … (reversed) and a GaussianRandomWalk with a ProductPrior
+    on 2, 5, 8, …; disjoint blocks, so every prior is carried."""
+    D, C, M = 33, 1024, 90
+    seed, mu, ts, obs, _ = sched_problem(D, shift=3.0)
+    A = np.random.default_rng(4).standard_normal((11, 11))
+    ups = [oracle.mwg_update(1, range(0, D, 3), eps=[0.1] * 11, pos=[True] * 11, adapt=dict(ADAPT, k=20)),
+           oracle.mwg_update(2, list(range(1, D, 3))[::-1], sigma=s2(11, f=0.5) * (A @ A.T / 11 + np.eye(11))),
+           oracle.mwg_update(2, range(2, D, 3), sigma=s2(11) * np.eye(11), prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, 11, [(G_, 6.0, 0.5)] * 11)])]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, steps=full_steps(M, 3), spl=11)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 3)
+
+
+def test_overlapping_updates_evaluate_both_priors(oracle):
+    """Updates sharing coordinates 10..19 (no log-prior carry: the other update moves θ_local),
+    an exclusion schedule (update 2 off on iterations 20:35) and three run calls."""
+    D, C, M = 30, 1024, 80
+    seed, mu, ts, obs, _ = sched_problem(D, shift=2.0)
+    ups = [oracle.mwg_update(2, range(0, 20), sigma=s2(20) * np.eye(20), prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, 20, [(N_, 2.0, 2.0)] * 20)]),
+           oracle.mwg_update(1, range(10, 30), eps=[0.15] * 20, prior=L.PRIOR_STANDARD,
+                             factors=[(MV_, 20, 2.0 * np.ones(20), np.eye(20) + 0.1 * np.ones((20, 20)))])]
+    steps = [(s.mcmciter, s.pidx) for s in MCMCSchedule(M, 2, [(2, range(20, 36))])]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, steps=steps, spl=13,
+                                 calls=[(0, 50), (50, 51), (51, len(steps))])
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 2)
+
+
+def test_d64_two_blocks_of_32_with_a_prior(oracle):
+    """D = 64 as two GaussianRandomWalk blocks of 32 (the wide kernel's NU = 32 case), one with a
+    ProductPrior of Normals."""
+    D, C, M = 64, 1024, 60
+    seed, mu, ts, obs, _ = sched_problem(D)
+    ups = [oracle.mwg_update(2, range(0, 32), sigma=s2(32) * np.eye(32), prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, 32, [(N_, 0.0, 4.0)] * 32)]),
+           oracle.mwg_update(2, range(32, 64), sigma=s2(32) * np.eye(32))]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, steps=full_steps(M, 2))
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 2)
+
+
+def test_one_update_over_a_subset(oracle):
+    """P = 1 over coordinates 5..24 of D = 30: P°.θ keeps the target's μ outside them
+    (set_parameters! writes the update's coordinates only)."""
+    D, C, M = 30, 1024, 80
+    seed, mu, ts, obs, _ = sched_problem(D)
+    ups = [oracle.mwg_update(1, range(5, 25), eps=[0.08] * 20, prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, 20, [(LA_, 0.0, 2.0)] * 20)])]
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_two_blocks_on_a_user_law(oracle):
+    """Two UniformRandomWalk blocks on the user logistic law (D = 20, P = 2)."""
+    D, C, M, n = 20, 512, 60, 60
+    rng = np.random.default_rng(13)
+    X = rng.standard_normal((n, D)) / np.sqrt(D)
+    beta = rng.normal(scale=0.3, size=D)
+    y = (rng.uniform(size=n) < 1.0 / (1.0 + np.exp(-(X @ beta)))).astype(float)
+    obs = np.column_stack([X, y])
+    fn, src = oracle.user_loglik("logistic_regression")
+    ups = [oracle.mwg_update(1, range(0, 10), eps=[0.3] * 10),
+           oracle.mwg_update(1, range(10, 20), eps=[0.3] * 10, prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, 10, [(N_, 0.0, 1.0)] * 10)])]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, None, None, obs, 43, np.zeros((C, D)), user=(fn, src),
+                                 steps=full_steps(M, 2))
+    assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 2)

@@ -23,11 +23,29 @@ def test_prebuild_compiles_a_shape_into_the_cache(cache):
     assert len(list(cache.glob("*.co"))) == 1
 
 
-@pytest.mark.parametrize("case", ["coords", "mix", "small_d"])
+def test_prebuild_compiles_a_two_update_schedule(cache):
+    """Metropolis-within-Gibbs: two GaussianRandomWalk blocks over interleaved coordinates, one
+    with a ProductPrior, one reversed — one kernel for the schedule."""
+    D = 24
+    a, ka = Engine.gaussian_rw_desc(range(0, D, 2), 0.01 * np.eye(D // 2), prior=L.PRIOR_PRODUCT,
+                                    prior_factors=[(L.DIST_PRODUCT, D // 2, [(L.DIST_NORMAL, 0.0, 1.0)] * (D // 2))])
+    b, kb = Engine.gaussian_rw_desc(list(range(1, D, 2))[::-1], 0.01 * np.eye(D // 2))
+    L.prebuild_rw_block_kernel(D, [a, b])
+    assert len(list(cache.glob("*.co"))) == 1
+
+
+@pytest.mark.parametrize("case", ["mix", "small_d", "mala"])
 def test_prebuild_refuses_other_shapes(cache, case):
     D = 20 if case != "small_d" else 8
-    coords = list(range(D))[::-1] if case == "coords" else range(D)
-    if case == "mix":
+    coords = range(D)
+    if case == "mala":
+        u = L.EmcmcUpdateDesc()
+        u.kernel = L.MALA
+        c = np.arange(D, dtype=np.uint32)
+        e = np.array([0.1])
+        u.num_coords, u.coords, u.epsilon = D, L.u32ptr(c), L.dptr(e)
+        keep = [c, e]
+    elif case == "mix":
         u = L.EmcmcUpdateDesc()
         u.kernel = L.RW_GAUSSIAN_MIX
         c = np.arange(D, dtype=np.uint32)

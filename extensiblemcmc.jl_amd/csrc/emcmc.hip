@@ -17,6 +17,8 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <string>
 #include <tuple>
 #include <utility>
@@ -483,18 +485,53 @@ emcmc_status allow_lds(emcmc_handle *h, const void *fn, size_t bytes) {
 // Load a run-time compiled code object as the handle's module (kept while the
 // same kernel stays selected).
 emcmc_status load_rtc_module(emcmc_handle *h, const RtcKernel &k) {
-    const std::string key = k.name + '|' + k.lowered + '|' + std::to_string(std::hash<std::string>{}(
-                                std::string(k.code.begin(), k.code.end())));
+    const std::string key = std::to_string(h->cfg.device) + '|' + k.name + '|' + k.lowered + '|' +
+                            std::to_string(std::hash<std::string>{}(std::string(k.code.begin(), k.code.end())));
     h->rtc_origin = k.origin;
     h->rtc_seconds = k.seconds;
     if (key == h->umod_key) return EMCMC_OK;
-    if (h->umod) (void)hipModuleUnload(h->umod);
-    h->umod = nullptr;
-    h->umod_key.clear();
-    HIPCHK(h, hipSetDevice(h->cfg.device));
-    HIPCHK(h, hipModuleLoadData(&h->umod, k.code.data()));
+    // Loaded modules stay loaded for the life of the process, one per (device, code object),
+    // shared by every handle that selects the kernel: a handle never unloads code another
+    // handle (or a later allocation at the same addresses) could meet, and re-creating an
+    // engine for a known kernel costs no load.
+    static std::mutex mu;
+    static std::map<std::string, hipModule_t> loaded;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = loaded.find(key);
+    if (it == loaded.end()) {
+        HIPCHK(h, hipSetDevice(h->cfg.device));
+        hipModule_t m = nullptr;
+        HIPCHK(h, hipModuleLoadData(&m, k.code.data()));
+        it = loaded.emplace(key, m).first;
+    }
+    h->umod = it->second;
     h->umod_key = key;
     return EMCMC_OK;
+}
+
+// Every ahead-of-time code object of the library (one per translation unit) is loaded when
+// the first handle of a device is created, before that process loads any run-time module or
+// allocates any handle buffer; HIP would otherwise load a translation unit's code object at
+// the first launch of one of its kernels, in the middle of a run.
+void load_aot_code_objects(int device) {
+    static std::mutex mu;
+    static std::vector<int> done;
+    std::lock_guard<std::mutex> lock(mu);
+    if (std::find(done.begin(), done.end(), device) != done.end()) return;
+    done.push_back(device);
+    hipFuncAttributes at;
+    auto touch = [&](const void *fn) {
+        if (fn) (void)hipFuncGetAttributes(&at, fn);
+    };
+    for (const auto *tab : {&diag_table(), &diag2_table(), &chol_table()})
+        if (!tab->empty()) touch(reinterpret_cast<const void *>(tab->front().fn));
+    if (!mwg_table().empty()) touch(reinterpret_cast<const void *>(mwg_table().front().full_perobs));
+    if (!block_table().empty()) touch(reinterpret_cast<const void *>(block_table().front().fn));
+    for (const auto *tab : {&mix_table(), &mixchol_table()})
+        if (!tab->empty()) touch(reinterpret_cast<const void *>(tab->front().fn));
+    if (!mixres_table().empty()) touch(reinterpret_cast<const void *>(mixres_table().front().fn));
+    touch(reinterpret_cast<const void *>(mala_lookup(32, true, 0)));
+    touch(reinterpret_cast<const void *>(&gather_hist_kernel));
 }
 
 // mwg_block_kernel's shapes: one MALA or user update (kinds 4, 5) over coords 1:D in order,
@@ -685,10 +722,23 @@ emcmc_status select_mwg(emcmc_handle *h) {
         }
         if (emcmc_status st = load_rtc_module(h, k)) return st;
         HIPCHK(h, hipModuleGetFunction(&v.ufn, h->umod, k.lowered.c_str()));
-        v.name = k.name;
-        v.block = true;
-        if (!user) {
-            if (emcmc_status st = upload_block_consts(h)) return st;
+        // Register-resident or not at all: a schedule whose state does not fit the register
+        // file (e.g. D = 64 with P°.θ, a dense 40-coordinate Σ and a dense target: 512 VGPRs,
+        // 256 AGPRs, 3,322 SGPR spills, 660 B of scratch per lane) goes to the wide kernel.
+        // That code object gave wrong bits on MI355X; every shape measured
+        // and tested on this kernel needs no scratch.
+        int scratch = 0;
+        HIPCHK(h, hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, v.ufn));
+        if (scratch == 0) {
+            v.name = k.name;
+            v.block = true;
+            if (!user) {
+                if (emcmc_status st = upload_block_consts(h)) return st;
+            }
+        } else {
+            v.ufn = nullptr;
+            h->rtc_origin = 0;
+            h->rtc_seconds = 0.0;
         }
     }
     // one MALA or user update over all 17 ≤ D ≤ 64 coordinates: mwg_block_kernel (emcmc_block.h),
@@ -1715,9 +1765,12 @@ emcmc_status emcmc_create(emcmc_handle **out, const emcmc_config *cfg) {
     if (const char *e = getenv("EMCMC_THETA_LIVE")) h->theta_live_ok = atoi(e) != 0;
     if (h->sync_mode && hipEventCreateWithFlags(&h->sync_ev, hipEventDisableTiming) != hipSuccess) h->sync_mode = 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+        if (h->sync_ev) (void)hipEventDestroy(h->sync_ev);
+        (void)hipStreamDestroy(h->cstream);
         delete h;
         return EMCMC_HIP_ERROR;
     }
+    load_aot_code_objects(cfg->device);
     *out = h;
     return EMCMC_OK;
 }
@@ -2465,9 +2518,9 @@ void emcmc_destroy(emcmc_handle *h) {
         fprintf(stderr, "[emcmc host] emcmc_run %.2f us x %llu, emcmc_synchronize %.2f us x %llu (sync mode %d)\n",
                 h->ht_runs ? h->ht_run_us / h->ht_runs : 0.0, (unsigned long long)h->ht_runs,
                 h->ht_syncs ? h->ht_sync_us / h->ht_syncs : 0.0, (unsigned long long)h->ht_syncs, h->sync_mode);
-    if (h->sync_ev) (void)hipEventDestroy(h->sync_ev);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->cstream) (void)hipStreamSynchronize(h->cstream);
+    if (h->sync_ev) (void)hipEventDestroy(h->sync_ev);
     for (auto &c : h->copies) (void)hipEventDestroy(c.ev);
     if (h->d_stage) (void)hipFree(h->d_stage);
     if (h->cstream) (void)hipStreamDestroy(h->cstream);
@@ -2485,7 +2538,7 @@ void emcmc_destroy(emcmc_handle *h) {
                     h->d_ll_prop,   h->d_uparams,   h->d_gcache,  h->d_bconsts};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    if (h->umod) (void)hipModuleUnload(h->umod);
+    // h->umod belongs to the process-wide module table (load_rtc_module)
     if (h->h_fault_flag) (void)hipHostFree(h->h_fault_flag);
     if (h->stream) (void)hipStreamDestroy(h->stream);
     delete h;

@@ -41,11 +41,17 @@ def main():
     ap.add_argument("--haario-iters", type=int, default=400)
     ap.add_argument("--only", default="", help="comma-separated workload names (default: all)")
     ap.add_argument("--variant", type=int, default=0, help="emcmc_config.kernel_variant (EMCMC_VARIANT_* A/B flags)")
+    ap.add_argument("--inproc", action="store_true",
+                    help="run every selected workload in this process (default: one child process each)")
+    ap.add_argument("--child-timeout", type=float, default=300.0, help="seconds per workload process")
     a = ap.parse_args()
+    only = set(filter(None, a.only.split(",")))
+    names = [n for n in WORKLOADS if not only or n in only]
+    if not a.inproc and len(names) > 1:
+        return run_isolated(names, a)
     C, M = a.chains, a.iters
     w = W.cfg2(8)
     out = []
-    only = set(filter(None, a.only.split(",")))
 
     def want(name):
         return not only or name in only
@@ -83,6 +89,31 @@ def main():
         for suffix, variant in (("", a.variant), ("_wide", L.VARIANT_NO_BLOCK)):
             if want(name + suffix) or (not only and suffix == ""):
                 rw_prior(name, suffix, C, M, report, variant)
+
+
+# every workload, in the order one run measures them
+WORKLOADS = ["mwg_d32_two_blocks", "mwg_d32_two_blocks_wide", "mwg_d64_two_blocks", "mwg_d64_two_blocks_wide",
+             "dense_d32_joint", "dense_d32_joint_suffstat", "user_student_t_d4", "haario_dense_d32",
+             "haario_dense_d32_general", "mala_gsn_d32", "pcn_user_d32", "rw_product_normal_d32",
+             "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32", "rw_standard_mvnormal_d32_wide",
+             "unif_pos_d32", "unif_pos_d32_wide"]
+
+
+def run_isolated(names, a):
+    """One child process per workload (each measured with a fresh allocator, fresh streams and
+    only its own code objects loaded), under a time limit; a child that fails ends the run."""
+    import subprocess
+    fwd = ["--chains", str(a.chains), "--iters", str(a.iters), "--haario-chains", str(a.haario_chains),
+           "--haario-iters", str(a.haario_iters), "--variant", str(a.variant), "--inproc"]
+    for n in names:
+        only = "dense_d32_joint" if n == "dense_d32_joint_suffstat" else n  # one function measures both
+        if n == "dense_d32_joint_suffstat" and "dense_d32_joint" in names:
+            continue
+        r = subprocess.run([sys.executable, "-u", __file__, "--only", only] + fwd, timeout=a.child_timeout)
+        if r.returncode != 0:
+            print(f"bench_general: workload {n} exited with {r.returncode}", file=sys.stderr, flush=True)
+            return r.returncode
+    return 0
 
 
 def corr_d32(seed=32, D=32, nobs=10):
@@ -244,4 +275,4 @@ def user_student_t(C, M, report):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

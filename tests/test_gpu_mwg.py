@@ -256,6 +256,9 @@ def test_d64_general_kernel_blocks_and_dense(oracle):
     steps = full_steps(M, 3)
     eng, st, h = run_both(oracle, D, C, M, ups, mu, ts, obs, steps, 31)
     assert "D=64" in eng.kernel_name()
+    # as mwg_rw_block_kernel this schedule needs scratch (θ, P°.θ, a dense 40-block and the
+    # dense target's sweeps exceed the register file), so the wide kernel runs it
+    assert eng.kernel_name().startswith("mwg_wide_kernel"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 3)
 
 

@@ -311,6 +311,24 @@ def test_d64_two_blocks_of_32_with_a_prior(oracle):
     check(oracle, eng, st, h, steps, ups, 2)
 
 
+def test_dense_target_three_blocks_d40(oracle):
+    """D = 40 on a dense Σ_t (the GsnSweep<true> sweeps): a diagonal Gaussian block of 16, a
+    correlated Gaussian block of 16 and a UniformRandomWalk block of 8 with a ProductPrior —
+    test_gpu_mwg's D = 64 schedule at a size whose compiled kernel needs no scratch."""
+    D, C, M = 40, 1024, 80
+    seed, mu, ts, obs = problem(D, dense_t=True)
+    B = np.random.default_rng(3).standard_normal((16, 16))
+    ups = [oracle.mwg_update(2, range(0, 16), sigma=0.01 * np.eye(16)),
+           oracle.mwg_update(2, range(16, 32), sigma=0.002 * (B @ B.T / 16 + np.eye(16))),
+           oracle.mwg_update(1, range(32, 40), eps=[0.05] * 8, prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, 8, [(N_, 0.0, 3.0)] * 8)])]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.zeros((C, D)),
+                                 steps=full_steps(M, 3))
+    assert_block(eng, D)
+    assert "DENSE_T" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 3)
+
+
 def test_one_update_over_a_subset(oracle):
     """P = 1 over coordinates 5..24 of D = 30: P°.θ keeps the target's μ outside them
     (set_parameters! writes the update's coordinates only)."""

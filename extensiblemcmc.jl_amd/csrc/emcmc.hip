@@ -729,7 +729,11 @@ emcmc_status select_mwg(emcmc_handle *h) {
         // and tested on this kernel needs no scratch.
         int scratch = 0;
         HIPCHK(h, hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, v.ufn));
-        if (scratch == 0) {
+        static const bool allow_scratch = [] {  // A/B builds only (EMCMC_RTC_EXTRA occupancy trials)
+            const char *e = getenv("EMCMC_RW_ALLOW_SCRATCH");
+            return e && *e && *e != '0';
+        }();
+        if (scratch == 0 || allow_scratch) {
             v.name = k.name;
             v.block = true;
             if (!user) {

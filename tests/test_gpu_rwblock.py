@@ -362,3 +362,61 @@ def test_two_blocks_on_a_user_law(oracle):
                                  steps=full_steps(M, 2))
     assert_block(eng, D)
     check(oracle, eng, st, h, steps, ups, 2)
+
+
+# ---- engine lifetime: run-time modules shared per process, handles created after others -------
+def two_block_engine(C, M, variant=0, seed=None):
+    w = W.cfg2(8)
+    eng = Engine(EngineConfig(dim=32, num_chains=C, num_mcmc_steps=M, seed=w.seed if seed is None else seed,
+                              kernel_variant=variant))
+    for blk in (range(0, 16), range(16, 32)):
+        eng.add_gaussian_rw_update(np.array(blk), np.asarray(w.rw_sigma)[:16, :16] * 2.0)
+    eng.set_gsn_target(w.mu_true, w.t_sigma, w.obs)
+    eng.set_state(np.zeros((C, 32)))
+    return eng
+
+
+def test_schedule_kernel_then_wide_kernel_at_full_size():
+    """bench_general's in-process sequence at its size (65,536 chains, P = 2): the schedule
+    kernel's handle destroyed, then a handle on the wide kernel — which once hung in its first
+    launch (module and code-object lifetime).  The two kernels' bits agree over
+    every chain: accept streams, θ and ll."""
+    C, M = 65536, 60
+    steps = full_steps(M, 2)
+    out = []
+    for variant in (0, L.VARIANT_NO_BLOCK):
+        eng = two_block_engine(C, M, variant)
+        eng.run(steps)
+        eng.synchronize(allow_faults=True)
+        out.append((eng.kernel_name(), eng.get_state(), eng.get_history(L.H_ACCEPT, 1, M)))
+        eng.close()
+    assert out[0][0].startswith("mwg_rw_block_kernel<D=32") and out[1][0].startswith("mwg_wide_kernel<D=32")
+    for x, y in zip(out[0][1], out[1][1]):
+        assert np.array_equal(x, y)
+    assert np.array_equal(out[0][2], out[1][2])
+
+
+def test_handles_share_a_module_and_outlive_each_other():
+    """Two handles select the same compiled schedule (one module, loaded once per process); the
+    first is destroyed between the second's launches, and the second's chains still equal a
+    third handle's that ran alone afterwards."""
+    C, M = 4096, 40
+    steps = full_steps(M, 2)
+    a, b = two_block_engine(C, M), two_block_engine(C, M)
+    assert a.kernel_name() == b.kernel_name() and a.kernel_name().startswith("mwg_rw_block_kernel")
+    a.run(steps[:40])
+    b.run(steps[:40])
+    a.synchronize(allow_faults=True)
+    a.close()
+    b.run(steps[40:])
+    b.synchronize(allow_faults=True)
+    got = (b.get_state(), b.get_history(L.H_ACCEPT, 1, M))
+    b.close()
+    c = two_block_engine(C, M)
+    c.run(steps)
+    c.synchronize(allow_faults=True)
+    want = (c.get_state(), c.get_history(L.H_ACCEPT, 1, M))
+    c.close()
+    for x, y in zip(got[0], want[0]):
+        assert np.array_equal(x, y)
+    assert np.array_equal(got[1], want[1])

@@ -916,6 +916,101 @@ bool fused_eligible(const emcmc_handle *h) {
     return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
 }
 
+// The fused diagonal step with a separable prior (emcmc_fprior.h): the joint GaussianRandomWalk
+// with a diagonal Σ and no positivity flags on a diagonal GsnTargetLaw, with ONE ProductPrior /
+// StandardPrior factor that is a Product of D univariates (no "reads θ[1]" factor, no MvNormal)
+// whose families repeat across the chain's lanes (family of coordinate i = that of i mod D/LPC).
+int fused_lpc(const emcmc_handle *h) {
+    return h->cfg.lanes_per_chain ? (int)h->cfg.lanes_per_chain : auto_lpc((int)h->cfg.dim);
+}
+bool fused_prior_eligible(const emcmc_handle *h) {
+    if ((h->cfg.kernel_variant & EMCMC_VARIANT_NO_FUSED_PRIOR) || !joint_all_coords(h) || h->cfg.chain_moments)
+        return false;
+    const UpdateHost &u = h->updates[0];
+    const int D = (int)h->cfg.dim;
+    if (u.kernel != EMCMC_RW_GAUSSIAN || u.adaptation != EMCMC_ADPT_NONE || !u.diag || !h->target.diag ||
+        h->target.kind != EMCMC_TARGET_GSN || D > 64)
+        return false;
+    for (uint8_t f : u.pos)
+        if (f) return false;
+    if (u.prior != EMCMC_PRIOR_PRODUCT && u.prior != EMCMC_PRIOR_STANDARD) return false;
+    if (u.nslot != (uint32_t)D || u.pmvn || u.psrc0 || u.pstart != 1ull || u.pend != (1ull << (D - 1))) return false;
+    const int lpc = fused_lpc(h);
+    if ((lpc != 1 && lpc != 2 && lpc != 4) || D % lpc || (lpc > 1 && (D / lpc) % 8)) return false;
+    for (int i = 0; i < D; ++i)
+        if (u.pfam[i] != u.pfam[i % (D / lpc)]) return false;
+    return true;
+}
+
+// EMCMC_UNSUPPORTED_PLUGIN when the shape does not fit (its LDS or a code object that needs
+// scratch): the caller falls back to the schedule kernels.
+emcmc_status select_fused_prior(emcmc_handle *h) {
+    const UpdateHost &u = h->updates[0];
+    const TargetHost &t = h->target;
+    const int D = (int)h->cfg.dim;
+    const bool full = h->cfg.history_mode == EMCMC_HIST_FULL;
+    const int ll = (int)t.ll_mode;
+    const int lpc = fused_lpc(h);
+    bool unit = true;
+    for (int i = 0; i < D; ++i) unit = unit && t.invdiag[i] == 1.0;
+    const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
+    const size_t lds = lds_align16((7 * (size_t)D + obs_doubles) * sizeof(double));
+    if (kZigLdsBytes + lds > kMaxLds) return EMCMC_UNSUPPORTED_PLUGIN;  // the schedule kernel reads them from HBM
+    std::string label, sname;
+    const std::string shape = rw_sched_source(h->updates, label, sname);
+    // two waves per SIMD (512-thread blocks, sibling pacing) where the step fits 256 registers, else
+    // one; register-resident or not at all (as mwg_rw_block_kernel, select_mwg)
+    Variant v;
+    int minw = 0;
+    for (int w : {2, 1}) {
+        RtcKernel k;
+        const std::string log = rtc_compile_fused_prior(D, lpc, w, full, ll, unit, shape, sname,
+                                                        label.substr(label.find(',') + 1), k);
+        if (!log.empty()) return fail(h, EMCMC_HIP_ERROR, "run-time kernel build failed:\n%s", log.c_str());
+        if (emcmc_status st = load_rtc_module(h, k)) return st;
+        HIPCHK(h, hipModuleGetFunction(&v.ffn, h->umod, k.lowered.c_str()));
+        int scratch = 0;
+        HIPCHK(h, hipFuncGetAttribute(&scratch, HIP_FUNC_ATTRIBUTE_LOCAL_SIZE_BYTES, v.ffn));
+        if (scratch == 0) {
+            minw = w;
+            v.name = k.name;
+            break;
+        }
+    }
+    if (!minw) {
+        h->rtc_origin = 0;
+        h->rtc_seconds = 0.0;
+        return EMCMC_UNSUPPORTED_PLUGIN;
+    }
+    v.lpc = lpc;
+    v.dense = 0;
+    v.occ = minw;
+    v.unit = unit;
+    // the diag kernel's constants (L_ii, 1/L_ii, 1/L_t,ii, x̄), then the prior's a, b, c per coordinate
+    std::vector<double> c(7 * (size_t)D);
+    for (int i = 0; i < D; ++i) {
+        c[i] = u.L[(size_t)i * D + i];
+        c[D + i] = u.invdiag[i];
+        c[2 * D + i] = t.invdiag[i];
+        c[3 * D + i] = t.xbar[i];
+        c[4 * D + i] = u.pa[i];
+        c[5 * D + i] = u.pb[i];
+        c[6 * D + i] = u.pc[i];
+    }
+    if (h->d_consts) (void)hipFree(h->d_consts);
+    HIPCHK(h, hipMalloc(&h->d_consts, c.size() * sizeof(double)));
+    HIPCHK(h, hipMemcpy(h->d_consts, c.data(), c.size() * sizeof(double), hipMemcpyHostToDevice));
+    if (h->d_obs) (void)hipFree(h->d_obs);
+    h->d_obs = nullptr;
+    if (t.nobs) {
+        HIPCHK(h, hipMalloc(&h->d_obs, t.obs.size() * sizeof(double)));
+        HIPCHK(h, hipMemcpy(h->d_obs, t.obs.data(), t.obs.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
+    h->lds_bytes = lds;
+    h->var = v;
+    return EMCMC_OK;
+}
+
 // chains per 256-thread block of mix_readjust_kernel<D> (R lanes per chain)
 int readjust_chains_per_block(int D) {
     int r = 1;
@@ -1086,6 +1181,13 @@ emcmc_status select_variant(emcmc_handle *h) {
     for (const auto &u : h->updates)
         if (u.kernel == EMCMC_RW_GAUSSIAN_MIX) return select_mwg(h);
     if (h->cfg.chain_moments) return select_mwg(h);
+    if (fused_prior_eligible(h)) {
+        const std::string keep = h->err;
+        const emcmc_status st = select_fused_prior(h);
+        if (st != EMCMC_UNSUPPORTED_PLUGIN) return st;
+        h->err = keep;
+        return select_mwg(h);
+    }
     if (!fused_eligible(h)) return select_mwg(h);
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
@@ -2295,6 +2397,44 @@ emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode,
                                                 target_options ? target_options : "", k);
     copy_log(log, log_out, log_len);
     return log.empty() ? EMCMC_OK : user ? EMCMC_INVALID_ARG : EMCMC_HIP_ERROR;
+}
+
+emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_chain, uint32_t history_mode,
+                                               uint32_t ll_mode, int unit_target, const emcmc_update_desc *update,
+                                               char *log_out, size_t log_len) {
+    copy_log("", log_out, log_len);
+    if (!update || dim == 0 || dim > (uint32_t)kMwgMaxD || history_mode > 1 || ll_mode > 1) return EMCMC_INVALID_ARG;
+    emcmc_handle tmp;  // no device: the update, the target's kind and diagonal flag are all selection reads
+    tmp.cfg.dim = dim;
+    tmp.cfg.lanes_per_chain = lanes_per_chain;
+    tmp.target.kind = EMCMC_TARGET_GSN;
+    tmp.target.diag = true;
+    UpdateHost uh;
+    if (emcmc_status st = build_update(&tmp, update, uh)) {
+        copy_log(tmp.err, log_out, log_len);
+        return st;
+    }
+    tmp.updates.push_back(std::move(uh));
+    if (!fused_prior_eligible(&tmp)) {
+        copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk over coords 0..dim-1 without positivity "
+                 "flags, a ProductPrior / StandardPrior that is one Product of dim univariates whose families "
+                 "repeat across the chain's lanes",
+                 log_out, log_len);
+        return EMCMC_INVALID_ARG;
+    }
+    std::string label, sname;
+    const std::string shape = rw_sched_source(tmp.updates, label, sname);
+    RtcKernel k;
+    for (int w : {2, 1}) {  // both occupancies select_fused_prior may try
+        const std::string log = rtc_compile_fused_prior((int)dim, fused_lpc(&tmp), w, history_mode == EMCMC_HIST_FULL,
+                                                        (int)ll_mode, unit_target != 0, shape, sname,
+                                                        label.substr(label.find(',') + 1), k);
+        if (!log.empty()) {
+            copy_log(log, log_out, log_len);
+            return EMCMC_HIP_ERROR;
+        }
+    }
+    return EMCMC_OK;
 }
 
 emcmc_status emcmc_set_state(emcmc_handle *h, const double *theta, const double *ll) {

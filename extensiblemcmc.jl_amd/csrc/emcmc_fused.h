@@ -40,9 +40,22 @@ struct SiblingPace {
     }
 };
 
+// The prior term of the fused step.  NoFusedPrior: ImproperPrior (the cfg 2 kernel, whose
+// ratio adds + 0.0 − 0.0).  A separable prior (emcmc_fprior.h FusedPrior, compiled at run
+// time) supplies kOn, its constants per coordinate (kConsts doubles per coordinate, staged in
+// LDS after the kernel's own), eval<D, LPC, DPL>(consts, d0, x) = logpdf(prior, θ) of the
+// chain (every lane of the chain gets the same double), the proposal! redraw cap and its
+// fault bit.
+struct NoFusedPrior {
+    static constexpr bool kOn = false;
+    static constexpr int kConsts = 0;
+};
+
 // MINW = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
-template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1>
+// PR: the prior term (NoFusedPrior for ImproperPrior; emcmc_fprior.h FusedPrior<S>, compiled at
+// run time for a separable prior's structure).
+template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1, class PR = NoFusedPrior>
 __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(const StepParams a) {
     static_assert(D % LPC == 0, "D must split evenly over the chain's lanes");
     constexpr int DPL = D / LPC;  // coordinates per lane
@@ -51,7 +64,8 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
 
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const uint32_t nobs = a.nobs;
-    const int nconst = 4 * D;
+    constexpr int kPrc = PR::kConsts;  // prior constants per coordinate, after the kernel's own 4
+    const int nconst = (4 + kPrc) * D;
     constexpr bool kPace = MINW == 2;
     constexpr int kWavesPerBlock = diag_block(MINW) / 64;
     __shared__ uint32_t pace_prog[kWavesPerBlock], pace_simd[kWavesPerBlock];
@@ -93,6 +107,10 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     }
     AcceptStream accs;
     const PhiloxVKeys vkeys = philox_vkeys(a.key0, a.key1);
+    // log_prior(::Previous) carried: logpdf(prior, θ) at the launch's start, then the accepted
+    // step's log_prior(::Proposal) (the same doubles)
+    double lpc = 0.0;
+    if constexpr (PR::kOn) lpc = PR::template eval<D, LPC, DPL>(cst0 + 4 * D, d0, th);
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
@@ -102,11 +120,27 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         const double *iLrw = cst + D;
         const double *iLt = cst + 2 * D;
         const double *xbar = cst + 3 * D;
-        const double *X = cst + 4 * D;
-        // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151)
+        const double *X = cst + (4 + kPrc) * D;
+        // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151); with a prior, drawn
+        // again while logpdf(prior, θ°) === −Inf (updates.jl:191-196), redraw r from normals
+        // (r << 17) | j
         double thp[DPL];
-        propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults,
-                                vkeys);
+        double lpp = 0.0;
+        if constexpr (PR::kOn) {
+            for (uint32_t rs = 0;; ++rs) {
+                propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (rs << 17) + (uint32_t)d0, th,
+                                        Lrw + d0, thp, faults, vkeys);
+                lpp = PR::template eval<D, LPC, DPL>(cst + 4 * D, d0, thp);
+                if (!(lpp == -__builtin_inf())) break;
+                if (rs >= PR::kCap) {
+                    faults |= PR::kFault;
+                    break;
+                }
+            }
+        } else {
+            propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults,
+                                    vkeys);
+        }
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
         const double ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
@@ -171,9 +205,10 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         }
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
         // ---- accept_reject! (run.jl:271-278), left-associative as written
-        const double llr = ((((llp - ll) + ltd) - ltd) + 0.0) - 0.0;
+        const double llr = ((((llp - ll) + ltd) - ltd) + lpp) - lpc;
         const double E = accs.next<true>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
         const bool acc = E > -llr;
+        if constexpr (PR::kOn) lpc = acc ? lpp : lpc;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
         if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)

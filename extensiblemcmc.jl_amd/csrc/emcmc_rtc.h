@@ -122,13 +122,21 @@ std::string rtc_compile_block(int D, bool full, int ll_mode, bool tdense, const 
                               const std::string &opts, const std::string &usrc, const std::string &uopts,
                               RtcKernel &out);
 
-// mwg_rw_block_kernel<D, FULL, LL, TGT, RwShape> (emcmc_rwblock.h): one UniformRandomWalk or
-// GaussianRandomWalk update over all 17 ≤ D ≤ 64 coordinates with any prior, positivity flags
-// and AdaptationUnifRW.  shape: the source of `namespace emcmc { struct <shape_struct> { … }; }`,
-// the update's compile-time structure (emcmc.hip rw_shape_source); shape_name: its label in the
-// kernel name; src / opts: a user law, else the built-in GsnTargetLaw (GsnSweep<tdense>).
+// mwg_rw_block_kernel<D, FULL, LL, TGT, RwSched> (emcmc_rwblock.h): a schedule of 1–8
+// UniformRandomWalk / GaussianRandomWalk updates over any coordinate subsets at 17 ≤ D ≤ 64 with
+// any prior, positivity flags and AdaptationUnifRW.  shape: the source of the schedule's
+// compile-time structure `struct <shape_struct>` with one U<p> per update (emcmc.hip
+// rw_sched_source); shape_name: its label in the kernel name; src / opts: a user law, else the
+// built-in GsnTargetLaw (GsnSweep<tdense>).
 std::string rtc_compile_rwblock(int D, bool full, int ll_mode, bool tdense, const std::string &shape,
                                 const std::string &shape_struct, const std::string &shape_name,
                                 const std::string &src, const std::string &opts, RtcKernel &out);
+
+// rwm_gsn_diag_kernel<D, LPC, FULL, LL, UNIT_T, MINW, FusedPrior<shape_struct>> (emcmc_fused.h,
+// emcmc_fprior.h): the fused diagonal step with a separable ProductPrior / StandardPrior of D
+// univariate factors (the schedule source's U<0> gives the families).
+std::string rtc_compile_fused_prior(int D, int lpc, int minw, bool full, int ll_mode, bool unit_t,
+                                   const std::string &shape, const std::string &shape_struct,
+                                   const std::string &shape_name, RtcKernel &out);
 
 }  // namespace emcmc

@@ -253,6 +253,8 @@ const std::vector<std::string> kBlockDeps = {"emcmc_tables.h", "emcmc_math.h", "
                                              "emcmc_block.h"};
 const std::vector<std::string> kRwBlockDeps = {"emcmc_tables.h", "emcmc_math.h",  "emcmc_kernels.h",
                                                "emcmc_mwg.h",    "emcmc_block.h", "emcmc_rwblock.h"};
+const std::vector<std::string> kFusedPriorDeps = {"emcmc_tables.h", "emcmc_math.h",  "emcmc_kernels.h",
+                                                  "emcmc_mwg.h",    "emcmc_fused.h", "emcmc_fprior.h"};
 
 std::string compile_kernel(const std::string &key, const std::string &prog_src, const char *file,
                            const std::string &ex, const std::string &name, const std::vector<std::string> &extra,
@@ -465,6 +467,25 @@ std::string rtc_compile_rwblock(int D, bool full, int ll_mode, bool tdense, cons
     for (std::string w; is >> w;) extra.push_back(w);
     return compile_kernel(key.str(), prog_src, user ? "user_target.hip" : "rw_block_kernel.hip", expr.str(),
                           name.str(), extra, out, kRwBlockDeps);
+}
+
+std::string rtc_compile_fused_prior(int D, int lpc, int minw, bool full, int ll_mode, bool unit_t,
+                                   const std::string &shape, const std::string &shape_struct,
+                                   const std::string &shape_name, RtcKernel &out) {
+    if (D < 1 || D > 64 || (lpc != 1 && lpc != 2 && lpc != 4) || D % lpc != 0 || (lpc > 1 && (D / lpc) % 8 != 0))
+        return "rwm_gsn_diag_kernel with a prior: D ≤ 64, 1, 2 or 4 lanes per chain over whole 8-blocks";
+    std::ostringstream key, expr, name;
+    key << "fprior|" << D << '|' << lpc << '|' << minw << '|' << full << '|' << ll_mode << '|' << unit_t << '|' << shape;
+    if (cache_get(key.str(), out)) return "";
+    expr << "emcmc::rwm_gsn_diag_kernel<" << D << ", " << lpc << ", " << (full ? "true" : "false") << ", " << ll_mode
+         << ", " << (unit_t ? "true" : "false") << ", " << minw << ", emcmc::FusedPrior<emcmc::" << shape_struct
+         << ">>";
+    name << "rwm_gsn_diag_kernel<D=" << D << ",LPC=" << lpc << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
+         << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << (unit_t ? ",UNIT_T" : "") << (minw == 2 ? ",MINW=2," : ",")
+         << shape_name << "[hiprtc]>";
+    const std::string prog_src = "#include \"emcmc_fprior.h\"\n" + shape;
+    return compile_kernel(key.str(), prog_src, "fused_prior_kernel.hip", expr.str(), name.str(),
+                          {"-ftemplate-depth=2048"}, out, kFusedPriorDeps);
 }
 
 const char *rtc_builtin_law(const char *name) {

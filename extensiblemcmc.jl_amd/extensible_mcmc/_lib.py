@@ -57,7 +57,8 @@ VARIANT_NO_XCD_ORDER = 16
 VARIANT_NO_RTC_CHOL = 32
 VARIANT_NO_MIX_CHOL = 64
 VARIANT_UNCAPPED = 128  # diag kernel without the 2-waves-per-SIMD register cap
-VARIANT_NO_BLOCK = 256  # one MALA / user update over all D > 16 coordinates: the wide kernel, not mwg_block_kernel
+VARIANT_NO_BLOCK = 256  # MALA / user updates over all D > 16 coordinates and random-walk schedules at D > 16: the wide kernel
+VARIANT_NO_FUSED_PRIOR = 512  # joint diagonal GaussianRandomWalk with a Product of univariates: not the fused kernel
 
 
 class EmcmcConfig(C.Structure):
@@ -287,6 +288,8 @@ SIGNATURES = {
     "emcmc_prebuild_rw_block_kernel": (
         _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_uint32, C.c_char_p, C.c_char_p,
               C.c_char_p, C.c_size_t]),
+    "emcmc_prebuild_fused_prior_kernel": (
+        _ST, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int, C.c_void_p, C.c_char_p, C.c_size_t]),
     "emcmc_probe_variates": (
         _ST,
         [C.c_int, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint64, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
@@ -454,6 +457,16 @@ def prebuild_rw_block_kernel(dim: int, update_descs, history_mode: int = 0, ll_m
         raise EMCMCError(st, "emcmc_prebuild_rw_block_kernel", buf.value.decode(errors="replace"))
 
 
+
+def prebuild_fused_prior_kernel(dim: int, update_desc, lanes_per_chain: int = 0, history_mode: int = 0,
+                                ll_mode: int = 0, unit_target: bool = True) -> None:
+    """Compile the fused diagonal step with the update's separable prior (rwm_gsn_diag_kernel +
+    FusedPrior) into the on-disk code-object cache (no device needed)."""
+    buf = C.create_string_buffer(1 << 16)
+    st = lib().emcmc_prebuild_fused_prior_kernel(dim, lanes_per_chain, history_mode, ll_mode, int(bool(unit_target)),
+                                                 C.cast(C.byref(update_desc), C.c_void_p), buf, len(buf))
+    if st != OK:
+        raise EMCMCError(st, "emcmc_prebuild_fused_prior_kernel", buf.value.decode(errors="replace"))
 def device_count() -> int:
     n = C.c_int(0)
     lib().emcmc_device_count(C.byref(n))

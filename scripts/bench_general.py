@@ -83,10 +83,12 @@ def main():
         mala_gsn(C, M, report, a.variant)
     if want("pcn_user_d32"):
         pcn_user(C, M, report, a.variant)
-    # (5) one random-walk update over all 32 coordinates with a prior / positivity flags
-    # (mwg_rw_block_kernel; the "_wide" twins run the same schedule on mwg_wide_kernel)
+    # (5) one random-walk update over all 32 coordinates with a prior / positivity flags: the
+    # fused diagonal kernel with the prior compiled in where the prior is a Product of univariates,
+    # else mwg_rw_block_kernel; the "_block" twins force the schedule kernel, "_wide" the wide one
     for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32"):
-        for suffix, variant in (("", a.variant), ("_wide", L.VARIANT_NO_BLOCK)):
+        for suffix, variant in (("", a.variant), ("_block", L.VARIANT_NO_FUSED_PRIOR),
+                                ("_wide", L.VARIANT_NO_BLOCK | L.VARIANT_NO_FUSED_PRIOR)):
             if want(name + suffix) or (not only and suffix == ""):
                 rw_prior(name, suffix, C, M, report, variant)
 
@@ -95,8 +97,8 @@ def main():
 WORKLOADS = ["mwg_d32_two_blocks", "mwg_d32_two_blocks_wide", "mwg_d64_two_blocks", "mwg_d64_two_blocks_wide",
              "dense_d32_joint", "dense_d32_joint_suffstat", "user_student_t_d4", "haario_dense_d32",
              "haario_dense_d32_general", "mala_gsn_d32", "pcn_user_d32", "rw_product_normal_d32",
-             "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32", "rw_standard_mvnormal_d32_wide",
-             "unif_pos_d32", "unif_pos_d32_wide"]
+             "rw_product_normal_d32_block", "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32",
+             "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_wide"]
 
 
 def run_isolated(names, a):

@@ -1,0 +1,68 @@
+"""The fused diagonal step with a separable prior, host side on CPU (no device):
+emcmc_prebuild_fused_prior_kernel compiles rwm_gsn_diag_kernel + FusedPrior (emcmc_fprior.h) for
+an update's prior into the on-disk cache — both occupancies select_fused_prior may take — and
+refuses the shapes the kernel does not serve (they run on the schedule kernels)."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc.engine import Engine
+
+N_, G_, U_, MV_, P_ = L.DIST_NORMAL, L.DIST_GAMMA, L.DIST_UNIFORM, L.DIST_MVNORMAL, L.DIST_PRODUCT
+
+
+@pytest.fixture
+def cache(tmp_path, monkeypatch):
+    d = tmp_path / "rtc"
+    monkeypatch.setenv("EMCMC_RTC_CACHE", str(d))
+    return d
+
+
+@pytest.mark.parametrize("D,lanes", [(32, 0), (16, 0), (24, 0), (32, 1)])
+def test_prebuild_compiles_both_occupancies(cache, D, lanes):
+    u, keep = Engine.gaussian_rw_desc(range(D), 0.01 * np.eye(D), prior=L.PRIOR_PRODUCT,
+                                      prior_factors=[(P_, D, [(N_, 0.0, 2.0), (G_, 3.0, 1.0)] * (D // 2))])
+    L.prebuild_fused_prior_kernel(D, u, lanes_per_chain=lanes)
+    assert len(list(cache.glob("*.co"))) == 2
+
+
+def test_standard_prior_of_a_product(cache):
+    D = 64
+    u, keep = Engine.gaussian_rw_desc(range(D), 0.01 * np.eye(D), prior=L.PRIOR_STANDARD,
+                                      prior_factors=[(P_, D, [(N_, 0.0, 2.0)] * D)])
+    L.prebuild_fused_prior_kernel(D, u, history_mode=L.HIST_ACCEPT_ONLY, ll_mode=L.LL_SUFFSTAT, unit_target=False)
+    assert len(list(cache.glob("*.co"))) == 2
+
+
+@pytest.mark.parametrize("case", ["mvnormal", "dims1", "asymmetric", "pos", "uniform_rw", "dense", "subset",
+                                  "improper"])
+def test_refuses_other_shapes(cache, case):
+    D = 32
+    coords, sigma = range(D), 0.01 * np.eye(D)
+    pri, fac, pos = L.PRIOR_PRODUCT, [(P_, D, [(N_, 0.0, 2.0)] * D)], None
+    if case == "mvnormal":
+        pri, fac = L.PRIOR_STANDARD, [(MV_, D, np.zeros(D), np.eye(D))]
+    elif case == "dims1":  # ProductPrior([Normal]*32, [1]*32): every factor reads θ[1] (priors.jl:64-79)
+        fac = [(N_, 1, 0.0, 2.0)] * D
+    elif case == "asymmetric":  # a Gamma on lane 0's coordinate 3 only (two lanes of 16)
+        comps = [(N_, 0.0, 2.0)] * D
+        comps[3] = (G_, 2.0, 1.0)
+        fac = [(P_, D, comps)]
+    elif case == "pos":
+        pos = [j % 2 for j in range(D)]
+    elif case == "dense":
+        sigma = 0.01 * (np.eye(D) + 0.1 * np.ones((D, D)))
+    elif case == "subset":
+        coords, sigma = range(8), 0.01 * np.eye(8)
+        fac = [(P_, 8, [(N_, 0.0, 2.0)] * 8)]
+    elif case == "improper":
+        pri, fac = L.PRIOR_IMPROPER, None
+    if case == "uniform_rw":
+        u, keep = Engine.uniform_rw_desc(coords, 0.1, prior=pri, prior_factors=fac)
+    else:
+        u, keep = Engine.gaussian_rw_desc(coords, sigma, pos=pos, prior=pri, prior_factors=fac)
+    with pytest.raises(L.EMCMCError) as e:
+        L.prebuild_fused_prior_kernel(D, u)
+    assert e.value.status == L.INVALID_ARG
+    assert "not a fused-prior shape" in str(e.value)
+    assert not list(cache.glob("*.co"))

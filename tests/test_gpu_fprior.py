@@ -1,0 +1,137 @@
+"""The fused diagonal step with a separable prior (rwm_gsn_diag_kernel + FusedPrior, emcmc_fused.h /
+emcmc_fprior.h): the joint GaussianRandomWalk with a diagonal Σ over coords 1:D on a diagonal
+GsnTargetLaw, with ProductPrior([Product(u_1 … u_D)]) or StandardPrior(Product(…))
+(priors.jl:18-88), the proposal! redraw loop (updates.jl:191-196) and the log-prior carry, the
+prior's left fold continued lane to lane across the chain's LPC lanes — against the oracle
+(orc_run_mwg kind 2, the restatement the schedule kernels are checked against), bit for bit:
+accept streams, θ / θ° / ll histories, rolling acceptance, fault bits.  EMCMC_VARIANT_NO_FUSED_PRIOR
+runs the same update on the schedule kernel with the same bits."""
+import numpy as np
+import pytest
+
+from extensible_mcmc import _lib as L
+from extensible_mcmc.engine import Engine, EngineConfig
+from test_gpu_mwg import check, full_steps
+from test_gpu_rwblock import problem, run_pair
+
+pytestmark = pytest.mark.gpu
+
+N_, U_, E_, G_, LN_ = L.DIST_NORMAL, L.DIST_UNIFORM, L.DIST_EXPONENTIAL, L.DIST_GAMMA, L.DIST_LOGNORMAL
+B_, IG_, C_, LA_, T_ = L.DIST_BETA, L.DIST_INVERSE_GAMMA, L.DIST_CAUCHY, L.DIST_LAPLACE, L.DIST_TDIST
+P_ = L.DIST_PRODUCT
+
+
+@pytest.fixture(autouse=True)
+def _gpu(require_gpu):
+    pass
+
+
+def s2(D, n=10, f=1.0):
+    return f * (2.38 / np.sqrt(D * n)) ** 2
+
+
+def assert_fused(eng, D, lpc):
+    name = eng.kernel_name()
+    assert name.startswith(f"rwm_gsn_diag_kernel<D={D},LPC={lpc},") and "Prior" in name, name
+
+
+def normals(D, sd=3.0):
+    return [(P_, D, [(N_, 0.0, sd)] * D)]
+
+
+@pytest.mark.parametrize("ll_mode", [L.LL_PER_OBS, L.LL_SUFFSTAT])
+@pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
+def test_d32_product_of_normals(oracle, ll_mode, hist):
+    """The VERDICT r5 shape (GaussianRandomWalk(σ²I) + ProductPrior of 32 Normals) at two lanes per
+    chain: each lane's 16 logpdfs, the fold continued from lane 0 to lane 1."""
+    D, C, M = 32, 2048, 120
+    seed, mu, ts, obs = problem(D)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_PRODUCT, factors=normals(D))]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), ll_mode=ll_mode,
+                                 hist=hist)
+    assert_fused(eng, D, 2)
+    check(oracle, eng, st, h, steps, ups, 1, full=(hist == L.HIST_FULL))
+
+
+FAMILIES = [(N_, 2.0, 1.0), (G_, 4.0, 0.5), (LN_, 0.6, 0.4), (U_, 1.75, 2.4), (E_, 0.5, 0.0), (B_, 3.0, 2.0),
+            (IG_, 3.0, 4.0), (C_, 2.0, 0.7), (LA_, 2.0, 0.5), (T_, 5.0, 0.0), (N_, 1.0, 0.2), (U_, 1.9, 2.2),
+            (G_, 2.0, 1.5), (LN_, 0.7, 0.1), (B_, 5.0, 1.5), (LA_, 1.8, 1.0)]
+
+
+def mixed_families(n, period=16):
+    """The first `period` of 16 families / parameters, repeated (the families must repeat across
+    the chain's lanes): supports that make proposal! redraw (Uniform, Beta, Gamma, LogNormal,
+    Exponential, InverseGamma near their edges) beside unbounded ones."""
+    return [FAMILIES[i % period] for i in range(n)]
+
+
+def mixed_start(n, period=16):
+    """θ inside every support: 2.0, the Beta coordinates at 0.5 / 0.8."""
+    th = np.full(n, 2.0)
+    for i in range(n):
+        if FAMILIES[i % period][0] == B_:
+            th[i] = 0.5 if (i % period) == 5 else 0.8
+    return th
+
+
+def test_d32_mixed_families_with_redraws(oracle):
+    """Ten families across the two lanes, several with bounded support around the chains: the
+    redraw loop runs (a chain whose θ° leaves a Uniform / Beta support draws again, r > 0
+    normals), the carry holds across launches of 13 steps."""
+    D, C, M = 32, 2048, 90
+    seed, mu, ts, obs = problem(D)
+    mu = mixed_start(D)
+    obs = mu + np.random.default_rng(3).normal(scale=0.3, size=(10, D))
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=4.0) * np.eye(D), prior=L.PRIOR_PRODUCT,
+                             factors=[(P_, D, mixed_families(D))])]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), spl=13)
+    assert_fused(eng, D, 2)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+@pytest.mark.parametrize("D,lpc", [(16, 2), (64, 4), (24, 1)])
+def test_lanes_per_chain(oracle, D, lpc):
+    """The fold over 1, 2 and 4 lanes (auto_lpc: D = 24 → 1, 16 → 2, 64 → 4), StandardPrior(Product)
+    at D = 64 (no 0.0 + in front of the fold), a non-unit diagonal Σ_t at D = 24."""
+    C, M = 1024, 60
+    seed, mu, ts, obs = problem(D)
+    prior = L.PRIOR_STANDARD if D == 64 else L.PRIOR_PRODUCT
+    if D == 24:
+        ts = np.diag(np.linspace(0.5, 2.0, D))
+    period = D // lpc if lpc > 1 else 16
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=prior,
+                             factors=[(P_, D, mixed_families(D, period) if D != 64 else [(N_, 0.0, 2.0)] * D)])]
+    if D != 64:
+        mu = mixed_start(D, period)
+        obs = mu + np.random.default_rng(4).normal(scale=0.3, size=(10, D))
+    th0 = np.tile(mu, (C, 1))
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    assert_fused(eng, D, lpc)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_forced_one_lane_per_chain_and_the_schedule_kernel_agree():
+    """lanes_per_chain = 1 at D = 32 (the whole fold on one lane) and EMCMC_VARIANT_NO_FUSED_PRIOR
+    (mwg_rw_block_kernel) give the default kernel's bits over every chain."""
+    D, C, M = 32, 4096, 50
+    seed, mu, ts, obs = problem(D)
+    out = []
+    for lanes, variant in ((0, 0), (1, 0), (0, L.VARIANT_NO_FUSED_PRIOR)):
+        eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, lanes_per_chain=lanes,
+                                  kernel_variant=variant))
+        eng.add_gaussian_rw_update(np.arange(D), s2(D) * np.eye(D), prior=L.PRIOR_PRODUCT,
+                                   prior_factors=normals(D, 1.5))
+        eng.set_gsn_target(mu, ts, obs)
+        eng.set_state(np.tile(mu, (C, 1)))
+        eng.run(full_steps(M, 1))
+        eng.synchronize(allow_faults=True)
+        out.append((eng.kernel_name(), eng.get_state(), eng.get_history(L.H_ACCEPT, 1, M),
+                    eng.get_history(L.H_PROPOSAL, 1, M)))
+        eng.close()
+    assert out[0][0].startswith("rwm_gsn_diag_kernel<D=32,LPC=2")
+    assert out[1][0].startswith("rwm_gsn_diag_kernel<D=32,LPC=1")
+    assert out[2][0].startswith("mwg_rw_block_kernel<D=32")
+    for o in out[1:]:
+        for x, y in zip(out[0][1], o[1]):
+            assert np.array_equal(x, y)
+        assert np.array_equal(out[0][2], o[2]) and np.array_equal(out[0][3], o[3])

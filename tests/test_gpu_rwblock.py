@@ -59,9 +59,9 @@ def engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIS
 
 
 def run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, theta0, steps=None, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL,
-             spl=0, user=None, calls=None):
+             spl=0, user=None, calls=None, variant=0):
     steps = steps or full_steps(M, 1)
-    eng = engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode, hist, spl, theta0=theta0,
+    eng = engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode, hist, spl, variant=variant, theta0=theta0,
                      user=None if user is None else user[1])
     for a, b in (calls or [(0, len(steps))]):
         eng.run(steps[a:b])
@@ -83,13 +83,16 @@ def s2(D, n=10, f=1.0):
 @pytest.mark.parametrize("hist", [L.HIST_FULL, L.HIST_ACCEPT_ONLY])
 def test_d32_gaussian_rw_product_prior_normal(oracle, ll_mode, hist):
     """VERDICT shape 1: D = 32 joint GaussianRandomWalk + ProductPrior of Normal factors
-    (one Product of 32 Normals: the logpdf folded left over the components)."""
+    (one Product of 32 Normals: the logpdf folded left over the components), on the schedule
+    kernel (EMCMC_VARIANT_NO_FUSED_PRIOR: by default the fused kernel takes it,
+    tests/test_gpu_fprior.py)."""
     D, C, M = 32, 2048, 160
     seed, mu, ts, obs = problem(D)
     ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_PRODUCT,
                              factors=[(P_, D, [(N_, 0.1 * j, 1.0 + 0.05 * j) for j in range(D)])])]
     th0 = np.tile(mu, (C, 1))
-    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, ll_mode=ll_mode, hist=hist)
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, ll_mode=ll_mode, hist=hist,
+                                 variant=L.VARIANT_NO_FUSED_PRIOR)
     assert_block(eng, D)
     check(oracle, eng, st, h, steps, ups, 1, full=(hist == L.HIST_FULL))
     assert 0.1 < h["acc"].mean() < 0.6
@@ -184,10 +187,12 @@ def test_gaussian_rw_with_pos_round_trips(oracle, D):
     check(oracle, eng, st, h, steps, ups, 1)
 
 
-def test_schedule_gap_and_launch_cuts(oracle):
+@pytest.mark.parametrize("variant", [L.VARIANT_NO_FUSED_PRIOR, 0])
+def test_schedule_gap_and_launch_cuts(oracle, variant):
     """The update excluded on iterations 31:50 (rolling_ar restarts from 0.0) and launches
     of 9 steps across three run calls: the log-prior is re-evaluated at each launch's
-    first step and carried inside it."""
+    first step and carried inside it — on the schedule kernel and on the fused kernel with the
+    prior compiled in (variant 0: a Product of Cauchy factors is its shape)."""
     D, C, M = 32, 1024, 110
     seed, mu, ts, obs = problem(D)
     ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_PRODUCT,
@@ -195,8 +200,11 @@ def test_schedule_gap_and_launch_cuts(oracle):
     steps = [(s.mcmciter, s.pidx) for s in MCMCSchedule(M, 1, [(1, range(31, 51))])]
     th0 = np.tile(mu, (C, 1))
     eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, steps=steps, spl=9,
-                                 calls=[(0, 25), (25, 26), (26, len(steps))])
-    assert_block(eng, D)
+                                 calls=[(0, 25), (25, 26), (26, len(steps))], variant=variant)
+    if variant:
+        assert_block(eng, D)
+    else:
+        assert eng.kernel_name().startswith("rwm_gsn_diag_kernel<D=32,LPC=2"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
 
 

@@ -916,10 +916,13 @@ bool fused_eligible(const emcmc_handle *h) {
     return u.kernel == EMCMC_RW_GAUSSIAN && u.adaptation == EMCMC_ADPT_NONE;
 }
 
-// The fused diagonal step with a separable prior (emcmc_fprior.h): the joint GaussianRandomWalk
-// with a diagonal Σ and no positivity flags on a diagonal GsnTargetLaw, with ONE ProductPrior /
-// StandardPrior factor that is a Product of D univariates (no "reads θ[1]" factor, no MvNormal)
-// whose families repeat across the chain's lanes (family of coordinate i = that of i mod D/LPC).
+// The fused diagonal step with the update's separable terms compiled in (emcmc_fprior.h
+// FusedUpdate): ONE update over coords 0..D−1 in order on a diagonal GsnTargetLaw —
+// GaussianRandomWalk with a diagonal Σ and no positivity flags, or UniformRandomWalk (positivity
+// flags allowed), no adaptation — whose prior is ImproperPrior (UniformRandomWalk; the Gaussian
+// one is the plain fused kernel), ImproperPosPrior, or ONE ProductPrior / StandardPrior factor that
+// is a Product of D univariates (no "reads θ[1]" dims-1 factor, no MvNormal); the families and
+// positivity flags repeat across the chain's lanes (those of coordinate i = those of i mod D/LPC).
 int fused_lpc(const emcmc_handle *h) {
     return h->cfg.lanes_per_chain ? (int)h->cfg.lanes_per_chain : auto_lpc((int)h->cfg.dim);
 }
@@ -928,17 +931,25 @@ bool fused_prior_eligible(const emcmc_handle *h) {
         return false;
     const UpdateHost &u = h->updates[0];
     const int D = (int)h->cfg.dim;
-    if (u.kernel != EMCMC_RW_GAUSSIAN || u.adaptation != EMCMC_ADPT_NONE || !u.diag || !h->target.diag ||
-        h->target.kind != EMCMC_TARGET_GSN || D > 64)
+    const bool uni = u.kernel == EMCMC_RW_UNIFORM;
+    if ((u.kernel != EMCMC_RW_GAUSSIAN && !uni) || u.adaptation != EMCMC_ADPT_NONE || !h->target.diag ||
+        h->target.kind != EMCMC_TARGET_GSN || D > 64 || (!uni && !u.diag))
         return false;
-    for (uint8_t f : u.pos)
-        if (f) return false;
-    if (u.prior != EMCMC_PRIOR_PRODUCT && u.prior != EMCMC_PRIOR_STANDARD) return false;
-    if (u.nslot != (uint32_t)D || u.pmvn || u.psrc0 || u.pstart != 1ull || u.pend != (1ull << (D - 1))) return false;
+    bool anypos = false;
+    for (uint8_t f : u.pos) anypos = anypos || f;
+    if (!uni && anypos) return false;  // GaussianRandomWalk's positivity round trips: the schedule kernels
+    const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
+    if (u.prior == EMCMC_PRIOR_IMPROPER ? !uni : (!slots && u.prior != EMCMC_PRIOR_IMPROPER_POS)) return false;
+    if (slots && (u.nslot != (uint32_t)D || u.pmvn || u.psrc0 || u.pstart != 1ull || u.pend != (1ull << (D - 1))))
+        return false;
     const int lpc = fused_lpc(h);
     if ((lpc != 1 && lpc != 2 && lpc != 4) || D % lpc || (lpc > 1 && (D / lpc) % 8)) return false;
-    for (int i = 0; i < D; ++i)
-        if (u.pfam[i] != u.pfam[i % (D / lpc)]) return false;
+    const int dpl = D / lpc;
+    for (int i = 0; i < D; ++i) {
+        if (slots && u.pfam[i] != u.pfam[i % dpl]) return false;
+        const bool pi = i < (int)u.pos.size() && u.pos[i], pj = (i % dpl) < (int)u.pos.size() && u.pos[i % dpl];
+        if (pi != pj) return false;
+    }
     return true;
 }
 
@@ -953,8 +964,11 @@ emcmc_status select_fused_prior(emcmc_handle *h) {
     const int lpc = fused_lpc(h);
     bool unit = true;
     for (int i = 0; i < D; ++i) unit = unit && t.invdiag[i] == 1.0;
+    const bool uni = u.kernel == EMCMC_RW_UNIFORM;
+    const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
+    const size_t nconst = (slots ? 7 : 4) * (size_t)D;  // FusedUpdate::kConsts = 3 with slots
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
-    const size_t lds = lds_align16((7 * (size_t)D + obs_doubles) * sizeof(double));
+    const size_t lds = lds_align16((nconst + obs_doubles) * sizeof(double));
     if (kZigLdsBytes + lds > kMaxLds) return EMCMC_UNSUPPORTED_PLUGIN;  // the schedule kernel reads them from HBM
     std::string label, sname;
     const std::string shape = rw_sched_source(h->updates, label, sname);
@@ -965,7 +979,7 @@ emcmc_status select_fused_prior(emcmc_handle *h) {
     for (int w : {2, 1}) {
         RtcKernel k;
         const std::string log = rtc_compile_fused_prior(D, lpc, w, full, ll, unit, shape, sname,
-                                                        label.substr(label.find(',') + 1), k);
+                                                        uni ? label : label.substr(label.find(',') + 1), k);
         if (!log.empty()) return fail(h, EMCMC_HIP_ERROR, "run-time kernel build failed:\n%s", log.c_str());
         if (emcmc_status st = load_rtc_module(h, k)) return st;
         HIPCHK(h, hipModuleGetFunction(&v.ffn, h->umod, k.lowered.c_str()));
@@ -986,16 +1000,19 @@ emcmc_status select_fused_prior(emcmc_handle *h) {
     v.dense = 0;
     v.occ = minw;
     v.unit = unit;
-    // the diag kernel's constants (L_ii, 1/L_ii, 1/L_t,ii, x̄), then the prior's a, b, c per coordinate
-    std::vector<double> c(7 * (size_t)D);
+    // the diag kernel's constants (L_ii, 1/L_ii — UniformRandomWalk: ϵ_i, −log 2ϵ_i with the device's
+    // log — 1/L_t,ii, x̄), then the prior's a, b, c per coordinate
+    std::vector<double> c(nconst);
     for (int i = 0; i < D; ++i) {
-        c[i] = u.L[(size_t)i * D + i];
-        c[D + i] = u.invdiag[i];
+        c[i] = uni ? u.eps[i] : u.L[(size_t)i * D + i];
+        c[D + i] = uni ? -log_any(2.0 * u.eps[i]) : u.invdiag[i];
         c[2 * D + i] = t.invdiag[i];
         c[3 * D + i] = t.xbar[i];
-        c[4 * D + i] = u.pa[i];
-        c[5 * D + i] = u.pb[i];
-        c[6 * D + i] = u.pc[i];
+        if (slots) {
+            c[4 * D + i] = u.pa[i];
+            c[5 * D + i] = u.pb[i];
+            c[6 * D + i] = u.pc[i];
+        }
     }
     if (h->d_consts) (void)hipFree(h->d_consts);
     HIPCHK(h, hipMalloc(&h->d_consts, c.size() * sizeof(double)));
@@ -2416,19 +2433,21 @@ emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_
     }
     tmp.updates.push_back(std::move(uh));
     if (!fused_prior_eligible(&tmp)) {
-        copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk over coords 0..dim-1 without positivity "
-                 "flags, a ProductPrior / StandardPrior that is one Product of dim univariates whose families "
-                 "repeat across the chain's lanes",
+        copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk (no positivity flags) or UniformRandomWalk "
+                 "over coords 0..dim-1 without adaptation, with ImproperPosPrior or a ProductPrior / StandardPrior "
+                 "that is one Product of dim univariates (UniformRandomWalk: ImproperPrior too), families and "
+                 "positivity flags repeating across the chain's lanes",
                  log_out, log_len);
         return EMCMC_INVALID_ARG;
     }
     std::string label, sname;
     const std::string shape = rw_sched_source(tmp.updates, label, sname);
     RtcKernel k;
+    const bool uni = tmp.updates[0].kernel == EMCMC_RW_UNIFORM;
     for (int w : {2, 1}) {  // both occupancies select_fused_prior may try
         const std::string log = rtc_compile_fused_prior((int)dim, fused_lpc(&tmp), w, history_mode == EMCMC_HIST_FULL,
                                                         (int)ll_mode, unit_target != 0, shape, sname,
-                                                        label.substr(label.find(',') + 1), k);
+                                                        uni ? label : label.substr(label.find(',') + 1), k);
         if (!log.empty()) {
             copy_log(log, log_out, log_len);
             return EMCMC_HIP_ERROR;

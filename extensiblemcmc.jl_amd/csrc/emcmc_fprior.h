@@ -1,20 +1,24 @@
-// emcmc_fprior.h — a separable prior on the fused diagonal step kernel (gfx950).
+// emcmc_fprior.h — separable random-walk updates on the fused diagonal step kernel (gfx950).
 //
 // rwm_gsn_diag_kernel (emcmc_fused.h) runs the joint GaussianRandomWalk with a diagonal Σ on a
 // diagonal GsnTargetLaw with LPC lanes per chain and two waves per SIMD: the cfg 2 kernel.  With
-// ImproperPrior its ratio adds + 0.0 − 0.0.  FusedPrior<S> gives it the log-prior of one
-// ProductPrior([Product(u_1 … u_D)]) or StandardPrior(Product(u_1 … u_D)) over coords 1:D
-// (priors.jl:18-88) — D univariate factors, lane-symmetric families (the family of coordinate i
-// equals that of i + k·D/LPC, so every lane of a chain runs the same code on its own
-// coordinates) — compiled at run time for the families (hiprtc, emcmc_rtc.hip), its parameters
-// per coordinate in LDS after the kernel's own constants.
+// ImproperPrior its ratio adds + 0.0 − 0.0.  FusedUpdate<S> widens it to the joint updates over
+// coords 1:D whose every term separates over coordinates:
+//   - the proposal: GaussianRandomWalk with a diagonal Σ (no positivity flags), or
+//     UniformRandomWalk(ϵ) with positivity flags (random_walk.jl:45-94: θ° = θ·e^U + copysign(0, U)
+//     where pos, θ + U elsewhere; logpdf terms −log 2ϵ_j − log θ°_j folded left over j);
+//   - the prior: ImproperPrior, ImproperPosPrior (−Σ log θ_j), or ONE ProductPrior /
+//     StandardPrior factor that is a Product of D univariates (priors.jl:18-88);
+// compiled at run time for the structure (hiprtc, emcmc_rtc.hip) from the schedule struct S of
+// mwg_rw_block_kernel (S::U<0>: kind, pos mask, families).  The families and pos flags repeat
+// across the chain's lanes (those of coordinate i are those of i mod D/LPC), so every lane of a
+// chain runs the same code on its own coordinates; ϵ, −log 2ϵ and the prior's parameters per
+// coordinate sit in LDS with the kernel's constants.
 //
-// logpdf(prior, θ) = 0.0 + (((v_1 + v_2) + v_3) + … + v_D) (ProductPrior; StandardPrior without
-// the 0.0 +), v_i the component's logpdf (univariate_logpdf, the oracle's and the schedule
-// kernels' formulas).  Each lane forms the v_i of its D/LPC coordinates at once; the left fold
-// runs segment by segment, each lane continuing from the previous lane's partial sum (a DPP
-// move), and the last lane's total is broadcast to the chain's lanes: the same additions in the
-// same order as one lane folding all D.
+// Every left fold over the D coordinates (the prior, the two transition-density sums) runs
+// segment by segment: lane 0 folds its coordinates, lane k continues from lane k−1's partial sum
+// (a DPP move), the last lane's total is broadcast to the chain's lanes — the same additions in
+// the same order as one lane folding all D (the oracle's orc_run_mwg and rw_step's order).
 #pragma once
 
 #include "emcmc_fused.h"
@@ -23,13 +27,15 @@
 namespace emcmc {
 
 template <class S>
-struct FusedPrior {
+struct FusedUpdate {
     using U = typename S::template U<0>;
-    static constexpr bool kOn = true;
-    static constexpr int kConsts = 3;  // a, b, c of univariate_logpdf, [3][D] in LDS
-    static constexpr uint32_t kCap = kMaxResampleGsn;
+    static constexpr bool kUniform = U::kind == 1u;  // else GaussianRandomWalk
+    static constexpr bool kOn = U::prior != kPriorImproper;  // a prior term (and proposal! redraws)
+    static constexpr bool kSlots = U::prior == kPriorProduct || U::prior == kPriorStandard;
+    static constexpr int kConsts = kSlots ? 3 : 0;  // a, b, c of univariate_logpdf, [3][D] in LDS
+    static constexpr uint32_t kCap = kUniform ? kMaxResample : kMaxResampleGsn;
     static constexpr uint32_t kFault = kFaultPriorResample;
-    static_assert(U::prior == kPriorProduct || U::prior == kPriorStandard, "ProductPrior or StandardPrior");
+    static constexpr bool kPos = kUniform && U::pos != 0ull;
 
     // lane k of an LPC group takes lane k−1's value (quad_perm [0,0,2,2] / [0,0,1,2])
     template <int LPC>
@@ -44,10 +50,31 @@ struct FusedPrior {
         else return dpp_perm<0xFF>(v);
     }
 
+    // (((v_1 + v_2) + v_3) + … + v_D) over the chain's D values, DPL per lane
+    template <int LPC, int DPL>
+    __device__ __forceinline__ static double fold(const double (&v)[DPL]) {
+        static_assert(LPC == 1 || LPC == 2 || LPC == 4, "lanes per chain: 1, 2 or 4 (one quad)");
+        double s = 0.0, carry = 0.0;
+        static_for<0, LPC>([&](auto KC) {
+            constexpr int k = decltype(KC)::value;  // the lane whose segment this pass folds
+            s = (k == 0) ? v[0] : carry + v[0];
+#pragma unroll
+            for (int i = 1; i < DPL; ++i) s = s + v[i];
+            if constexpr (k + 1 < LPC) carry = from_previous_lane<LPC>(s);
+        });
+        if constexpr (LPC > 1) s = from_last_lane<LPC>(s);
+        return s;
+    }
+
+    // logpdf(prior, x) of the chain (every lane gets the same double)
     template <int D, int LPC, int DPL>
     __device__ __forceinline__ static double eval(const double *pc, int d0, const double (&x)[DPL]) {
-        static_assert(LPC == 1 || LPC == 2 || LPC == 4, "lanes per chain: 1, 2 or 4 (one quad)");
-        if constexpr (LPC == 1) {  // one lane folds as it goes: no vector of logpdfs stays live
+        if constexpr (U::prior == kPriorImproperPos) {  // −sum(log.(θ))
+            double v[DPL];
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) v[i] = log_real(x[i]);
+            return -fold<LPC, DPL>(v);
+        } else if constexpr (LPC == 1) {  // one lane folds as it goes: no vector of logpdfs stays live
             double s = 0.0;
             static_for<0, DPL>([&](auto IC) {
                 constexpr int i = decltype(IC)::value;
@@ -61,17 +88,56 @@ struct FusedPrior {
                 constexpr int i = decltype(IC)::value;
                 v[i] = univariate_logpdf(U::fam[i], pc[d0 + i], pc[D + d0 + i], pc[2 * D + d0 + i], x[i]);
             });
-            double s = 0.0, carry = 0.0;
-            static_for<0, LPC>([&](auto KC) {
-                constexpr int k = decltype(KC)::value;  // the lane whose segment this pass folds
-                s = (k == 0) ? v[0] : carry + v[0];
-#pragma unroll
-                for (int i = 1; i < DPL; ++i) s = s + v[i];
-                if constexpr (k + 1 < LPC) carry = from_previous_lane<LPC>(s);
-            });
-            s = from_last_lane<LPC>(s);
+            const double s = fold<LPC, DPL>(v);
             return (U::prior == kPriorProduct) ? 0.0 + s : s;
         }
+    }
+
+    // The reverse sum logpdf(rw, θ°, θ) = fold of −log 2ϵ_j − log θ_j depends on θ alone, so the
+    // kernel carries it: rev_terms(θ) at the launch's start, then the accepted step's forward sum
+    // (the same operations on the same doubles: θ_next = θ°).
+    template <int D, int LPC, int DPL>
+    __device__ __forceinline__ static double rev_terms(int d0, const double *uc, const double (&th)[DPL]) {
+        double g[DPL];
+        static_for<0, DPL>([&](auto QC) {
+            constexpr int q = decltype(QC)::value;
+            if constexpr (((U::pos >> q) & 1ull) != 0ull) g[q] = uc[d0 + q] - log_any(th[q]);
+            else g[q] = 0.0;
+        });
+        return fold<LPC, DPL>(g);
+    }
+
+    // UniformRandomWalk's proposal draw rs (random_walk.jl:63-80) for this lane's coordinates
+    // d0 … d0+DPL−1: θ° and, with positivity flags, logpdf(rw, θ, θ°) (random_walk.jl:81-94; 0.0
+    // for the coordinates without the flag, 0.0 without any).  eps / uc: ϵ_j and −log(2ϵ_j) per
+    // coordinate (LDS).
+    template <int D, int LPC, int DPL>
+    __device__ __forceinline__ static void propose_uniform(const PhiloxVKeys &vk, uint32_t gid, uint32_t iter,
+                                                           uint32_t pidx0, uint32_t rs, int d0, const double *eps,
+                                                           const double *uc, const double (&th)[DPL],
+                                                           double (&tp)[DPL], double &ltd_fwd) {
+        double f[DPL];
+        static_for<0, DPL / 2>([&](auto PC) {
+            constexpr int j = 2 * decltype(PC)::value;
+            sbar();  // one Philox block at a time
+            const u32x4 r = draw_vk(vk, gid, iter, (rs << 16) | ((uint32_t)(d0 + j) >> 1), pidx0);
+            auto one = [&](auto QC, uint32_t hi, uint32_t lo) {
+                constexpr int q = decltype(QC)::value;
+                const double e = eps[d0 + q];
+                const double Uq = (-e) + (e - (-e)) * u01_closed0(hi, lo);
+                if constexpr (((U::pos >> q) & 1ull) != 0ull) {
+                    tp[q] = th[q] * exp_any(Uq) + copysign(0.0, Uq);
+                    f[q] = uc[d0 + q] - log_any(tp[q]);
+                } else {
+                    tp[q] = th[q] * 1.0 + Uq;
+                    f[q] = 0.0;
+                }
+            };
+            one(IntC<j>{}, r.x, r.y);
+            one(IntC<j + 1>{}, r.z, r.w);
+        });
+        if constexpr (kPos) ltd_fwd = fold<LPC, DPL>(f);
+        else ltd_fwd = 0.0;
     }
 };
 

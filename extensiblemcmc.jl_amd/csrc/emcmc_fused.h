@@ -40,21 +40,23 @@ struct SiblingPace {
     }
 };
 
-// The prior term of the fused step.  NoFusedPrior: ImproperPrior (the cfg 2 kernel, whose
-// ratio adds + 0.0 − 0.0).  A separable prior (emcmc_fprior.h FusedPrior, compiled at run
-// time) supplies kOn, its constants per coordinate (kConsts doubles per coordinate, staged in
-// LDS after the kernel's own), eval<D, LPC, DPL>(consts, d0, x) = logpdf(prior, θ) of the
-// chain (every lane of the chain gets the same double), the proposal! redraw cap and its
-// fault bit.
+// The update's separable terms in the fused step.  NoFusedPrior: GaussianRandomWalk with
+// ImproperPrior (the cfg 2 kernel, whose ratio adds + 0.0 − 0.0).  emcmc_fprior.h FusedUpdate<S>
+// (compiled at run time) supplies kOn (a prior term), kUniform (UniformRandomWalk's proposal and
+// transition densities, propose_uniform), the prior's constants per coordinate (kConsts doubles
+// per coordinate, staged in LDS after the kernel's own), eval<D, LPC, DPL>(consts, d0, x) =
+// logpdf(prior, θ) of the chain (every lane of the chain gets the same double), the proposal!
+// redraw cap and its fault bit.
 struct NoFusedPrior {
     static constexpr bool kOn = false;
+    static constexpr bool kUniform = false;
     static constexpr int kConsts = 0;
 };
 
 // MINW = minimum waves per SIMD the register allocation must allow
 // (__launch_bounds__ second argument; 4 ⇒ ≤ 128 VGPRs).
-// PR: the prior term (NoFusedPrior for ImproperPrior; emcmc_fprior.h FusedPrior<S>, compiled at
-// run time for a separable prior's structure).
+// PR: the update's separable terms (NoFusedPrior: GaussianRandomWalk, ImproperPrior; emcmc_fprior.h
+// FusedUpdate<S>, compiled at run time for the structure).
 template <int D, int LPC, bool FULL, int LLMODE, bool UNIT_T, int MINW = 1, class PR = NoFusedPrior>
 __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(const StepParams a) {
     static_assert(D % LPC == 0, "D must split evenly over the chain's lanes");
@@ -111,6 +113,10 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     // step's log_prior(::Proposal) (the same doubles)
     double lpc = 0.0;
     if constexpr (PR::kOn) lpc = PR::template eval<D, LPC, DPL>(cst0 + 4 * D, d0, th);
+    // UniformRandomWalk with positivity flags: logpdf(rw, θ°, θ) carried the same way
+    double ltd_rev_c = 0.0;
+    if constexpr (PR::kUniform)
+        if constexpr (PR::kPos) ltd_rev_c = PR::template rev_terms<D, LPC, DPL>(d0, cst0 + D, th);
 
     for (uint32_t s = 0; s < a.nsteps; ++s) {
         const uint32_t iter = a.iter0 + s;  // consecutive (host splits gaps)
@@ -124,12 +130,21 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         // ---- proposal!: θ° = θ + L z, z ~ N(0, I) (random_walk.jl:145-151); with a prior, drawn
         // again while logpdf(prior, θ°) === −Inf (updates.jl:191-196), redraw r from normals
         // (r << 17) | j
+        // (UniformRandomWalk, PR::kUniform: θ° from ϵ and the positivity flags, emcmc_fprior.h, with the
+        // two transition-density sums formed as θ° is; the Lrw / iLrw slots hold ϵ and −log 2ϵ)
         double thp[DPL];
-        double lpp = 0.0;
-        if constexpr (PR::kOn) {
-            for (uint32_t rs = 0;; ++rs) {
+        double lpp = 0.0, ltd_fwd = 0.0;
+        auto propose = [&](uint32_t rs) {
+            if constexpr (PR::kUniform)
+                PR::template propose_uniform<D, LPC, DPL>(vkeys, gid, iter, a.pidx0, rs, d0, Lrw, iLrw, th, thp,
+                                                          ltd_fwd);
+            else
                 propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (rs << 17) + (uint32_t)d0, th,
                                         Lrw + d0, thp, faults, vkeys);
+        };
+        if constexpr (PR::kOn) {
+            for (uint32_t rs = 0;; ++rs) {
+                propose(rs);
                 lpp = PR::template eval<D, LPC, DPL>(cst + 4 * D, d0, thp);
                 if (!(lpp == -__builtin_inf())) break;
                 if (rs >= PR::kCap) {
@@ -137,14 +152,18 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
                     break;
                 }
             }
+        } else if constexpr (PR::kUniform) {
+            propose(0u);
         } else {
             propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults,
                                     vkeys);
         }
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
-        const double ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
-                               a.rw_c0);  // = c0 − q/2 (q/2 exact)
+        double ltd = 0.0;
+        if constexpr (!PR::kUniform)
+            ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
+                      a.rw_c0);  // = c0 − q/2 (q/2 exact)
         // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
         double llp;
         if constexpr (LLMODE == LL_PER_OBS) {
@@ -205,10 +224,13 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         }
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
         // ---- accept_reject! (run.jl:271-278), left-associative as written
-        const double llr = ((((llp - ll) + ltd) - ltd) + lpp) - lpc;
+        double llr;
+        if constexpr (PR::kUniform) llr = ((((llp - ll) + ltd_rev_c) - ltd_fwd) + lpp) - lpc;
+        else llr = ((((llp - ll) + ltd) - ltd) + lpp) - lpc;
         const double E = accs.next<true>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
         const bool acc = E > -llr;
         if constexpr (PR::kOn) lpc = acc ? lpp : lpc;
+        if constexpr (PR::kUniform) ltd_rev_c = acc ? ltd_fwd : ltd_rev_c;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
         if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)

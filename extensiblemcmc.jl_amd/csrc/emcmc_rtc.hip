@@ -478,7 +478,7 @@ std::string rtc_compile_fused_prior(int D, int lpc, int minw, bool full, int ll_
     key << "fprior|" << D << '|' << lpc << '|' << minw << '|' << full << '|' << ll_mode << '|' << unit_t << '|' << shape;
     if (cache_get(key.str(), out)) return "";
     expr << "emcmc::rwm_gsn_diag_kernel<" << D << ", " << lpc << ", " << (full ? "true" : "false") << ", " << ll_mode
-         << ", " << (unit_t ? "true" : "false") << ", " << minw << ", emcmc::FusedPrior<emcmc::" << shape_struct
+         << ", " << (unit_t ? "true" : "false") << ", " << minw << ", emcmc::FusedUpdate<emcmc::" << shape_struct
          << ">>";
     name << "rwm_gsn_diag_kernel<D=" << D << ",LPC=" << lpc << "," << (full ? "FULL" : "ACCEPT_ONLY") << ","
          << (ll_mode == 0 ? "PER_OBS" : "SUFFSTAT") << (unit_t ? ",UNIT_T" : "") << (minw == 2 ? ",MINW=2," : ",")

@@ -98,7 +98,7 @@ WORKLOADS = ["mwg_d32_two_blocks", "mwg_d32_two_blocks_wide", "mwg_d64_two_block
              "dense_d32_joint", "dense_d32_joint_suffstat", "user_student_t_d4", "haario_dense_d32",
              "haario_dense_d32_general", "mala_gsn_d32", "pcn_user_d32", "rw_product_normal_d32",
              "rw_product_normal_d32_block", "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32",
-             "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_wide"]
+             "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_block", "unif_pos_d32_wide"]
 
 
 def run_isolated(names, a):

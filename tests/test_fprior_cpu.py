@@ -34,8 +34,19 @@ def test_standard_prior_of_a_product(cache):
     assert len(list(cache.glob("*.co"))) == 2
 
 
-@pytest.mark.parametrize("case", ["mvnormal", "dims1", "asymmetric", "pos", "uniform_rw", "dense", "subset",
-                                  "improper"])
+@pytest.mark.parametrize("pos,prior", [([1] * 32, L.PRIOR_IMPROPER), ([j % 4 != 3 for j in range(32)],
+                                                                      L.PRIOR_IMPROPER_POS), (None, L.PRIOR_PRODUCT)])
+def test_uniform_random_walks(cache, pos, prior):
+    D = 32
+    fac = [(P_, D, [(G_, 2.0, 1.0)] * D)] if prior == L.PRIOR_PRODUCT else None
+    u, keep = Engine.uniform_rw_desc(range(D), [0.05 + 0.001 * j for j in range(D)], pos=pos, prior=prior,
+                                     prior_factors=fac)
+    L.prebuild_fused_prior_kernel(D, u)
+    assert len(list(cache.glob("*.co"))) == 2
+
+
+@pytest.mark.parametrize("case", ["mvnormal", "dims1", "asymmetric", "pos", "uniform_asym_pos", "adaptive", "dense",
+                                  "subset", "improper"])
 def test_refuses_other_shapes(cache, case):
     D = 32
     coords, sigma = range(D), 0.01 * np.eye(D)
@@ -48,8 +59,10 @@ def test_refuses_other_shapes(cache, case):
         comps = [(N_, 0.0, 2.0)] * D
         comps[3] = (G_, 2.0, 1.0)
         fac = [(P_, D, comps)]
-    elif case == "pos":
+    elif case == "pos":  # GaussianRandomWalk's positivity round trips
         pos = [j % 2 for j in range(D)]
+    elif case == "uniform_asym_pos":  # flags on lane 0's coordinates only
+        pos = [j < 16 for j in range(D)]
     elif case == "dense":
         sigma = 0.01 * (np.eye(D) + 0.1 * np.ones((D, D)))
     elif case == "subset":
@@ -57,8 +70,11 @@ def test_refuses_other_shapes(cache, case):
         fac = [(P_, 8, [(N_, 0.0, 2.0)] * 8)]
     elif case == "improper":
         pri, fac = L.PRIOR_IMPROPER, None
-    if case == "uniform_rw":
-        u, keep = Engine.uniform_rw_desc(coords, 0.1, prior=pri, prior_factors=fac)
+    if case == "uniform_asym_pos":
+        u, keep = Engine.uniform_rw_desc(coords, 0.1, pos=pos, prior=pri, prior_factors=fac)
+    elif case == "adaptive":
+        adapt = dict(k=20, target=0.234, scale=0.02, min=1e-12, max=1e7, offset=100.0)
+        u, keep = Engine.uniform_rw_desc(coords, 0.1, adapt=adapt, prior=pri, prior_factors=fac)
     else:
         u, keep = Engine.gaussian_rw_desc(coords, sigma, pos=pos, prior=pri, prior_factors=fac)
     with pytest.raises(L.EMCMCError) as e:

@@ -1,8 +1,9 @@
-"""The fused diagonal step with a separable prior (rwm_gsn_diag_kernel + FusedPrior, emcmc_fused.h /
-emcmc_fprior.h): the joint GaussianRandomWalk with a diagonal Σ over coords 1:D on a diagonal
-GsnTargetLaw, with ProductPrior([Product(u_1 … u_D)]) or StandardPrior(Product(…))
-(priors.jl:18-88), the proposal! redraw loop (updates.jl:191-196) and the log-prior carry, the
-prior's left fold continued lane to lane across the chain's LPC lanes — against the oracle
+"""The fused diagonal step with the update's separable terms compiled in (rwm_gsn_diag_kernel +
+FusedUpdate, emcmc_fused.h / emcmc_fprior.h): the joint GaussianRandomWalk with a diagonal Σ or
+UniformRandomWalk (positivity flags) over coords 1:D on a diagonal GsnTargetLaw, with
+ProductPrior([Product(u_1 … u_D)]), StandardPrior(Product(…)) or ImproperPosPrior
+(priors.jl:18-88), the proposal! redraw loop (updates.jl:191-196) and the log-prior carry, every
+left fold continued lane to lane across the chain's LPC lanes — against the oracle
 (orc_run_mwg kind 2, the restatement the schedule kernels are checked against), bit for bit:
 accept streams, θ / θ° / ll histories, rolling acceptance, fault bits.  EMCMC_VARIANT_NO_FUSED_PRIOR
 runs the same update on the schedule kernel with the same bits."""
@@ -135,3 +136,33 @@ def test_forced_one_lane_per_chain_and_the_schedule_kernel_agree():
         for x, y in zip(out[0][1], o[1]):
             assert np.array_equal(x, y)
         assert np.array_equal(out[0][2], o[2]) and np.array_equal(out[0][3], o[3])
+
+
+@pytest.mark.parametrize("D,lpc,prior", [(32, 2, L.PRIOR_PRODUCT), (64, 4, L.PRIOR_IMPROPER_POS),
+                                         (24, 1, L.PRIOR_IMPROPER)])
+def test_uniform_random_walk_with_pos_flags(oracle, D, lpc, prior):
+    """UniformRandomWalk(ϵ_j) with positivity flags repeating across the lanes: θ·e^U, the two
+    transition-density sums (−log 2ϵ_j − log θ°_j, 0.0 off the flags) folded lane to lane, with a
+    Product of Gammas (redraws where a flag-less coordinate's θ° < 0), ImproperPosPrior or none."""
+    C, M = 2048, 80
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    dpl = D // lpc
+    pos = [(j % dpl) % 3 != 1 for j in range(D)]
+    eps = [0.04 + 0.003 * (j % dpl) for j in range(D)]
+    fac = [(P_, D, [(G_, 6.0, 0.5)] * D)] if prior == L.PRIOR_PRODUCT else None
+    ups = [oracle.mwg_update(1, range(D), eps=eps, pos=pos, prior=prior, factors=fac)]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), spl=11)
+    name = eng.kernel_name()
+    assert name.startswith(f"rwm_gsn_diag_kernel<D={D},LPC={lpc},") and "UniformRandomWalk" in name, name
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_gaussian_random_walk_with_improper_pos_prior(oracle):
+    """GaussianRandomWalk (no flags) with ImproperPosPrior: −Σ log θ_j folded lane to lane; θ° ≤ 0
+    makes the prior NaN / +Inf (log_real), which the ratio carries as the oracle does."""
+    D, C, M = 32, 2048, 80
+    seed, mu, ts, obs = problem(D, shift=2.0)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_IMPROPER_POS)]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)))
+    assert_fused(eng, D, 2)
+    check(oracle, eng, st, h, steps, ups, 1)

@@ -113,19 +113,24 @@ def test_d32_gaussian_rw_standard_prior_mvnormal(oracle):
     check(oracle, eng, st, h, steps, ups, 1)
 
 
+@pytest.mark.parametrize("variant", [L.VARIANT_NO_FUSED_PRIOR, 0])
 @pytest.mark.parametrize("prior", [L.PRIOR_IMPROPER, L.PRIOR_IMPROPER_POS])
-def test_d32_uniform_rw_with_pos_flags(oracle, prior):
+def test_d32_uniform_rw_with_pos_flags(oracle, prior, variant):
     """VERDICT shape 3: D = 32 joint UniformRandomWalk with positivity flags (θ° = θ·e^U on
     24 of 32 coordinates, the −log(2ϵ) − log θ° density terms folded left), ImproperPrior
-    and ImproperPosPrior."""
+    and ImproperPosPrior — on the schedule kernel and (variant 0: the flags repeat every 4
+    coordinates) on the fused kernel, the density sums folded lane to lane."""
     D, C, M = 32, 2048, 200
     seed, mu, ts, obs = problem(D, shift=4.0)
     pos = [j % 4 != 3 for j in range(D)]
     eps = [0.05 + 0.002 * j for j in range(D)]
     ups = [oracle.mwg_update(1, range(D), eps=eps, pos=pos, prior=prior)]
     th0 = np.tile(mu, (C, 1))
-    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
-    assert_block(eng, D)
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, variant=variant)
+    if variant:
+        assert_block(eng, D)
+    else:
+        assert eng.kernel_name().startswith("rwm_gsn_diag_kernel<D=32,LPC=2"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
     assert 0.05 < h["acc"].mean() < 0.9
 

@@ -184,9 +184,10 @@ typedef struct emcmc_config {
 #define EMCMC_VARIANT_NO_BLOCK 256u      /* one MALA / user update over all 17 ≤ D ≤ 64 coordinates, or a schedule
                                             of random-walk updates at 17 ≤ D ≤ 64: the general wide kernel
                                             instead of mwg_block_kernel / mwg_rw_block_kernel */
-#define EMCMC_VARIANT_NO_FUSED_PRIOR 512u /* the joint diagonal GaussianRandomWalk with a ProductPrior /
-                                            StandardPrior of univariates: the schedule kernels instead of
-                                            rwm_gsn_diag_kernel with the prior compiled in */
+#define EMCMC_VARIANT_NO_FUSED_PRIOR 512u /* one update over all coordinates whose terms separate (diagonal
+                                            GaussianRandomWalk or UniformRandomWalk with a Product of
+                                            univariates / ImproperPosPrior): the schedule kernels instead of
+                                            rwm_gsn_diag_kernel with those terms compiled in */
 
 /* `AdaptationUnifRW(θ; adapt_every_k_steps, target_accpt_rate, scale, min,
  * max, offset)` in its scalar form (transition_kernels/adaptation.jl:51-118,
@@ -441,11 +442,14 @@ emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode,
                                             const char *target_source, const char *target_options, char *log_out,
                                             size_t log_len);
 
-/* The same for the fused diagonal step with a prior (rwm_gsn_diag_kernel + FusedPrior), the kernel a
- * handle selects for ONE GaussianRandomWalk update over 0..dim-1 with a diagonal Σ and no positivity
- * flags whose prior is a ProductPrior / StandardPrior of one Product of dim univariates (families
- * repeating across the chain's lanes), on the built-in GsnTargetLaw with a diagonal Σ
- * (unit_target != 0: Σ = I).  lanes_per_chain as in emcmc_config (0 = automatic). */
+/* The same for the fused diagonal step with the update's separable terms compiled in
+ * (rwm_gsn_diag_kernel + FusedUpdate), the kernel a handle selects for ONE update over 0..dim-1
+ * without adaptation — a GaussianRandomWalk with a diagonal Σ and no positivity flags, or a
+ * UniformRandomWalk (flags allowed) — whose prior is ImproperPosPrior or one ProductPrior /
+ * StandardPrior Product of dim univariates (a UniformRandomWalk also ImproperPrior), families and
+ * flags repeating across the chain's lanes, on the built-in GsnTargetLaw with a diagonal Σ
+ * (unit_target != 0: Σ = I).  lanes_per_chain as in emcmc_config (0 = automatic).  Compiles both
+ * occupancies the handle may try (two waves per SIMD, then one). */
 emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_chain, uint32_t history_mode,
                                                uint32_t ll_mode, int unit_target, const emcmc_update_desc *update,
                                                char *log_out, size_t log_len);

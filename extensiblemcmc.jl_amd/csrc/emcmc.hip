@@ -921,10 +921,16 @@ bool fused_eligible(const emcmc_handle *h) {
 // GaussianRandomWalk with a diagonal Σ and no positivity flags, or UniformRandomWalk (positivity
 // flags allowed), no adaptation — whose prior is ImproperPrior (UniformRandomWalk; the Gaussian
 // one is the plain fused kernel), ImproperPosPrior, or ONE ProductPrior / StandardPrior factor that
-// is a Product of D univariates (no "reads θ[1]" dims-1 factor, no MvNormal); the families and
-// positivity flags repeat across the chain's lanes (those of coordinate i = those of i mod D/LPC).
+// is a Product of D univariates (no "reads θ[1]" dims-1 factor) or one MvNormal over all D (one or
+// two lanes per chain); the families and positivity flags repeat across the chain's lanes (those of
+// coordinate i = those of i mod D/LPC).
+bool fused_prior_mvn(const UpdateHost &u) {
+    return (u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD) && u.pmvn != 0ull;
+}
 int fused_lpc(const emcmc_handle *h) {
-    return h->cfg.lanes_per_chain ? (int)h->cfg.lanes_per_chain : auto_lpc((int)h->cfg.dim);
+    if (h->cfg.lanes_per_chain) return (int)h->cfg.lanes_per_chain;
+    const int a = auto_lpc((int)h->cfg.dim);
+    return (!h->updates.empty() && fused_prior_mvn(h->updates[0]) && a > 2) ? 2 : a;
 }
 bool fused_prior_eligible(const emcmc_handle *h) {
     if ((h->cfg.kernel_variant & EMCMC_VARIANT_NO_FUSED_PRIOR) || !joint_all_coords(h) || h->cfg.chain_moments)
@@ -940,13 +946,18 @@ bool fused_prior_eligible(const emcmc_handle *h) {
     if (!uni && anypos) return false;  // GaussianRandomWalk's positivity round trips: the schedule kernels
     const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
     if (u.prior == EMCMC_PRIOR_IMPROPER ? !uni : (!slots && u.prior != EMCMC_PRIOR_IMPROPER_POS)) return false;
-    if (slots && (u.nslot != (uint32_t)D || u.pmvn || u.psrc0 || u.pstart != 1ull || u.pend != (1ull << (D - 1))))
+    if (slots && (u.nslot != (uint32_t)D || u.psrc0 || u.pstart != 1ull || u.pend != (1ull << (D - 1))))
         return false;
+    const bool mvn = fused_prior_mvn(u);  // then every slot is a row of it (one factor: pmvs = 0)
+    if (mvn && u.pmvn != (D == 64 ? ~0ull : (1ull << D) - 1ull)) return false;
     const int lpc = fused_lpc(h);
-    if ((lpc != 1 && lpc != 2 && lpc != 4) || D % lpc || (lpc > 1 && (D / lpc) % 8)) return false;
+    if ((lpc != 1 && lpc != 2 && lpc != 4) || D % lpc || (mvn && lpc > 2)) return false;
     const int dpl = D / lpc;
+    // the likelihood's canonical sum (SumShape: blocks of 8, a pairwise tree over the blocks) splits
+    // across the lanes only where each lane's blocks form one subtree: D/LPC = 8·2^k
+    if (lpc > 1 && (dpl % 8 || ((dpl / 8) & (dpl / 8 - 1)))) return false;
     for (int i = 0; i < D; ++i) {
-        if (slots && u.pfam[i] != u.pfam[i % dpl]) return false;
+        if (slots && !mvn && u.pfam[i] != u.pfam[i % dpl]) return false;
         const bool pi = i < (int)u.pos.size() && u.pos[i], pj = (i % dpl) < (int)u.pos.size() && u.pos[i % dpl];
         if (pi != pj) return false;
     }
@@ -966,7 +977,9 @@ emcmc_status select_fused_prior(emcmc_handle *h) {
     for (int i = 0; i < D; ++i) unit = unit && t.invdiag[i] == 1.0;
     const bool uni = u.kernel == EMCMC_RW_UNIFORM;
     const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
-    const size_t nconst = (slots ? 7 : 4) * (size_t)D;  // FusedUpdate::kConsts = 3 with slots
+    const bool mvn = fused_prior_mvn(u);
+    // staged in LDS; FusedUpdate::kConsts = 3 with univariate slots
+    const size_t nconst = (slots && !mvn ? 7 : 4) * (size_t)D;
     const size_t obs_doubles = (ll == LL_PER_OBS) ? t.nobs * (size_t)D : 0;
     const size_t lds = lds_align16((nconst + obs_doubles) * sizeof(double));
     if (kZigLdsBytes + lds > kMaxLds) return EMCMC_UNSUPPORTED_PLUGIN;  // the schedule kernel reads them from HBM
@@ -1001,14 +1014,25 @@ emcmc_status select_fused_prior(emcmc_handle *h) {
     v.occ = minw;
     v.unit = unit;
     // the diag kernel's constants (L_ii, 1/L_ii — UniformRandomWalk: ϵ_i, −log 2ϵ_i with the device's
-    // log — 1/L_t,ii, x̄), then the prior's a, b, c per coordinate
-    std::vector<double> c(nconst);
+    // log — 1/L_t,ii, x̄), then the prior's a, b, c per coordinate, or — an MvNormal factor, read
+    // from global memory — μ, 1/L_jj, L packed lower row-major, c0 (FusedUpdate::eval_mvn)
+    const size_t nmvn = mvn ? 2 * (size_t)D + (size_t)D * (D + 1) / 2 + 1 : 0;
+    std::vector<double> c(nconst + nmvn);
+    if (mvn) {
+        double *g = c.data() + nconst;
+        for (int j = 0, q = 2 * D; j < D; ++j) {
+            g[j] = u.pmu[j];
+            g[D + j] = u.piL[j];
+            for (int m = 0; m <= j; ++m) g[q++] = u.pL[(size_t)j * kMwgMaxD + m];
+        }
+        g[nmvn - 1] = u.pc[D - 1];
+    }
     for (int i = 0; i < D; ++i) {
         c[i] = uni ? u.eps[i] : u.L[(size_t)i * D + i];
         c[D + i] = uni ? -log_any(2.0 * u.eps[i]) : u.invdiag[i];
         c[2 * D + i] = t.invdiag[i];
         c[3 * D + i] = t.xbar[i];
-        if (slots) {
+        if (slots && !mvn) {
             c[4 * D + i] = u.pa[i];
             c[5 * D + i] = u.pb[i];
             c[6 * D + i] = u.pc[i];
@@ -2435,8 +2459,9 @@ emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_
     if (!fused_prior_eligible(&tmp)) {
         copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk (no positivity flags) or UniformRandomWalk "
                  "over coords 0..dim-1 without adaptation, with ImproperPosPrior or a ProductPrior / StandardPrior "
-                 "that is one Product of dim univariates (UniformRandomWalk: ImproperPrior too), families and "
-                 "positivity flags repeating across the chain's lanes",
+                 "that is one Product of dim univariates or one MvNormal over all dim coordinates (one or two lanes "
+                 "per chain; UniformRandomWalk: ImproperPrior too), families and positivity flags repeating across "
+                 "the chain's lanes",
                  log_out, log_len);
         return EMCMC_INVALID_ARG;
     }

@@ -32,7 +32,10 @@ struct FusedUpdate {
     static constexpr bool kUniform = U::kind == 1u;  // else GaussianRandomWalk
     static constexpr bool kOn = U::prior != kPriorImproper;  // a prior term (and proposal! redraws)
     static constexpr bool kSlots = U::prior == kPriorProduct || U::prior == kPriorStandard;
-    static constexpr int kConsts = kSlots ? 3 : 0;  // a, b, c of univariate_logpdf, [3][D] in LDS
+    static constexpr bool kMvn = kSlots && U::pmvn != 0ull;  // one MvNormal factor over all D
+    // univariates: a, b, c of univariate_logpdf, [3][D] staged in LDS; an MvNormal factor reads its
+    // μ, 1/L_jj, packed lower factor and c0 from global memory through the scalar cache
+    static constexpr int kConsts = (kSlots && !kMvn) ? 3 : 0;
     static constexpr uint32_t kCap = kUniform ? kMaxResample : kMaxResampleGsn;
     static constexpr uint32_t kFault = kFaultPriorResample;
     static constexpr bool kPos = kUniform && U::pos != 0ull;
@@ -66,10 +69,61 @@ struct FusedUpdate {
         return s;
     }
 
-    // logpdf(prior, x) of the chain (every lane gets the same double)
+    // logpdf(MvNormal(μ, LLᵀ), x) − as rw_log_prior's MvNormal rows: y = L⁻¹(x − μ) row by row
+    // (row j: x_j − μ_j, then −L_jm·y_m for m ascending, times 1/L_jj), its squares folded left,
+    // c0 − s/2.  Pass k solves lane k's rows: every lane runs it with the same (scalar-loaded) rows,
+    // lane k's results are the ones kept; lane k−1's y's and running sum reach lane k by DPP.
+    // gc: μ[D] | 1/L_jj[D] | L packed lower row-major [D(D+1)/2] | c0.
     template <int D, int LPC, int DPL>
-    __device__ __forceinline__ static double eval(const double *pc, int d0, const double (&x)[DPL]) {
-        if constexpr (U::prior == kPriorImproperPos) {  // −sum(log.(θ))
+    __device__ __forceinline__ static double eval_mvn(const double *gc, const double (&x)[DPL]) {
+        static_assert(LPC == 1 || LPC == 2, "an MvNormal prior on one or two lanes per chain");
+        constexpr int kL = 2 * D, kC = 2 * D + D * (D + 1) / 2;
+        double y[DPL];
+        double s = 0.0;
+        static_for<0, DPL>([&](auto IC) {  // lane 0's rows 0 … DPL−1
+            constexpr int i = decltype(IC)::value;
+            cdouble *t = opaque_cptr(gc);  // per row: one row's loads in flight
+            double acc = x[i] - t[i];
+            static_for<0, i>([&](auto MC) {
+                constexpr int m = decltype(MC)::value;
+                acc = fma(-t[kL + i * (i + 1) / 2 + m], y[m], acc);
+            });
+            y[i] = acc * t[D + i];
+            s = (i == 0) ? y[i] * y[i] : fma(y[i], y[i], s);
+        });
+        if constexpr (LPC == 2) {  // lane 1's rows DPL … D−1, after lane 0's y's in ascending m
+            double y0[DPL];
+#pragma unroll
+            for (int m = 0; m < DPL; ++m) y0[m] = from_previous_lane<2>(y[m]);
+            const double s0 = from_previous_lane<2>(s);
+            static_for<0, DPL>([&](auto IC) {
+                constexpr int i = decltype(IC)::value, r = DPL + i;
+                cdouble *t = opaque_cptr(gc);
+                double acc = x[i] - t[r];
+                static_for<0, DPL>([&](auto MC) {
+                    constexpr int m = decltype(MC)::value;
+                    acc = fma(-t[kL + r * (r + 1) / 2 + m], y0[m], acc);
+                });
+                static_for<0, i>([&](auto MC) {
+                    constexpr int m = decltype(MC)::value;
+                    acc = fma(-t[kL + r * (r + 1) / 2 + DPL + m], y[m], acc);
+                });
+                y[i] = acc * t[D + r];
+                s = (i == 0) ? fma(y[i], y[i], s0) : fma(y[i], y[i], s);
+            });
+            s = from_last_lane<2>(s);
+        }
+        const double fv = opaque_cptr(gc)[kC] - s / 2.0;
+        return (U::prior == kPriorProduct) ? 0.0 + fv : fv;
+    }
+
+    // logpdf(prior, x) of the chain (every lane gets the same double); pc: the LDS constants of the
+    // univariate factors, gc: the MvNormal factor's tables in global memory
+    template <int D, int LPC, int DPL>
+    __device__ __forceinline__ static double eval(const double *pc, const double *gc, int d0, const double (&x)[DPL]) {
+        if constexpr (kMvn) {
+            return eval_mvn<D, LPC, DPL>(gc, x);
+        } else if constexpr (U::prior == kPriorImproperPos) {  // −sum(log.(θ))
             double v[DPL];
 #pragma unroll
             for (int i = 0; i < DPL; ++i) v[i] = log_real(x[i]);

@@ -112,7 +112,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     // log_prior(::Previous) carried: logpdf(prior, θ) at the launch's start, then the accepted
     // step's log_prior(::Proposal) (the same doubles)
     double lpc = 0.0;
-    if constexpr (PR::kOn) lpc = PR::template eval<D, LPC, DPL>(cst0 + 4 * D, d0, th);
+    if constexpr (PR::kOn) lpc = PR::template eval<D, LPC, DPL>(cst0 + 4 * D, a.consts + 4 * D, d0, th);
     // UniformRandomWalk with positivity flags: logpdf(rw, θ°, θ) carried the same way
     double ltd_rev_c = 0.0;
     if constexpr (PR::kUniform)
@@ -145,7 +145,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         if constexpr (PR::kOn) {
             for (uint32_t rs = 0;; ++rs) {
                 propose(rs);
-                lpp = PR::template eval<D, LPC, DPL>(cst + 4 * D, d0, thp);
+                lpp = PR::template eval<D, LPC, DPL>(cst + 4 * D, a.consts + 4 * D, d0, thp);
                 if (!(lpp == -__builtin_inf())) break;
                 if (rs >= PR::kCap) {
                     faults |= PR::kFault;

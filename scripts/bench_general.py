@@ -84,8 +84,8 @@ def main():
     if want("pcn_user_d32"):
         pcn_user(C, M, report, a.variant)
     # (5) one random-walk update over all 32 coordinates with a prior / positivity flags: the
-    # fused diagonal kernel with the prior compiled in where the prior is a Product of univariates,
-    # else mwg_rw_block_kernel; the "_block" twins force the schedule kernel, "_wide" the wide one
+    # fused diagonal kernel with the prior compiled in where the prior is a Product of univariates
+    # or one MvNormal, else mwg_rw_block_kernel; the "_block" twins force the schedule kernel, "_wide" the wide one
     for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32"):
         for suffix, variant in (("", a.variant), ("_block", L.VARIANT_NO_FUSED_PRIOR),
                                 ("_wide", L.VARIANT_NO_BLOCK | L.VARIANT_NO_FUSED_PRIOR)):
@@ -98,7 +98,7 @@ WORKLOADS = ["mwg_d32_two_blocks", "mwg_d32_two_blocks_wide", "mwg_d64_two_block
              "dense_d32_joint", "dense_d32_joint_suffstat", "user_student_t_d4", "haario_dense_d32",
              "haario_dense_d32_general", "mala_gsn_d32", "pcn_user_d32", "rw_product_normal_d32",
              "rw_product_normal_d32_block", "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32",
-             "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_block", "unif_pos_d32_wide"]
+             "rw_standard_mvnormal_d32_block", "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_block", "unif_pos_d32_wide"]
 
 
 def run_isolated(names, a):

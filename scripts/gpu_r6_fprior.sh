@@ -12,6 +12,6 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_fprior.py tests/test_gpu_rw
 rc=$?; echo "rc=$rc"; tail -12 "$OUT/pytest.txt" | cut -c1-250
 [ $rc = 0 ] || exit $rc
 echo "== lines $(date +%T)"
-timeout -k 10 300 python3 -u scripts/bench_general.py --only rw_product_normal_d32,rw_product_normal_d32_block,unif_pos_d32,unif_pos_d32_block > "$OUT/lines.jsonl" 2> "$OUT/lines.err"
+timeout -k 10 300 python3 -u scripts/bench_general.py --only ${LINES:-rw_product_normal_d32,rw_product_normal_d32_block,unif_pos_d32,unif_pos_d32_block} > "$OUT/lines.jsonl" 2> "$OUT/lines.err"
 rc=$?; echo "rc=$rc"; cut -c1-250 "$OUT/lines.jsonl"
 exit $rc

@@ -1,7 +1,8 @@
 """The fused diagonal step with the update's separable terms compiled in (rwm_gsn_diag_kernel +
 FusedUpdate, emcmc_fused.h / emcmc_fprior.h): the joint GaussianRandomWalk with a diagonal Σ or
 UniformRandomWalk (positivity flags) over coords 1:D on a diagonal GsnTargetLaw, with
-ProductPrior([Product(u_1 … u_D)]), StandardPrior(Product(…)) or ImproperPosPrior
+ProductPrior([Product(u_1 … u_D)]), StandardPrior(Product(…)), one MvNormal(μ, Σ) over all D
+or ImproperPosPrior
 (priors.jl:18-88), the proposal! redraw loop (updates.jl:191-196) and the log-prior carry, every
 left fold continued lane to lane across the chain's LPC lanes — against the oracle
 (orc_run_mwg kind 2, the restatement the schedule kernels are checked against), bit for bit:
@@ -19,7 +20,7 @@ pytestmark = pytest.mark.gpu
 
 N_, U_, E_, G_, LN_ = L.DIST_NORMAL, L.DIST_UNIFORM, L.DIST_EXPONENTIAL, L.DIST_GAMMA, L.DIST_LOGNORMAL
 B_, IG_, C_, LA_, T_ = L.DIST_BETA, L.DIST_INVERSE_GAMMA, L.DIST_CAUCHY, L.DIST_LAPLACE, L.DIST_TDIST
-P_ = L.DIST_PRODUCT
+P_, MV_ = L.DIST_PRODUCT, L.DIST_MVNORMAL
 
 
 @pytest.fixture(autouse=True)
@@ -165,4 +166,42 @@ def test_gaussian_random_walk_with_improper_pos_prior(oracle):
     ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_IMPROPER_POS)]
     eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)))
     assert_fused(eng, D, 2)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def dense_cov(D, seed=9):
+    B = np.random.default_rng(seed).standard_normal((D, D))
+    return B @ B.T / D + 0.5 * np.eye(D)
+
+
+@pytest.mark.parametrize("D,lanes,prior,ll_mode", [(32, 0, L.PRIOR_STANDARD, L.LL_SUFFSTAT),
+                                                   (32, 1, L.PRIOR_PRODUCT, L.LL_PER_OBS),
+                                                   (16, 0, L.PRIOR_PRODUCT, L.LL_PER_OBS)])
+def test_mvnormal_prior(oracle, D, lanes, prior, ll_mode):
+    """StandardPrior(MvNormal(μ0, Σ0)) / ProductPrior([MvNormal]) with Σ0 dense: y = L⁻¹(θ − μ0) row
+    by row from the scalar-loaded factor, lane 1's rows continuing from lane 0's y's and sum of
+    squares (two lanes per chain, auto at D = 16 and 32), one lane forced at D = 32."""
+    C, M = 2048, 100
+    seed, mu, ts, obs = problem(D)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=prior,
+                             factors=[(MV_, D, 0.3 * np.ones(D), dense_cov(D))])]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), ll_mode=ll_mode,
+                                 lanes=lanes)
+    assert_fused(eng, D, lanes or 2)
+    assert "MvNormal" in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+@pytest.mark.parametrize("D,lanes,factors", [(48, 0, "mvn"), (64, 0, "mvn"), (48, 2, "normals")])
+def test_shapes_the_fused_kernel_declines(oracle, D, lanes, factors):
+    """Shapes that run elsewhere with the oracle's bits: an MvNormal at D = 64 (two lanes of 32 rows
+    spill at either occupancy: the scratch gate), and two lanes of 24 at D = 48 (the likelihood's
+    canonical sum — blocks of 8 under a pairwise tree — does not split into two subtrees of 24),
+    whether auto (an MvNormal caps three lanes at two) or forced with a Product of Normals."""
+    C, M = 1024, 40
+    seed, mu, ts, obs = problem(D)
+    fac = [(MV_, D, 0.3 * np.ones(D), dense_cov(D))] if factors == "mvn" else normals(D)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_STANDARD, factors=fac)]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), lanes=lanes)
+    assert not eng.kernel_name().startswith("rwm_gsn_diag_kernel"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)

@@ -41,9 +41,9 @@ def problem(D, shift=0.0, dense_t=False, seed=5):
 
 
 def engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL, spl=0, variant=0,
-               theta0=None, user=None):
+               theta0=None, user=None, lanes=0):
     eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, history_mode=hist,
-                              steps_per_launch=spl, kernel_variant=variant))
+                              steps_per_launch=spl, kernel_variant=variant, lanes_per_chain=lanes))
     for u in ups:
         pr = dict(prior=u.get("prior", 0), prior_factors=u.get("factors") or None)
         if u["kind"] == 1:
@@ -59,10 +59,10 @@ def engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode=L.LL_PER_OBS, hist=L.HIS
 
 
 def run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, theta0, steps=None, ll_mode=L.LL_PER_OBS, hist=L.HIST_FULL,
-             spl=0, user=None, calls=None, variant=0):
+             spl=0, user=None, calls=None, variant=0, lanes=0):
     steps = steps or full_steps(M, 1)
     eng = engine_for(D, C, M, ups, mu, ts, obs, seed, ll_mode, hist, spl, variant=variant, theta0=theta0,
-                     user=None if user is None else user[1])
+                     user=None if user is None else user[1], lanes=lanes)
     for a, b in (calls or [(0, len(steps))]):
         eng.run(steps[a:b])
     st = oracle.MWGState(np.array(theta0, dtype=np.float64), mu if user is None else np.zeros(D), ups)
@@ -98,9 +98,11 @@ def test_d32_gaussian_rw_product_prior_normal(oracle, ll_mode, hist):
     assert 0.1 < h["acc"].mean() < 0.6
 
 
-def test_d32_gaussian_rw_standard_prior_mvnormal(oracle):
+@pytest.mark.parametrize("variant", [L.VARIANT_NO_FUSED_PRIOR, 0])
+def test_d32_gaussian_rw_standard_prior_mvnormal(oracle, variant):
     """VERDICT shape 2: D = 32 joint GaussianRandomWalk + StandardPrior(MvNormal(μ0, Σ0)),
-    Σ0 dense (the forward substitution over the prior's factor, squares folded left)."""
+    Σ0 dense (the forward substitution over the prior's factor, squares folded left) — on the
+    schedule kernel and (variant 0) on the fused kernel, lane 1's rows after lane 0's."""
     D, C, M = 32, 2048, 160
     seed, mu, ts, obs = problem(D)
     B = np.random.default_rng(9).standard_normal((D, D))
@@ -108,8 +110,11 @@ def test_d32_gaussian_rw_standard_prior_mvnormal(oracle):
     ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_STANDARD,
                              factors=[(MV_, D, 0.3 * np.ones(D), S0)])]
     th0 = np.tile(mu, (C, 1))
-    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
-    assert_block(eng, D)
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, variant=variant)
+    if variant:
+        assert_block(eng, D)
+    else:
+        assert eng.kernel_name().startswith("rwm_gsn_diag_kernel<D=32,LPC=2,"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
 
 

@@ -921,16 +921,13 @@ bool fused_eligible(const emcmc_handle *h) {
 // GaussianRandomWalk with a diagonal Σ and no positivity flags, or UniformRandomWalk (positivity
 // flags allowed), no adaptation — whose prior is ImproperPrior (UniformRandomWalk; the Gaussian
 // one is the plain fused kernel), ImproperPosPrior, or ONE ProductPrior / StandardPrior factor that
-// is a Product of D univariates (no "reads θ[1]" dims-1 factor) or one MvNormal over all D (one or
-// two lanes per chain); the families and positivity flags repeat across the chain's lanes (those of
+// is a Product of D univariates (no "reads θ[1]" dims-1 factor) or one MvNormal over all D; the families and positivity flags repeat across the chain's lanes (those of
 // coordinate i = those of i mod D/LPC).
 bool fused_prior_mvn(const UpdateHost &u) {
     return (u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD) && u.pmvn != 0ull;
 }
 int fused_lpc(const emcmc_handle *h) {
-    if (h->cfg.lanes_per_chain) return (int)h->cfg.lanes_per_chain;
-    const int a = auto_lpc((int)h->cfg.dim);
-    return (!h->updates.empty() && fused_prior_mvn(h->updates[0]) && a > 2) ? 2 : a;
+    return h->cfg.lanes_per_chain ? (int)h->cfg.lanes_per_chain : auto_lpc((int)h->cfg.dim);
 }
 bool fused_prior_eligible(const emcmc_handle *h) {
     if ((h->cfg.kernel_variant & EMCMC_VARIANT_NO_FUSED_PRIOR) || !joint_all_coords(h) || h->cfg.chain_moments)
@@ -951,7 +948,7 @@ bool fused_prior_eligible(const emcmc_handle *h) {
     const bool mvn = fused_prior_mvn(u);  // then every slot is a row of it (one factor: pmvs = 0)
     if (mvn && u.pmvn != (D == 64 ? ~0ull : (1ull << D) - 1ull)) return false;
     const int lpc = fused_lpc(h);
-    if ((lpc != 1 && lpc != 2 && lpc != 4) || D % lpc || (mvn && lpc > 2)) return false;
+    if ((lpc != 1 && lpc != 2 && lpc != 4) || D % lpc) return false;
     const int dpl = D / lpc;
     // the likelihood's canonical sum (SumShape: blocks of 8, a pairwise tree over the blocks) splits
     // across the lanes only where each lane's blocks form one subtree: D/LPC = 8·2^k
@@ -2459,9 +2456,9 @@ emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_
     if (!fused_prior_eligible(&tmp)) {
         copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk (no positivity flags) or UniformRandomWalk "
                  "over coords 0..dim-1 without adaptation, with ImproperPosPrior or a ProductPrior / StandardPrior "
-                 "that is one Product of dim univariates or one MvNormal over all dim coordinates (one or two lanes "
-                 "per chain; UniformRandomWalk: ImproperPrior too), families and positivity flags repeating across "
-                 "the chain's lanes",
+                 "that is one Product of dim univariates or one MvNormal over all dim coordinates (UniformRandomWalk: "
+                 "ImproperPrior too), families and positivity flags repeating across the chain's lanes, dim/lanes = "
+                 "8·2^k with more than one lane per chain",
                  log_out, log_len);
         return EMCMC_INVALID_ARG;
     }

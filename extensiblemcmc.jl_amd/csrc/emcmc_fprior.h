@@ -75,7 +75,75 @@ struct FusedUpdate {
     // lane k's results are the ones kept; lane k−1's y's and running sum reach lane k by DPP.
     // gc: μ[D] | 1/L_jj[D] | L packed lower row-major [D(D+1)/2] | c0.
     template <int D, int LPC, int DPL>
-    __device__ __forceinline__ static double eval_mvn(const double *gc, const double (&x)[DPL]) {
+    __device__ __forceinline__ static double eval_mvn(const double *gc, int d0, const double (&x)[DPL]) {
+        if constexpr (LPC == 4) {
+            return eval_mvn_quad<D, DPL>(gc, d0 / DPL, x);
+        } else {
+            return eval_mvn_pair<D, LPC, DPL>(gc, x);
+        }
+    }
+
+    // every lane of the quad takes lane K's value (quad_perm [K,K,K,K])
+    template <int K>
+    __device__ __forceinline__ static double from_quad_lane(double v) {
+        return dpp_perm<K * 0x55>(v);
+    }
+
+    // Four lanes per chain: pass k forms lane k's rows in accumulators — x − μ, then the columns of
+    // lanes 0 … k−1 (each of their y's broadcast across the quad once, used by the DPL rows), then
+    // the lane's own columns — so every row still takes its terms m ascending; lane k keeps the
+    // pass's y's, the running sum moves on from lane k−1 by DPP.  Live: y and the accumulators
+    // (2·DPL), where carrying the earlier lanes' y's would take D.
+    template <int D, int DPL>
+    __device__ __forceinline__ static double eval_mvn_quad(const double *gc, int kl, const double (&x)[DPL]) {
+        constexpr int kL = 2 * D, kC = 2 * D + D * (D + 1) / 2;
+        double y[DPL];
+        double s = 0.0, carry = 0.0;
+        static_for<0, 4>([&](auto KC) {
+            constexpr int k = decltype(KC)::value;
+            double acc[DPL];
+            {
+                cdouble *t = opaque_cptr(gc);
+                static_for<0, DPL>([&](auto IC) {
+                    constexpr int i = decltype(IC)::value;
+                    acc[i] = x[i] - t[k * DPL + i];
+                });
+            }
+            static_for<0, k>([&](auto SC) {  // the earlier lanes' columns, ascending
+                constexpr int sl = decltype(SC)::value;
+                static_for<0, DPL>([&](auto MC) {
+                    constexpr int m = sl * DPL + decltype(MC)::value;
+                    const double b = from_quad_lane<sl>(y[decltype(MC)::value]);
+                    cdouble *t = opaque_cptr(gc);  // per column: one column's loads in flight
+                    static_for<0, DPL>([&](auto IC) {
+                        constexpr int i = decltype(IC)::value, r = k * DPL + i;
+                        acc[i] = fma(-t[kL + r * (r + 1) / 2 + m], b, acc[i]);
+                    });
+                });
+            });
+            static_for<0, DPL>([&](auto IC) {  // the lane's own rows: forward substitution
+                constexpr int i = decltype(IC)::value, r = k * DPL + i;
+                cdouble *t = opaque_cptr(gc);
+                static_for<0, i>([&](auto MC) {
+                    constexpr int m = decltype(MC)::value;
+                    acc[i] = fma(-t[kL + r * (r + 1) / 2 + k * DPL + m], acc[m], acc[i]);
+                });
+                acc[i] = acc[i] * t[D + r];
+                if constexpr (k == 0 && i == 0) s = acc[i] * acc[i];
+                else if constexpr (i == 0) s = fma(acc[i], acc[i], carry);
+                else s = fma(acc[i], acc[i], s);
+            });
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) y[i] = (kl == k) ? acc[i] : y[i];
+            if constexpr (k < 3) carry = from_previous_lane<4>(s);
+        });
+        s = from_last_lane<4>(s);
+        const double fv = opaque_cptr(gc)[kC] - s / 2.0;
+        return (U::prior == kPriorProduct) ? 0.0 + fv : fv;
+    }
+
+    template <int D, int LPC, int DPL>
+    __device__ __forceinline__ static double eval_mvn_pair(const double *gc, const double (&x)[DPL]) {
         static_assert(LPC == 1 || LPC == 2, "an MvNormal prior on one or two lanes per chain");
         constexpr int kL = 2 * D, kC = 2 * D + D * (D + 1) / 2;
         double y[DPL];
@@ -122,7 +190,7 @@ struct FusedUpdate {
     template <int D, int LPC, int DPL>
     __device__ __forceinline__ static double eval(const double *pc, const double *gc, int d0, const double (&x)[DPL]) {
         if constexpr (kMvn) {
-            return eval_mvn<D, LPC, DPL>(gc, x);
+            return eval_mvn<D, LPC, DPL>(gc, d0, x);
         } else if constexpr (U::prior == kPriorImproperPos) {  // −sum(log.(θ))
             double v[DPL];
 #pragma unroll

@@ -446,10 +446,10 @@ emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode,
  * (rwm_gsn_diag_kernel + FusedUpdate), the kernel a handle selects for ONE update over 0..dim-1
  * without adaptation — a GaussianRandomWalk with a diagonal Σ and no positivity flags, or a
  * UniformRandomWalk (flags allowed) — whose prior is ImproperPosPrior or one ProductPrior /
- * StandardPrior factor: a Product of dim univariates or an MvNormal over all dim coordinates (one
- * or two lanes per chain) (a UniformRandomWalk also ImproperPrior), families and flags repeating
- * across the chain's lanes, on the built-in GsnTargetLaw with a diagonal Σ (unit_target != 0:
- * Σ = I).  lanes_per_chain as in emcmc_config (0 = automatic; at most 2 with an MvNormal).  Compiles both
+ * StandardPrior factor: a Product of dim univariates or an MvNormal over all dim coordinates (a
+ * UniformRandomWalk also ImproperPrior), families and flags repeating across the chain's lanes,
+ * dim / lanes = 8·2^k with more than one lane, on the built-in GsnTargetLaw with a diagonal Σ
+ * (unit_target != 0: Σ = I).  lanes_per_chain as in emcmc_config (0 = automatic).  Compiles both
  * occupancies the handle may try (two waves per SIMD, then one). */
 emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_chain, uint32_t history_mode,
                                                uint32_t ll_mode, int unit_target, const emcmc_update_desc *update,

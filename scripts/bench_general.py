@@ -86,11 +86,13 @@ def main():
     # (5) one random-walk update over all 32 coordinates with a prior / positivity flags: the
     # fused diagonal kernel with the prior compiled in where the prior is a Product of univariates
     # or one MvNormal, else mwg_rw_block_kernel; the "_block" twins force the schedule kernel, "_wide" the wide one
-    for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32"):
+    for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32", "rw_standard_mvnormal_d64"):
         for suffix, variant in (("", a.variant), ("_block", L.VARIANT_NO_FUSED_PRIOR),
                                 ("_wide", L.VARIANT_NO_BLOCK | L.VARIANT_NO_FUSED_PRIOR)):
             if want(name + suffix) or (not only and suffix == ""):
                 rw_prior(name, suffix, C, M, report, variant)
+    if want("rw_standard_mvnormal_d32_lpc4"):  # four lanes per chain instead of auto's two
+        rw_prior("rw_standard_mvnormal_d32", "_lpc4", C, M, report, a.variant, lanes=4)
 
 
 # every workload, in the order one run measures them
@@ -98,7 +100,8 @@ WORKLOADS = ["mwg_d32_two_blocks", "mwg_d32_two_blocks_wide", "mwg_d64_two_block
              "dense_d32_joint", "dense_d32_joint_suffstat", "user_student_t_d4", "haario_dense_d32",
              "haario_dense_d32_general", "mala_gsn_d32", "pcn_user_d32", "rw_product_normal_d32",
              "rw_product_normal_d32_block", "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32",
-             "rw_standard_mvnormal_d32_block", "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_block", "unif_pos_d32_wide"]
+             "rw_standard_mvnormal_d32_block", "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_block", "unif_pos_d32_wide",
+             "rw_standard_mvnormal_d32_lpc4", "rw_standard_mvnormal_d64", "rw_standard_mvnormal_d64_wide"]
 
 
 def run_isolated(names, a):
@@ -180,23 +183,25 @@ def pcn_user(C, M, report, variant=0):
     eng.close()
 
 
-def rw_prior(name, suffix, C, M, report, variant=0):
+def rw_prior(name, suffix, C, M, report, variant=0, lanes=0):
     """One joint update over D = 32 coordinates on cfg 2's target (10 observations, per
     observation likelihood, full histories), VERDICT r5 next-step 2's shapes:
       rw_product_normal_d32     GaussianRandomWalk(σ²I) + ProductPrior([Product(32 × Normal)])
       rw_standard_mvnormal_d32  GaussianRandomWalk(σ²I) + StandardPrior(MvNormal(μ0, Σ0)), Σ0 dense
-      unif_pos_d32              UniformRandomWalk(ϵ) with positivity flags on every coordinate"""
-    D = 32
-    w = W.cfg2(8)
+      unif_pos_d32              UniformRandomWalk(ϵ) with positivity flags on every coordinate
+    and rw_standard_mvnormal_d64, the MvNormal shape over D = 64 on the 64-dimensional target."""
+    D = 64 if name.endswith("_d64") else 32
+    w = W.cfg2(8, D=D)
     shift = 4.0 if name == "unif_pos_d32" else 0.0
     mu = np.asarray(w.mu_true) + shift
     obs = np.asarray(w.obs) - np.asarray(w.mu_true) + mu
     s2 = (2.38 / np.sqrt(D * 10)) ** 2
-    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed, kernel_variant=variant))
+    eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=2 * M, seed=w.seed, kernel_variant=variant,
+                              lanes_per_chain=lanes))
     if name == "rw_product_normal_d32":
         eng.add_gaussian_rw_update(np.arange(D), s2 * np.eye(D), prior=L.PRIOR_PRODUCT,
                                    prior_factors=[(L.DIST_PRODUCT, D, [(L.DIST_NORMAL, 0.0, 3.0)] * D)])
-    elif name == "rw_standard_mvnormal_d32":
+    elif name.startswith("rw_standard_mvnormal"):
         B = np.random.default_rng(9).standard_normal((D, D))
         eng.add_gaussian_rw_update(np.arange(D), s2 * np.eye(D), prior=L.PRIOR_STANDARD,
                                    prior_factors=[(L.DIST_MVNORMAL, D, np.zeros(D), B @ B.T / D + np.eye(D))])

@@ -45,9 +45,10 @@ def test_uniform_random_walks(cache, pos, prior):
     assert len(list(cache.glob("*.co"))) == 2
 
 
-@pytest.mark.parametrize("D,lanes,prior", [(32, 0, L.PRIOR_STANDARD), (32, 1, L.PRIOR_PRODUCT), (16, 0, L.PRIOR_STANDARD)])
+@pytest.mark.parametrize("D,lanes,prior", [(32, 0, L.PRIOR_STANDARD), (32, 1, L.PRIOR_PRODUCT), (16, 0, L.PRIOR_STANDARD),
+                                           (32, 4, L.PRIOR_STANDARD)])
 def test_mvnormal_prior(cache, D, lanes, prior):
-    """One MvNormal over all D: one or two lanes per chain (auto caps it at two)."""
+    """One MvNormal over all D on one, two or four lanes per chain."""
     u, keep = Engine.gaussian_rw_desc(range(D), 0.01 * np.eye(D), prior=prior,
                                       prior_factors=[(MV_, D, np.zeros(D), np.eye(D) + 0.1 * np.ones((D, D)))])
     L.prebuild_fused_prior_kernel(D, u, lanes_per_chain=lanes)
@@ -56,9 +57,8 @@ def test_mvnormal_prior(cache, D, lanes, prior):
 
 @pytest.mark.parametrize("D,lanes,mvn", [(48, 2, False), (48, 0, True), (24, 2, False)])
 def test_refuses_lane_splits_of_the_canonical_sum(cache, D, lanes, mvn):
-    """Two lanes of 24 (or 12): the likelihood's blocks of 8 under a pairwise tree do not split
-    into one subtree per lane (D/LPC must be 8·2^k); an MvNormal at D = 48 caps auto's three lanes
-    at two, so it is refused too."""
+    """Two lanes of 24 (or 12), three of 16 (auto at D = 48): the likelihood's blocks of 8 under a
+    pairwise tree do not split into one subtree per lane (D/LPC must be 8·2^k, LPC ∈ {1, 2, 4})."""
     fac = [(MV_, D, np.zeros(D), np.eye(D))] if mvn else [(P_, D, [(N_, 0.0, 2.0)] * D)]
     u, keep = Engine.gaussian_rw_desc(range(D), 0.01 * np.eye(D), prior=L.PRIOR_STANDARD, prior_factors=fac)
     with pytest.raises(L.EMCMCError) as e:
@@ -66,7 +66,7 @@ def test_refuses_lane_splits_of_the_canonical_sum(cache, D, lanes, mvn):
     assert "not a fused-prior shape" in str(e.value)
 
 
-@pytest.mark.parametrize("case", ["mvnormal_part", "mvnormal_4lanes", "dims1", "asymmetric", "pos", "uniform_asym_pos", "adaptive", "dense",
+@pytest.mark.parametrize("case", ["mvnormal_part", "dims1", "asymmetric", "pos", "uniform_asym_pos", "adaptive", "dense",
                                   "subset", "improper"])
 def test_refuses_other_shapes(cache, case):
     D = 32
@@ -74,8 +74,6 @@ def test_refuses_other_shapes(cache, case):
     pri, fac, pos = L.PRIOR_PRODUCT, [(P_, D, [(N_, 0.0, 2.0)] * D)], None
     if case == "mvnormal_part":  # an MvNormal over 16 of the 32 slots beside a Product
         pri, fac = L.PRIOR_PRODUCT, [(MV_, 16, np.zeros(16), np.eye(16)), (P_, 16, [(N_, 0.0, 2.0)] * 16)]
-    elif case == "mvnormal_4lanes":
-        pri, fac = L.PRIOR_STANDARD, [(MV_, D, np.zeros(D), np.eye(D))]
     elif case == "dims1":  # ProductPrior([Normal]*32, [1]*32): every factor reads θ[1] (priors.jl:64-79)
         fac = [(N_, 1, 0.0, 2.0)] * D
     elif case == "asymmetric":  # a Gamma on lane 0's coordinate 3 only (two lanes of 16)
@@ -101,7 +99,7 @@ def test_refuses_other_shapes(cache, case):
     else:
         u, keep = Engine.gaussian_rw_desc(coords, sigma, pos=pos, prior=pri, prior_factors=fac)
     with pytest.raises(L.EMCMCError) as e:
-        L.prebuild_fused_prior_kernel(D, u, lanes_per_chain=4 if case == "mvnormal_4lanes" else 0)
+        L.prebuild_fused_prior_kernel(D, u)
     assert e.value.status == L.INVALID_ARG
     assert "not a fused-prior shape" in str(e.value)
     assert not list(cache.glob("*.co"))

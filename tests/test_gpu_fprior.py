@@ -176,28 +176,31 @@ def dense_cov(D, seed=9):
 
 @pytest.mark.parametrize("D,lanes,prior,ll_mode", [(32, 0, L.PRIOR_STANDARD, L.LL_SUFFSTAT),
                                                    (32, 1, L.PRIOR_PRODUCT, L.LL_PER_OBS),
-                                                   (16, 0, L.PRIOR_PRODUCT, L.LL_PER_OBS)])
+                                                   (16, 0, L.PRIOR_PRODUCT, L.LL_PER_OBS),
+                                                   (32, 4, L.PRIOR_PRODUCT, L.LL_PER_OBS),
+                                                   (64, 0, L.PRIOR_STANDARD, L.LL_PER_OBS)])
 def test_mvnormal_prior(oracle, D, lanes, prior, ll_mode):
     """StandardPrior(MvNormal(μ0, Σ0)) / ProductPrior([MvNormal]) with Σ0 dense: y = L⁻¹(θ − μ0) row
     by row from the scalar-loaded factor, lane 1's rows continuing from lane 0's y's and sum of
-    squares (two lanes per chain, auto at D = 16 and 32), one lane forced at D = 32."""
+    squares (two lanes per chain, auto at D = 16 and 32), one lane forced at D = 32; four lanes
+    (forced at D = 32, auto at D = 64): lane k's rows take the earlier lanes' y's as quad
+    broadcasts, one column at a time."""
     C, M = 2048, 100
     seed, mu, ts, obs = problem(D)
     ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=prior,
                              factors=[(MV_, D, 0.3 * np.ones(D), dense_cov(D))])]
     eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), ll_mode=ll_mode,
                                  lanes=lanes)
-    assert_fused(eng, D, lanes or 2)
+    assert_fused(eng, D, lanes or (4 if D == 64 else 2))
     assert "MvNormal" in eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
 
 
-@pytest.mark.parametrize("D,lanes,factors", [(48, 0, "mvn"), (64, 0, "mvn"), (48, 2, "normals")])
+@pytest.mark.parametrize("D,lanes,factors", [(48, 0, "mvn"), (48, 2, "normals")])
 def test_shapes_the_fused_kernel_declines(oracle, D, lanes, factors):
-    """Shapes that run elsewhere with the oracle's bits: an MvNormal at D = 64 (two lanes of 32 rows
-    spill at either occupancy: the scratch gate), and two lanes of 24 at D = 48 (the likelihood's
-    canonical sum — blocks of 8 under a pairwise tree — does not split into two subtrees of 24),
-    whether auto (an MvNormal caps three lanes at two) or forced with a Product of Normals."""
+    """Shapes that run elsewhere with the oracle's bits: D = 48 on three lanes (auto) or two lanes
+    of 24 (forced) — the likelihood's canonical sum (blocks of 8 under a pairwise tree) does not
+    split into one subtree per lane."""
     C, M = 1024, 40
     seed, mu, ts, obs = problem(D)
     fac = [(MV_, D, 0.3 * np.ones(D), dense_cov(D))] if factors == "mvn" else normals(D)

@@ -582,8 +582,18 @@ emcmc_status upload_block_consts(emcmc_handle *h) {
 // updates; the built-in GsnTargetLaw over μ (d = D) or a user law.  (A single GaussianRandomWalk
 // over coords 1:D with ImproperPrior and no flags on the built-in target never reaches select_mwg:
 // the fused kernels take it.)
+// A GaussianRandomWalk's positivity round trips keep up to six vectors of its coordinates live
+// (emcmc_rwblock.h): with more than 32 flagged coordinates the kernel always needs scratch (33, 40,
+// 48 measured) — the scratch gate would discard it — and at 64 the gfx950 backend aborts the process
+// compiling it (LLVM ERROR: Unsupported instruction).  Such updates go to the wide kernel uncompiled.
+constexpr int kRwBlockMaxGaussianPos = 32;
 bool rwblock_update_ok(const UpdateHost &u) {
     if (u.kernel != EMCMC_RW_UNIFORM && u.kernel != EMCMC_RW_GAUSSIAN) return false;
+    if (u.kernel == EMCMC_RW_GAUSSIAN) {
+        int npos = 0;
+        for (uint8_t f : u.pos) npos += f ? 1 : 0;
+        if (npos > kRwBlockMaxGaussianPos) return false;
+    }
     return u.adaptation == EMCMC_ADPT_NONE || (u.kernel == EMCMC_RW_UNIFORM && u.adaptation == EMCMC_ADPT_UNIF_RW);
 }
 bool rwblock_eligible(const std::vector<UpdateHost> &ups, uint32_t D) {
@@ -918,9 +928,9 @@ bool fused_eligible(const emcmc_handle *h) {
 
 // The fused diagonal step with the update's separable terms compiled in (emcmc_fprior.h
 // FusedUpdate): ONE update over coords 0..D−1 in order on a diagonal GsnTargetLaw —
-// GaussianRandomWalk with a diagonal Σ and no positivity flags, or UniformRandomWalk (positivity
-// flags allowed), no adaptation — whose prior is ImproperPrior (UniformRandomWalk; the Gaussian
-// one is the plain fused kernel), ImproperPosPrior, or ONE ProductPrior / StandardPrior factor that
+// GaussianRandomWalk with a diagonal Σ or UniformRandomWalk (positivity flags allowed on either),
+// no adaptation — whose prior is ImproperPrior (with flags, or UniformRandomWalk; the flag-less
+// Gaussian one is the plain fused kernel), ImproperPosPrior, or ONE ProductPrior / StandardPrior factor that
 // is a Product of D univariates (no "reads θ[1]" dims-1 factor) or one MvNormal over all D; the families and positivity flags repeat across the chain's lanes (those of
 // coordinate i = those of i mod D/LPC).
 bool fused_prior_mvn(const UpdateHost &u) {
@@ -940,9 +950,10 @@ bool fused_prior_eligible(const emcmc_handle *h) {
         return false;
     bool anypos = false;
     for (uint8_t f : u.pos) anypos = anypos || f;
-    if (!uni && anypos) return false;  // GaussianRandomWalk's positivity round trips: the schedule kernels
     const bool slots = u.prior == EMCMC_PRIOR_PRODUCT || u.prior == EMCMC_PRIOR_STANDARD;
-    if (u.prior == EMCMC_PRIOR_IMPROPER ? !uni : (!slots && u.prior != EMCMC_PRIOR_IMPROPER_POS)) return false;
+    // ImproperPrior without flags on a GaussianRandomWalk: the plain (ahead-of-time) fused kernel
+    if (u.prior == EMCMC_PRIOR_IMPROPER ? (!uni && !anypos) : (!slots && u.prior != EMCMC_PRIOR_IMPROPER_POS))
+        return false;
     if (slots && (u.nslot != (uint32_t)D || u.psrc0 || u.pstart != 1ull || u.pend != (1ull << (D - 1))))
         return false;
     const bool mvn = fused_prior_mvn(u);  // then every slot is a row of it (one factor: pmvs = 0)
@@ -2422,7 +2433,8 @@ emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode,
     }
     if (!rwblock_eligible(tmp.updates, dim)) {
         copy_log("not a mwg_rw_block_kernel schedule: 1..8 UniformRandomWalk / GaussianRandomWalk updates "
-                 "(AdaptationUnifRW on a UniformRandomWalk only) at 17 <= dim <= 64",
+                 "(AdaptationUnifRW on a UniformRandomWalk only, at most 32 positivity flags on a "
+                 "GaussianRandomWalk) at 17 <= dim <= 64",
                  log_out, log_len);
         return EMCMC_INVALID_ARG;
     }
@@ -2454,10 +2466,10 @@ emcmc_status emcmc_prebuild_fused_prior_kernel(uint32_t dim, uint32_t lanes_per_
     }
     tmp.updates.push_back(std::move(uh));
     if (!fused_prior_eligible(&tmp)) {
-        copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk (no positivity flags) or UniformRandomWalk "
+        copy_log("not a fused-prior shape: one diagonal GaussianRandomWalk or UniformRandomWalk "
                  "over coords 0..dim-1 without adaptation, with ImproperPosPrior or a ProductPrior / StandardPrior "
-                 "that is one Product of dim univariates or one MvNormal over all dim coordinates (UniformRandomWalk: "
-                 "ImproperPrior too), families and positivity flags repeating across the chain's lanes, dim/lanes = "
+                 "that is one Product of dim univariates or one MvNormal over all dim coordinates (ImproperPrior too "
+                 "with positivity flags or a UniformRandomWalk), families and positivity flags repeating across the chain's lanes, dim/lanes = "
                  "8·2^k with more than one lane per chain",
                  log_out, log_len);
         return EMCMC_INVALID_ARG;

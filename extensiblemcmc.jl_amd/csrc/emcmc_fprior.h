@@ -4,9 +4,10 @@
 // diagonal GsnTargetLaw with LPC lanes per chain and two waves per SIMD: the cfg 2 kernel.  With
 // ImproperPrior its ratio adds + 0.0 − 0.0.  FusedUpdate<S> widens it to the joint updates over
 // coords 1:D whose every term separates over coordinates:
-//   - the proposal: GaussianRandomWalk with a diagonal Σ (no positivity flags), or
-//     UniformRandomWalk(ϵ) with positivity flags (random_walk.jl:45-94: θ° = θ·e^U + copysign(0, U)
-//     where pos, θ + U elsewhere; logpdf terms −log 2ϵ_j − log θ°_j folded left over j);
+//   - the proposal: GaussianRandomWalk with a diagonal Σ — with positivity flags, the reference's
+//     exp/log round trips of θ and θ° (random_walk.jl:136-171) — or UniformRandomWalk(ϵ) with
+//     positivity flags (random_walk.jl:45-94: θ° = θ·e^U + copysign(0, U) where pos, θ + U
+//     elsewhere; logpdf terms −log 2ϵ_j − log θ°_j folded left over j);
 //   - the prior: ImproperPrior, ImproperPosPrior (−Σ log θ_j), or ONE ProductPrior /
 //     StandardPrior factor that is a Product of D univariates (priors.jl:18-88);
 // compiled at run time for the structure (hiprtc, emcmc_rtc.hip) from the schedule struct S of
@@ -39,6 +40,16 @@ struct FusedUpdate {
     static constexpr uint32_t kCap = kUniform ? kMaxResample : kMaxResampleGsn;
     static constexpr uint32_t kFault = kFaultPriorResample;
     static constexpr bool kPos = kUniform && U::pos != 0ull;
+    // GaussianRandomWalk with positivity flags: the reference's in-place exp/log round trips
+    // (random_walk.jl:136-171), as mwg_rw_block_kernel's RT branch; no log-prior carry
+    static constexpr bool kRoundTrip = !kUniform && U::pos != 0ull;
+    template <int q>
+    __device__ static constexpr bool pos_at() { return ((U::pos >> q) & 1ull) != 0ull; }
+    __host__ __device__ static constexpr int first_pos() {
+        int q = 0;
+        while (q < 64 && ((U::pos >> q) & 1ull) == 0ull) ++q;
+        return q;
+    }
 
     // lane k of an LPC group takes lane k−1's value (quad_perm [0,0,2,2] / [0,0,1,2])
     template <int LPC>
@@ -213,6 +224,101 @@ struct FusedUpdate {
             const double s = fold<LPC, DPL>(v);
             return (U::prior == kPriorProduct) ? 0.0 + s : s;
         }
+    }
+
+    // (((v_p1 + v_p2) + …) over the flagged coordinates only, ascending, continued lane to lane (the
+    // flags repeat across the lanes, so every lane holds flagged coordinates at the same offsets)
+    template <int LPC, int DPL>
+    __device__ __forceinline__ static double fold_pos(const double (&v)[DPL]) {
+        double s = 0.0, carry = 0.0;
+        static_for<0, LPC>([&](auto KC) {
+            constexpr int k = decltype(KC)::value;
+            static_for<0, DPL>([&](auto QC) {
+                constexpr int q = decltype(QC)::value;
+                if constexpr (q == first_pos()) s = (k == 0) ? v[q] : carry + v[q];
+                else if constexpr (pos_at<q>()) s = s + v[q];
+            });
+            if constexpr (k + 1 < LPC) carry = from_previous_lane<LPC>(s);
+        });
+        if constexpr (LPC > 1) s = from_last_lane<LPC>(s);
+        return s;
+    }
+
+    // GaussianRandomWalk's proposal draw rs with positivity flags (random_walk.jl:136-151): a redraw
+    // first leaves θ ← exp(log θ) where flagged (the previous rand!'s round trip, cumulative over
+    // redraws, on the step's local copy tl); θ° = exp(log θ + L z) where flagged, θ + L z elsewhere.
+    // The normals are propose_diag's ((r << 17) | j); a flagged coordinate takes 0.0 + L z from it,
+    // which enters log θ + · as L z does (x + ±0 differ only at x = −0, and exp(±0) = 1).
+    template <int D, int LPC, int DPL>
+    __device__ __forceinline__ static void propose_round_trip(const ZigTabs &zt, uint32_t key0, uint32_t key1,
+                                                              const PhiloxVKeys &vk, uint32_t gid, uint32_t iter,
+                                                              uint32_t pidx0, uint32_t rs, int d0, const double *Lrw,
+                                                              double (&tl)[DPL], double (&tp)[DPL],
+                                                              uint32_t &faults) {
+        if (rs > 0) {
+            static_for<0, DPL>([&](auto QC) {
+                constexpr int q = decltype(QC)::value;
+                if constexpr (pos_at<q>()) tl[q] = exp_any(log_any(tl[q]));
+            });
+        }
+        double base[DPL];
+        static_for<0, DPL>([&](auto QC) {
+            constexpr int q = decltype(QC)::value;
+            base[q] = pos_at<q>() ? 0.0 : tl[q];
+        });
+        propose_diag<DPL, true>(zt, key0, key1, gid, iter, pidx0, (rs << 17) + (uint32_t)d0, base, Lrw + d0, tp,
+                                faults, vk);
+        static_for<0, DPL>([&](auto QC) {
+            constexpr int q = decltype(QC)::value;
+            if constexpr (pos_at<q>()) tp[q] = exp_any(log_any(tl[q]) + tp[q]);
+        });
+    }
+
+    // Both transition densities with the reference's round trips (mwg_rw_block_kernel's RT branch):
+    // logpdf(rw, θ°, θ) logs θ₁ = exp(log θ) and θ°, adds −Σ log θ₁ over the flags; logpdf(rw, θ, θ°)
+    // exponentiates both back and logs them again.  ta = θ°₃ (what an accept stores), t3 = θ₃
+    // (log_prior(::Previous)).  The squared norms in the canonical order, split across the lanes.
+    template <int D, int LPC, int DPL>
+    __device__ __forceinline__ static void ltd_round_trip(int d0, const double *iLrw, double c0,
+                                                          const double (&tl)[DPL], const double (&tp)[DPL],
+                                                          double (&ta)[DPL], double (&t3)[DPL], double &ltd_rev,
+                                                          double &ltd_fwd) {
+        double a1[DPL], b1[DPL], lv[DPL];
+        static_for<0, DPL>([&](auto QC) {
+            constexpr int q = decltype(QC)::value;
+            if constexpr (pos_at<q>()) {
+                const double v = log_any(exp_any(log_any(tl[q])));  // log θ₁
+                lv[q] = v;
+                a1[q] = log_any(tp[q]);  // μ = log θ°₁
+                b1[q] = v;               // x = log θ₁
+            } else {
+                lv[q] = 0.0;
+                a1[q] = tp[q];
+                b1[q] = tl[q];
+            }
+        });
+        const double lj1 = fold_pos<LPC, DPL>(lv);
+        const double q1 = canon_sumsq_f<D, LPC, DPL>([&](int i) { return (b1[i] - a1[i]) * iLrw[d0 + i]; });
+        ltd_rev = (c0 - q1 / 2.0) + (-lj1);
+        double r[DPL];
+        static_for<0, DPL>([&](auto QC) {
+            constexpr int q = decltype(QC)::value;
+            if constexpr (pos_at<q>()) {
+                const double v = log_any(exp_any(a1[q]));   // log θ°₂
+                const double a2 = log_any(exp_any(b1[q]));  // μ = log θ₂
+                lv[q] = v;
+                r[q] = v - a2;
+                ta[q] = exp_any(v);   // θ°₃
+                t3[q] = exp_any(a2);  // θ₃
+            } else {
+                r[q] = a1[q] - b1[q];
+                ta[q] = a1[q];
+                t3[q] = b1[q];
+            }
+        });
+        const double lj2 = fold_pos<LPC, DPL>(lv);
+        const double q2 = canon_sumsq_f<D, LPC, DPL>([&](int i) { return r[i] * iLrw[d0 + i]; });
+        ltd_fwd = (c0 - q2 / 2.0) + (-lj2);
     }
 
     // The reverse sum logpdf(rw, θ°, θ) = fold of −log 2ϵ_j − log θ_j depends on θ alone, so the

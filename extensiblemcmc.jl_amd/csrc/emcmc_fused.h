@@ -50,6 +50,7 @@ struct SiblingPace {
 struct NoFusedPrior {
     static constexpr bool kOn = false;
     static constexpr bool kUniform = false;
+    static constexpr bool kRoundTrip = false;  // GaussianRandomWalk's positivity round trips
     static constexpr int kConsts = 0;
 };
 
@@ -112,7 +113,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
     // log_prior(::Previous) carried: logpdf(prior, θ) at the launch's start, then the accepted
     // step's log_prior(::Proposal) (the same doubles)
     double lpc = 0.0;
-    if constexpr (PR::kOn) lpc = PR::template eval<D, LPC, DPL>(cst0 + 4 * D, a.consts + 4 * D, d0, th);
+    if constexpr (PR::kOn && !PR::kRoundTrip) lpc = PR::template eval<D, LPC, DPL>(cst0 + 4 * D, a.consts + 4 * D, d0, th);
     // UniformRandomWalk with positivity flags: logpdf(rw, θ°, θ) carried the same way
     double ltd_rev_c = 0.0;
     if constexpr (PR::kUniform)
@@ -134,8 +135,17 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         // two transition-density sums formed as θ° is; the Lrw / iLrw slots hold ϵ and −log 2ϵ)
         double thp[DPL];
         double lpp = 0.0, ltd_fwd = 0.0;
+        // PR::kRoundTrip: the step's local θ, which a redraw's round trip changes (θ itself does not)
+        double tl[PR::kRoundTrip ? DPL : 1];
+        if constexpr (PR::kRoundTrip) {
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) tl[i] = th[i];
+        }
         auto propose = [&](uint32_t rs) {
-            if constexpr (PR::kUniform)
+            if constexpr (PR::kRoundTrip)
+                PR::template propose_round_trip<D, LPC, DPL>(zt, a.key0, a.key1, vkeys, gid, iter, a.pidx0, rs, d0, Lrw,
+                                                             tl, thp, faults);
+            else if constexpr (PR::kUniform)
                 PR::template propose_uniform<D, LPC, DPL>(vkeys, gid, iter, a.pidx0, rs, d0, Lrw, iLrw, th, thp,
                                                           ltd_fwd);
             else
@@ -152,7 +162,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
                     break;
                 }
             }
-        } else if constexpr (PR::kUniform) {
+        } else if constexpr (PR::kUniform || PR::kRoundTrip) {
             propose(0u);
         } else {
             propose_diag<DPL, true>(zt, a.key0, a.key1, gid, iter, a.pidx0, (uint32_t)d0, th, Lrw + d0, thp, faults,
@@ -161,7 +171,7 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
         // ---- log_transition_density both ways (random_walk.jl:161-171):
         // sqmahal(θ°−θ) == sqmahal(θ−θ°) bitwise, so one evaluation serves both
         double ltd = 0.0;
-        if constexpr (!PR::kUniform)
+        if constexpr (!PR::kUniform && !PR::kRoundTrip)
             ltd = fma(-0.5, canon_sumsq_f<D, LPC, DPL>([&](int i) { return (thp[i] - th[i]) * iLrw[d0 + i]; }),
                       a.rw_c0);  // = c0 − q/2 (q/2 exact)
         // ---- compute_ll!: Σ_k logpdf(N(θ°, Σ_t), x_k) (gsn_target.jl:23-29)
@@ -223,19 +233,38 @@ __global__ void __launch_bounds__(diag_block(MINW), MINW) rwm_gsn_diag_kernel(co
             llp = a.n_tc0 - (a.S_c + a.nobs_d * qv) * 0.5;
         }
         if (!(llp - llp == 0.0)) faults |= 1u;  // NaN or ±Inf
+        // PR::kRoundTrip: θ° is stored before its round trips; then both densities, θ°₃ / θ₃ and
+        // the prior at each (no carry: θ₃ is not the θ the previous step's prior saw)
+        double ta[PR::kRoundTrip ? DPL : 1];
+        double ltd_rev_rt = 0.0;
+        if constexpr (PR::kRoundTrip) {
+            if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
+            double t3[DPL];
+            PR::template ltd_round_trip<D, LPC, DPL>(d0, iLrw, a.rw_c0, tl, thp, ta, t3, ltd_rev_rt, ltd_fwd);
+            if constexpr (PR::kOn) {
+                lpp = PR::template eval<D, LPC, DPL>(cst + 4 * D, a.consts + 4 * D, d0, ta);
+                lpc = PR::template eval<D, LPC, DPL>(cst + 4 * D, a.consts + 4 * D, d0, t3);
+            }
+        }
         // ---- accept_reject! (run.jl:271-278), left-associative as written
         double llr;
-        if constexpr (PR::kUniform) llr = ((((llp - ll) + ltd_rev_c) - ltd_fwd) + lpp) - lpc;
+        if constexpr (PR::kRoundTrip) llr = ((((llp - ll) + ltd_rev_rt) - ltd_fwd) + lpp) - lpc;
+        else if constexpr (PR::kUniform) llr = ((((llp - ll) + ltd_rev_c) - ltd_fwd) + lpp) - lpc;
         else llr = ((((llp - ll) + ltd) - ltd) + lpp) - lpc;
         const double E = accs.next<true>(zt, a.key0, a.key1, gid, iter, a.pidx0, s == 0, faults, vkeys);
         const bool acc = E > -llr;
-        if constexpr (PR::kOn) lpc = acc ? lpp : lpc;
+        if constexpr (PR::kOn && !PR::kRoundTrip) lpc = acc ? lpp : lpc;
         if constexpr (PR::kUniform) ltd_rev_c = acc ? ltd_fwd : ltd_rev_c;
         // ---- set_proposal! history: θ° with coords replaced (run.jl:237-239)
-        if constexpr (FULL) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
+        if constexpr (FULL && !PR::kRoundTrip) store_slot<D>(a.hist_prop + slot * D * C, hoff, thp);
         // ---- register_accept_reject_results! / set_chain_param! (run.jl:312-335)
+        if constexpr (PR::kRoundTrip) {
 #pragma unroll
-        for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
+            for (int i = 0; i < DPL; ++i) th[i] = acc ? ta[i] : th[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < DPL; ++i) th[i] = acc ? thp[i] : th[i];
+        }
         if (s + 1 == a.nsteps && sub == 0) chain_elem(a.ll_prop, c32) = llp;  // sub_ws°.ll after the launch
         ll = acc ? llp : ll;
         nacc += acc ? 1u : 0u;

@@ -86,7 +86,8 @@ def main():
     # (5) one random-walk update over all 32 coordinates with a prior / positivity flags: the
     # fused diagonal kernel with the prior compiled in where the prior is a Product of univariates
     # or one MvNormal, else mwg_rw_block_kernel; the "_block" twins force the schedule kernel, "_wide" the wide one
-    for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32", "rw_standard_mvnormal_d64"):
+    for name in ("rw_product_normal_d32", "rw_standard_mvnormal_d32", "unif_pos_d32", "rw_standard_mvnormal_d64",
+                 "gauss_pos_d32"):
         for suffix, variant in (("", a.variant), ("_block", L.VARIANT_NO_FUSED_PRIOR),
                                 ("_wide", L.VARIANT_NO_BLOCK | L.VARIANT_NO_FUSED_PRIOR)):
             if want(name + suffix) or (not only and suffix == ""):
@@ -101,7 +102,8 @@ WORKLOADS = ["mwg_d32_two_blocks", "mwg_d32_two_blocks_wide", "mwg_d64_two_block
              "haario_dense_d32_general", "mala_gsn_d32", "pcn_user_d32", "rw_product_normal_d32",
              "rw_product_normal_d32_block", "rw_product_normal_d32_wide", "rw_standard_mvnormal_d32",
              "rw_standard_mvnormal_d32_block", "rw_standard_mvnormal_d32_wide", "unif_pos_d32", "unif_pos_d32_block", "unif_pos_d32_wide",
-             "rw_standard_mvnormal_d32_lpc4", "rw_standard_mvnormal_d64", "rw_standard_mvnormal_d64_wide"]
+             "rw_standard_mvnormal_d32_lpc4", "rw_standard_mvnormal_d64", "rw_standard_mvnormal_d64_wide",
+             "gauss_pos_d32", "gauss_pos_d32_wide"]
 
 
 def run_isolated(names, a):
@@ -189,10 +191,11 @@ def rw_prior(name, suffix, C, M, report, variant=0, lanes=0):
       rw_product_normal_d32     GaussianRandomWalk(σ²I) + ProductPrior([Product(32 × Normal)])
       rw_standard_mvnormal_d32  GaussianRandomWalk(σ²I) + StandardPrior(MvNormal(μ0, Σ0)), Σ0 dense
       unif_pos_d32              UniformRandomWalk(ϵ) with positivity flags on every coordinate
+      gauss_pos_d32             GaussianRandomWalk(σ²I) with positivity flags on every coordinate
     and rw_standard_mvnormal_d64, the MvNormal shape over D = 64 on the 64-dimensional target."""
     D = 64 if name.endswith("_d64") else 32
     w = W.cfg2(8, D=D)
-    shift = 4.0 if name == "unif_pos_d32" else 0.0
+    shift = 4.0 if name in ("unif_pos_d32", "gauss_pos_d32") else 0.0
     mu = np.asarray(w.mu_true) + shift
     obs = np.asarray(w.obs) - np.asarray(w.mu_true) + mu
     s2 = (2.38 / np.sqrt(D * 10)) ** 2
@@ -205,6 +208,8 @@ def rw_prior(name, suffix, C, M, report, variant=0, lanes=0):
         B = np.random.default_rng(9).standard_normal((D, D))
         eng.add_gaussian_rw_update(np.arange(D), s2 * np.eye(D), prior=L.PRIOR_STANDARD,
                                    prior_factors=[(L.DIST_MVNORMAL, D, np.zeros(D), B @ B.T / D + np.eye(D))])
+    elif name == "gauss_pos_d32":
+        eng.add_gaussian_rw_update(np.arange(D), 0.05 * s2 * np.eye(D), pos=np.ones(D))
     else:
         eng.add_uniform_rw_update(np.arange(D), 0.06, pos=np.ones(D))
     eng.set_gsn_target(mu, np.eye(D), obs)

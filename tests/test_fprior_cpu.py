@@ -66,7 +66,16 @@ def test_refuses_lane_splits_of_the_canonical_sum(cache, D, lanes, mvn):
     assert "not a fused-prior shape" in str(e.value)
 
 
-@pytest.mark.parametrize("case", ["mvnormal_part", "dims1", "asymmetric", "pos", "uniform_asym_pos", "adaptive", "dense",
+@pytest.mark.parametrize("pos,prior", [([1] * 32, L.PRIOR_IMPROPER), ([j % 2 for j in range(32)], L.PRIOR_IMPROPER_POS)])
+def test_gaussian_random_walk_with_pos_flags(cache, pos, prior):
+    """GaussianRandomWalk's positivity round trips on the fused kernel (ImproperPrior too: the
+    flags alone take it off the plain fused kernel)."""
+    u, keep = Engine.gaussian_rw_desc(range(32), 0.001 * np.eye(32), pos=pos, prior=prior)
+    L.prebuild_fused_prior_kernel(32, u)
+    assert len(list(cache.glob("*.co"))) == 2
+
+
+@pytest.mark.parametrize("case", ["mvnormal_part", "dims1", "asymmetric", "gaussian_asym_pos", "uniform_asym_pos", "adaptive", "dense",
                                   "subset", "improper"])
 def test_refuses_other_shapes(cache, case):
     D = 32
@@ -80,8 +89,8 @@ def test_refuses_other_shapes(cache, case):
         comps = [(N_, 0.0, 2.0)] * D
         comps[3] = (G_, 2.0, 1.0)
         fac = [(P_, D, comps)]
-    elif case == "pos":  # GaussianRandomWalk's positivity round trips
-        pos = [j % 2 for j in range(D)]
+    elif case == "gaussian_asym_pos":  # flags on lane 1's coordinates only
+        pos = [j >= 16 for j in range(D)]
     elif case == "uniform_asym_pos":  # flags on lane 0's coordinates only
         pos = [j < 16 for j in range(D)]
     elif case == "dense":

@@ -208,3 +208,29 @@ def test_shapes_the_fused_kernel_declines(oracle, D, lanes, factors):
     eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), lanes=lanes)
     assert not eng.kernel_name().startswith("rwm_gsn_diag_kernel"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
+
+
+@pytest.mark.parametrize("D,lanes,pos,prior", [(32, 0, "all", L.PRIOR_IMPROPER), (32, 0, "odd", L.PRIOR_IMPROPER_POS),
+                                               (64, 0, "all", L.PRIOR_IMPROPER), (24, 0, "all", L.PRIOR_IMPROPER),
+                                               (16, 0, "all", L.PRIOR_PRODUCT), (32, 2, "odd", L.PRIOR_PRODUCT)])
+def test_gaussian_random_walk_with_pos_round_trips(oracle, D, lanes, pos, prior):
+    """GaussianRandomWalk with positivity flags on the fused kernel: θ° = exp(log θ + L z) where
+    flagged, both densities through the reference's exp/log round trips (θ°₃ stored on accept,
+    the prior at θ°₃ and θ₃, no carry), −Σ log θ₁ folded over the flagged coordinates lane to lane;
+    with a Product of Gammas the flag-less coordinates leave the support and redraw, and each
+    redraw round-trips the step's local θ first (cumulative over redraws)."""
+    C, M = 2048, 60
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    lpc = lanes or {16: 2, 24: 1, 32: 2, 64: 4}[D]
+    dpl = D // lpc
+    flags = [True] * D if pos == "all" else [(j % dpl) % 2 == 1 for j in range(D)]
+    th0 = np.tile(mu, (C, 1))
+    fac = None
+    if prior == L.PRIOR_PRODUCT:  # Gammas where flagged, Uniform(2, 4) elsewhere: those redraw
+        fac = [(P_, D, [(G_, 6.0, 0.5) if flags[j] else (U_, 2.0, 4.0) for j in range(D)])]
+        th0 = np.full((C, D), 3.0)
+    f = 2.0 if prior == L.PRIOR_PRODUCT else 0.05
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=f) * np.eye(D), pos=flags, prior=prior, factors=fac)]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, lanes=lanes, spl=13)
+    assert_fused(eng, D, lpc)
+    check(oracle, eng, st, h, steps, ups, 1)

@@ -182,18 +182,33 @@ def test_d24_dense_sigma_all_families_and_redraws(oracle):
 def test_gaussian_rw_with_pos_round_trips(oracle, D):
     """GaussianRandomWalk with positivity flags on half the coordinates: the reference's
     in-place exp/log round trips (θ°₃, θ₃), ImproperPosPrior (no log-prior carry), odd and
-    even D.  At D = 33 the round trips' vectors exceed the register file (the code object
-    needs scratch), so the schedule runs on the wide kernel: the same bits either way."""
+    even D, on the schedule kernel (EMCMC_VARIANT_NO_FUSED_PRIOR; tests/test_gpu_fprior.py runs
+    the fused one).  At D = 33 the round trips' vectors exceed the register file (the code
+    object needs scratch), so the schedule runs on the wide kernel: the same bits either way."""
     C, M = 1024, 120
     seed, mu, ts, obs = problem(D, shift=3.0)
     pos = [j % 2 == 1 for j in range(D)]
     ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=0.05) * np.eye(D), pos=pos, prior=L.PRIOR_IMPROPER_POS)]
     th0 = np.tile(mu, (C, 1))
-    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0)
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, variant=L.VARIANT_NO_FUSED_PRIOR)
     if D == 33:
         assert eng.kernel_name().startswith("mwg_wide_kernel<D=33"), eng.kernel_name()
     else:
         assert_block(eng, D)
+    check(oracle, eng, st, h, steps, ups, 1)
+
+
+def test_gaussian_rw_with_64_pos_flags_runs_on_the_wide_kernel(oracle):
+    """GaussianRandomWalk over all 64 coordinates with every one flagged, off the fused kernel
+    (EMCMC_VARIANT_NO_FUSED_PRIOR): the schedule kernel is not compiled (more than 32 flagged
+    coordinates always need scratch, and at 64 the gfx950 backend aborts the compiling process),
+    the wide kernel runs it with the oracle's bits."""
+    D, C, M = 64, 512, 24
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=0.05) * np.eye(D), pos=[True] * D)]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)),
+                                 variant=L.VARIANT_NO_FUSED_PRIOR)
+    assert eng.kernel_name().startswith("mwg_wide_kernel<D=64"), eng.kernel_name()
     check(oracle, eng, st, h, steps, ups, 1)
 
 

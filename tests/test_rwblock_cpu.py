@@ -34,11 +34,17 @@ def test_prebuild_compiles_a_two_update_schedule(cache):
     assert len(list(cache.glob("*.co"))) == 1
 
 
-@pytest.mark.parametrize("case", ["mix", "small_d", "mala"])
+@pytest.mark.parametrize("case", ["mix", "small_d", "mala", "gaussian_pos_64", "gaussian_pos_33"])
 def test_prebuild_refuses_other_shapes(cache, case):
-    D = 20 if case != "small_d" else 8
+    """... and a GaussianRandomWalk with more than 32 positivity flags: its round trips always need
+    scratch, and at 64 flags the gfx950 backend aborts the compiling process — the shape is refused
+    before hiprtc sees it (the wide kernel runs it)."""
+    D = {"small_d": 8, "gaussian_pos_64": 64, "gaussian_pos_33": 40}.get(case, 20)
     coords = range(D)
-    if case == "mala":
+    if case.startswith("gaussian_pos"):
+        n = 64 if case == "gaussian_pos_64" else 33
+        u, keep = Engine.gaussian_rw_desc(range(n), 0.001 * np.eye(n), pos=[1] * n)
+    elif case == "mala":
         u = L.EmcmcUpdateDesc()
         u.kernel = L.MALA
         c = np.arange(D, dtype=np.uint32)
@@ -58,3 +64,11 @@ def test_prebuild_refuses_other_shapes(cache, case):
         L.prebuild_rw_block_kernel(D, u)
     assert e.value.status == L.INVALID_ARG
     assert not list(cache.glob("*.co"))
+
+
+def test_prebuild_compiles_32_gaussian_pos_flags(cache):
+    """The limit's edge: 32 flagged coordinates (every other one of 64) still compile."""
+    D = 64
+    u, keep = Engine.gaussian_rw_desc(range(D), 0.001 * np.eye(D), pos=[j % 2 for j in range(D)])
+    L.prebuild_rw_block_kernel(D, u)
+    assert len(list(cache.glob("*.co"))) == 1

@@ -444,10 +444,10 @@ emcmc_status emcmc_prebuild_rw_block_kernel(uint32_t dim, uint32_t history_mode,
 
 /* The same for the fused diagonal step with the update's separable terms compiled in
  * (rwm_gsn_diag_kernel + FusedUpdate), the kernel a handle selects for ONE update over 0..dim-1
- * without adaptation — a GaussianRandomWalk with a diagonal Σ and no positivity flags, or a
- * UniformRandomWalk (flags allowed) — whose prior is ImproperPosPrior or one ProductPrior /
- * StandardPrior factor: a Product of dim univariates or an MvNormal over all dim coordinates (a
- * UniformRandomWalk also ImproperPrior), families and flags repeating across the chain's lanes,
+ * without adaptation — a GaussianRandomWalk with a diagonal Σ or a UniformRandomWalk, positivity
+ * flags allowed on either — whose prior is ImproperPosPrior or one ProductPrior / StandardPrior
+ * factor: a Product of dim univariates or an MvNormal over all dim coordinates (ImproperPrior too
+ * with flags or a UniformRandomWalk), families and flags repeating across the chain's lanes,
  * dim / lanes = 8·2^k with more than one lane, on the built-in GsnTargetLaw with a diagonal Σ
  * (unit_target != 0: Σ = I).  lanes_per_chain as in emcmc_config (0 = automatic).  Compiles both
  * occupancies the handle may try (two waves per SIMD, then one). */

@@ -234,3 +234,50 @@ def test_gaussian_random_walk_with_pos_round_trips(oracle, D, lanes, pos, prior)
     eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, th0, lanes=lanes, spl=13)
     assert_fused(eng, D, lpc)
     check(oracle, eng, st, h, steps, ups, 1)
+
+
+@pytest.mark.parametrize("shape", ["gauss_pos", "mvnormal"])
+def test_accept_only_suffstat_launch_cuts_non_unit_target(oracle, shape):
+    """The new shapes under the other modes: accept-only histories, the sufficient-statistic
+    likelihood, a non-unit diagonal Σ_t, launches of 7 steps across three run calls (the round
+    trips carry nothing; the MvNormal prior's carry is re-evaluated at each launch's start)."""
+    D, C, M = 32, 2048, 70
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    ts = np.diag(np.linspace(0.5, 2.0, D))
+    if shape == "gauss_pos":
+        ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=0.05) * np.eye(D), pos=[j % 4 != 0 for j in range(D)],
+                                 prior=L.PRIOR_IMPROPER_POS)]
+    else:
+        ups = [oracle.mwg_update(2, range(D), sigma=s2(D) * np.eye(D), prior=L.PRIOR_STANDARD,
+                                 factors=[(MV_, D, 3.0 * np.ones(D), dense_cov(D, seed=4))])]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), ll_mode=L.LL_SUFFSTAT,
+                                 hist=L.HIST_ACCEPT_ONLY, spl=7, calls=[(0, 17), (17, 40), (40, M)])
+    assert_fused(eng, D, 2)
+    assert "UNIT_T" not in eng.kernel_name()
+    check(oracle, eng, st, h, steps, ups, 1, full=False)
+
+
+def test_gaussian_round_trips_fused_and_schedule_kernel_agree_at_scale():
+    """GaussianRandomWalk with every other coordinate flagged at D = 32 over 16,384 chains: the
+    fused kernel (two lanes per chain) and mwg_rw_block_kernel (EMCMC_VARIANT_NO_FUSED_PRIOR)
+    give the same θ, ll and θ° / accept histories on every chain."""
+    D, C, M = 32, 16384, 40
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    out = []
+    for variant in (0, L.VARIANT_NO_FUSED_PRIOR):
+        eng = Engine(EngineConfig(dim=D, num_chains=C, num_mcmc_steps=M, seed=seed, kernel_variant=variant))
+        eng.add_gaussian_rw_update(np.arange(D), s2(D, f=0.05) * np.eye(D), pos=[j % 2 for j in range(D)],
+                                   prior=L.PRIOR_IMPROPER_POS)
+        eng.set_gsn_target(mu, ts, obs)
+        eng.set_state(np.tile(mu, (C, 1)))
+        eng.run(full_steps(M, 1))
+        eng.synchronize(allow_faults=True)
+        out.append((eng.kernel_name(), eng.get_state(), eng.get_history(L.H_ACCEPT, 1, M),
+                    eng.get_history(L.H_PROPOSAL, 1, M), eng.get_history(L.H_STATE, 1, M)))
+        eng.close()
+    assert out[0][0].startswith("rwm_gsn_diag_kernel<D=32,LPC=2"), out[0][0]
+    assert out[1][0].startswith("mwg_rw_block_kernel<D=32"), out[1][0]
+    for x, y in zip(out[0][1], out[1][1]):
+        assert np.array_equal(x, y)
+    for k in (2, 3, 4):
+        assert np.array_equal(out[0][k], out[1][k])

@@ -259,8 +259,9 @@ def test_accept_only_suffstat_launch_cuts_non_unit_target(oracle, shape):
 
 def test_gaussian_round_trips_fused_and_schedule_kernel_agree_at_scale():
     """GaussianRandomWalk with every other coordinate flagged at D = 32 over 16,384 chains: the
-    fused kernel (two lanes per chain) and mwg_rw_block_kernel (EMCMC_VARIANT_NO_FUSED_PRIOR)
-    give the same θ, ll and θ° / accept histories on every chain."""
+    fused kernel (two lanes per chain) and the schedule path (EMCMC_VARIANT_NO_FUSED_PRIOR; with
+    ImproperPosPrior the schedule kernel needs scratch, so the wide kernel runs it) give the same
+    θ, ll and θ° / accept histories on every chain."""
     D, C, M = 32, 16384, 40
     seed, mu, ts, obs = problem(D, shift=3.0)
     out = []
@@ -276,7 +277,7 @@ def test_gaussian_round_trips_fused_and_schedule_kernel_agree_at_scale():
                     eng.get_history(L.H_PROPOSAL, 1, M), eng.get_history(L.H_STATE, 1, M)))
         eng.close()
     assert out[0][0].startswith("rwm_gsn_diag_kernel<D=32,LPC=2"), out[0][0]
-    assert out[1][0].startswith("mwg_rw_block_kernel<D=32"), out[1][0]
+    assert out[1][0].startswith(("mwg_rw_block_kernel<D=32", "mwg_wide_kernel<D=32")), out[1][0]
     for x, y in zip(out[0][1], out[1][1]):
         assert np.array_equal(x, y)
     for k in (2, 3, 4):

@@ -282,3 +282,24 @@ def test_gaussian_round_trips_fused_and_schedule_kernel_agree_at_scale():
         assert np.array_equal(x, y)
     for k in (2, 3, 4):
         assert np.array_equal(out[0][k], out[1][k])
+
+
+@pytest.mark.parametrize("kind", ["gaussian", "uniform"])
+def test_mvnormal_prior_with_pos_flags(oracle, kind):
+    """An MvNormal prior beside positivity flags: with GaussianRandomWalk's round trips it is
+    evaluated at θ°₃ and θ₃ (no carry); with UniformRandomWalk it is carried and its −Inf-free
+    values drive no redraws (an MvNormal has full support)."""
+    D, C, M = 32, 2048, 60
+    seed, mu, ts, obs = problem(D, shift=3.0)
+    flags = [(j % 16) % 3 != 2 for j in range(D)]
+    fac = [(MV_, D, 3.0 * np.ones(D), dense_cov(D, seed=7))]
+    if kind == "gaussian":
+        ups = [oracle.mwg_update(2, range(D), sigma=s2(D, f=0.05) * np.eye(D), pos=flags, prior=L.PRIOR_STANDARD,
+                                 factors=fac)]
+    else:
+        ups = [oracle.mwg_update(1, range(D), eps=[0.03 + 0.002 * (j % 16) for j in range(D)], pos=flags,
+                                 prior=L.PRIOR_PRODUCT, factors=fac)]
+    eng, st, h, steps = run_pair(oracle, D, C, M, ups, mu, ts, obs, seed, np.tile(mu, (C, 1)), spl=9)
+    name = eng.kernel_name()
+    assert name.startswith("rwm_gsn_diag_kernel<D=32,LPC=2,") and "MvNormal" in name, name
+    check(oracle, eng, st, h, steps, ups, 1)
